@@ -1,0 +1,130 @@
+"""In-tree native build for every C++/HIP component of the framework.
+
+Everything is compiled for gfx950 only (``--offload-arch=gfx950``) with ``hipcc``; host-only
+C++ (the node agent library and CLIs) is built with ``g++``. Artefacts land in
+``gpu_operator_amd/_native/`` so they travel with the repository snapshot to the GPU box
+(they are git-ignored, not gpurun-ignored).
+
+Usage::
+
+    python -m gpu_operator_amd._build          # build what is stale
+    python -m gpu_operator_amd._build --force  # rebuild everything
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import List, Sequence
+
+REPO = Path(__file__).resolve().parent.parent
+NATIVE_SRC = REPO / "native"
+OUT = Path(__file__).resolve().parent / "_native"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("AMDGO_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    cand = ROCM / "bin" / "hipcc"
+    return str(cand) if cand.exists() else "hipcc"
+
+
+@dataclass
+class Target:
+    name: str                     # output file name (relative to OUT)
+    sources: Sequence[str]        # relative to native/
+    kind: str                     # "hip-shared" | "hip-exe" | "cxx-shared" | "cxx-exe" | "pyext"
+    flags: List[str] = field(default_factory=list)
+    libs: List[str] = field(default_factory=list)
+    headers: Sequence[str] = ()   # extra dependency files (relative to native/)
+
+    @property
+    def output(self) -> Path:
+        return OUT / self.name
+
+    def deps(self) -> List[Path]:
+        return [NATIVE_SRC / s for s in list(self.sources) + list(self.headers)]
+
+    def stale(self) -> bool:
+        if not self.output.exists():
+            return True
+        out_m = self.output.stat().st_mtime
+        return any(p.stat().st_mtime > out_m for p in self.deps() if p.exists())
+
+    def command(self) -> List[str]:
+        srcs = [str(NATIVE_SRC / s) for s in self.sources]
+        inc = [f"-I{NATIVE_SRC / 'include'}"]
+        if self.kind.startswith("hip"):
+            base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wall",
+                    "-Wno-unused-function", "-Wno-unused-result"] + inc
+            if self.kind == "hip-shared":
+                base += ["-fPIC", "-shared"]
+            return base + self.flags + srcs + ["-o", str(self.output)] + self.libs
+        if self.kind == "pyext":
+            import pybind11  # noqa: WPS433 (build-time only)
+            py_inc = sysconfig.get_paths()["include"]
+            suffix_ok = self.name.endswith(sysconfig.get_config_var("EXT_SUFFIX") or ".so")
+            assert suffix_ok, self.name
+            return (["g++", "-O2", "-std=c++17", "-Wall", "-fPIC", "-shared",
+                     f"-I{py_inc}", f"-I{pybind11.get_include()}"] + inc + self.flags + srcs
+                    + ["-o", str(self.output)] + self.libs)
+        base = ["g++", "-O2", "-std=c++17", "-Wall", "-Wextra"] + inc
+        if self.kind == "cxx-shared":
+            base += ["-fPIC", "-shared"]
+        return base + self.flags + srcs + ["-o", str(self.output)] + self.libs
+
+
+def _pyext_name(stem: str) -> str:
+    return stem + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
+
+
+TARGETS: List[Target] = [
+    # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.
+    Target("libamdgo_hip.so", ["hip/gemm_bf16.hip", "hip/smoke.hip"], "hip-shared"),
+]
+
+
+def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> List[Path]:
+    OUT.mkdir(parents=True, exist_ok=True)
+    (OUT / "bin").mkdir(exist_ok=True)
+    todo = [t for t in TARGETS if force or t.stale()]
+
+    def run(t: Target) -> Path:
+        cmd = t.command()
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        t.output.parent.mkdir(parents=True, exist_ok=True)
+        proc = subprocess.run(cmd, capture_output=True, text=True)
+        if proc.returncode != 0:
+            raise RuntimeError(f"build of {t.name} failed:\n{' '.join(cmd)}\n{proc.stderr[-6000:]}")
+        return t.output
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        built = list(ex.map(run, todo))
+    return built
+
+
+def main(argv: Sequence[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    if shutil.which(hipcc()) is None and not Path(hipcc()).exists():
+        print("hipcc not found", file=sys.stderr)
+        return 1
+    built = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    for p in built:
+        print(f"built {p.relative_to(REPO)}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,112 @@
+"""Validator GEMM: hand-written CDNA4 MFMA bf16 kernel (``native/hip/gemm_bf16.hip``).
+
+``C[M,N] = A[M,K] @ Bt[N,K].T`` with bf16 operands, fp32 accumulation and bf16 output.
+Both operands are K-major, the layout the MFMA 16x16x32 fragments read without a transpose.
+
+Replaces the reference validator's ``vectorAdd`` pass/fail probe
+(reference: validator/cuda-workload-validation.yaml:20) with a matrix-core
+throughput probe whose result feeds ``amd_gpu_operator_validator_gemm_tflops``.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+from . import _lib
+
+
+def _stream_ptr(torch, device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _check_operand(t, name: str, rows: int, k: int) -> None:
+    import torch
+
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name} must be bfloat16, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if tuple(t.shape) != (rows, k) or not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous [{rows},{k}], got {tuple(t.shape)}")
+
+
+def gemm_bf16(a, bt, out=None, *, generic: bool = False):
+    """Compute ``a @ bt.T`` on the MFMA kernel. ``a``: [M,K], ``bt``: [N,K] (bf16, contiguous)."""
+    import torch
+
+    m, k = a.shape
+    n = bt.shape[0]
+    _check_operand(a, "a", m, k)
+    _check_operand(bt, "bt", n, k)
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    else:
+        _check_operand(out, "out", m, n)
+    lib = _lib.load()
+    fn = lib.amdgo_gemm_bf16_generic if generic else lib.amdgo_gemm_bf16
+    err = fn(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k, _stream_ptr(torch, a.device))
+    _lib.check(err, "amdgo_gemm_bf16")
+    return out
+
+
+def fast_path_supported(m: int, n: int, k: int) -> bool:
+    lib = _lib.load()
+    return m % lib.amdgo_gemm_tile_m() == 0 and n % lib.amdgo_gemm_tile_n() == 0 \
+        and k % lib.amdgo_gemm_tile_k() == 0
+
+
+def fill_uniform_(t, seed: int = 1234):
+    """Fill a bf16 GPU tensor with deterministic uniform [-1, 1) values (native kernel)."""
+    import torch
+
+    if t.dtype != torch.bfloat16 or not t.is_cuda or not t.is_contiguous():
+        raise ValueError("fill_uniform_ needs a contiguous bf16 GPU tensor")
+    lib = _lib.load()
+    _lib.check(lib.amdgo_fill_uniform_bf16(t.data_ptr(), t.numel(), seed & 0xFFFFFFFF,
+                                           _stream_ptr(torch, t.device)), "fill_uniform")
+    return t
+
+
+def reference_rows(a, bt, rows):
+    """fp32 reference of selected output rows, computed by an independent scalar HIP kernel."""
+    import torch
+
+    rows_t = torch.as_tensor(rows, dtype=torch.int32, device=a.device).contiguous()
+    n, k = bt.shape
+    out = torch.empty((rows_t.numel(), n), dtype=torch.float32, device=a.device)
+    lib = _lib.load()
+    _lib.check(lib.amdgo_gemm_ref_rows(a.data_ptr(), bt.data_ptr(), rows_t.data_ptr(),
+                                       rows_t.numel(), out.data_ptr(), n, k,
+                                       _stream_ptr(torch, a.device)), "gemm_ref_rows")
+    return out
+
+
+@dataclass
+class GemmCheck:
+    max_abs_err: float
+    max_rel_err: float
+    tol: float
+    ok: bool
+
+
+def verify(a, bt, c, nrows: int = 64, seed: int = 0, rows: Optional[list] = None) -> GemmCheck:
+    """Compare sampled output rows of ``c`` with an fp32 reference (tolerance for bf16 output)."""
+    import torch
+
+    m, k = a.shape
+    g = torch.Generator().manual_seed(seed)
+    if rows is None:
+        rows = torch.randint(0, m, (min(nrows, m),), generator=g).tolist()
+    ref = reference_rows(a, bt, rows)
+    got = c[torch.as_tensor(rows, device=c.device)].float()
+    err = (got - ref).abs()
+    scale = ref.abs().clamp_min(1.0)
+    # bf16 output rounding (2^-8 relative) + fp32 accumulation-order differences.
+    tol = 1.0 / 128
+    max_rel = float((err / scale).max())
+    return GemmCheck(float(err.max()), max_rel, tol, max_rel <= tol)
+
+
+def tflops(m: int, n: int, k: int, seconds: float) -> float:
+    return 2.0 * m * n * k / seconds / 1e12

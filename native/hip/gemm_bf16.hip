@@ -1,0 +1,313 @@
+// CDNA4 (gfx950) bf16 GEMM for the node validator workload.
+//
+//   C[M,N] (bf16) = A[M,K] (bf16, K-major) * Bt[N,K]^T (bf16, K-major), fp32 accumulation.
+//
+// This replaces the reference operator's only GPU code, the prebuilt CUDA-samples
+// `vectorAdd` binary that its validator image copies in (validator/Dockerfile:33-35,
+// validator/cuda-workload-validation.yaml:20). There the kernel was a pass/fail
+// check; here it is a throughput probe that exercises the matrix cores, LDS and HBM.
+//
+// Design (MI355X-first, see docs/validator-gemm.md):
+//   * 256x256 output tile per 512-thread workgroup (8 wave64s laid out 2(M) x 4(N)),
+//     each wave owns a 128x64 sub-tile = 8x4 MFMA 16x16x32 accumulators (128 AGPR/VGPR).
+//   * K-step BK=64. Global->LDS staging with `global_load_lds_dwordx4` (LDS-DMA, no VGPR
+//     round trip). The LDS image is lane-linear (hardware rule) so the bank-conflict XOR
+//     swizzle is applied to the per-lane SOURCE address and again on the ds_read side.
+//   * Two LDS buffers (2 x 64 KiB); the next K-tile's DMA is issued before the current
+//     tile's ds_read+MFMA work so HBM latency hides behind 64 MFMAs per wave.
+//   * Operands are swapped in the MFMA (Bt fragment as "A") so every lane ends up holding
+//     4 consecutive N-columns of one output row: 8-byte packed bf16 stores in the epilogue.
+//   * XCD-aware, bijective blockIdx remap (8 XCDs, private 4 MiB L2 each) followed by a
+//     grouped (GROUP_M) raster so co-resident tiles on one XCD share A/B panels in L2.
+//
+// A bounds-checked generic kernel handles shapes that are not multiples of the tile.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+constexpr int BM = 256;
+constexpr int BN = 256;
+constexpr int BK = 64;
+constexpr int NTHREADS = 512;
+constexpr int ROW_BYTES = BK * 2;             // 128 B per staged row
+constexpr int PANEL_BYTES = BM * ROW_BYTES;   // 32 KiB per operand per K-tile
+constexpr int BUF_BYTES = 2 * PANEL_BYTES;    // A + B
+constexpr int LDS_BYTES = 2 * BUF_BYTES;      // double buffered: 128 KiB
+constexpr int GROUP_M = 8;
+constexpr int NXCD = 8;
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // Bijective for any nwg: blocks b and b+8 share an XCD (observed round-robin dispatch);
+  // give each XCD a contiguous run of logical tiles.
+  const int xcd = bid % NXCD;
+  const int q = nwg / NXCD;
+  const int r = nwg % NXCD;
+  const int start = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return start + bid / NXCD;
+}
+
+__device__ __forceinline__ void tile_coords(int wgid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  tm = first_m + in_group % gsize;
+  tn = in_group / gsize;
+}
+
+// Stage one 256-row x 64-k panel (32 KiB) of a K-major operand into LDS.
+// 32 wave-instructions of 1 KiB (8 rows each); wave w issues rows blocks {w, w+8, w+16, w+24}.
+__device__ __forceinline__ void stage_panel(const __bf16* __restrict__ g, int ld, int k0,
+                                            char* lds_panel, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rblk = i * 8 + wid;           // 8-row block index 0..31
+    const int r = rblk * 8 + (lane >> 3);   // row inside the panel
+    const int pc = lane & 7;                // physical 16-B chunk this lane writes
+    const int c = pc ^ ((r >> 1) & 7);      // logical chunk it must fetch (XOR involution)
+    const __bf16* src = g + (size_t)r * ld + k0 + c * 8;
+    char* dst = lds_panel + rblk * 1024;    // wave-uniform base; HW adds lane*16
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(NTHREADS)
+gemm_bf16_256x256(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                  __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2;   // 0..1  -> 128-row half of the tile
+  const int wc = wid & 3;    // 0..3  -> 64-col quarter of the tile
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+
+  // Per-lane LDS read offsets for the two 32-deep k-steps of a BK=64 tile.
+  // Row within a 16-row fragment = lane&15; logical chunk = kk*4 + (lane>>4);
+  // swizzle term ((row>>1)&7) only depends on lane because fragment bases are 16-row aligned.
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_row0 = wr * 128;   // first A row (panel-local) this wave reads
+  const int b_row0 = wc * 64;    // first Bt row (panel-local) this wave reads
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ktiles = K / BK;
+
+  stage_panel(gA, K, 0, smem, wid, lane);
+  stage_panel(gB, K, 0, smem + PANEL_BYTES, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < ktiles; ++t) {
+    char* cur = smem + (t & 1) * BUF_BYTES;
+    if (t + 1 < ktiles) {
+      char* nxt = smem + ((t + 1) & 1) * BUF_BYTES;
+      stage_panel(gA, K, (t + 1) * BK, nxt, wid, lane);
+      stage_panel(gB, K, (t + 1) * BK, nxt + PANEL_BYTES, wid, lane);
+    }
+    const char* la = cur + a_row0 * ROW_BYTES;
+    const char* lb = cur + PANEL_BYTES + b_row0 * ROW_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        bfr[n] = *reinterpret_cast<const bf16x8*>(lb + n * 16 * ROW_BYTES + lane_off[kk]);
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+        af[m] = *reinterpret_cast<const bf16x8*>(la + m * 16 * ROW_BYTES + lane_off[kk]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n], af[m], acc[m][n], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // Epilogue: lane holds C[row = m*16 + (lane&15)][col = n*16 + 4*(lane>>4) + j], j = 0..3.
+  const int row_base = tm * BM + wr * 128 + (lane & 15);
+  const int col_base = tn * BN + wc * 64 + 4 * (lane >> 4);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    __bf16* crow = C + (size_t)(row_base + m * 16) * N + col_base;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 v;
+      v[0] = (__bf16)acc[m][n][0];
+      v[1] = (__bf16)acc[m][n][1];
+      v[2] = (__bf16)acc[m][n][2];
+      v[3] = (__bf16)acc[m][n][3];
+      *reinterpret_cast<bf16x4*>(crow + n * 16) = v;
+    }
+  }
+}
+
+// Generic bounds-checked MFMA kernel (64x64 tile, 4 waves of 32x32), register-staged.
+// Used for shapes that are not multiples of 256/256/64 and as a second, independent
+// implementation for cross-checking the fast path.
+constexpr int GBM = 64, GBN = 64, GBK = 32;
+
+__global__ void __launch_bounds__(256)
+gemm_bf16_generic(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                  __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) __bf16 sa[GBM][GBK + 8];
+  __shared__ __attribute__((aligned(16))) __bf16 sb[GBN][GBK + 8];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // 256 threads x 8 elements = 64 rows x 32 k per operand.
+  const int lr = threadIdx.x >> 2;        // row 0..63
+  const int lk = (threadIdx.x & 3) * 8;   // k offset 0,8,16,24
+  for (int k0 = 0; k0 < K; k0 += GBK) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = k0 + lk + e;
+      const int ra = m0 + lr, rb = n0 + lr;
+      sa[lr][lk + e] = (ra < M && k < K) ? A[(size_t)ra * K + k] : (__bf16)0.f;
+      sb[lr][lk + e] = (rb < N && k < K) ? Bt[(size_t)rb * K + k] : (__bf16)0.f;
+    }
+    __syncthreads();
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        af[i][e] = sa[wr * 32 + i * 16 + (lane & 15)][8 * (lane >> 4) + e];
+        bfr[i][e] = sb[wc * 32 + i * 16 + (lane & 15)][8 * (lane >> 4) + e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wr * 32 + i * 16 + (lane & 15);
+        const int col = n0 + wc * 32 + j * 16 + 4 * (lane >> 4) + e;
+        if (row < M && col < N) C[(size_t)row * N + col] = (__bf16)acc[i][j][e];
+      }
+}
+
+// fp32-accumulating reference (one thread per output element; sampled rows only).
+__global__ void gemm_ref_rows(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                              const int* __restrict__ rows, int nrows, float* __restrict__ out,
+                              int N, int K) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ri = blockIdx.y;
+  if (col >= N || ri >= nrows) return;
+  const __bf16* a = A + (size_t)rows[ri] * K;
+  const __bf16* b = Bt + (size_t)col * K;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += (float)a[k] * (float)b[k];
+  out[(size_t)ri * N + col] = s;
+}
+
+// Deterministic uniform [-1,1) bf16 fill (counter-based hash), so validator runs on
+// random data (zero-filled operands inflate MFMA clocks and hide layout bugs).
+__global__ void fill_uniform_bf16(__bf16* p, size_t n, uint32_t seed) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t x = (uint32_t)i * 0x9E3779B1u ^ seed;
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    const float u = (float)(x >> 8) * (1.0f / 16777216.0f);
+    p[i] = (__bf16)(2.0f * u - 1.0f);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
+int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  if (M % BM == 0 && N % BN == 0 && K % BK == 0) {
+    const int nwg = (M / BM) * (N / BN);
+    hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
+                       (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+  } else {
+    dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
+    hipLaunchKernelGGL(gemm_bf16_generic, grid, dim3(256), 0, s,
+                       (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+  }
+  return (int)hipGetLastError();
+}
+
+// Force the generic kernel (independent implementation used by tests).
+int amdgo_gemm_bf16_generic(const void* A, const void* Bt, void* C, int M, int N, int K,
+                            void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
+  hipLaunchKernelGGL(gemm_bf16_generic, grid, dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+  return (int)hipGetLastError();
+}
+
+int amdgo_gemm_ref_rows(const void* A, const void* Bt, const int* rows, int nrows, float* out,
+                        int N, int K, void* stream) {
+  dim3 grid((N + 255) / 256, nrows);
+  hipLaunchKernelGGL(gemm_ref_rows, grid, dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)A, (const __bf16*)Bt, rows, nrows, out, N, K);
+  return (int)hipGetLastError();
+}
+
+int amdgo_fill_uniform_bf16(void* p, size_t n, uint32_t seed, void* stream) {
+  hipLaunchKernelGGL(fill_uniform_bf16, dim3(2048), dim3(256), 0, (hipStream_t)stream,
+                     (__bf16*)p, n, seed);
+  return (int)hipGetLastError();
+}
+
+// Tile constraints of the fast path (for host-side shape checks).
+int amdgo_gemm_tile_m() { return BM; }
+int amdgo_gemm_tile_n() { return BN; }
+int amdgo_gemm_tile_k() { return BK; }
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+"""Numerics of the hand-written CDNA4 MFMA GEMM against a plain PyTorch fp32 reference."""
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(a, bt):
+    return a.float() @ bt.float().t()
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 256), (1024, 1024, 1024),
+                                   (2048, 512, 4096), (768, 2304, 640)])
+def test_fast_path_matches_fp32_reference(cuda_device, m, n, k):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    assert G.fast_path_supported(m, n, k)
+    g = torch.Generator(device=cuda_device).manual_seed(m + n + k)
+    a = (torch.rand((m, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+    bt = (torch.rand((n, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+    c = G.gemm_bf16(a, bt)
+    ref = _ref(a, bt)
+    torch.testing.assert_close(c.float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (17, 33, 70), (300, 129, 65), (256, 256, 32)])
+def test_generic_path_odd_shapes(cuda_device, m, n, k):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    a = (torch.rand((m, k), device=cuda_device) * 2 - 1).to(torch.bfloat16)
+    bt = (torch.rand((n, k), device=cuda_device) * 2 - 1).to(torch.bfloat16)
+    c = G.gemm_bf16(a, bt)
+    torch.testing.assert_close(c.float(), _ref(a, bt), atol=3e-2, rtol=1e-2)
+
+
+def test_identity_with_asymmetric_b_catches_transposes(cuda_device):
+    """A = I with an asymmetric, exactly-representable B: C must equal B^T exactly."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    n = 512
+    a = torch.eye(n, device=cuda_device, dtype=torch.bfloat16)
+    idx = torch.arange(n, device=cuda_device)
+    b = ((idx[:, None] * 3 + idx[None, :] * 7) % 61 - 30).to(torch.bfloat16)  # B[k][j]
+    bt = b.t().contiguous()                                                     # Bt[j][k]
+    for generic in (False, True):
+        c = G.gemm_bf16(a, bt, generic=generic)
+        assert torch.equal(c, b), f"generic={generic}"
+
+
+def test_fast_and_generic_agree_on_8k_slice(cuda_device):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    m, n, k = 1024, 2048, 8192
+    a = torch.empty((m, k), dtype=torch.bfloat16, device=cuda_device)
+    bt = torch.empty((n, k), dtype=torch.bfloat16, device=cuda_device)
+    G.fill_uniform_(a, 1)
+    G.fill_uniform_(bt, 2)
+    c = G.gemm_bf16(a, bt)
+    chk = G.verify(a, bt, c, nrows=64)
+    assert chk.ok, chk
+    torch.testing.assert_close(c.float(), _ref(a, bt), atol=0.15, rtol=1e-2)
+
+
+def test_fill_uniform_range_and_determinism(cuda_device):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    t1 = G.fill_uniform_(torch.empty(1 << 20, dtype=torch.bfloat16, device=cuda_device), 5)
+    t2 = G.fill_uniform_(torch.empty(1 << 20, dtype=torch.bfloat16, device=cuda_device), 5)
+    assert torch.equal(t1, t2)
+    assert float(t1.float().min()) >= -1.0 and float(t1.float().max()) < 1.0
+    assert abs(float(t1.float().mean())) < 0.01
+
+
+def test_smoke_vector_add(cuda_device):
+    from gpu_operator_amd.ops import smoke
+
+    assert smoke.smoke(n=50_000, device=str(cuda_device))
+    assert smoke.smoke(n=1_000_003, device=str(cuda_device))

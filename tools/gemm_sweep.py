@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""GEMM shape sweep: hand-written MFMA kernel vs hipBLASLt (torch.matmul) on the same random data.
+
+Shapes follow SURVEY.md §7.5: M=N=K in {1024, 4096, 8192, 16384} plus skinny 16384x16384x1024.
+Interleaves the two implementations in one process (methodology rule: A/B in one process).
+Prints one JSON line per shape.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def time_fn(fn, iters, torch):
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(iters):
+        fn()
+    end.record()
+    torch.cuda.synchronize()
+    return start.elapsed_time(end) / iters / 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="1024,4096,8192,16384,16384x16384x1024")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    dev = torch.device("cuda", 0)
+    for s in a.shapes.split(","):
+        if "x" in s:
+            m, n, k = map(int, s.split("x"))
+        else:
+            m = n = k = int(s)
+        A = torch.empty((m, k), dtype=torch.bfloat16, device=dev)
+        Bt = torch.empty((n, k), dtype=torch.bfloat16, device=dev)
+        G.fill_uniform_(A, 1)
+        G.fill_uniform_(Bt, 2)
+        C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+        G.gemm_bf16(A, Bt, C)
+        chk = G.verify(A, Bt, C, nrows=16)
+        ours, blas = [], []
+        for _ in range(a.rounds):
+            for _ in range(3):
+                G.gemm_bf16(A, Bt, C)
+            ours.append(time_fn(lambda: G.gemm_bf16(A, Bt, C), a.iters, torch))
+            for _ in range(3):
+                torch.matmul(A, Bt.t())
+            blas.append(time_fn(lambda: torch.matmul(A, Bt.t(), out=C), a.iters, torch))
+        t_o, t_b = min(ours), min(blas)
+        print(json.dumps({"m": m, "n": n, "k": k, "ours_tflops": round(G.tflops(m, n, k, t_o), 1),
+                          "hipblaslt_tflops": round(G.tflops(m, n, k, t_b), 1),
+                          "ratio": round(t_b / t_o, 3), "check_ok": chk.ok,
+                          "max_rel_err": chk.max_rel_err}), flush=True)
+        del A, Bt, C
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
