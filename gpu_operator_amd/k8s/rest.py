@@ -1,0 +1,294 @@
+"""Kubernetes API client over HTTPS (``requests``), in-cluster or from a kubeconfig.
+
+Implements the :class:`~gpu_operator_amd.k8s.client.Client` protocol: discovery-based
+kind->resource mapping, CRUD, status subresource, merge patches, the pods/eviction
+subresource, events and list+watch streams with resourceVersion resume.
+"""
+
+from __future__ import annotations
+
+import base64
+import json
+import logging
+import os
+import tempfile
+import threading
+import time
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import yaml
+
+from . import errors
+from . import objects as o
+from .client import ADDED, DELETED, MODIFIED, Obj, WatchCallback, WatchEvent
+
+log = logging.getLogger(__name__)
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class Config:
+    def __init__(self, host: str, token: Optional[str] = None, ca_file: Optional[str] = None,
+                 cert_file: Optional[str] = None, key_file: Optional[str] = None,
+                 verify: bool = True, token_file: Optional[str] = None):
+        self.host = host.rstrip("/")
+        self.token = token
+        self.token_file = token_file
+        self.ca_file = ca_file
+        self.cert_file = cert_file
+        self.key_file = key_file
+        self.verify = verify
+
+    def bearer(self) -> Optional[str]:
+        if self.token_file and os.path.exists(self.token_file):
+            with open(self.token_file) as f:   # projected tokens rotate: re-read
+                return f.read().strip()
+        return self.token
+
+    @classmethod
+    def in_cluster(cls) -> "Config":
+        host = os.environ.get("KUBERNETES_SERVICE_HOST")
+        port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        if not host:
+            raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset)")
+        if ":" in host and not host.startswith("["):
+            host = f"[{host}]"
+        return cls(f"https://{host}:{port}", ca_file=f"{SA_DIR}/ca.crt", token_file=f"{SA_DIR}/token")
+
+    @classmethod
+    def from_kubeconfig(cls, path: Optional[str] = None, context: Optional[str] = None) -> "Config":
+        path = path or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
+        with open(path) as f:
+            kc = yaml.safe_load(f)
+        ctx_name = context or kc.get("current-context")
+        ctx = next(c["context"] for c in kc["contexts"] if c["name"] == ctx_name)
+        cluster = next(c["cluster"] for c in kc["clusters"] if c["name"] == ctx["cluster"])
+        user = next((u["user"] for u in kc.get("users", []) if u["name"] == ctx.get("user")), {})
+
+        def materialise(data_key: str, file_key: str, src: Dict[str, Any]) -> Optional[str]:
+            if src.get(file_key):
+                return src[file_key]
+            if src.get(data_key):
+                fd, p = tempfile.mkstemp(prefix="kc-")
+                with os.fdopen(fd, "wb") as fh:
+                    fh.write(base64.b64decode(src[data_key]))
+                return p
+            return None
+
+        return cls(cluster["server"], token=user.get("token"),
+                   ca_file=materialise("certificate-authority-data", "certificate-authority", cluster),
+                   cert_file=materialise("client-certificate-data", "client-certificate", user),
+                   key_file=materialise("client-key-data", "client-key", user),
+                   verify=not cluster.get("insecure-skip-tls-verify", False))
+
+    @classmethod
+    def auto(cls) -> "Config":
+        if os.environ.get("KUBERNETES_SERVICE_HOST") and os.path.exists(f"{SA_DIR}/token"):
+            return cls.in_cluster()
+        return cls.from_kubeconfig()
+
+
+class RestClient:
+    def __init__(self, config: Optional[Config] = None, timeout: float = 30.0):
+        import requests
+
+        self.cfg = config or Config.auto()
+        self.timeout = timeout
+        self.session = requests.Session()
+        if self.cfg.cert_file:
+            self.session.cert = (self.cfg.cert_file, self.cfg.key_file)
+        self.session.verify = self.cfg.ca_file if (self.cfg.verify and self.cfg.ca_file) else self.cfg.verify
+        self._resources: Dict[str, Dict[str, Tuple[str, bool]]] = {}
+        self._lock = threading.Lock()
+
+    # -- plumbing -------------------------------------------------------------------------
+    def _headers(self, content_type: str = "application/json") -> Dict[str, str]:
+        h = {"Accept": "application/json", "Content-Type": content_type}
+        tok = self.cfg.bearer()
+        if tok:
+            h["Authorization"] = f"Bearer {tok}"
+        return h
+
+    def _request(self, method: str, path: str, body: Any = None, params: Optional[Dict[str, Any]] = None,
+                 content_type: str = "application/json", stream: bool = False, timeout=None):
+        url = self.cfg.host + path
+        data = json.dumps(body) if body is not None else None
+        r = self.session.request(method, url, data=data, params=params, stream=stream,
+                                 headers=self._headers(content_type),
+                                 timeout=timeout if timeout is not None else self.timeout)
+        if r.status_code >= 400:
+            try:
+                st = r.json()
+                msg, reason = st.get("message", r.text), st.get("reason", "")
+            except ValueError:
+                msg, reason = r.text, ""
+            raise errors.from_status(r.status_code, msg, reason)
+        return r
+
+    def _discover(self, api_version: str) -> Dict[str, Tuple[str, bool]]:
+        with self._lock:
+            if api_version in self._resources:
+                return self._resources[api_version]
+        path = "/api/v1" if api_version == "v1" else f"/apis/{api_version}"
+        try:
+            res = self._request("GET", path).json()
+        except errors.NotFound:
+            res = {"resources": []}
+        m = {r["kind"]: (r["name"], r["namespaced"]) for r in res.get("resources", []) if "/" not in r["name"]}
+        with self._lock:
+            self._resources[api_version] = m
+        return m
+
+    def _path(self, api_version: str, kind: str, namespace: str = "", name: str = "",
+              sub: str = "") -> str:
+        res = self._discover(api_version).get(kind)
+        if res is None:
+            raise errors.NoKindMatch(f"no matches for kind {kind} in version {api_version}")
+        plural, namespaced = res
+        base = "/api/v1" if api_version == "v1" else f"/apis/{api_version}"
+        p = base
+        if namespaced and namespace:
+            p += f"/namespaces/{namespace}"
+        p += f"/{plural}"
+        if name:
+            p += f"/{name}"
+        if sub:
+            p += f"/{sub}"
+        return p
+
+    # -- Client protocol ------------------------------------------------------------------
+    def get(self, api_version: str, kind: str, name: str, namespace: str = "") -> Obj:
+        return self._request("GET", self._path(api_version, kind, namespace, name)).json()
+
+    def list(self, api_version: str, kind: str, namespace: str = "", label_selector: Any = None,
+             field_selector: Optional[str] = None) -> List[Obj]:
+        params: Dict[str, Any] = {}
+        if isinstance(label_selector, dict):
+            label_selector = ",".join(f"{k}={v}" for k, v in label_selector.items())
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        items: List[Obj] = []
+        while True:
+            body = self._request("GET", self._path(api_version, kind, namespace), params=params).json()
+            for it in body.get("items", []):
+                it.setdefault("apiVersion", api_version)
+                it.setdefault("kind", kind)
+                items.append(it)
+            cont = (body.get("metadata") or {}).get("continue")
+            if not cont:
+                return items
+            params["continue"] = cont
+
+    def create(self, obj: Obj) -> Obj:
+        return self._request("POST", self._path(obj["apiVersion"], obj["kind"], o.namespace(obj)),
+                             body=obj).json()
+
+    def update(self, obj: Obj) -> Obj:
+        return self._request("PUT", self._path(obj["apiVersion"], obj["kind"], o.namespace(obj), o.name(obj)),
+                             body=obj).json()
+
+    def update_status(self, obj: Obj) -> Obj:
+        return self._request("PUT", self._path(obj["apiVersion"], obj["kind"], o.namespace(obj), o.name(obj),
+                                               "status"), body=obj).json()
+
+    def patch(self, api_version: str, kind: str, name: str, patch: Obj, namespace: str = "",
+              patch_type: str = "merge") -> Obj:
+        ct = {"merge": "application/merge-patch+json", "strategic": "application/strategic-merge-patch+json",
+              "json": "application/json-patch+json"}[patch_type]
+        sub = "status" if set(patch.keys()) == {"status"} else ""
+        return self._request("PATCH", self._path(api_version, kind, namespace, name, sub), body=patch,
+                             content_type=ct).json()
+
+    def delete(self, api_version: str, kind: str, name: str, namespace: str = "",
+               propagation: Optional[str] = None, grace_period_seconds: Optional[int] = None) -> None:
+        body: Dict[str, Any] = {"kind": "DeleteOptions", "apiVersion": "v1"}
+        if propagation:
+            body["propagationPolicy"] = propagation
+        if grace_period_seconds is not None:
+            body["gracePeriodSeconds"] = grace_period_seconds
+        self._request("DELETE", self._path(api_version, kind, namespace, name), body=body)
+
+    def evict(self, name: str, namespace: str, grace_period_seconds: Optional[int] = None) -> None:
+        body: Dict[str, Any] = {"apiVersion": "policy/v1", "kind": "Eviction",
+                                "metadata": {"name": name, "namespace": namespace}}
+        if grace_period_seconds is not None:
+            body["deleteOptions"] = {"gracePeriodSeconds": grace_period_seconds}
+        self._request("POST", self._path("v1", "Pod", namespace, name, "eviction"), body=body)
+
+    def has_kind(self, api_version: str, kind: str) -> bool:
+        return kind in self._discover(api_version)
+
+    def server_version(self) -> str:
+        return self._request("GET", "/version").json().get("gitVersion", "")
+
+    def create_event(self, involved: Obj, reason: str, message: str, type_: str = "Normal") -> None:
+        ns = o.namespace(involved) or "default"
+        now = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+        ev = {"apiVersion": "v1", "kind": "Event",
+              "metadata": {"generateName": f"{o.name(involved)}.", "namespace": ns},
+              "involvedObject": {"apiVersion": involved.get("apiVersion"), "kind": involved.get("kind"),
+                                 "name": o.name(involved), "namespace": o.namespace(involved),
+                                 "uid": (involved.get("metadata") or {}).get("uid")},
+              "reason": reason, "message": message, "type": type_, "firstTimestamp": now,
+              "lastTimestamp": now, "count": 1, "source": {"component": "amd-gpu-operator"}}
+        try:
+            self.create(ev)
+        except errors.ApiError as e:   # events are best effort
+            log.debug("event creation failed: %s", e)
+
+    def watch(self, api_version: str, kind: str, callback: WatchCallback,
+              namespace: str = "") -> Callable[[], None]:
+        stop = threading.Event()
+
+        def run():
+            rv = ""
+            known: Dict[Tuple[str, str], Obj] = {}
+            while not stop.is_set():
+                try:
+                    if not rv:
+                        body = self._request("GET", self._path(api_version, kind, namespace)).json()
+                        rv = body["metadata"]["resourceVersion"]
+                        fresh = {}
+                        for it in body.get("items", []):
+                            it.setdefault("apiVersion", api_version)
+                            it.setdefault("kind", kind)
+                            fresh[(o.namespace(it), o.name(it))] = it
+                            callback(WatchEvent(MODIFIED if (o.namespace(it), o.name(it)) in known else ADDED, it))
+                        for k, gone in known.items():
+                            if k not in fresh:
+                                callback(WatchEvent(DELETED, gone))
+                        known = fresh
+                    r = self._request("GET", self._path(api_version, kind, namespace),
+                                      params={"watch": "1", "resourceVersion": rv,
+                                              "allowWatchBookmarks": "true", "timeoutSeconds": "300"},
+                                      stream=True, timeout=(10, 330))
+                    for line in r.iter_lines():
+                        if stop.is_set():
+                            break
+                        if not line:
+                            continue
+                        ev = json.loads(line)
+                        t, obj = ev.get("type"), ev.get("object") or {}
+                        if t == "ERROR":
+                            rv = ""     # 410 Gone: relist
+                            break
+                        rv = (obj.get("metadata") or {}).get("resourceVersion", rv)
+                        if t == "BOOKMARK":
+                            continue
+                        k = (o.namespace(obj), o.name(obj))
+                        old = known.get(k)
+                        if t == DELETED:
+                            known.pop(k, None)
+                        else:
+                            known[k] = obj
+                        callback(WatchEvent(t, obj, old))
+                except Exception as e:  # noqa: BLE001 - a watch must survive API hiccups
+                    log.warning("watch %s/%s failed: %s; retrying", api_version, kind, e)
+                    rv = ""
+                    stop.wait(2.0)
+
+        th = threading.Thread(target=run, name=f"watch-{kind}", daemon=True)
+        th.start()
+        return stop.set

@@ -1,0 +1,108 @@
+"""Minimal in-process simulation of the cluster-side controllers the operator depends on:
+the DaemonSet controller (pods per matching node, ControllerRevisions, DaemonSet status) and
+a kubelet that runs pods to Running/Ready (optionally gated by a readiness function).
+
+Together with :class:`~gpu_operator_amd.k8s.fake.FakeClient` this gives the multi-node
+"envtest" the reference never had ("There is no kind, KWOK or envtest
+cluster test"): the reconciler can be driven to ``ready`` over N synthetic GPU nodes.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional
+
+from . import errors
+from . import objects as o
+from .fake import FakeClient
+
+ReadyFn = Callable[[Dict, Dict], bool]   # (pod, node) -> ready?
+
+
+def _node_matches(pod_spec: Dict, node: Dict) -> bool:
+    sel = pod_spec.get("nodeSelector") or {}
+    labels = o.get_labels(node)
+    if any(labels.get(k) != v for k, v in sel.items()):
+        return False
+    if (node.get("spec") or {}).get("unschedulable"):
+        tol = pod_spec.get("tolerations") or []
+        if not any(t.get("key") == "node.kubernetes.io/unschedulable" for t in tol):
+            return False
+    return True
+
+
+class ClusterSim:
+    def __init__(self, client: FakeClient, ready_fn: Optional[ReadyFn] = None):
+        self.client = client
+        self.ready_fn = ready_fn or (lambda pod, node: True)
+
+    def _revision(self, ds: Dict) -> str:
+        return o.stable_hash(ds["spec"].get("template"))[:10]
+
+    def sync(self) -> None:
+        """One pass of DaemonSet controller + kubelet over every DaemonSet."""
+        nodes = {o.name(n): n for n in self.client.list("v1", "Node")}
+        for ds in self.client.list("apps/v1", "DaemonSet"):
+            self._sync_ds(ds, nodes)
+
+    def _sync_ds(self, ds: Dict, nodes: Dict[str, Dict]) -> None:
+        ns, name = o.namespace(ds), o.name(ds)
+        tmpl = ds["spec"]["template"]
+        rev = self._revision(ds)
+        rev_name = f"{name}-{rev}"
+        revs = self.client.list("apps/v1", "ControllerRevision", ns)
+        mine = [r for r in revs if o.owned_by(r, ds["metadata"]["uid"])]
+        if not any(o.name(r) == rev_name for r in mine):
+            nxt = max([r.get("revision", 0) for r in mine] or [0]) + 1
+            cr = {"apiVersion": "apps/v1", "kind": "ControllerRevision",
+                  "metadata": {"name": rev_name, "namespace": ns,
+                               "labels": dict((ds["spec"].get("selector") or {}).get("matchLabels") or {})},
+                  "revision": nxt, "data": {}}
+            o.set_controller_reference(ds, cr)
+            self.client.create(cr)
+        on_delete = (ds["spec"].get("updateStrategy") or {}).get("type") == "OnDelete"
+        want = {n for n, node in nodes.items() if _node_matches(tmpl.get("spec") or {}, node)}
+        pods = [p for p in self.client.list("v1", "Pod", ns) if o.owned_by(p, ds["metadata"]["uid"])]
+        by_node = {(p.get("spec") or {}).get("nodeName"): p for p in pods}
+        for node_name, pod in list(by_node.items()):
+            stale = o.get_labels(pod).get("controller-revision-hash") != rev
+            if node_name not in want or (stale and not on_delete):
+                try:
+                    self.client.delete("v1", "Pod", o.name(pod), ns)
+                except errors.NotFound:
+                    pass
+                by_node.pop(node_name)
+        for node_name in sorted(want):
+            if node_name in by_node:
+                continue
+            labels = dict((tmpl.get("metadata") or {}).get("labels") or {})
+            labels["controller-revision-hash"] = rev
+            pod = {"apiVersion": "v1", "kind": "Pod",
+                   "metadata": {"name": f"{name}-{node_name}", "namespace": ns, "labels": labels},
+                   "spec": dict(tmpl.get("spec") or {}, nodeName=node_name),
+                   "status": {"phase": "Pending"}}
+            o.set_controller_reference(ds, pod)
+            by_node[node_name] = self.client.create(pod)
+        available = 0
+        for node_name, pod in by_node.items():
+            ready = self.ready_fn(pod, nodes[node_name])
+            cstat = [{"name": c["name"], "ready": ready} for c in (pod["spec"].get("containers") or [])]
+            st = {"phase": "Running" if ready else "Pending", "containerStatuses": cstat}
+            if pod.get("status") != st:
+                pod = self.client.get("v1", "Pod", o.name(pod), ns)
+                pod["status"] = st
+                self.client.update_status(pod)
+            available += 1 if ready else 0
+        desired = len(want)
+        status = {"observedGeneration": ds["metadata"].get("generation", 1),
+                  "desiredNumberScheduled": desired, "currentNumberScheduled": len(by_node),
+                  "numberReady": available, "numberAvailable": available,
+                  "numberUnavailable": desired - available,
+                  "updatedNumberScheduled": sum(1 for p in by_node.values()
+                                                if o.get_labels(p).get("controller-revision-hash") == rev)}
+        if ds.get("status") != status:
+            cur = self.client.get("apps/v1", "DaemonSet", name, ns)
+            cur["status"] = status
+            self.client.update_status(cur)
+
+    def pods_on(self, node_name: str) -> List[Dict]:
+        return [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node_name}")]
