@@ -262,7 +262,9 @@ def control_daemonset(n, state, obj: Obj) -> str:
         return READY
     variants = n.daemonset_variants(base)
     if variants is None:
-        return _apply_one_daemonset(n, obj)
+        pending = n.cleanup_stale_variants(base, None) if base in n.FANOUT_BASES else False
+        st = _apply_one_daemonset(n, obj)
+        return NOT_READY if pending else st
     # fan-out: one DaemonSet per kernel (precompiled), RHCOS version (DTK) or node OS
     pending = n.cleanup_stale_variants(base, variants)
     overall = NOT_READY if pending else READY

@@ -469,9 +469,11 @@ class StateManager:
         return [d for d in self.client.list("apps/v1", "DaemonSet", self.namespace, label_selector={"app": base})
                 if o.name(d) != base]
 
-    def cleanup_stale_variants(self, base: str, variants: List[Dict[str, str]]) -> bool:
+    FANOUT_BASES = (C.DS_DRIVER, C.DS_MXGPU_MANAGER)
+
+    def cleanup_stale_variants(self, base: str, variants: Optional[List[Dict[str, str]]]) -> bool:
         """Delete DaemonSets of other flavours/kernels/OSes; True while their pods remain."""
-        want = {self.variant_name(base, v) for v in variants}
+        want = {base} if variants is None else {self.variant_name(base, v) for v in variants}
         pending = False
         existing = self.client.list("apps/v1", "DaemonSet", self.namespace, label_selector={"app": base})
         for ds in existing:

@@ -21,13 +21,9 @@ ReadyFn = Callable[[Dict, Dict], bool]   # (pod, node) -> ready?
 def _node_matches(pod_spec: Dict, node: Dict) -> bool:
     sel = pod_spec.get("nodeSelector") or {}
     labels = o.get_labels(node)
-    if any(labels.get(k) != v for k, v in sel.items()):
-        return False
-    if (node.get("spec") or {}).get("unschedulable"):
-        tol = pod_spec.get("tolerations") or []
-        if not any(t.get("key") == "node.kubernetes.io/unschedulable" for t in tol):
-            return False
-    return True
+    # DaemonSet pods tolerate node.kubernetes.io/unschedulable (added by the DS controller),
+    # so a cordoned node keeps its operand pods.
+    return not any(labels.get(k) != v for k, v in sel.items())
 
 
 class ClusterSim:

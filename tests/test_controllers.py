@@ -1,0 +1,511 @@
+"""ClusterPolicy reconciler, state manager and operand transforms against the fake API server.
+
+Mirrors the reference's controller tests (reference: controllers/object_controls_test.go:
+TestDriver :509-572, TestDevicePlugin :631-703, TestVGPUManager :752-800,
+TestSandboxDevicePlugin :863-904; controllers/state_manager_test.go) and adds what it lacks
+(SURVEY.md §4 gaps): toolkit, telemetry, labeller, partition manager and validator
+transforms, readiness logic, the reconcile loop, multi-node and fault injection.
+"""
+
+import pytest
+
+from gpu_operator_amd.controllers import consts as C
+from gpu_operator_amd.controllers import state_manager as S
+from gpu_operator_amd.k8s import errors
+from gpu_operator_amd.k8s import objects as o
+from gpu_operator_amd.k8s.sim import ClusterSim
+from k8s_helpers import NS, cluster, container, daemonset, env, gpu_node, reconciler, run_until_ready, sample_cp
+
+
+def reconcile_once(client):
+    rec = reconciler(client)
+    rec.reconcile(("", "cluster-policy"))
+    return rec
+
+
+# ------------------------------------------------------------------------------ driver
+def test_driver_default():
+    c = cluster()
+    reconcile_once(c)
+    ds = daemonset(c, C.DS_DRIVER)
+    drv = container(ds, "amdgpu-driver-ctr")
+    assert drv["image"] == "registry.example.com/amd/amdgpu-driver:6.12.12-ubuntu22.04"
+    assert container(ds, "amd-driver-manager", init=True)["image"] == \
+        "registry.example.com/amd/amd-gpu-operator-node:v0.1.0"
+    assert container(ds, "rdma-validation", init=True) is None          # RDMA off
+    assert ds["spec"]["updateStrategy"]["type"] == "OnDelete"           # never rolled automatically
+    assert drv["startupProbe"]["initialDelaySeconds"] == 0 and drv["startupProbe"]["periodSeconds"] == 2
+    assert ds["metadata"]["ownerReferences"][0]["kind"] == "ClusterPolicy"
+    # explicit manager env from the CR wins
+    assert env(container(ds, "amd-driver-manager", init=True))["ENABLE_GPU_POD_EVICTION"] == "true"
+
+
+def test_driver_manager_defers_eviction_to_upgrade_controller():
+    c = cluster(cp=sample_cp(**{"driver.manager.env": []}))
+    reconcile_once(c)
+    e = env(container(daemonset(c, C.DS_DRIVER), "amd-driver-manager", init=True))
+    assert e["ENABLE_GPU_POD_EVICTION"] == "false" and e["ENABLE_AUTO_DRAIN"] == "false"
+
+
+def test_driver_precompiled_fans_out_per_kernel():
+    nodes = [gpu_node("a"), gpu_node("b"), gpu_node("c", kernel="6.8.0-50-generic")]
+    c = cluster(nodes, sample_cp(**{"driver.usePrecompiled": True}))
+    reconcile_once(c)
+    dss = [d for d in c.objects("DaemonSet") if o.name(d).startswith(C.DS_DRIVER)]
+    names = sorted(o.name(d) for d in dss)
+    assert names == ["amdgpu-driver-daemonset-6.8.0-45-generic-ubuntu22.04",
+                     "amdgpu-driver-daemonset-6.8.0-50-generic-ubuntu22.04"]
+    for d in dss:
+        kernel = d["spec"]["template"]["spec"]["nodeSelector"][C.NFD_KERNEL_LABEL]
+        assert container(d, "amdgpu-driver-ctr")["image"] == \
+            f"registry.example.com/amd/amdgpu-driver:6.12.12-{kernel}-ubuntu22.04"
+        assert o.get_labels(d)[C.PRECOMPILED_LABEL] == "true"
+
+
+def test_precompiled_kernel_upgrade_removes_stale_daemonset():
+    c = cluster([gpu_node("a")], sample_cp(**{"driver.usePrecompiled": True}))
+    rec = reconcile_once(c)
+    n = c.get("v1", "Node", "a")
+    n["metadata"]["labels"][C.NFD_KERNEL_LABEL] = "6.9.0-1-generic"
+    c.update(n)
+    rec.reconcile(("", "cluster-policy"))
+    names = sorted(o.name(d) for d in c.objects("DaemonSet") if o.name(d).startswith(C.DS_DRIVER))
+    assert names == ["amdgpu-driver-daemonset-6.9.0-1-generic-ubuntu22.04"]
+
+
+def test_switching_precompiled_off_removes_per_kernel_daemonsets():
+    c = cluster([gpu_node("a")], sample_cp(**{"driver.usePrecompiled": True}))
+    rec = reconcile_once(c)
+    cp = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    cp["spec"]["driver"]["usePrecompiled"] = False
+    c.update(cp)
+    rec.reconcile(("", "cluster-policy"))
+    names = sorted(o.name(d) for d in c.objects("DaemonSet") if o.name(d).startswith(C.DS_DRIVER))
+    assert names == [C.DS_DRIVER]
+
+
+def test_mixed_os_cluster_gets_one_driver_daemonset_per_os():
+    """The reference assumes every GPU node runs the first node's OS."""
+    c = cluster([gpu_node("a"), gpu_node("b", os_id="rhel", os_ver="9.4")])
+    reconcile_once(c)
+    dss = {o.name(d): d for d in c.objects("DaemonSet") if o.name(d).startswith(C.DS_DRIVER)}
+    assert set(dss) == {"amdgpu-driver-daemonset-rhel9.4", "amdgpu-driver-daemonset-ubuntu22.04"}
+    rh = dss["amdgpu-driver-daemonset-rhel9.4"]
+    assert container(rh, "amdgpu-driver-ctr")["image"].endswith("-rhel9.4")
+    assert rh["spec"]["template"]["spec"]["nodeSelector"][C.NFD_OS_ID_LABEL] == "rhel"
+
+
+def test_driver_rdma_repo_cert_and_module_config_follow_node_os():
+    cp = sample_cp(**{"driver.rdma": {"enabled": True, "useHostMofed": True},
+                      "driver.repoConfig": {"configMapName": "repo"},
+                      "driver.certConfig": {"name": "certs"},
+                      "driver.kernelModuleConfig": {"name": "amdgpu-params"}})
+    c = cluster([gpu_node("a", os_id="rhel", os_ver="9.4")], cp)
+    reconcile_once(c)
+    ds = daemonset(c, C.DS_DRIVER)
+    drv = container(ds, "amdgpu-driver-ctr")
+    assert container(ds, "rdma-validation", init=True) is not None
+    e = env(drv)
+    assert e["RDMA_ENABLED"] == "true" and e["USE_HOST_MOFED"] == "true"
+    assert e["KERNEL_MODULE_PARAMS"] == "/drivers/amdgpu.conf"
+    mounts = {m["name"]: m["mountPath"] for m in drv["volumeMounts"]}
+    assert mounts["repo-config"] == "/etc/yum.repos.d"
+    assert mounts["cert-config"] == "/etc/pki/ca-trust/extracted/pem"
+
+
+def test_driver_without_nfd_os_labels_is_an_error_not_a_guess():
+    n = gpu_node("a")
+    del n["metadata"]["labels"][C.NFD_OS_ID_LABEL]
+    c = cluster([n])
+    rec = reconciler(c)
+    with pytest.raises(Exception, match="OS unknown"):
+        rec.reconcile(("", "cluster-policy"))
+    assert c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")["status"]["state"] == "notReady"
+
+
+# ------------------------------------------------------------------------------ device plugin
+def test_device_plugin_default():
+    c = cluster()
+    reconcile_once(c)
+    ds = daemonset(c, C.DS_DEVICE_PLUGIN)
+    main = container(ds, "amd-device-plugin")
+    assert main["image"] == "registry.example.com/amd/amd-gpu-operator-node:v0.1.0"
+    assert container(ds, "config-manager-init", init=True) is None
+    assert container(ds, "config-manager") is None
+    assert env(main)["PARTITION_STRATEGY"] == "single"
+    assert ds["spec"]["template"]["spec"]["runtimeClassName"] == "amd"
+
+
+def test_device_plugin_custom_config_adds_config_manager():
+    c = cluster(cp=sample_cp(**{"devicePlugin.config": {"name": "plugin-config", "default": "default"}}))
+    reconcile_once(c)
+    ds = daemonset(c, C.DS_DEVICE_PLUGIN)
+    assert container(ds, "config-manager-init", init=True) is not None
+    side = container(ds, "config-manager")
+    assert env(side)["NODE_LABEL"] == C.DEVICE_PLUGIN_CONFIG_LABEL and env(side)["DEFAULT_CONFIG"] == "default"
+    assert env(container(ds, "amd-device-plugin"))["CONFIG_FILE"] == "/config/config.yaml"
+    assert ds["spec"]["template"]["spec"]["shareProcessNamespace"] is True
+
+
+def test_cdi_enabled_sets_runtime_class_and_env():
+    c = cluster(cp=sample_cp(**{"cdi": {"enabled": True, "default": True}}))
+    reconcile_once(c)
+    assert c.get("node.k8s.io/v1", "RuntimeClass", "amd-cdi")
+    e = env(container(daemonset(c, C.DS_DEVICE_PLUGIN), "amd-device-plugin"))
+    assert e["CDI_ENABLED"] == "true" and e["DEVICE_LIST_STRATEGY"] == "cdi-annotations"
+    assert env(container(daemonset(c, C.DS_TOOLKIT), "amd-container-toolkit-ctr"))["AMD_RUNTIME_MODE"] == "cdi"
+
+
+# ------------------------------------------------------------------------------ toolkit
+@pytest.mark.parametrize("rt,runtime,cfg", [
+    ("containerd://1.7.2", "containerd", "/runtime/config-dir/config.toml"),
+    ("docker://24.0.1", "docker", "/runtime/config-dir/daemon.json"),
+    ("cri-o://1.28.1", "crio", "/runtime/config-dir/99-amd.conf"),
+])
+def test_toolkit_runtime_wiring(rt, runtime, cfg):
+    c = cluster([gpu_node("a", runtime=rt)])
+    reconcile_once(c)
+    ds = daemonset(c, C.DS_TOOLKIT)
+    e = env(container(ds, "amd-container-toolkit-ctr"))
+    assert e["RUNTIME"] == runtime and e["RUNTIME_CONFIG"] == cfg
+    assert e["ROOT"] == "/usr/local/amd" and e["RUNTIME_CLASS"] == "amd"
+    assert container(ds, "driver-validation", init=True)["image"].endswith("amd-gpu-operator-node:v0.1.0")
+
+
+@pytest.mark.parametrize("rtv,want", [("docker://24", "docker"), ("containerd://1.7", "containerd"),
+                                      ("cri-o://1.28", "crio"), ("podman://4", None)])
+def test_runtime_string(rtv, want):
+    """Reference: controllers/state_manager_test.go (getRuntimeString)."""
+    assert S.runtime_of({"status": {"nodeInfo": {"containerRuntimeVersion": rtv}}}) == want
+
+
+def test_runtime_detection_prefers_containerd_then_falls_back_to_default():
+    c = cluster([gpu_node("a", runtime="docker://24"), gpu_node("b", runtime="containerd://1.7")])
+    rec = reconcile_once(c)
+    assert rec.sm.runtime == "containerd"
+    c2 = cluster([gpu_node("a", runtime="weird://1")], sample_cp(**{"operator.defaultRuntime": "crio"}))
+    assert reconcile_once(c2).sm.runtime == "crio"
+
+
+# ------------------------------------------------------------------------------ telemetry etc.
+def test_metrics_exporter_attaches_to_rdc_when_enabled():
+    c = cluster(cp=sample_cp(**{"rdc.enabled": True, "rdc.hostPort": 50555,
+                                "metricsExporter.config": {"name": "my-fields"}}))
+    reconcile_once(c)
+    ex = daemonset(c, C.DS_METRICS_EXPORTER)
+    assert ex["spec"]["template"]["spec"]["hostNetwork"] is True
+    assert env(container(ex, "amd-metrics-exporter"))["RDC_HOST"] == "localhost:50555"
+    vols = {v["name"]: v for v in ex["spec"]["template"]["spec"]["volumes"]}
+    assert vols["fields"]["configMap"]["name"] == "my-fields"
+    rdc = daemonset(c, C.DS_RDC)
+    port = container(rdc, "amd-rdc-ctr")["ports"][0]
+    assert port["hostPort"] == 50555
+
+
+def test_service_monitor_requires_crd_when_enabled():
+    c = cluster(cp=sample_cp(**{"metricsExporter.serviceMonitor": {"enabled": True}}))
+    rec = reconciler(c)
+    with pytest.raises(errors.NoKindMatch):
+        rec.reconcile(("", "cluster-policy"))
+    c2 = cluster(cp=sample_cp(**{"metricsExporter.serviceMonitor": {
+        "enabled": True, "interval": "10s", "honorLabels": True, "additionalLabels": {"team": "ml"}}}),
+        unserved=())
+    reconcile_once(c2)
+    sm = c2.get("monitoring.coreos.com/v1", "ServiceMonitor", "amd-metrics-exporter", NS)
+    assert sm["spec"]["endpoints"][0]["interval"] == "10s" and sm["metadata"]["labels"]["team"] == "ml"
+    assert c2.get("monitoring.coreos.com/v1", "PrometheusRule", "amd-gpu-operator-alerts", NS)
+
+
+def test_validator_transform_components_and_spawn_env():
+    cp = sample_cp(**{"validator.hip": {"env": [{"name": "GEMM_SHAPES", "value": "4096"}]},
+                      "validator.rccl": {"env": [{"name": "RCCL_MAX_BYTES", "value": "1024"}]}})
+    c = cluster(cp=cp)
+    reconcile_once(c)
+    ds = daemonset(c, C.DS_VALIDATOR)
+    names = [x["name"] for x in ds["spec"]["template"]["spec"]["initContainers"]]
+    assert names == ["driver-validation", "toolkit-validation", "hip-validation", "plugin-validation",
+                     "rccl-validation"]
+    hip = env(container(ds, "hip-validation", init=True))
+    assert hip["GEMM_SHAPES"] == "4096" and hip["VALIDATOR_IMAGE"].endswith("amd-gpu-operator-node:v0.1.0")
+    assert hip["VALIDATOR_RUNTIME_CLASS"] == "amd"
+    assert env(container(ds, "rccl-validation", init=True))["RCCL_MAX_BYTES"] == "1024"
+    assert env(container(ds, "plugin-validation", init=True))["WITH_WORKLOAD"] == "false"
+
+
+def test_validator_drops_gpu_requesting_probes_without_device_plugin():
+    c = cluster(cp=sample_cp(**{"devicePlugin.enabled": False}))
+    reconcile_once(c)
+    names = [x["name"] for x in daemonset(c, C.DS_VALIDATOR)["spec"]["template"]["spec"]["initContainers"]]
+    assert "plugin-validation" not in names and "rccl-validation" not in names
+    with pytest.raises(errors.NotFound):
+        daemonset(c, C.DS_DEVICE_PLUGIN)
+
+
+def test_partition_manager_config_and_node_default_label():
+    n = gpu_node("a", extra_labels={C.PARTITION_CAPABLE_LABEL: "true"})
+    c = cluster([n, gpu_node("b")])
+    reconcile_once(c)
+    a, b = c.get("v1", "Node", "a"), c.get("v1", "Node", "b")
+    assert o.get_labels(a)[C.PARTITION_MANAGER_DEPLOY_LABEL] == "true"
+    assert o.get_labels(a)[C.PARTITION_CONFIG_LABEL] == "spx-nps1"
+    assert C.PARTITION_MANAGER_DEPLOY_LABEL not in o.get_labels(b)
+    ds = daemonset(c, C.DS_PARTITION_MANAGER)
+    e = env(container(ds, "amd-partition-manager"))
+    assert e["DEFAULT_PARTITION_CONFIG"] == "spx-nps1"
+
+
+def test_daemonsets_common_config_labels_annotations_tolerations():
+    cp = sample_cp(**{"daemonsets.labels": {"team": "ml", "app": "hijack"},
+                      "daemonsets.annotations": {"a": "b"},
+                      "daemonsets.rollingUpdate": {"maxUnavailable": "20%"}})
+    c = cluster(cp=cp)
+    reconcile_once(c)
+    ds = daemonset(c, C.DS_DEVICE_PLUGIN)
+    tl = ds["spec"]["template"]["metadata"]["labels"]
+    assert tl["team"] == "ml" and tl["app"] == C.DS_DEVICE_PLUGIN
+    assert ds["spec"]["template"]["metadata"]["annotations"]["a"] == "b"
+    assert ds["spec"]["updateStrategy"] == {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": "20%"}}
+    assert daemonset(c, C.DS_DRIVER)["spec"]["updateStrategy"]["type"] == "OnDelete"
+
+
+# ------------------------------------------------------------------------------ sandbox
+def sandbox_cp(**kw):
+    base = {"sandboxWorkloads": {"enabled": True, "defaultWorkload": "vm-passthrough"},
+            "mxgpuManager.enabled": True, "kataManager.enabled": True}
+    base.update(kw)
+    return sample_cp(**base)
+
+
+def test_sandbox_workload_labels_per_node():
+    nodes = [gpu_node("pt"), gpu_node("mx", extra_labels={C.WORKLOAD_CONFIG_LABEL: "vm-mxgpu"}),
+             gpu_node("ctr", extra_labels={C.WORKLOAD_CONFIG_LABEL: "container"})]
+    c = cluster(nodes, sandbox_cp())
+    reconcile_once(c)
+    lab = {n: o.get_labels(c.get("v1", "Node", n)) for n in ("pt", "mx", "ctr")}
+    assert lab["pt"].get("amd.com/gpu.deploy.vfio-manager") == "true"
+    assert "amd.com/gpu.deploy.driver" not in lab["pt"]
+    assert lab["mx"].get("amd.com/gpu.deploy.mxgpu-manager") == "true"
+    assert "amd.com/gpu.deploy.vfio-manager" not in lab["mx"]
+    assert lab["ctr"].get("amd.com/gpu.deploy.driver") == "true"
+
+
+def test_sandbox_states_create_operands():
+    c = cluster([gpu_node("a")], sandbox_cp())
+    reconcile_once(c)
+    for name in (C.DS_MXGPU_MANAGER, C.DS_MXGPU_DEVICE_MANAGER, C.DS_SANDBOX_VALIDATOR, C.DS_VFIO_MANAGER,
+                 C.DS_SANDBOX_DEVICE_PLUGIN, C.DS_KATA_MANAGER):
+        assert daemonset(c, name)
+    mx = daemonset(c, C.DS_MXGPU_MANAGER)
+    assert container(mx, "amd-mxgpu-manager-ctr")["image"] == \
+        "registry.example.com/amd/amd-mxgpu-driver:8.1.0-ubuntu22.04"
+    sv = daemonset(c, C.DS_SANDBOX_VALIDATOR)
+    assert env(container(sv, "vfio-pci-validation", init=True))["DEFAULT_GPU_WORKLOAD_CONFIG"] == "vm-passthrough"
+    # kata: config rendered, runtime class generated, pods roll on config change
+    cm = c.get("v1", "ConfigMap", "amd-kata-manager-config", NS)
+    assert "kata-amd-gpu" in cm["data"]["config.yaml"]
+    rc = c.get("node.k8s.io/v1", "RuntimeClass", "kata-amd-gpu")
+    assert rc["handler"] == "kata-amd-gpu"
+    h1 = daemonset(c, C.DS_KATA_MANAGER)["spec"]["template"]["metadata"]["annotations"][C.KATA_CONFIG_HASH_ANNOTATION]
+    cp = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    cp["spec"]["kataManager"]["config"]["runtimeClasses"] = [
+        {"name": "kata-amd-gpu-snp", "artifacts": {"url": "registry.example.com/amd/kata:snp"}}]
+    c.update(cp)
+    reconcile_once(c)
+    h2 = daemonset(c, C.DS_KATA_MANAGER)["spec"]["template"]["metadata"]["annotations"][C.KATA_CONFIG_HASH_ANNOTATION]
+    assert h1 != h2
+    with pytest.raises(errors.NotFound):
+        c.get("node.k8s.io/v1", "RuntimeClass", "kata-amd-gpu")          # stale class removed
+    assert c.get("node.k8s.io/v1", "RuntimeClass", "kata-amd-gpu-snp")
+
+
+def test_sandbox_disabled_removes_sandbox_operands():
+    c = cluster([gpu_node("a")], sandbox_cp())
+    rec = reconcile_once(c)
+    cp = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    cp["spec"]["sandboxWorkloads"]["enabled"] = False
+    c.update(cp)
+    rec.reconcile(("", "cluster-policy"))
+    for name in (C.DS_VFIO_MANAGER, C.DS_SANDBOX_DEVICE_PLUGIN, C.DS_KATA_MANAGER):
+        with pytest.raises(errors.NotFound):
+            daemonset(c, name)
+    assert o.get_labels(c.get("v1", "Node", "a")).get("amd.com/gpu.deploy.driver") == "true"
+
+
+# ------------------------------------------------------------------------------ node labelling
+def test_operands_disabled_label_removes_deploy_labels():
+    c = cluster([gpu_node("a", extra_labels={C.OPERANDS_LABEL: "false"})])
+    reconcile_once(c)
+    lab = o.get_labels(c.get("v1", "Node", "a"))
+    assert lab[C.COMMON_GPU_LABEL] == "true"
+    assert not any(k.startswith("amd.com/gpu.deploy.") and k != C.OPERANDS_LABEL for k in lab)
+
+
+def test_node_losing_gpu_is_reset():
+    c = cluster([gpu_node("a")])
+    rec = reconcile_once(c)
+    n = c.get("v1", "Node", "a")
+    del n["metadata"]["labels"]["feature.node.kubernetes.io/pci-1002.present"]
+    c.update(n)
+    rec.reconcile(("", "cluster-policy"))
+    lab = o.get_labels(c.get("v1", "Node", "a"))
+    assert lab[C.COMMON_GPU_LABEL] == "false" and "amd.com/gpu.deploy.driver" not in lab
+
+
+def test_user_set_deploy_label_value_is_honoured():
+    c = cluster([gpu_node("a", extra_labels={"amd.com/gpu.deploy.metrics-exporter": "false"})])
+    reconcile_once(c)
+    assert o.get_labels(c.get("v1", "Node", "a"))["amd.com/gpu.deploy.metrics-exporter"] == "false"
+
+
+def test_driver_auto_upgrade_annotation_follows_policy():
+    c = cluster([gpu_node("a")])
+    rec = reconcile_once(c)
+    assert o.get_annotations(c.get("v1", "Node", "a"))[C.DRIVER_AUTO_UPGRADE_ANNOTATION] == "true"
+    cp = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    cp["spec"]["driver"]["upgradePolicy"]["autoUpgrade"] = False
+    c.update(cp)
+    rec.reconcile(("", "cluster-policy"))
+    assert C.DRIVER_AUTO_UPGRADE_ANNOTATION not in o.get_annotations(c.get("v1", "Node", "a"))
+
+
+def test_psa_labels_namespace():
+    c = cluster(cp=sample_cp(**{"psa.enabled": True}))
+    reconcile_once(c)
+    lab = o.get_labels(c.get("v1", "Namespace", NS))
+    assert all(lab[f"pod-security.kubernetes.io/{m}"] == "privileged" for m in ("enforce", "audit", "warn"))
+
+
+# ------------------------------------------------------------------------------ reconcile loop
+def test_reconcile_reaches_ready_with_simulated_cluster():
+    c = cluster([gpu_node(f"n{i}") for i in range(4)])
+    rec = reconciler(c)
+    res, state = run_until_ready(c, rec)
+    assert state == "ready" and res.requeue_after == 0
+    cpst = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")["status"]
+    assert cpst["conditions"][0]["status"] == "True" and cpst["namespace"] == NS
+    assert rec.metrics.gpu_nodes_total._value.get() == 4
+    assert rec.metrics.reconciliation_status._value.get() == 1
+
+
+def test_not_ready_requeues_after_5s_and_lists_states():
+    c = cluster()
+    rec = reconciler(c)
+    res = rec.reconcile(("", "cluster-policy"))
+    assert res.requeue_after == 5.0
+    st = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")["status"]
+    assert "state-driver" in st["notReadyStates"]
+
+
+def test_no_nfd_labels_requeues_after_45s():
+    c = cluster([{"apiVersion": "v1", "kind": "Node", "metadata": {"name": "cpu-only", "labels": {}}}])
+    rec = reconciler(c)
+    res = rec.reconcile(("", "cluster-policy"))
+    assert res.requeue_after == 45.0
+    assert rec.metrics.reconciliation_has_nfd_labels._value.get() == 0
+
+
+def test_steady_state_does_not_rewrite_objects():
+    c = cluster()
+    rec = reconciler(c)
+    run_until_ready(c, rec)
+    before = len(c.calls)
+    rec.reconcile(("", "cluster-policy"))
+    verbs = [v for v, _, _ in c.calls[before:]]
+    assert "update" not in verbs and "create" not in verbs
+
+
+def test_spec_change_updates_only_affected_daemonset():
+    c = cluster()
+    rec = reconciler(c)
+    run_until_ready(c, rec)
+    cp = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    cp["spec"]["devicePlugin"]["env"].append({"name": "LOG_LEVEL", "value": "debug"})
+    c.update(cp)
+    before = len(c.calls)
+    rec.reconcile(("", "cluster-policy"))
+    updated = [(k, n) for v, k, n in c.calls[before:] if v == "update"]
+    assert updated == [("DaemonSet", C.DS_DEVICE_PLUGIN)]
+
+
+def test_second_clusterpolicy_is_ignored_and_status_persisted():
+    c = cluster()
+    second = sample_cp()
+    second["metadata"]["name"] = "zz-second"
+    c.create(second)
+    rec = reconciler(c)
+    rec.reconcile(("", "cluster-policy"))
+    rec.reconcile(("", "zz-second"))
+    assert c.get("amd.com/v1", "ClusterPolicy", "zz-second")["status"]["state"] == "ignored"
+
+
+def test_deleting_clusterpolicy_garbage_collects_operands():
+    c = cluster()
+    rec = reconciler(c)
+    run_until_ready(c, rec)
+    c.delete("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    assert c.objects("DaemonSet") == [] and c.objects("Pod") == []
+    rec.reconcile(("", "cluster-policy"))
+    assert rec.metrics.reconciliation_status._value.get() == -1
+
+
+def test_transient_api_errors_fail_the_pass_then_recover():
+    c = cluster()
+    rec = reconciler(c)
+    c.fail_on("create", "DaemonSet", errors.ApiError("etcd timeout", status=500), times=1)
+    with pytest.raises(errors.ApiError):
+        rec.reconcile(("", "cluster-policy"))
+    assert rec.metrics.reconciliation_failed._value.get() >= 1
+    _, state = run_until_ready(c, rec)
+    assert state == "ready"
+
+
+def test_ondelete_driver_readiness_requires_latest_revision():
+    c = cluster([gpu_node("a")])
+    rec = reconciler(c)
+    sim = ClusterSim(c)
+    run_until_ready(c, rec, sim)
+    # change the driver spec: OnDelete => the old pod stays on the old revision => not ready
+    cp = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    cp["spec"]["driver"]["version"] = "6.13.0"
+    c.update(cp)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    rec.reconcile(("", "cluster-policy"))
+    assert rec.last_states["state-driver"] == "notReady"
+    # deleting the pod (what the upgrade controller does) lets it come back on the new revision
+    for p in c.objects("Pod"):
+        if p["metadata"]["name"].startswith(C.DS_DRIVER):
+            c.delete("v1", "Pod", p["metadata"]["name"], NS)
+    sim.sync()
+    rec.reconcile(("", "cluster-policy"))
+    assert rec.last_states["state-driver"] == "ready"
+
+
+def test_node_watch_predicate():
+    from gpu_operator_amd.controllers.clusterpolicy_controller import ClusterPolicyReconciler as R
+    from gpu_operator_amd.k8s.client import WatchEvent
+    n = gpu_node("a")
+    assert R.node_predicate(WatchEvent("ADDED", n))
+    labelled = {**n, "metadata": {**n["metadata"], "labels": {**n["metadata"]["labels"], C.COMMON_GPU_LABEL: "true",
+                                                                **C.GPU_STATE_LABELS["container"]}}}
+    assert not R.node_predicate(WatchEvent("MODIFIED", labelled, labelled))
+    off = {**labelled, "metadata": {**labelled["metadata"],
+                                    "labels": {**labelled["metadata"]["labels"], C.OPERANDS_LABEL: "false"}}}
+    assert R.node_predicate(WatchEvent("MODIFIED", off, labelled))
+    cpu = {"metadata": {"name": "c", "labels": {}}}
+    assert not R.node_predicate(WatchEvent("ADDED", cpu))
+
+
+def test_watch_driven_controller_converges_without_timers():
+    """Events (CR, Node, owned DaemonSet status) drive passes: the reconciler reaches ready
+    through the controller queue with no 5 s timer elapsing."""
+    c = cluster()
+    rec = reconciler(c)
+    ctl = rec.controller()
+    ctl.start_watches(c)
+    sim = ClusterSim(c)
+    for _ in range(6):
+        ctl.drain()
+        sim.sync()
+    ctl.drain()
+    assert c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")["status"]["state"] == "ready"
