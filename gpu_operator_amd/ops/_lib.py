@@ -47,6 +47,9 @@ def load() -> ctypes.CDLL:
         lib.amdgo_fill_uniform_bf16.restype = i
         lib.amdgo_vector_add_f32.argtypes = [vp, vp, vp, sz, vp]
         lib.amdgo_vector_add_f32.restype = i
+        lib.amdgo_gemm_set_variant.argtypes = [i]
+        lib.amdgo_gemm_set_variant.restype = None
+        lib.amdgo_gemm_get_variant.restype = i
         for f in ("amdgo_gemm_tile_m", "amdgo_gemm_tile_n", "amdgo_gemm_tile_k"):
             getattr(lib, f).restype = i
         _LIB = lib

@@ -50,6 +50,15 @@ def gemm_bf16(a, bt, out=None, *, generic: bool = False):
     return out
 
 
+def set_variant(v: int) -> None:
+    """Select the fast-path kernel generation (1: baseline, 2: fragment-pipelined)."""
+    _lib.load().amdgo_gemm_set_variant(int(v))
+
+
+def get_variant() -> int:
+    return _lib.load().amdgo_gemm_get_variant()
+
+
 def fast_path_supported(m: int, n: int, k: int) -> bool:
     lib = _lib.load()
     return m % lib.amdgo_gemm_tile_m() == 0 and n % lib.amdgo_gemm_tile_n() == 0 \

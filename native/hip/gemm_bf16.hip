@@ -24,6 +24,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -173,6 +174,118 @@ gemm_bf16_256x256(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
   }
 }
 
+// v2: same tile/LDS image as v1, software-pipelined at the fragment level.
+//   Two fragment register sets R0/R1 (k-steps kk=0/1 of a BK=64 tile). Per tile t:
+//     issue ds_read (t,kk1)->R1 ; MFMA R0 ; [vmcnt(0) lgkmcnt(0) ; barrier]
+//     issue LDS-DMA of tile t+2 into the buffer tile t used ; ds_read (t+1,kk0)->R0 ; MFMA R1
+//   The single barrier per tile sits mid-tile: the next tile's first fragment reads are
+//   in flight under the current tile's second MFMA cluster, and each LDS-DMA has a full
+//   tile of MFMAs (64 per wave) to land. WAR on the refilled buffer is covered by the
+//   lgkmcnt(0) + barrier (every wave's reads of tile t have completed).
+__global__ void __launch_bounds__(NTHREADS)
+gemm_bf16_256x256_v2(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                     __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2;
+  const int wc = wid & 3;
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * ROW_BYTES;
+  const int b_off = PANEL_BYTES + wc * 64 * ROW_BYTES;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 a0[8], b0[4], a1[8], b1[4];
+  auto read_frags = [&](const char* buf, int kk, bf16x8 (&af)[8], bf16x8 (&bfr)[4]) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      bfr[n] = *reinterpret_cast<const bf16x8*>(buf + b_off + n * 16 * ROW_BYTES + lane_off[kk]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      af[m] = *reinterpret_cast<const bf16x8*>(buf + a_off + m * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  auto mfma_all = [&](const bf16x8 (&af)[8], const bf16x8 (&bfr)[4]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n], af[m], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int ktiles = K / BK;
+
+  // prologue: tile 0 resident, tile 1 in flight, (0,kk0) fragments loaded
+  stage_panel(gA, K, 0, smem, wid, lane);
+  stage_panel(gB, K, 0, smem + PANEL_BYTES, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (ktiles > 1) {
+    stage_panel(gA, K, BK, smem + BUF_BYTES, wid, lane);
+    stage_panel(gB, K, BK, smem + BUF_BYTES + PANEL_BYTES, wid, lane);
+  }
+  read_frags(smem, 0, a0, b0);
+
+  for (int t = 0; t < ktiles; ++t) {
+    char* cur = smem + (t & 1) * BUF_BYTES;
+    char* nxt = smem + ((t + 1) & 1) * BUF_BYTES;
+    read_frags(cur, 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_all(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 2 < ktiles) {
+      stage_panel(gA, K, (t + 2) * BK, cur, wid, lane);
+      stage_panel(gB, K, (t + 2) * BK, cur + PANEL_BYTES, wid, lane);
+    }
+    if (t + 1 < ktiles) read_frags(nxt, 0, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_all(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  const int row_base = tm * BM + wr * 128 + (lane & 15);
+  const int col_base = tn * BN + wc * 64 + 4 * (lane >> 4);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    __bf16* crow = C + (size_t)(row_base + m * 16) * N + col_base;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 v;
+      v[0] = (__bf16)acc[m][n][0];
+      v[1] = (__bf16)acc[m][n][1];
+      v[2] = (__bf16)acc[m][n][2];
+      v[3] = (__bf16)acc[m][n][3];
+      *reinterpret_cast<bf16x4*>(crow + n * 16) = v;
+    }
+  }
+}
+
 // Generic bounds-checked MFMA kernel (64x64 tile, 4 waves of 32x32), register-staged.
 // Used for shapes that are not multiples of 256/256/64 and as a second, independent
 // implementation for cross-checking the fast path.
@@ -263,7 +376,20 @@ __global__ void fill_uniform_bf16(__bf16* p, size_t n, uint32_t seed) {
 
 }  // namespace
 
+static int g_variant = -1;
+
+static int variant() {
+  if (g_variant < 0) {
+    const char* e = getenv("AMDGO_GEMM_VARIANT");
+    g_variant = e ? atoi(e) : 2;
+  }
+  return g_variant;
+}
+
 extern "C" {
+
+void amdgo_gemm_set_variant(int v) { g_variant = v; }
+int amdgo_gemm_get_variant() { return variant(); }
 
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
@@ -271,8 +397,12 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   hipStream_t s = (hipStream_t)stream;
   if (M % BM == 0 && N % BN == 0 && K % BK == 0) {
     const int nwg = (M / BM) * (N / BN);
-    hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
-                       (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    if (variant() == 1)
+      hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else
+      hipLaunchKernelGGL(gemm_bf16_256x256_v2, dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
   } else {
     dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
     hipLaunchKernelGGL(gemm_bf16_generic, grid, dim3(256), 0, s,

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--shapes", default="1024,4096,8192,16384,16384x16384x1024")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="1,2")
     a = ap.parse_args()
     import torch
     from gpu_operator_amd.ops import gemm as G
@@ -44,21 +45,32 @@ def main():
         G.fill_uniform_(A, 1)
         G.fill_uniform_(Bt, 2)
         C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
-        G.gemm_bf16(A, Bt, C)
-        chk = G.verify(A, Bt, C, nrows=16)
-        ours, blas = [], []
+        variants = [int(v) for v in a.variants.split(",")]
+        checks = {}
+        for v in variants:
+            G.set_variant(v)
+            C.zero_()
+            G.gemm_bf16(A, Bt, C)
+            checks[v] = G.verify(A, Bt, C, nrows=16)
+        ours = {v: [] for v in variants}
+        blas = []
         for _ in range(a.rounds):
-            for _ in range(3):
-                G.gemm_bf16(A, Bt, C)
-            ours.append(time_fn(lambda: G.gemm_bf16(A, Bt, C), a.iters, torch))
+            for v in variants:
+                G.set_variant(v)
+                for _ in range(3):
+                    G.gemm_bf16(A, Bt, C)
+                ours[v].append(time_fn(lambda: G.gemm_bf16(A, Bt, C), a.iters, torch))
             for _ in range(3):
                 torch.matmul(A, Bt.t())
             blas.append(time_fn(lambda: torch.matmul(A, Bt.t(), out=C), a.iters, torch))
-        t_o, t_b = min(ours), min(blas)
-        print(json.dumps({"m": m, "n": n, "k": k, "ours_tflops": round(G.tflops(m, n, k, t_o), 1),
-                          "hipblaslt_tflops": round(G.tflops(m, n, k, t_b), 1),
-                          "ratio": round(t_b / t_o, 3), "check_ok": chk.ok,
-                          "max_rel_err": chk.max_rel_err}), flush=True)
+        t_b = min(blas)
+        rec = {"m": m, "n": n, "k": k, "hipblaslt_tflops": round(G.tflops(m, n, k, t_b), 1)}
+        for v in variants:
+            t_o = min(ours[v])
+            rec[f"v{v}_tflops"] = round(G.tflops(m, n, k, t_o), 1)
+            rec[f"v{v}_median_tflops"] = round(G.tflops(m, n, k, sorted(ours[v])[len(ours[v]) // 2]), 1)
+            rec[f"v{v}_check_ok"] = checks[v].ok
+        print(json.dumps(rec), flush=True)
         del A, Bt, C
         torch.cuda.empty_cache()
 
