@@ -88,6 +88,13 @@ def _pyext_name(stem: str) -> str:
 TARGETS: List[Target] = [
     # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.
     Target("libamdgo_hip.so", ["hip/gemm_bf16.hip", "hip/smoke.hip"], "hip-shared"),
+    # Node agent library (sysfs/KFD topology, partitions, telemetry, inotify barriers).
+    Target(_pyext_name("_amdnode"), ["node/pybind.cpp", "node/amdnode.cpp"], "pyext",
+           headers=["include/amdnode.h"]),
+    Target("bin/amd-barrier-wait", ["node/barrier_wait.cpp", "node/amdnode.cpp"], "cxx-exe",
+           flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
+    Target("bin/amd-node-probe", ["node/node_probe.cpp", "node/amdnode.cpp"], "cxx-exe",
+           flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
 ]
 
 

@@ -1,0 +1,133 @@
+"""Build fake sysfs/KFD trees of AMD GPU nodes for tests and dry runs.
+
+Mirrors the files libamdnode reads on a real MI355X node: KFD topology nodes (one CPU agent
+per socket + one GPU agent per XCP partition) with xGMI/PCIe io_links, PCI device
+directories with VRAM, partition and hwmon files, the amdgpu module state and /dev/kfd.
+The reference ships no fake GPU or sysfs for its validator.
+"""
+
+from __future__ import annotations
+
+import os
+from pathlib import Path
+from typing import Dict, Optional
+
+MI355X_DEVICE_ID = 0x75A3
+MI355X_CUS = 256
+MI355X_VRAM = 288 * (1 << 30)          # 288 GiB HBM3E
+PARTITION_XCDS = {"SPX": 8, "DPX": 4, "QPX": 2, "CPX": 1}
+GFX950 = 90500
+
+
+def _w(p: Path, content) -> None:
+    p.parent.mkdir(parents=True, exist_ok=True)
+    p.write_text(f"{content}\n")
+
+
+def _props(p: Path, kv: Dict[str, int]) -> None:
+    _w(p, "\n".join(f"{k} {v}" for k, v in kv.items()))
+
+
+def make_node(root, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", driver: str = "amdgpu",
+              live: bool = True, kfd: bool = True, hive_id: int = 0x5A5A_0001, device_id: int = MI355X_DEVICE_ID,
+              driver_version: str = "6.12.12", sriov_totalvfs: int = 0, vfio_bound: bool = False,
+              product: Optional[str] = "AMD Instinct MI355X") -> Path:
+    """Create a fake node under ``root``; returns the root path."""
+    root = Path(root)
+    nparts = 8 // PARTITION_XCDS[compute]
+    cus = MI355X_CUS // nparts
+    vram_per_part = MI355X_VRAM // (nparts if memory != "NPS1" else 1) if memory != "NPS1" else MI355X_VRAM
+    if live:
+        _w(root / "sys/module/amdgpu/initstate", "live")
+        if driver_version:
+            _w(root / "sys/module/amdgpu/version", driver_version)
+    if kfd:
+        (root / "dev").mkdir(parents=True, exist_ok=True)
+        (root / "dev/kfd").write_text("")
+    topo = root / "sys/class/kfd/kfd/topology/nodes"
+    _props(topo / "0/properties", {"cpu_cores_count": 128, "simd_count": 0, "mem_banks_count": 1})
+    _w(topo / "0/gpu_id", 0)
+    node = 1
+    gpu_nodes = []
+    for g in range(n_gpus):
+        bus = 0x05 + 0x10 * g
+        bdf = f"0000:{bus:02x}:00.0"
+        dev = root / "sys/bus/pci/devices" / bdf
+        _w(dev / "vendor", "0x1002")
+        _w(dev / "device", f"0x{device_id:04x}")
+        _w(dev / "subsystem_device", "0x0b00")
+        _w(dev / "class", "0x120000")
+        _w(dev / "numa_node", g // 4)
+        _w(dev / "mem_info_vram_total", MI355X_VRAM)
+        _w(dev / "mem_info_vram_used", 1 << 30)
+        if product:
+            _w(dev / "product_name", product)
+        _w(dev / "vbios_version", "113-MI355X-001")
+        _w(dev / "current_compute_partition", compute)
+        _w(dev / "available_compute_partition", "SPX, DPX, QPX, CPX")
+        _w(dev / "current_memory_partition", memory)
+        _w(dev / "available_memory_partition", "NPS1, NPS2")
+        _w(dev / "xgmi_hive_info/xgmi_hive_id", hive_id)
+        _w(dev / "gpu_busy_percent", 37)
+        _w(dev / "mem_busy_percent", 12)
+        _w(dev / "pp_dpm_sclk", "0: 500Mhz\n1: 2100Mhz *\n2: 2400Mhz")
+        _w(dev / "pp_dpm_mclk", "0: 900Mhz\n1: 1900Mhz *")
+        _w(dev / "ras/umc_err_count", "ue: 0\nce: 3")
+        hw = dev / "hwmon/hwmon3"
+        _w(hw / "power1_average", 750_000_000)
+        for i, (label, t) in enumerate((("edge", 45000), ("junction", 61000), ("mem", 52000)), start=1):
+            _w(hw / f"temp{i}_label", label)
+            _w(hw / f"temp{i}_input", t)
+        (dev / "drm" / f"card{g}").mkdir(parents=True, exist_ok=True)
+        (dev / "drm" / f"renderD{128 + g}").mkdir(parents=True, exist_ok=True)
+        drv_dir = root / "sys/bus/pci/drivers" / ("vfio-pci" if vfio_bound else driver)
+        drv_dir.mkdir(parents=True, exist_ok=True)
+        link = dev / "driver"
+        if link.is_symlink() or link.exists():
+            link.unlink()
+        os.symlink(os.path.relpath(drv_dir, dev), link)
+        grp = root / "sys/kernel/iommu_groups" / str(10 + g)
+        grp.mkdir(parents=True, exist_ok=True)
+        ig = dev / "iommu_group"
+        if not ig.exists():
+            os.symlink(os.path.relpath(grp, dev), ig)
+        if sriov_totalvfs:
+            _w(dev / "sriov_totalvfs", sriov_totalvfs)
+            _w(dev / "sriov_numvfs", 0)
+        for p in range(nparts):
+            nd = topo / str(node)
+            _props(nd / "properties", {
+                "cpu_cores_count": 0, "simd_count": cus * 4, "mem_banks_count": 1,
+                "simd_per_cu": 4, "max_waves_per_simd": 8, "lds_size_in_kb": 160,
+                "gfx_target_version": GFX950, "vendor_id": 0x1002, "device_id": device_id,
+                "location_id": bus << 8, "domain": 0, "drm_render_minor": 128 + g * nparts + p,
+                "unique_id": 0x1000_0000_0000_0000 + g * 16 + p, "num_xcc": PARTITION_XCDS[compute],
+                "hive_id": hive_id,
+            })
+            _w(nd / "gpu_id", 40000 + node)
+            gpu_nodes.append(node)
+            node += 1
+    # io links: every GPU agent has a PCIe link to the CPU and xGMI links to every GPU agent
+    # of the other physical GPUs (fully connected 8-GPU mesh)
+    for i, a in enumerate(gpu_nodes):
+        links = [(2, 0, 20)]
+        for j, b in enumerate(gpu_nodes):
+            if a != b and (i // nparts) != (j // nparts):
+                links.append((11, b, 15))
+        for li, (t, to, w) in enumerate(links):
+            _props(topo / str(a) / "io_links" / str(li) / "properties",
+                   {"type": t, "node_from": a, "node_to": to, "weight": w,
+                    "min_bandwidth": 50000 if t == 11 else 32000, "max_bandwidth": 153000 if t == 11 else 64000})
+    return root
+
+
+def set_compute_partition(root, compute: str, memory: Optional[str] = None) -> None:
+    """Re-enumerate the fake node as the driver does after a partition change."""
+    import shutil
+    root = Path(root)
+    pci = root / "sys/bus/pci/devices"
+    n = len([d for d in pci.iterdir()]) if pci.exists() else 8
+    mem = memory or (root / "sys/bus/pci/devices").iterdir().__next__().joinpath(
+        "current_memory_partition").read_text().strip()
+    shutil.rmtree(root / "sys/class/kfd", ignore_errors=True)
+    make_node(root, n_gpus=n, compute=compute, memory=mem)
