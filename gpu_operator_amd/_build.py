@@ -66,6 +66,8 @@ class Target:
                     "-Wno-unused-function", "-Wno-unused-result"] + inc
             if self.kind == "hip-shared":
                 base += ["-fPIC", "-shared"]
+            else:
+                base += [f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}"]
             return base + self.flags + srcs + ["-o", str(self.output)] + self.libs
         if self.kind == "pyext":
             import pybind11  # noqa: WPS433 (build-time only)
@@ -93,6 +95,12 @@ TARGETS: List[Target] = [
            headers=["include/amdnode.h"]),
     Target("bin/amd-barrier-wait", ["node/barrier_wait.cpp", "node/amdnode.cpp"], "cxx-exe",
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
+    # Validator workload binaries (run inside the validation pods).
+    Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip"], "hip-exe",
+           flags=["-x", "hip"]),
+    Target("bin/amd-hip-smoke", ["hip/hip_smoke_main.cpp", "hip/smoke.hip"], "hip-exe", flags=["-x", "hip"]),
+    Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp"], "hip-exe", flags=["-x", "hip"],
+           libs=["-lrccl"]),
     Target("bin/amd-node-probe", ["node/node_probe.cpp", "node/amdnode.cpp"], "cxx-exe",
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
 ]

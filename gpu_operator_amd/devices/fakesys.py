@@ -105,6 +105,9 @@ def make_node(root, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
                 "hive_id": hive_id,
             })
             _w(nd / "gpu_id", 40000 + node)
+            if kfd:
+                (root / "dev/dri").mkdir(parents=True, exist_ok=True)
+                (root / "dev/dri" / f"renderD{128 + g * nparts + p}").write_text("")
             gpu_nodes.append(node)
             node += 1
     # io links: every GPU agent has a PCIe link to the CPU and xGMI links to every GPU agent

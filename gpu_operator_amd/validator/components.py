@@ -1,0 +1,395 @@
+"""Validator components: each validates one layer of the node and writes its barrier.
+
+Reference counterparts (validator/main.go): Driver :607-708, Toolkit :775-801, CUDA
+:1176-1293 (-> HIP here), Plugin :803-1015, MOFED :847-912 (-> RDMA), VfioPCI :1301-1356,
+VGPUManager :1358-1426 (-> MxGPU manager), VGPUDevices :1428-1501 (-> MxGPU devices),
+workload-type :405-437. New: RCCL (all-GPU all-reduce over xGMI).
+
+Every wait is event-driven and bounded (the reference's ``--with-wait`` loops forever,
+SURVEY.md §7.7 quirk 6; its toolkit validation relies on crash-loop back-off, quirk 6).
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import os
+import shutil
+import subprocess
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+from .. import devices
+from ..k8s import errors
+from ..k8s import objects as o
+from . import status as S
+from . import workload as W
+
+log = logging.getLogger("amd-validator")
+
+GPU_RESOURCE = "amd.com/gpu"
+PARTITION_RESOURCE_PREFIX = "amd.com/partition-"
+MELLANOX_LABEL = "feature.node.kubernetes.io/pci-15b3.present"
+WORKLOAD_CONFIG_LABEL = "amd.com/gpu.workload.config"
+
+
+class ValidationError(Exception):
+    pass
+
+
+@dataclass
+class Context:
+    status: S.StatusDir
+    node_name: str = ""
+    namespace: str = ""
+    client: Any = None
+    host_root: str = "/host"         # host filesystem as mounted in the container
+    sys_root: str = "/"              # sysfs root (the container's /sys is the host's)
+    dev_root: str = "/"
+    driver_root: str = "/run/amd/driver"
+    with_wait: bool = False
+    with_workload: bool = False
+    sleep_interval: float = 5.0
+    wait_timeout: float = 3600.0     # bound on any --with-wait (the reference waits forever)
+    pod_timeout: float = 300.0       # validation pod completion (reference: 60 x 5 s)
+    resource_timeout: float = 150.0  # GPU resources in node capacity (reference: 30 x 5 s)
+    partition_strategy: str = "single"
+    default_workload: str = "vm-passthrough"
+    env: Dict[str, str] = field(default_factory=lambda: dict(os.environ))
+    run: Callable[..., subprocess.CompletedProcess] = subprocess.run
+    clock: Callable[[], float] = time.monotonic
+
+
+def retry(ctx: Context, what: str, fn: Callable[[], Any]) -> Any:
+    """Run ``fn`` once, or until it stops raising (bounded by ctx.wait_timeout) in wait mode."""
+    deadline = ctx.clock() + ctx.wait_timeout
+    delay = 0.2
+    while True:
+        try:
+            return fn()
+        except ValidationError as e:
+            if not ctx.with_wait or ctx.clock() >= deadline:
+                raise
+            log.info("%s not ready (%s); retrying in %.1fs", what, e, delay)
+            time.sleep(delay)
+            delay = min(ctx.sleep_interval, delay * 2)
+
+
+# ---------------------------------------------------------------------------------------------
+# driver
+# ---------------------------------------------------------------------------------------------
+HOST_DRIVER_MARKERS = ("/usr/bin/amd-smi", "/opt/rocm/bin/amd-smi", "/usr/sbin/amdgpu-install")
+
+
+def host_driver_installed(ctx: Context) -> bool:
+    mode = ctx.env.get("DRIVER_ROOT_MODE", "")
+    if mode:
+        return mode == "host"
+    return any(os.path.exists(ctx.host_root + m) for m in HOST_DRIVER_MARKERS)
+
+
+def check_driver(ctx: Context) -> Dict[str, Any]:
+    st = devices.driver_state(ctx.sys_root, ctx.dev_root)
+    if not st["module_loaded"]:
+        raise ValidationError("amdgpu module not loaded")
+    if not st["live"]:
+        raise ValidationError("amdgpu initstate is not live")
+    if not st["kfd_present"]:
+        raise ValidationError("/dev/kfd missing")
+    if st["kfd_gpu_nodes"] == 0:
+        raise ValidationError("KFD reports no GPU agents")
+    gpus = devices.enumerate_gpus(ctx.sys_root)
+    pci = [f for f in devices.scan_pci(ctx.sys_root) if not f["is_virtfn"] and f["driver"] == "amdgpu"]
+    bound = {g["pci_bdf"] for g in gpus}
+    missing = [f["bdf"] for f in pci if f["bdf"] not in bound]
+    if missing:
+        raise ValidationError(f"amdgpu-bound GPUs without a KFD agent: {missing}")
+    return {"driver_version": st["version"] or "inbox", "gpus": len({g["pci_bdf"] for g in gpus}),
+            "kfd_agents": st["kfd_gpu_nodes"], "gfx": sorted({g["gfx_target"] for g in gpus}),
+            "products": sorted({g["product_name"] for g in gpus if g["product_name"]})}
+
+
+def validate_driver(ctx: Context) -> Dict[str, Any]:
+    host = host_driver_installed(ctx)
+    if not host:
+        # driver container: its startup probe writes .driver-ctr-ready once amdgpu is live
+        t = None if not ctx.with_wait else ctx.wait_timeout
+        if not ctx.status.exists(S.DRIVER_CTR_READY):
+            if not ctx.with_wait:
+                raise ValidationError("driver container not ready (.driver-ctr-ready missing)")
+            if not ctx.status.wait([S.DRIVER_CTR_READY], timeout=t):
+                raise ValidationError("timed out waiting for the driver container")
+    info = retry(ctx, "driver", lambda: check_driver(ctx))
+    info["mode"] = "host" if host else "container"
+    ctx.status.delete(S.DRIVER_READY)
+    ctx.status.delete(S.HOST_DRIVER_READY)
+    ctx.status.create(S.HOST_DRIVER_READY if host else S.DRIVER_READY, info)
+    return info
+
+
+# ---------------------------------------------------------------------------------------------
+# runtime hook (toolkit)
+# ---------------------------------------------------------------------------------------------
+def check_toolkit(ctx: Context) -> Dict[str, Any]:
+    """Inside a container started through the AMD runtime hook with AMD_VISIBLE_DEVICES=all,
+    /dev/kfd and the render nodes of every GPU must have been injected."""
+    kfd = os.path.join(ctx.dev_root, "dev/kfd")
+    if not os.path.exists(kfd):
+        raise ValidationError("/dev/kfd not injected into the container")
+    dri = os.path.join(ctx.dev_root, "dev/dri")
+    render = sorted(x for x in (os.listdir(dri) if os.path.isdir(dri) else []) if x.startswith("renderD"))
+    gpus = devices.enumerate_gpus(ctx.sys_root)
+    want = {f"renderD{g['drm_render_minor']}" for g in gpus if g["drm_render_minor"] >= 0}
+    missing = sorted(want - set(render))
+    if missing:
+        raise ValidationError(f"render nodes not injected: {missing}")
+    return {"render_nodes": len(render), "kfd": True}
+
+
+def validate_toolkit(ctx: Context) -> Dict[str, Any]:
+    info = retry(ctx, "toolkit", lambda: check_toolkit(ctx))
+    ctx.status.create(S.TOOLKIT_READY, info)
+    return info
+
+
+# ---------------------------------------------------------------------------------------------
+# HIP (matrix-core GEMM + smoke) -- replaces the CUDA vectorAdd validation
+# ---------------------------------------------------------------------------------------------
+def _validator_env(ctx: Context) -> Dict[str, str]:
+    return {k: v for k, v in ctx.env.items() if k.startswith("VALIDATOR_")}
+
+
+def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
+    agg = [r for r in results if r.get("event") == "aggregate"]
+    per = [r for r in results if r.get("event") == "gemm"]
+    smoke = [r for r in results if r.get("event") == "hip-smoke"]
+    out: Dict[str, Any] = {"gemm": per, "aggregate": agg}
+    if agg:
+        head = max(agg, key=lambda r: r["m"] * r["n"] * r["k"])
+        out["gemm_tflops_total"] = head["total_tflops"]
+        out["gemm_tflops_per_gpu"] = head["per_gpu_tflops"]
+        out["gpus"] = head["gpus"]
+    if smoke:
+        out["smoke_ok"] = all(s.get("ok") for s in smoke)
+    out["counters"] = [r for r in results if r.get("event") == "counters"]
+    return out
+
+
+def validate_hip(ctx: Context) -> Dict[str, Any]:
+    mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
+    if mode == "local":
+        from .workload_main import run_hip
+        results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run)
+    else:
+        res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                                 _validator_env(ctx), timeout=ctx.pod_timeout)
+        results = res["results"]
+    info = summarize_gemm(results)
+    bad = [r for r in info["gemm"] if not r.get("ok")]
+    if bad or info.get("smoke_ok") is False:
+        raise ValidationError(f"HIP validation failed: {bad or 'hip-smoke'}")
+    ctx.status.create(S.HIP_READY, info)
+    return info
+
+
+# ---------------------------------------------------------------------------------------------
+# device plugin
+# ---------------------------------------------------------------------------------------------
+def gpu_resources(node: Dict[str, Any], strategy: str) -> Dict[str, int]:
+    cap = ((node.get("status") or {}).get("capacity") or {})
+    out = {}
+    for k, v in cap.items():
+        if k == GPU_RESOURCE or (strategy == "mixed" and k.startswith(PARTITION_RESOURCE_PREFIX)):
+            try:
+                n = int(v)
+            except (TypeError, ValueError):
+                continue
+            if n > 0:
+                out[k] = n
+    return out
+
+
+def wait_gpu_resources(ctx: Context) -> Dict[str, int]:
+    """Watch the Node (event-driven) until it advertises GPU resources, bounded."""
+    done = threading.Event()
+    found: Dict[str, int] = {}
+
+    def on_event(ev):
+        if o.name(ev.obj) != ctx.node_name:
+            return
+        r = gpu_resources(ev.obj, ctx.partition_strategy)
+        if r:
+            found.update(r)
+            done.set()
+    stop = ctx.client.watch("v1", "Node", on_event)
+    try:
+        deadline = ctx.clock() + ctx.resource_timeout
+        while not done.is_set():
+            r = gpu_resources(ctx.client.get("v1", "Node", ctx.node_name), ctx.partition_strategy)
+            if r:
+                return r
+            remaining = deadline - ctx.clock()
+            if remaining <= 0:
+                raise ValidationError(f"no {GPU_RESOURCE} resources on node {ctx.node_name} after "
+                                      f"{ctx.resource_timeout:.0f}s")
+            done.wait(min(remaining, 2.0))
+    finally:
+        stop()
+    return found
+
+
+def validate_plugin(ctx: Context) -> Dict[str, Any]:
+    res = wait_gpu_resources(ctx)
+    info: Dict[str, Any] = {"resources": res, "devices": sum(res.values())}
+    if ctx.with_workload:
+        # prefer a partition resource (like the reference prefers MIG), else one whole GPU
+        name = next((k for k in sorted(res) if k.startswith(PARTITION_RESOURCE_PREFIX)), GPU_RESOURCE)
+        out = W.run_workload_pod(ctx.client, "plugin-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                                 _validator_env(ctx), timeout=ctx.pod_timeout, gpu_limit={name: 1})
+        info["workload"] = summarize_gemm(out["results"])
+    ctx.status.create(S.PLUGIN_READY, info)
+    return info
+
+
+# ---------------------------------------------------------------------------------------------
+# RCCL all-reduce over xGMI (new)
+# ---------------------------------------------------------------------------------------------
+def summarize_rccl(results: List[Dict[str, Any]]) -> Dict[str, Any]:
+    sweep = [r for r in results if r.get("event") == "allreduce"]
+    summ = next((r for r in results if r.get("event") == "summary"), {})
+    return {"sweep": sweep, "ranks": summ.get("ranks"), "peak_busbw_gbps": summ.get("peak_busbw_gbps"),
+            "ok": bool(summ.get("ok")) and all(r.get("ok") for r in sweep)}
+
+
+def validate_rccl(ctx: Context) -> Dict[str, Any]:
+    node = ctx.client.get("v1", "Node", ctx.node_name)
+    ngpu = int(((node.get("status") or {}).get("allocatable") or {}).get(GPU_RESOURCE, 0) or 0)
+    if ngpu < 2:
+        info = {"skipped": f"{ngpu} GPU(s) allocatable: no fabric to validate", "ok": True}
+        ctx.status.create(S.RCCL_READY, info)
+        return info
+    out = W.run_workload_pod(ctx.client, "rccl-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                             _validator_env(ctx), timeout=ctx.pod_timeout, gpu_limit={GPU_RESOURCE: ngpu})
+    info = summarize_rccl(out["results"])
+    if not info["ok"]:
+        raise ValidationError(f"RCCL all-reduce validation failed: {info}")
+    ctx.status.create(S.RCCL_READY, info)
+    return info
+
+
+# ---------------------------------------------------------------------------------------------
+# RDMA (reference: MOFED validation)
+# ---------------------------------------------------------------------------------------------
+def validate_rdma(ctx: Context) -> Dict[str, Any]:
+    if ctx.env.get("RDMA_ENABLED", "false") != "true":
+        return {"skipped": "RDMA disabled"}
+    if ctx.client is not None and ctx.node_name:
+        node = ctx.client.get("v1", "Node", ctx.node_name)
+        if o.get_labels(node).get(MELLANOX_LABEL) != "true":
+            return {"skipped": "no Mellanox NIC on node"}
+
+    def check():
+        if ctx.env.get("USE_HOST_MOFED") == "true":
+            if not os.path.isdir(os.path.join(ctx.sys_root, "sys/module/mlx5_core")):
+                raise ValidationError("mlx5_core not loaded on host")
+        elif not os.path.exists("/run/mellanox/drivers/.driver-ready"):
+            raise ValidationError("MOFED driver container not ready")
+        return {"rdma": True}
+    info = retry(ctx, "rdma", check)
+    ctx.status.create(S.RDMA_READY, info)
+    return info
+
+
+# ---------------------------------------------------------------------------------------------
+# sandbox components
+# ---------------------------------------------------------------------------------------------
+def workload_type(ctx: Context) -> str:
+    wt = ctx.default_workload
+    if ctx.client is not None and ctx.node_name:
+        node = ctx.client.get("v1", "Node", ctx.node_name)
+        v = o.get_labels(node).get(WORKLOAD_CONFIG_LABEL)
+        if v in ("container", "vm-passthrough", "vm-mxgpu"):
+            wt = v
+    ctx.status.write_raw(S.WORKLOAD_TYPE, wt)
+    return wt
+
+
+def validate_vfio_pci(ctx: Context) -> Dict[str, Any]:
+    if workload_type(ctx) != "vm-passthrough":
+        return {"skipped": "not a passthrough node"}
+
+    def check():
+        fns = [f for f in devices.scan_pci(ctx.sys_root) if not f["is_virtfn"]]
+        if not fns:
+            raise ValidationError("no AMD GPU PCI functions found")
+        bad = [f["bdf"] for f in fns if f["driver"] != "vfio-pci"]
+        if bad:
+            raise ValidationError(f"not bound to vfio-pci: {bad}")
+        return {"devices": len(fns)}
+    info = retry(ctx, "vfio-pci", check)
+    ctx.status.create(S.VFIO_PCI_READY, info)
+    return info
+
+
+def validate_mxgpu_manager(ctx: Context) -> Dict[str, Any]:
+    if workload_type(ctx) != "vm-mxgpu":
+        return {"skipped": "not an MxGPU node"}
+    host = os.path.isdir(os.path.join(ctx.host_root, "lib/modules")) and \
+        ctx.env.get("MXGPU_HOST_DRIVER", "") == "true"
+
+    def check():
+        gim = os.path.join(ctx.sys_root, "sys/module/gim")
+        if not os.path.isdir(gim):
+            raise ValidationError("MxGPU host driver (gim) not loaded")
+        return {"gim_version": (open(os.path.join(gim, "version")).read().strip()
+                                if os.path.exists(os.path.join(gim, "version")) else "")}
+    info = retry(ctx, "mxgpu-manager", check)
+    ctx.status.create(S.HOST_MXGPU_MANAGER_READY if host else S.MXGPU_MANAGER_READY, info)
+    return info
+
+
+def validate_mxgpu_devices(ctx: Context) -> Dict[str, Any]:
+    if workload_type(ctx) != "vm-mxgpu":
+        return {"skipped": "not an MxGPU node"}
+
+    def check():
+        vfs = [f for f in devices.scan_pci(ctx.sys_root) if f["is_virtfn"]]
+        pfs = [f for f in devices.scan_pci(ctx.sys_root) if not f["is_virtfn"] and f["sriov_numvfs"] > 0]
+        if not vfs and not pfs:
+            raise ValidationError("no MxGPU virtual functions created")
+        return {"virtual_functions": max(len(vfs), sum(f["sriov_numvfs"] for f in pfs))}
+    info = retry(ctx, "mxgpu-devices", check)
+    ctx.status.create(S.MXGPU_DEVICES_READY, info)
+    return info
+
+
+def sandbox_ready_wait(ctx: Context) -> Dict[str, Any]:
+    """Init container of the sandbox device plugin: wait for the workload type, then for the
+    barrier its workload needs (reference: assets/state-sandbox-device-plugin/0500_daemonset.yaml:31-50)."""
+    if not ctx.status.wait([S.WORKLOAD_TYPE], timeout=ctx.wait_timeout):
+        raise ValidationError("workload-type barrier never appeared")
+    wt = open(ctx.status.file(S.WORKLOAD_TYPE)).read().strip()
+    need = {"vm-passthrough": [S.VFIO_PCI_READY], "vm-mxgpu": [S.MXGPU_DEVICES_READY]}.get(wt, [])
+    if need and not ctx.status.wait(need, timeout=ctx.wait_timeout):
+        raise ValidationError(f"timed out waiting for {need}")
+    return {"workload_type": wt}
+
+
+COMPONENTS: Dict[str, Callable[[Context], Dict[str, Any]]] = {
+    "driver": validate_driver,
+    "toolkit": validate_toolkit,
+    "hip": validate_hip,
+    "cuda": validate_hip,           # reference component name, kept for migration
+    "plugin": validate_plugin,
+    "rccl": validate_rccl,
+    "rdma": validate_rdma,
+    "mofed": validate_rdma,         # reference component name
+    "vfio-pci": validate_vfio_pci,
+    "mxgpu-manager": validate_mxgpu_manager,
+    "vgpu-manager": validate_mxgpu_manager,
+    "mxgpu-devices": validate_mxgpu_devices,
+    "vgpu-devices": validate_mxgpu_devices,
+    "sandbox-ready-wait": sandbox_ready_wait,
+}

@@ -1,0 +1,157 @@
+"""Node status exporter (``amd-validator --component metrics``), reference:
+validator/metrics.go:52-320 (same families, ``amd_gpu_operator_`` prefix).
+
+Refresh model: barrier files are watched with inotify (an open/closed barrier is reflected
+immediately, not after the reference's 30 s period); the driver check runs every 60 s, the
+node-capacity and PCI counts every 30/60 s. New gauges: node time-to-ready (driver ->
+validator), per-barrier timestamps, validator GEMM TFLOPS and RCCL all-reduce bus bandwidth
+(read from the barrier payloads).
+"""
+
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from typing import Any, Dict, Optional
+
+from prometheus_client import CollectorRegistry, Gauge
+
+from .. import devices
+from . import components as comp
+from . import status as S
+
+log = logging.getLogger("amd-validator.metrics")
+
+STATUS_PERIOD = 30.0
+DRIVER_PERIOD = 60.0
+PLUGIN_PERIOD = 30.0
+PCI_PERIOD = 60.0
+
+BARRIERS = {"driver": (S.DRIVER_READY, S.HOST_DRIVER_READY), "toolkit": (S.TOOLKIT_READY,),
+            "hip": (S.HIP_READY,), "plugin": (S.PLUGIN_READY,), "rccl": (S.RCCL_READY,)}
+
+
+class NodeMetrics:
+    def __init__(self, ctx: comp.Context, registry: Optional[CollectorRegistry] = None):
+        self.ctx = ctx
+        self.registry = registry or CollectorRegistry()
+        r, p, node = self.registry, "amd_gpu_operator_", ["node"]
+        self.ready_ts = Gauge(p + "node_metrics_ready_ts_seconds", "launch time of the node metrics exporter",
+                              node, registry=r)
+        self.barrier = {k: Gauge(p + f"node_{k}_ready", f"1 if the {k} barrier of the local node is open", node,
+                                 registry=r) for k in BARRIERS}
+        self.barrier_ts = Gauge(p + "node_barrier_ts_seconds", "time the barrier was opened", node + ["barrier"],
+                                registry=r)
+        self.ttr = Gauge(p + "node_time_to_ready_seconds",
+                         "driver ready -> last validator barrier (node bring-up critical path)", node, registry=r)
+        self.driver_validation = Gauge(p + "node_driver_validation", "1 if the driver check passed", node,
+                                       registry=r)
+        self.driver_last_success = Gauge(p + "node_driver_validation_last_success_ts_seconds",
+                                         "last successful driver check", node, registry=r)
+        self.devices_total = Gauge(p + "node_device_plugin_devices_total",
+                                   "GPU resources advertised on the node (-1 if unknown)", node, registry=r)
+        self.devices_last_success = Gauge(p + "node_device_plugin_validation_last_success_ts_seconds",
+                                          "last time GPU resources were found", node, registry=r)
+        self.pci_total = Gauge(p + "amd_pci_devices_total", "AMD GPU PCI functions (-1 if unknown)", node,
+                               registry=r)
+        self.gemm_tflops = Gauge(p + "validator_gemm_tflops", "validator MFMA GEMM throughput",
+                                 node + ["scope"], registry=r)
+        self.busbw = Gauge(p + "validator_allreduce_busbw_gbps", "validator RCCL all-reduce peak bus bandwidth",
+                           node + ["ranks"], registry=r)
+        self._stop = threading.Event()
+        self.ready_ts.labels(ctx.node_name).set(time.time())
+
+    # -- collectors ---------------------------------------------------------------------------
+    def refresh_status(self) -> None:
+        n = self.ctx.node_name
+        sd = self.ctx.status
+        for k, files in BARRIERS.items():
+            present = [sd.read(f) for f in files]
+            present = [d for d in present if d is not None]
+            self.barrier[k].labels(n).set(1 if present else 0)
+            if present:
+                self.barrier_ts.labels(n, k).set(min(d["ts"] for d in present))
+        ttr = S.time_to_ready(sd)
+        if ttr is not None:
+            self.ttr.labels(n).set(ttr)
+        hip = sd.read(S.HIP_READY) or {}
+        if "gemm_tflops_total" in hip:
+            self.gemm_tflops.labels(n, "node").set(hip["gemm_tflops_total"])
+            self.gemm_tflops.labels(n, "per_gpu").set(hip.get("gemm_tflops_per_gpu", 0))
+        rc = sd.read(S.RCCL_READY) or {}
+        if rc.get("peak_busbw_gbps") is not None:
+            self.busbw.labels(n, str(rc.get("ranks"))).set(rc["peak_busbw_gbps"])
+
+    def refresh_driver(self) -> None:
+        n = self.ctx.node_name
+        try:
+            comp.check_driver(self.ctx)
+            self.driver_validation.labels(n).set(1)
+            self.driver_last_success.labels(n).set(time.time())
+        except (comp.ValidationError, OSError, ImportError) as e:
+            log.info("driver check failed: %s", e)
+            self.driver_validation.labels(n).set(0)
+
+    def refresh_plugin(self) -> None:
+        n = self.ctx.node_name
+        try:
+            node = self.ctx.client.get("v1", "Node", n)
+            total = sum(comp.gpu_resources(node, "mixed").values())
+            self.devices_total.labels(n).set(total)
+            if total:
+                self.devices_last_success.labels(n).set(time.time())
+        except Exception as e:  # noqa: BLE001
+            log.info("node capacity check failed: %s", e)
+            self.devices_total.labels(n).set(-1)
+
+    def refresh_pci(self) -> None:
+        n = self.ctx.node_name
+        try:
+            self.pci_total.labels(n).set(len([f for f in devices.scan_pci(self.ctx.sys_root)
+                                              if not f["is_virtfn"]]))
+        except Exception:  # noqa: BLE001
+            self.pci_total.labels(n).set(-1)
+
+    def refresh_all(self) -> None:
+        self.refresh_status()
+        self.refresh_driver()
+        if self.ctx.client is not None:
+            self.refresh_plugin()
+        self.refresh_pci()
+
+    # -- loops --------------------------------------------------------------------------------
+    def _loop(self, period: float, fn) -> None:
+        while not self._stop.is_set():
+            fn()
+            self._stop.wait(period)
+
+    def _watch_barriers(self) -> None:
+        names = [f for files in BARRIERS.values() for f in files]
+        while not self._stop.is_set():
+            missing = [f for f in names if not self.ctx.status.exists(f)]
+            # wake on the next barrier creation (inotify); re-check at least every period
+            if missing:
+                self.ctx.status.wait(missing, any_of=True, timeout=STATUS_PERIOD)
+            else:
+                self._stop.wait(STATUS_PERIOD)
+            self.refresh_status()
+
+    def start(self, port: int) -> int:
+        from ..runtime.manager import _Server
+        from prometheus_client import generate_latest
+        from prometheus_client.exposition import CONTENT_TYPE_LATEST
+
+        self.refresh_all()
+        for period, fn in ((DRIVER_PERIOD, self.refresh_driver), (PCI_PERIOD, self.refresh_pci)):
+            threading.Thread(target=self._loop, args=(period, fn), daemon=True).start()
+        if self.ctx.client is not None:
+            threading.Thread(target=self._loop, args=(PLUGIN_PERIOD, self.refresh_plugin), daemon=True).start()
+        threading.Thread(target=self._watch_barriers, daemon=True).start()
+        srv = _Server(("0.0.0.0", port), {"/metrics": lambda: (200, CONTENT_TYPE_LATEST,
+                                                               generate_latest(self.registry))})
+        srv.start()
+        return srv.port
+
+    def stop(self) -> None:
+        self._stop.set()

@@ -1,0 +1,167 @@
+"""Spawned validation pods (reference: validator/main.go:931-1081, 1217-1293).
+
+The validator creates a pod pinned to its node (``nodeName``), owned by the validator
+DaemonSet's owners (so it is garbage-collected with the ClusterPolicy), tolerating what the
+validator tolerates, with the validator's own image / pull policy / secrets / runtime class
+(passed in by the operator through ``VALIDATOR_*`` env). It then waits for the pod to finish:
+event-driven on a pod watch with a bounded timeout, where the reference polls 60 x 5 s.
+
+The workload writes its JSON results to the termination message, which the validator reads
+back from the pod status and stores in the barrier file.
+"""
+
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import os
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+import yaml
+
+from ..k8s import errors
+from ..k8s import objects as o
+
+log = logging.getLogger("amd-validator.workload")
+
+MANIFEST_DIRS = ["/var/amd/manifests", os.path.join(os.path.dirname(__file__), "manifests")]
+
+
+def load_pod_spec(name: str) -> Dict[str, Any]:
+    for d in MANIFEST_DIRS:
+        p = os.path.join(d, name)
+        if os.path.exists(p):
+            with open(p) as f:
+                return yaml.safe_load(f)
+    raise FileNotFoundError(f"validation pod manifest {name} not found in {MANIFEST_DIRS}")
+
+
+def _validator_ds(client, namespace: str, app: str) -> Optional[Dict[str, Any]]:
+    try:
+        return client.get("apps/v1", "DaemonSet", app, namespace)
+    except errors.NotFound:
+        return None
+
+
+def prepare_pod(client, template: Dict[str, Any], namespace: str, node: str, env: Dict[str, str],
+                validator_app: str = "amd-operator-validator") -> Dict[str, Any]:
+    pod = copy.deepcopy(template)
+    md = o.meta(pod)
+    md["namespace"] = namespace
+    md["name"] = f"{md['name']}-{node}"[:63].rstrip("-")
+    spec = pod.setdefault("spec", {})
+    image = env.get("VALIDATOR_IMAGE", "")
+    if not image:
+        raise ValueError("VALIDATOR_IMAGE env not set")
+    policy = env.get("VALIDATOR_IMAGE_PULL_POLICY", "IfNotPresent")
+    for c in spec.get("initContainers", []) + spec.get("containers", []):
+        c["image"] = image
+        c["imagePullPolicy"] = policy
+        # termination message carries the workload's JSON result
+        c.setdefault("terminationMessagePolicy", "FallbackToLogsOnError")
+    secrets = [s for s in env.get("VALIDATOR_IMAGE_PULL_SECRETS", "").split(",") if s]
+    if secrets:
+        spec["imagePullSecrets"] = [{"name": s} for s in secrets]
+    if env.get("VALIDATOR_RUNTIME_CLASS"):
+        spec["runtimeClassName"] = env["VALIDATOR_RUNTIME_CLASS"]
+    spec["nodeName"] = node
+    ds = _validator_ds(client, namespace, validator_app)
+    if ds is not None:
+        # owned like the validator DaemonSet (by the ClusterPolicy): GC'd with it
+        owners = copy.deepcopy((ds.get("metadata") or {}).get("ownerReferences") or [])
+        if owners:
+            md["ownerReferences"] = owners
+        tol = ((ds.get("spec") or {}).get("template") or {}).get("spec", {}).get("tolerations")
+        if tol:
+            spec["tolerations"] = copy.deepcopy(tol)
+    return pod
+
+
+def delete_stale(client, namespace: str, app: str, node: str) -> None:
+    for p in client.list("v1", "Pod", namespace, label_selector={"app": app},
+                         field_selector=f"spec.nodeName={node}"):
+        try:
+            client.delete("v1", "Pod", o.name(p), namespace, grace_period_seconds=0)
+        except errors.NotFound:
+            pass
+
+
+def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0) -> Dict[str, Any]:
+    """Block until the pod Succeeds (returns it) or Fails / times out (raises)."""
+    done = threading.Event()
+    state: Dict[str, Any] = {}
+
+    def on_event(ev):
+        if o.name(ev.obj) != name or o.namespace(ev.obj) != namespace:
+            return
+        phase = (ev.obj.get("status") or {}).get("phase")
+        if ev.type == "DELETED":
+            state["error"] = "pod deleted"
+            done.set()
+        elif phase in ("Succeeded", "Failed"):
+            state["pod"] = ev.obj
+            done.set()
+    stop = client.watch("v1", "Pod", on_event, namespace=namespace)
+    try:
+        # the watch delivers the current object first; also re-check directly (fake clients)
+        deadline = time.monotonic() + timeout
+        while not done.is_set():
+            try:
+                cur = client.get("v1", "Pod", name, namespace)
+                if (cur.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+                    state["pod"] = cur
+                    break
+            except errors.NotFound:
+                pass
+            remaining = deadline - time.monotonic()
+            if remaining <= 0:
+                raise TimeoutError(f"pod {namespace}/{name} did not complete within {timeout:.0f}s")
+            done.wait(min(remaining, 2.0))
+    finally:
+        stop()
+    if "error" in state:
+        raise RuntimeError(state["error"])
+    pod = state["pod"]
+    if pod["status"]["phase"] != "Succeeded":
+        raise RuntimeError(f"pod {name} failed: {termination_message(pod)}")
+    return pod
+
+
+def termination_message(pod: Dict[str, Any]) -> str:
+    st = pod.get("status") or {}
+    msgs = []
+    for cs in (st.get("initContainerStatuses") or []) + (st.get("containerStatuses") or []):
+        term = ((cs.get("state") or {}).get("terminated") or (cs.get("lastState") or {}).get("terminated") or {})
+        if term.get("message"):
+            msgs.append(term["message"])
+    return "\n".join(msgs)
+
+
+def parse_results(msg: str) -> List[Dict[str, Any]]:
+    out = []
+    for line in msg.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                out.append(json.loads(line))
+            except ValueError:
+                continue
+    return out
+
+
+def run_workload_pod(client, manifest: str, namespace: str, node: str, env: Dict[str, str],
+                     timeout: float = 300.0, gpu_limit: Optional[Dict[str, int]] = None) -> Dict[str, Any]:
+    template = load_pod_spec(manifest)
+    pod = prepare_pod(client, template, namespace, node, env)
+    if gpu_limit:
+        for c in pod["spec"].get("initContainers", []):
+            c.setdefault("resources", {})["limits"] = dict(gpu_limit)
+    app = o.get_labels(pod).get("app", "")
+    delete_stale(client, namespace, app, node)
+    client.create(pod)
+    log.info("created validation pod %s/%s", namespace, o.name(pod))
+    done = wait_for_pod(client, namespace, o.name(pod), timeout)
+    return {"pod": o.name(pod), "results": parse_results(termination_message(done))}

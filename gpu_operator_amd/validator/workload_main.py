@@ -1,0 +1,145 @@
+"""``amd-validator-workload``: what runs inside the spawned validation pods.
+
+    amd-validator-workload hip  [--gemm-shapes 8192,...] [--counters]
+    amd-validator-workload rccl [--max-bytes N] [--dtype float|bf16]
+
+Runs the native workload binaries (``amd-hip-smoke``, ``amd-gemm-validate``,
+``amd-rccl-validate``), optionally collects rocprofv3 counters for one GEMM dispatch
+(MFMA ops, busy cycles, LDS bank conflicts, L2 hit/miss) and prints JSON result lines. The
+same lines go to ``/dev/termination-log`` so the validator reads them back from the pod
+status. Exit status is non-zero if any check failed.
+"""
+
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+from typing import Callable, Dict, List, Optional
+
+BIN_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native", "bin")
+PMC_COUNTERS = ["SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+                "TCC_HIT_sum", "TCC_MISS_sum"]
+
+
+def binary(name: str) -> str:
+    p = os.path.join(BIN_DIR, name)
+    if os.path.exists(p):
+        return p
+    found = shutil.which(name)
+    if found:
+        return found
+    raise FileNotFoundError(f"{name} not found in {BIN_DIR} or PATH")
+
+
+def _json_lines(text: str) -> List[Dict]:
+    out = []
+    for line in text.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                out.append(json.loads(line))
+            except ValueError:
+                pass
+    return out
+
+
+def run_json(cmd: List[str], run: Callable = subprocess.run, timeout: float = 600) -> (int, List[Dict]):
+    p = run(cmd, capture_output=True, text=True, timeout=timeout)
+    if p.stderr:
+        sys.stderr.write(p.stderr[-4000:])
+    return p.returncode, _json_lines(p.stdout)
+
+
+def collect_counters(shape: str, run: Callable = subprocess.run) -> List[Dict]:
+    """One profiled GEMM dispatch under rocprofv3 (counters only: no sys/runtime traces)."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return [{"event": "counters", "skipped": "rocprofv3 not available"}]
+    out = tempfile.mkdtemp(prefix="amdgo-pmc-")
+    try:
+        cmd = [prof, "--pmc", *PMC_COUNTERS, "--output-format", "csv", "-d", out, "--",
+               binary("amd-gemm-validate"), "--shapes", shape, "--iters", "1", "--warmup", "0",
+               "--devices", "0", "--check-rows", "1"]
+        p = run(cmd, capture_output=True, text=True, timeout=300)
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if p.returncode != 0 or not files:
+            return [{"event": "counters", "skipped": f"rocprofv3 exit {p.returncode}"}]
+        agg: Dict[str, float] = {}
+        with open(files[0]) as f:
+            for row in csv.DictReader(f):
+                if "gemm_bf16_256x256" not in row.get("Kernel_Name", ""):
+                    continue
+                agg[row["Counter_Name"]] = agg.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+        return [{"event": "counters", "kernel": "gemm_bf16_256x256", "shape": shape, **agg}]
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+def run_hip(shapes: List[str], counters: bool = False, iters: int = 20,
+            run: Callable = subprocess.run) -> List[Dict]:
+    results: List[Dict] = []
+    rc, r = run_json([binary("amd-hip-smoke")], run)
+    results += r or [{"event": "hip-smoke", "ok": False, "rc": rc}]
+    rc, r = run_json([binary("amd-gemm-validate"), "--shapes", ",".join(shapes), "--iters", str(iters)], run)
+    results += r
+    if rc != 0 and not any(x.get("event") == "gemm" for x in r):
+        results.append({"event": "gemm", "ok": False, "rc": rc})
+    if counters:
+        results += collect_counters(shapes[0], run)
+    return results
+
+
+def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run) -> List[Dict]:
+    rc, r = run_json([binary("amd-rccl-validate"), "--max-bytes", str(max_bytes), "--dtype", dtype,
+                      "--min-bytes", "1024"], run, timeout=1200)
+    if rc != 0 and not any(x.get("event") == "summary" for x in r):
+        r.append({"event": "summary", "ok": False, "rc": rc})
+    return r
+
+
+def emit(results: List[Dict], termination_log: Optional[str] = "/dev/termination-log") -> None:
+    text = "\n".join(json.dumps(r, separators=(",", ":")) for r in results)
+    print(text, flush=True)
+    if termination_log and os.path.isdir(os.path.dirname(termination_log)):
+        try:
+            # kubelet keeps at most 4 KiB: put the summary lines last-in-first-kept
+            keep = [json.dumps(r, separators=(",", ":")) for r in results
+                    if r.get("event") in ("aggregate", "summary", "hip-smoke", "counters")]
+            keep += [json.dumps(r, separators=(",", ":")) for r in results if r.get("event") == "gemm"]
+            msg = "\n".join(keep)
+            with open(termination_log, "w") as f:
+                f.write(msg[:4000])
+        except OSError:
+            pass
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="amd-validator-workload")
+    sub = ap.add_subparsers(dest="what", required=True)
+    h = sub.add_parser("hip")
+    h.add_argument("--gemm-shapes", default=os.environ.get("GEMM_SHAPES", "8192"))
+    h.add_argument("--iters", type=int, default=20)
+    h.add_argument("--counters", action="store_true")
+    r = sub.add_parser("rccl")
+    r.add_argument("--max-bytes", type=int, default=int(os.environ.get("RCCL_MAX_BYTES", 1 << 30)))
+    r.add_argument("--dtype", default="float")
+    a = ap.parse_args(argv)
+    if a.what == "hip":
+        results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters)
+        ok = all(x.get("ok", True) for x in results if x.get("event") in ("gemm", "hip-smoke"))
+    else:
+        results = run_rccl(a.max_bytes, a.dtype)
+        ok = all(x.get("ok", False) for x in results if x.get("event") == "summary")
+    emit(results)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,69 @@
+"""The validator's native workload binaries on a real MI355X."""
+
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpu_operator_amd", "_native", "bin")
+
+
+def run(*args, timeout=600):
+    p = subprocess.run([os.path.join(BIN, args[0]), *args[1:]], capture_output=True, text=True, timeout=timeout)
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_hip_smoke_binary():
+    rc, lines, err = run("amd-hip-smoke")
+    assert rc == 0, err
+    assert lines[-1]["ok"] and lines[-1]["devices"] >= 1
+
+
+def test_gemm_validate_binary_checks_and_reports_tflops():
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "4096,8192", "--iters", "10")
+    assert rc == 0, err
+    start = lines[0]
+    assert start["gcn_arch"].startswith("gfx950") and start["cus"] == 256
+    gemms = [x for x in lines if x["event"] == "gemm"]
+    assert gemms and all(g["ok"] for g in gemms)
+    agg = [x for x in lines if x["event"] == "aggregate" and x["m"] == 8192][0]
+    assert agg["per_gpu_tflops"] > 900           # MI355X bf16 dense, random operands
+
+
+def test_rccl_validate_binary():
+    rc, lines, err = run("amd-rccl-validate", "--max-bytes", str(1 << 26), "--iters", "5", "--warmup", "2")
+    assert rc == 0, err
+    summ = lines[-1]
+    assert summ["event"] == "summary" and summ["ok"]
+    assert all(x["ok"] for x in lines if x.get("event") == "allreduce")
+
+
+def test_node_probe_on_real_hardware():
+    rc, lines, err = run("amd-node-probe")
+    assert rc == 0, err
+    j = lines[0]
+    assert j["driver"]["live"] and j["driver"]["kfd"]
+    assert any(g["gfx"] == "gfx950" for g in j["gpus"])
+
+
+def test_validator_workload_hip_with_counters(tmp_path):
+    from gpu_operator_amd.validator import workload_main as W
+    results = W.run_hip(["4096"], counters=True, iters=5)
+    assert any(r.get("event") == "gemm" and r["ok"] for r in results)
+    ctr = [r for r in results if r.get("event") == "counters"]
+    assert ctr
+    if "skipped" not in ctr[0]:
+        assert ctr[0]["SQ_INSTS_VALU_MFMA_MOPS_BF16"] > 0
+
+
+def test_validator_hip_component_local_mode(tmp_path):
+    from gpu_operator_amd.validator import components as comp
+    from gpu_operator_amd.validator import status as S
+    ctx = comp.Context(status=S.StatusDir(str(tmp_path / "v")), env={"HIP_VALIDATION_MODE": "local",
+                                                                      "GEMM_SHAPES": "4096"})
+    info = comp.validate_hip(ctx)
+    assert info["gemm_tflops_per_gpu"] > 500 and ctx.status.exists(S.HIP_READY)
