@@ -1,0 +1,156 @@
+"""GPU telemetry exporter (``amd-metrics-exporter``): the DCGM-exporter role.
+
+Per-GPU gauges from the kernel's telemetry interfaces (hwmon power/temperatures, busy %,
+VRAM, DPM clocks, RAS ECC counters, PCIe bandwidth, xGMI links) read natively by libamdnode,
+published on ``:9400/metrics`` (reference default port, assets/state-dcgm-exporter). Which
+fields are exported comes from a CSV field list (``METRICS_EXPORTER_FIELDS``, overridable
+through ``spec.metricsExporter.config.name`` like the reference's DCGM counter CSV).
+
+With ``METRICS_EXPORTER_KUBERNETES=true`` every sample carries the pod/namespace/container
+that was allocated the GPU, resolved through the kubelet pod-resources API (device ids ->
+``amdgpu-<unique id>`` as advertised by the device plugin).
+"""
+
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import socket
+import sys
+import threading
+from typing import Dict, Iterable, List, Optional, Tuple
+
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
+from prometheus_client.registry import Collector, CollectorRegistry
+
+from .. import devices
+from . import kubeletapi as K
+
+log = logging.getLogger("amd-metrics-exporter")
+
+# field -> (telemetry key or callable, kind, help)
+FIELDS = {
+    "gpu_power_watts": ("power_w", "gauge", "Average package power (W)"),
+    "gpu_temperature_edge_celsius": ("temp_edge_c", "gauge", "Edge temperature (C)"),
+    "gpu_temperature_junction_celsius": ("temp_junction_c", "gauge", "Junction temperature (C)"),
+    "gpu_temperature_memory_celsius": ("temp_mem_c", "gauge", "HBM temperature (C)"),
+    "gpu_utilization_percent": ("gpu_busy_pct", "gauge", "GFX engine busy (%)"),
+    "gpu_memory_utilization_percent": ("mem_busy_pct", "gauge", "Memory controller busy (%)"),
+    "gpu_vram_used_bytes": ("vram_used", "gauge", "HBM in use (bytes)"),
+    "gpu_vram_total_bytes": ("vram_total", "gauge", "HBM capacity (bytes)"),
+    "gpu_sclk_mhz": ("sclk_mhz", "gauge", "Current shader clock (MHz)"),
+    "gpu_mclk_mhz": ("mclk_mhz", "gauge", "Current memory clock (MHz)"),
+    "gpu_ecc_correctable_total": ("ecc_correctable", "counter", "Correctable ECC errors"),
+    "gpu_ecc_uncorrectable_total": ("ecc_uncorrectable", "counter", "Uncorrectable ECC errors"),
+    "gpu_pcie_bandwidth_bytes": ("pcie_bw_bytes", "gauge", "PCIe bandwidth estimate (bytes/s)"),
+    "gpu_xgmi_link_count": ("xgmi_links", "gauge", "Active xGMI links"),
+}
+
+
+def load_fields(path: Optional[str]) -> List[str]:
+    if not path or not os.path.exists(path):
+        return list(FIELDS)
+    out = []
+    with open(path) as f:
+        for line in f:
+            line = line.split("#", 1)[0].strip()
+            if not line:
+                continue
+            name = line.split(",")[0].strip()
+            if name in FIELDS:
+                out.append(name)
+            else:
+                log.warning("unknown field %s ignored", name)
+    return out
+
+
+def pod_attribution(socket_path: str = K.POD_RESOURCES_SOCKET, timeout: float = 5.0) -> Dict[str, Tuple[str, str, str]]:
+    """device id -> (namespace, pod, container) from the kubelet pod-resources API."""
+    import grpc
+    out: Dict[str, Tuple[str, str, str]] = {}
+    if not os.path.exists(socket_path):
+        return out
+    with grpc.insecure_channel("unix://" + socket_path) as ch:
+        resp = K.pod_resources_stub(ch)(K.PR["ListPodResourcesRequest"](), timeout=timeout)
+    for pr in resp.pod_resources:
+        for c in pr.containers:
+            for d in c.devices:
+                if not d.resource_name.startswith("amd.com/"):
+                    continue
+                for did in d.device_ids:
+                    out[did.split("::")[0]] = (pr.namespace, pr.name, c.name)
+    return out
+
+
+class GPUCollector(Collector):
+    def __init__(self, fields: List[str], root: Optional[str] = None, hostname: str = "",
+                 kubernetes: bool = False, pod_socket: str = K.POD_RESOURCES_SOCKET):
+        self.fields = fields
+        self.root = root
+        self.hostname = hostname or socket.gethostname()
+        self.kubernetes = kubernetes
+        self.pod_socket = pod_socket
+
+    def collect(self) -> Iterable:
+        gpus = devices.enumerate_gpus(self.root)
+        tele = {t["index"]: t for t in devices.read_telemetry(self.root)}
+        pods = {}
+        if self.kubernetes:
+            try:
+                pods = pod_attribution(self.pod_socket)
+            except Exception as e:  # noqa: BLE001
+                log.warning("pod-resources query failed: %s", e)
+        labels = ["gpu", "gpu_uid", "bdf", "partition", "product", "hostname", "namespace", "pod", "container"]
+        fams = {}
+        for f in self.fields:
+            key, kind, help_ = FIELDS[f]
+            cls = CounterMetricFamily if kind == "counter" else GaugeMetricFamily
+            fams[f] = cls("amd_" + f.replace("_total", "") if kind == "counter" else "amd_" + f, help_,
+                          labels=labels)
+        for g in gpus:
+            t = tele.get(g["index"], {})
+            did = f"amdgpu-{g['unique_id']:016x}"
+            ns, pod, ctr = pods.get(did, ("", "", ""))
+            lv = [str(g["index"]), did, g["pci_bdf"], g["compute_partition"] or "SPX", g["product_name"],
+                  self.hostname, ns, pod, ctr]
+            for f in self.fields:
+                key = FIELDS[f][0]
+                v = t.get(key) if key in t else g.get(key)
+                if v is None or (isinstance(v, (int, float)) and v < 0):
+                    continue
+                fams[f].add_metric(lv, float(v))
+        yield from fams.values()
+
+
+def build_registry(fields: List[str], root: Optional[str] = None, kubernetes: bool = False,
+                   pod_socket: str = K.POD_RESOURCES_SOCKET, hostname: str = "") -> CollectorRegistry:
+    reg = CollectorRegistry()
+    reg.register(GPUCollector(fields, root, hostname=hostname, kubernetes=kubernetes, pod_socket=pod_socket))
+    return reg
+
+
+def main(argv=None) -> int:
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    ap = argparse.ArgumentParser(prog="amd-metrics-exporter")
+    ap.add_argument("--listen", default=os.environ.get("METRICS_EXPORTER_LISTEN", ":9400"))
+    ap.add_argument("--fields", default=os.environ.get("METRICS_EXPORTER_FIELDS"))
+    ap.add_argument("--kubernetes", default=os.environ.get("METRICS_EXPORTER_KUBERNETES", "false"))
+    a = ap.parse_args(argv)
+    from prometheus_client import generate_latest
+    from prometheus_client.exposition import CONTENT_TYPE_LATEST
+
+    from ..runtime.manager import _Server
+    reg = build_registry(load_fields(a.fields), kubernetes=a.kubernetes == "true",
+                         hostname=os.environ.get("NODE_NAME", ""))
+    host, _, port = a.listen.rpartition(":")
+    srv = _Server((host or "0.0.0.0", int(port)), {"/metrics": lambda: (200, CONTENT_TYPE_LATEST,
+                                                                        generate_latest(reg))})
+    srv.start()
+    log.info("serving GPU metrics on %s", a.listen)
+    threading.Event().wait()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,270 @@
+"""Node labeller, partition manager and metrics exporter against fake MI355X sysfs trees."""
+
+import os
+import threading
+import time
+
+import pytest
+import yaml
+
+from gpu_operator_amd import devices as D
+from gpu_operator_amd.devices import fakesys
+from gpu_operator_amd.k8s import objects as o
+from gpu_operator_amd.k8s.fake import FakeClient
+from gpu_operator_amd.operands import metrics_exporter as me
+from gpu_operator_amd.operands import node_labeller as nl
+from gpu_operator_amd.operands import partition_manager as pm
+
+from k8s_helpers import gpu_node
+
+
+@pytest.fixture
+def spx(tmp_path):
+    return str(fakesys.make_node(tmp_path / "root"))
+
+
+# -- node labeller ---------------------------------------------------------------------------------
+
+def test_labels_spx(spx):
+    L = nl.compute_labels(spx)
+    assert L["amd.com/gpu.product"] == "AMD-Instinct-MI355X"
+    assert L["amd.com/gpu.family"] == "cdna4" and L["amd.com/gpu.gfx"] == "gfx950"
+    assert L["amd.com/gpu.device-id"] == "75a3"
+    assert L["amd.com/gpu.count"] == "8" and L["amd.com/gpu.partition.count"] == "8"
+    assert L["amd.com/gpu.cu-count"] == "256" and L["amd.com/gpu.lds-kib"] == "160"
+    assert L["amd.com/gpu.vram"] == "288G"
+    assert L["amd.com/gpu.compute-partition"] == "SPX" and L["amd.com/gpu.memory-partition"] == "NPS1"
+    assert L["amd.com/gpu.xgmi.links"] == "7" and L["amd.com/gpu.xgmi.fully-connected"] == "true"
+    assert L["amd.com/gpu.numa-nodes"] == "2" and L["amd.com/gpu.driver-version"] == "6.12.12"
+    assert L["amd.com/gpu.partition.capable"] == "true"
+    for k, v in L.items():
+        assert len(v) <= 63 and nl.OWNED.match(k), k
+
+
+def test_labels_cpx(tmp_path):
+    root = str(fakesys.make_node(tmp_path / "r", compute="CPX", memory="NPS2"))
+    L = nl.compute_labels(root)
+    assert L["amd.com/gpu.count"] == "8" and L["amd.com/gpu.partition.count"] == "64"
+    assert L["amd.com/gpu.cu-count"] == "256"          # per physical GPU, not per partition
+    assert L["amd.com/gpu.compute-partition"] == "CPX" and L["amd.com/gpu.memory-partition"] == "NPS2"
+    assert L["amd.com/gpu.xgmi.links"] == "7"
+
+
+def test_labels_no_gpu(tmp_path):
+    os.makedirs(tmp_path / "empty")
+    assert nl.compute_labels(str(tmp_path / "empty")) == {}
+
+
+def test_label_patch_removes_stale_owned_only():
+    cur = {"amd.com/gpu.product": "x", "amd.com/gpu.vram": "1G", "amd.com/gpu.present": "true", "foo": "bar"}
+    want = {"amd.com/gpu.product": "x"}
+    assert nl.label_patch(cur, want) == {"amd.com/gpu.vram": None}
+
+
+def test_apply_node_and_nfd(spx, tmp_path):
+    c = FakeClient([gpu_node("n1", extra_labels={"amd.com/gpu.vram": "1G"})])
+    want = nl.compute_labels(spx)
+    patch = nl.apply_node(c, "n1", want)
+    assert patch["amd.com/gpu.vram"] == "288G"
+    labels = o.get_labels(c.get("v1", "Node", "n1"))
+    assert all(labels[k] == v for k, v in want.items())
+    assert nl.apply_node(c, "n1", want) == {}                    # idempotent
+    f = tmp_path / "features.d" / "amd-gpu"
+    nl.write_nfd(str(f), want)
+    lines = f.read_text().splitlines()
+    assert "amd.com/gpu.gfx=gfx950" in lines and len(lines) == len(want)
+
+
+def test_labeller_main_oneshot_nfd(spx, tmp_path, monkeypatch):
+    monkeypatch.setenv("AMD_SYSFS_ROOT", spx)
+    f = tmp_path / "out" / "amd-gpu"
+    assert nl.main(["--oneshot", "--output", "nfd", "--nfd-file", str(f)]) == 0
+    assert "amd.com/gpu.family=cdna4" in f.read_text()
+
+
+def test_wait_for_change_wakes_on_barrier(tmp_path):
+    d = tmp_path / "validations"
+    d.mkdir()
+    path = d / "partition-applied"
+    stop = threading.Event()
+    t0 = time.monotonic()
+    threading.Timer(0.3, lambda: path.write_text("{}")).start()
+    assert nl.wait_for_change(str(path), 10.0, stop)
+    assert time.monotonic() - t0 < 5.0
+    assert not nl.wait_for_change(str(path), 1.0, stop)           # exists, unchanged -> period expires
+
+
+def test_parse_duration():
+    assert nl.parse_duration("60s") == 60 and nl.parse_duration("2m") == 120
+    assert nl.parse_duration("500ms") == 0.5 and nl.parse_duration("5") == 5
+    with pytest.raises(ValueError):
+        nl.parse_duration("soon")
+
+
+# -- partition manager -----------------------------------------------------------------------------
+
+CONFIG = {"version": "v1", "partition-configs": {
+    "all-spx": [{"devices": "all", "compute": "SPX", "memory": "NPS1"}],
+    "all-cpx": [{"devices": "all", "compute": "CPX", "memory": "NPS2"}],
+    "bad-mode": [{"devices": "all", "compute": "XPX"}],
+    "bad-dev": [{"devices": [9], "compute": "CPX"}],
+    "unavailable": [{"devices": "all", "compute": "CPX", "memory": "NPS4"}],
+}}
+
+
+@pytest.fixture
+def cfg(tmp_path):
+    p = tmp_path / "config.yaml"
+    p.write_text(yaml.safe_dump(CONFIG))
+    return str(p)
+
+
+def _cluster(config_label=None):
+    extra = {"amd.com/gpu.deploy.device-plugin": "true", "amd.com/gpu.deploy.metrics-exporter": "true",
+             "amd.com/gpu.deploy.rdc": "false"}
+    if config_label:
+        extra[pm.CONFIG_LABEL] = config_label
+    return FakeClient([gpu_node("n1", extra_labels=extra)])
+
+
+def _mgr(c, spx, cfg, tmp_path, **kw):
+    return pm.PartitionManager(c, "n1", cfg, root=spx, barrier_dir=str(tmp_path / "barriers"),
+                               enum_timeout=3.0, pods_timeout=3.0, **kw)
+
+
+def test_desired_layout():
+    assert pm.desired_layout(CONFIG["partition-configs"]["all-cpx"], 2) == {0: ("CPX", "NPS2"), 1: ("CPX", "NPS2")}
+    with pytest.raises(pm.PartitionError):
+        pm.desired_layout(CONFIG["partition-configs"]["bad-mode"], 8)
+    with pytest.raises(pm.PartitionError):
+        pm.desired_layout(CONFIG["partition-configs"]["bad-dev"], 8)
+
+
+def test_partition_in_sync_marks_success(spx, cfg, tmp_path):
+    c = _cluster("all-spx")
+    assert _mgr(c, spx, cfg, tmp_path).reconcile() == "in-sync"
+    n = c.get("v1", "Node", "n1")
+    assert o.get_labels(n)[pm.STATE_LABEL] == "success"
+    assert o.get_annotations(n)[pm.APPLIED_ANNOTATION] == "all-spx"
+    assert (tmp_path / "barriers" / "partition-applied").exists()
+
+
+def test_partition_no_config(spx, cfg, tmp_path):
+    assert _mgr(_cluster(), spx, cfg, tmp_path).reconcile() == "no-config"
+
+
+def test_partition_apply_cpx(spx, cfg, tmp_path):
+    c = _cluster("all-cpx")
+    seen = []
+
+    def on_node(ev):
+        seen.append(dict(o.get_labels(ev.obj)))
+    c.watch("v1", "Node", on_node)
+    m = _mgr(c, spx, cfg, tmp_path, reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS2"))
+    assert m.reconcile() == "applied"
+    gpus = D.enumerate_gpus(spx)
+    assert len(gpus) == 64 and {g["compute_partition"] for g in gpus} == {"CPX"}
+    assert {g["memory_partition"] for g in gpus} == {"NPS2"}
+    labels = o.get_labels(c.get("v1", "Node", "n1"))
+    assert labels[pm.STATE_LABEL] == "success"
+    # clients were paused during the change and restored afterwards; disabled ones untouched
+    assert any(s.get("amd.com/gpu.deploy.device-plugin") == pm.PAUSED for s in seen)
+    assert any(s.get(pm.STATE_LABEL) == "pending" for s in seen)
+    assert labels["amd.com/gpu.deploy.device-plugin"] == "true"
+    assert labels["amd.com/gpu.deploy.metrics-exporter"] == "true"
+    assert labels["amd.com/gpu.deploy.rdc"] == "false"
+    # second pass is a no-op
+    assert m.reconcile() == "in-sync"
+
+
+def test_partition_waits_for_client_pods(spx, cfg, tmp_path):
+    c = _cluster("all-cpx")
+    c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "dp-1", "namespace": "gpu",
+                                                               "labels": {"app": "amd-device-plugin-daemonset"}},
+              "spec": {"nodeName": "n1"}})
+    threading.Timer(0.5, lambda: c.delete("v1", "Pod", "dp-1", "gpu")).start()
+    m = _mgr(c, spx, cfg, tmp_path, reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS2"))
+    assert m.reconcile() == "applied"
+
+
+def test_partition_failures(spx, cfg, tmp_path):
+    for name in ("missing-config", "bad-mode", "unavailable"):
+        c = _cluster(name)
+        assert _mgr(c, spx, cfg, tmp_path).reconcile() == "failed", name
+        assert o.get_labels(c.get("v1", "Node", "n1"))[pm.STATE_LABEL] == "failed"
+        assert any(e["reason"] == "PartitionFailed" for e in c.events)
+        # deploy labels restored even on failure
+        assert o.get_labels(c.get("v1", "Node", "n1"))["amd.com/gpu.deploy.device-plugin"] == "true"
+
+
+def test_partition_reenumeration_timeout(spx, cfg, tmp_path):
+    c = _cluster("all-cpx")
+    m = _mgr(c, spx, cfg, tmp_path)
+    m.enum_timeout = 0.5
+    assert m.reconcile() == "failed"                              # driver never re-enumerated
+    ev = [e for e in c.events if e["reason"] == "PartitionFailed"]
+    assert "re-enumeration" in ev[0]["message"]
+
+
+def test_partition_host_services(spx, cfg, tmp_path):
+    calls = []
+    c = _cluster("all-cpx")
+    m = _mgr(c, spx, cfg, tmp_path, host_services=["amd-smi-exporter"],
+             run=lambda argv, **kw: calls.append(argv[-2:]),
+             reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS2"))
+    assert m.reconcile() == "applied"
+    assert calls == [["stop", "amd-smi-exporter"], ["start", "amd-smi-exporter"]]
+
+
+# -- metrics exporter ------------------------------------------------------------------------------
+
+def test_metrics_registry(spx):
+    from prometheus_client import generate_latest
+    reg = me.build_registry(me.load_fields(None), root=spx, hostname="n1")
+    text = generate_latest(reg).decode()
+    assert 'amd_gpu_power_watts{bdf="0000:05:00.0"' in text
+    assert "amd_gpu_temperature_junction_celsius" in text
+    assert "amd_gpu_ecc_correctable_total" in text
+    samples = {(s.name, s.labels["gpu"]): s.value for m in reg.collect() for s in m.samples}
+    assert samples[("amd_gpu_power_watts", "0")] == pytest.approx(750.0)
+    assert samples[("amd_gpu_temperature_junction_celsius", "3")] == pytest.approx(61.0)
+    assert samples[("amd_gpu_utilization_percent", "7")] == 37
+    assert samples[("amd_gpu_ecc_correctable_total", "0")] == 3
+    assert samples[("amd_gpu_vram_total_bytes", "0")] == 288 * (1 << 30)
+    assert samples[("amd_gpu_xgmi_link_count", "0")] == 7
+
+
+def test_metrics_field_file(spx, tmp_path):
+    f = tmp_path / "fields.csv"
+    f.write_text("# comment\ngpu_power_watts, gauge\nnot_a_field\n")
+    assert me.load_fields(str(f)) == ["gpu_power_watts"]
+    reg = me.build_registry(me.load_fields(str(f)), root=spx)
+    assert [m.name for m in reg.collect()] == ["amd_gpu_power_watts"]
+
+
+def test_metrics_pod_attribution(spx, tmp_path):
+    import grpc
+    from concurrent import futures
+    from gpu_operator_amd.operands import kubeletapi as K
+    gpus = D.enumerate_gpus(spx)
+    did = f"amdgpu-{gpus[2]['unique_id']:016x}"
+
+    def list_fn(req, ctx):
+        r = K.PR["ListPodResourcesResponse"]()
+        p = r.pod_resources.add(name="train-0", namespace="ml")
+        cnt = p.containers.add(name="worker")
+        cnt.devices.add(resource_name="amd.com/gpu", device_ids=[did])
+        cnt.devices.add(resource_name="example.com/nic", device_ids=["x"])
+        return r
+    sock = str(tmp_path / "pr.sock")
+    srv = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+    srv.add_generic_rpc_handlers((K.pod_resources_handler(list_fn),))
+    srv.add_insecure_port("unix://" + sock)
+    srv.start()
+    try:
+        assert me.pod_attribution(sock) == {did: ("ml", "train-0", "worker")}
+        reg = me.build_registry(["gpu_power_watts"], root=spx, kubernetes=True, pod_socket=sock)
+        s = {x.labels["gpu"]: x.labels for m in reg.collect() for x in m.samples}
+        assert s["2"]["pod"] == "train-0" and s["2"]["namespace"] == "ml" and s["0"]["pod"] == ""
+    finally:
+        srv.stop(0)
