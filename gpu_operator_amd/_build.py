@@ -101,6 +101,10 @@ TARGETS: List[Target] = [
     Target("bin/amd-hip-smoke", ["hip/hip_smoke_main.cpp", "hip/smoke.hip"], "hip-exe", flags=["-x", "hip"]),
     Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp"], "hip-exe", flags=["-x", "hip"],
            libs=["-lrccl"]),
+    # OCI runtime shim injecting /dev/kfd + render nodes (legacy) or CDI edits into bundles.
+    # Fully static: it runs on the host (via containerd/CRI-O/docker), whatever its glibc.
+    Target("bin/amd-container-runtime", ["toolkit/amd_container_runtime.cpp", "node/amdnode.cpp"], "cxx-exe",
+           flags=["-static"], headers=["include/amdnode.h", "include/minijson.h"]),
     Target("bin/amd-node-probe", ["node/node_probe.cpp", "node/amdnode.cpp"], "cxx-exe",
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
 ]
