@@ -134,3 +134,65 @@ def set_compute_partition(root, compute: str, memory: Optional[str] = None) -> N
         "current_memory_partition").read_text().strip()
     shutil.rmtree(root / "sys/class/kfd", ignore_errors=True)
     make_node(root, n_gpus=n, compute=compute, memory=mem)
+
+
+MI355X_VF_DEVICE_ID = 0x75B3
+
+
+def create_vfs(root, pf_bdf: str, n: int, driver: str = "", device_id: int = MI355X_VF_DEVICE_ID) -> list:
+    """Instantiate ``n`` SR-IOV virtual functions of ``pf_bdf`` as the PF driver (GIM) does
+    after a write to ``sriov_numvfs``: VF devices with ``physfn`` links, ``virtfn<i>`` links on
+    the PF, own IOMMU groups; optionally pre-bound to ``driver``. Returns the VF BDFs."""
+    root = Path(root)
+    pci = root / "sys/bus/pci/devices"
+    pf = pci / pf_bdf
+    dom, bus, rest = pf_bdf.split(":")
+    out = []
+    for i in range(n):
+        bdf = f"{dom}:{int(bus, 16) + 1:02x}:{i // 8:02x}.{i % 8}"
+        vf = pci / bdf
+        _w(vf / "vendor", "0x1002")
+        _w(vf / "device", f"0x{device_id:04x}")
+        _w(vf / "class", "0x120000")
+        if not (vf / "physfn").is_symlink():
+            os.symlink(os.path.relpath(pf, vf), vf / "physfn")
+        link = pf / f"virtfn{i}"
+        if not link.is_symlink():
+            os.symlink(os.path.relpath(vf, pf), link)
+        grp = root / "sys/kernel/iommu_groups" / str(100 + int(bus, 16) * 8 + i)
+        grp.mkdir(parents=True, exist_ok=True)
+        if not (vf / "iommu_group").is_symlink():
+            os.symlink(os.path.relpath(grp, vf), vf / "iommu_group")
+        if driver:
+            drv_dir = root / "sys/bus/pci/drivers" / driver
+            drv_dir.mkdir(parents=True, exist_ok=True)
+            if (vf / "driver").is_symlink():
+                (vf / "driver").unlink()
+            os.symlink(os.path.relpath(drv_dir, vf), vf / "driver")
+        out.append(bdf)
+    _w(pf / "sriov_numvfs", n)
+    return out
+
+
+def remove_vfs(root, pf_bdf: str) -> None:
+    import shutil
+    root = Path(root)
+    pci = root / "sys/bus/pci/devices"
+    pf = pci / pf_bdf
+    for link in sorted(pf.glob("virtfn*")):
+        vf = (pf / os.readlink(link)).resolve()
+        shutil.rmtree(vf, ignore_errors=True)
+        link.unlink()
+    _w(pf / "sriov_numvfs", 0)
+
+
+def bind_driver(root, bdf: str, driver: str) -> None:
+    """Re-point ``bdf``'s driver link (what a write to drivers/<drv>/bind does)."""
+    root = Path(root)
+    dev = root / "sys/bus/pci/devices" / bdf
+    drv_dir = root / "sys/bus/pci/drivers" / driver
+    drv_dir.mkdir(parents=True, exist_ok=True)
+    if (dev / "driver").is_symlink():
+        (dev / "driver").unlink()
+    if driver:
+        os.symlink(os.path.relpath(drv_dir, dev), dev / "driver")

@@ -244,3 +244,33 @@ def revert(runtime: str, config: str, state_file: str = "") -> None:
         revert_crio(config)
     else:
         raise ValueError(f"unsupported runtime {runtime!r}")
+
+
+def set_containerd_runtimes(config: str, runtimes: Dict[str, Dict[str, Any]]) -> bool:
+    """Upsert arbitrary containerd runtime handlers (used by the kata manager). True if changed."""
+    doc: Dict[str, Any] = {}
+    if os.path.exists(config):
+        with open(config, "rb") as f:
+            doc = tomli.load(f)
+    doc.setdefault("version", 2)
+    rts = _dig(doc, _cri_path(doc)).setdefault("containerd", {}).setdefault("runtimes", {})
+    changed = False
+    for name, h in runtimes.items():
+        if rts.get(name) != h:
+            rts[name] = h
+            changed = True
+    if changed:
+        _write(config, tomlw.dumps(doc))
+    return changed
+
+
+def remove_containerd_runtimes(config: str, names: List[str]) -> bool:
+    if not os.path.exists(config):
+        return False
+    with open(config, "rb") as f:
+        doc = tomli.load(f)
+    rts = _dig(doc, _cri_path(doc)).setdefault("containerd", {}).setdefault("runtimes", {})
+    gone = [n for n in names if rts.pop(n, None) is not None]
+    if gone:
+        _write(config, tomlw.dumps(doc))
+    return bool(gone)
