@@ -20,6 +20,9 @@
 //   * XCD-aware, bijective blockIdx remap (8 XCDs, private 4 MiB L2 each) followed by a
 //     grouped (GROUP_M) raster so co-resident tiles on one XCD share A/B panels in L2.
 //
+// Variants (AMDGO_GEMM_VARIANT / amdgo_gemm_set_variant): 1 = double-buffered baseline, 2 = fragment
+// pipelined, 3 = ping-pong (two wave groups one barrier apart, half-tile LDS ring), 4 = v3 with
+// buffer_load...lds staging (default; K % 128 == 0, else v2). Measured: profiles/r1_gemm_v4/.
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
 
 #include <hip/hip_runtime.h>
@@ -286,6 +289,242 @@ gemm_bf16_256x256_v2(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   }
 }
 
+// v3: ping-pong schedule. Same 256x256x64 tile, 8 waves (2 groups of 4: one wave of each
+// group per SIMD), but the LDS image is cut into four 16 KiB half-tiles per K-tile that line
+// up with the waves' register quadrants:
+//     A_lo = A rows {0-63, 128-191}   A_hi = A rows {64-127, 192-255}
+//     B_lo = Bt rows {64w+0..31}      B_hi = Bt rows {64w+32..63}      (w = 0..3)
+// A K-tile is 4 phases, one output quadrant (4x2 fragments x K=64 = 16 MFMAs) each:
+//     P1 (lo,lo) reads A_lo+B_lo, P2 (lo,hi) reads B_hi, P3 (hi,hi) reads A_hi, P4 (hi,lo)
+//     reads nothing (B_lo kept in registers) — 24 ds_read_b128 per K-tile, the minimum.
+// Each phase: [ds_reads ; one half-tile of LDS-DMA prefetch] s_barrier [MFMA x16] s_barrier.
+// Group 1 runs one barrier behind group 0, so on every SIMD one wave issues MFMAs while the
+// other issues its reads and DMA: the matrix pipe never waits on LDS latency.
+// Two K-tile buffers (even/odd) = 128 KiB; a half-tile is restaged >= 2 phases after its last
+// read, and vmcnt(4) (two half-tiles in flight, never 0 in the steady loop) at P4/P8 retires
+// the buffer the next four phases read. See docs/validator-gemm.md for the full table.
+constexpr int HALF_BYTES = 128 * ROW_BYTES;   // 16 KiB
+constexpr int HB_A_LO = 0, HB_A_HI = HALF_BYTES, HB_B_LO = 2 * HALF_BYTES, HB_B_HI = 3 * HALF_BYTES;
+
+// LDS row r (0..127) of a half-tile -> row of the 256-row global panel.
+__device__ __forceinline__ int a_half_row(int r, int hi) { return (r & 63) + ((r >> 6) << 7) + (hi << 6); }
+__device__ __forceinline__ int b_half_row(int r, int hi) { return (r & 31) + ((r >> 5) << 6) + (hi << 5); }
+
+template <bool IS_A>
+__device__ __forceinline__ void stage_half(const __bf16* __restrict__ g, int ld, int k0, char* lds_half,
+                                           int hi, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rblk = i * 8 + wid;            // 8-row block 0..15
+    const int r = rblk * 8 + (lane >> 3);    // LDS row 0..127
+    const int pc = lane & 7;
+    const int c = pc ^ ((r >> 1) & 7);
+    const int gr = IS_A ? a_half_row(r, hi) : b_half_row(r, hi);
+    const __bf16* src = g + (size_t)gr * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds_half + rblk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// BUF=true (v4): the half-tile DMA is `buffer_load_dwordx4 ... lds` with a per-lane voffset fixed
+// for the whole kernel and the K offset in an SGPR — no per-load 64-bit VALU address math.
+template <bool BUF>
+__global__ void __launch_bounds__(NTHREADS)
+gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                     __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2;   // group: 0 or 1 (also the 128-row half of the output tile)
+  const int wc = wid & 3;
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
+  // per-lane byte offsets inside the panel: [A/B][hi][i]
+  uint32_t voff[2][2][2];
+#pragma unroll
+  for (int ab = 0; ab < 2; ++ab)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = (i * 8 + wid) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int gr = ab == 0 ? a_half_row(r, hi) : b_half_row(r, hi);
+        voff[ab][hi][i] = (uint32_t)gr * (uint32_t)K * 2u + (uint32_t)c * 16u;
+      }
+  auto stage = [&](int ab, int hi, int k0, char* lds_half) {
+    if constexpr (BUF) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ab == 0 ? rA : rB, (lds_void*)(lds_half + (i * 8 + wid) * 1024), 16,
+                                                 voff[ab][hi][i], k0 * 2, 0, 0);
+    } else {
+      if (ab == 0) stage_half<true>(gA, K, k0, lds_half, hi, wid, lane);
+      else stage_half<false>(gB, K, k0, lds_half, hi, wid, lane);
+    }
+  };
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 64 * ROW_BYTES;   // this wave's 64 rows inside A_lo / A_hi
+  const int b_off = wc * 32 * ROW_BYTES;   // this wave's 32 rows inside B_lo / B_hi
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2];        // A quadrant: 4 fragments x 2 k-steps
+  bf16x8 bq[2][2][2];     // B: [lo/hi][2 fragments][2 k-steps]
+
+  auto read_a = [&](const char* half) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        af[m][kk] = *reinterpret_cast<const bf16x8*>(half + a_off + m * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  auto read_b = [&](const char* half, int q) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        bq[q][n][kk] = *reinterpret_cast<const bf16x8*>(half + b_off + n * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  auto mfma_q = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[qm * 4 + m][qn * 2 + n] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[qn][n][kk], af[m][kk], acc[qm * 4 + m][qn * 2 + n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int ktiles = K / BK;            // even (host guarantees K % 128 == 0)
+  char* const E = smem;
+  char* const O = smem + BUF_BYTES;
+
+  // prologue: even buffer <- tile 0 (complete), odd A_lo/B_lo <- tile 1 (in flight)
+  stage(0, 0, 0, E + HB_A_LO);
+  stage(0, 1, 0, E + HB_A_HI);
+  stage(1, 0, 0, E + HB_B_LO);
+  stage(1, 1, 0, E + HB_B_HI);
+  stage(0, 0, BK, O + HB_A_LO);
+  stage(1, 0, BK, O + HB_B_LO);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  bar();
+  if (wr == 1) bar();   // stagger: group 1 runs one barrier behind group 0
+
+  for (int t = 0; t < ktiles; t += 2) {
+    const bool more = t + 2 < ktiles;
+    const int k1 = (t + 1) * BK, k2 = (t + 2) * BK, k3 = (t + 3) * BK;
+    // ---- even buffer (tile t) ----
+    // P1
+    read_b(E + HB_B_LO, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(E + HB_A_LO);
+    stage(1, 1, k1, O + HB_B_HI);
+    bar();
+    mfma_q(0, 0);
+    bar();
+    // P2
+    read_b(E + HB_B_HI, 1);
+    stage(0, 1, k1, O + HB_A_HI);
+    bar();
+    mfma_q(0, 1);
+    bar();
+    // P3
+    read_a(E + HB_A_HI);
+    if (more) stage(0, 0, k2, E + HB_A_LO);
+    bar();
+    mfma_q(1, 1);
+    bar();
+    // P4
+    if (more) {
+      stage(1, 0, k2, E + HB_B_LO);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    mfma_q(1, 0);
+    bar();
+    // ---- odd buffer (tile t+1) ----
+    // P5
+    read_b(O + HB_B_LO, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(O + HB_A_LO);
+    if (more) stage(1, 1, k2, E + HB_B_HI);
+    bar();
+    mfma_q(0, 0);
+    bar();
+    // P6
+    read_b(O + HB_B_HI, 1);
+    if (more) stage(0, 1, k2, E + HB_A_HI);
+    bar();
+    mfma_q(0, 1);
+    bar();
+    // P7
+    read_a(O + HB_A_HI);
+    if (more) stage(0, 0, k3, O + HB_A_LO);
+    bar();
+    mfma_q(1, 1);
+    bar();
+    // P8
+    if (more) {
+      stage(1, 0, k3, O + HB_B_LO);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    bar();
+    mfma_q(1, 0);
+    bar();
+  }
+  if (wr == 0) bar();   // re-align the groups' barrier counts
+
+  const int row_base = tm * BM + wr * 128 + (lane & 15);
+  const int col_base = tn * BN + wc * 64 + 4 * (lane >> 4);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    __bf16* crow = C + (size_t)(row_base + m * 16) * N + col_base;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 v;
+      v[0] = (__bf16)acc[m][n][0];
+      v[1] = (__bf16)acc[m][n][1];
+      v[2] = (__bf16)acc[m][n][2];
+      v[3] = (__bf16)acc[m][n][3];
+      *reinterpret_cast<bf16x4*>(crow + n * 16) = v;
+    }
+  }
+}
+
 // Generic bounds-checked MFMA kernel (64x64 tile, 4 waves of 32x32), register-staged.
 // Used for shapes that are not multiples of 256/256/64 and as a second, independent
 // implementation for cross-checking the fast path.
@@ -381,7 +620,7 @@ static int g_variant = -1;
 static int variant() {
   if (g_variant < 0) {
     const char* e = getenv("AMDGO_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 2;
+    g_variant = e ? atoi(e) : 4;
   }
   return g_variant;
 }
@@ -397,8 +636,15 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   hipStream_t s = (hipStream_t)stream;
   if (M % BM == 0 && N % BN == 0 && K % BK == 0) {
     const int nwg = (M / BM) * (N / BN);
-    if (variant() == 1)
+    const int v = variant();
+    if (v == 1)
       hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v == 3 && K % (2 * BK) == 0)
+      hipLaunchKernelGGL(gemm_bf16_256x256_pp<false>, dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v == 4 && K % (2 * BK) == 0)
+      hipLaunchKernelGGL(gemm_bf16_256x256_pp<true>, dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else
       hipLaunchKernelGGL(gemm_bf16_256x256_v2, dim3(nwg), dim3(NTHREADS), 0, s,

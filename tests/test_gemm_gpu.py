@@ -9,9 +9,18 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
+@pytest.fixture(params=[1, 2, 3, 4])
+def variant(request):
+    from gpu_operator_amd.ops import gemm as G
+    old = G.get_variant()
+    G.set_variant(request.param)
+    yield request.param
+    G.set_variant(old)
+
+
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 256), (1024, 1024, 1024),
-                                   (2048, 512, 4096), (768, 2304, 640)])
-def test_fast_path_matches_fp32_reference(cuda_device, m, n, k):
+                                   (2048, 512, 4096), (768, 2304, 640), (256, 512, 128)])
+def test_fast_path_matches_fp32_reference(cuda_device, variant, m, n, k):
     import torch
     from gpu_operator_amd.ops import gemm as G
 
@@ -50,7 +59,7 @@ def test_identity_with_asymmetric_b_catches_transposes(cuda_device):
         assert torch.equal(c, b), f"generic={generic}"
 
 
-def test_fast_and_generic_agree_on_8k_slice(cuda_device):
+def test_fast_and_generic_agree_on_8k_slice(cuda_device, variant):
     import torch
     from gpu_operator_amd.ops import gemm as G
 
