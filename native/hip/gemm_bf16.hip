@@ -22,7 +22,8 @@
 //
 // Variants (AMDGO_GEMM_VARIANT / amdgo_gemm_set_variant): 1 = double-buffered baseline, 2 = fragment
 // pipelined, 3 = ping-pong (two wave groups one barrier apart, half-tile LDS ring), 4 = v3 with
-// buffer_load...lds staging (default; K % 128 == 0, else v2). Measured: profiles/r1_gemm_v4/.
+// buffer_load...lds staging, 5 = v4 with an LDS-staged, fully coalesced epilogue (default;
+// K % 128 == 0, else v2). Measured: profiles/r1_gemm_v4/.
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
 
 #include <hip/hip_runtime.h>
@@ -333,7 +334,11 @@ __device__ __forceinline__ void bar() {
 
 // BUF=true (v4): the half-tile DMA is `buffer_load_dwordx4 ... lds` with a per-lane voffset fixed
 // for the whole kernel and the K offset in an SGPR — no per-load 64-bit VALU address math.
-template <bool BUF>
+// EPI_LDS (v5): the epilogue goes through LDS (the K loop's buffers are free by then): each wave
+// writes its bf16 128x64 sub-tile with ds_write_b64 (8-byte granules XOR-swizzled by row so the
+// 16 rows a lane group writes hit distinct banks), then every thread stores whole 16-byte
+// chunks, 32 lanes per 512-byte output row — fully coalesced global_store_dwordx4.
+template <bool BUF, bool EPI_LDS>
 __global__ void __launch_bounds__(NTHREADS)
 gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
@@ -507,6 +512,40 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   }
   if (wr == 0) bar();   // re-align the groups' barrier counts
 
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  if constexpr (EPI_LDS) {
+    bar();                // every wave is past its last ds_read of the K loop
+    constexpr int CROW = BN * 2;                     // 512-byte LDS row
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int r = wr * 128 + m * 16 + (lane & 15);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int g = (wc * 64 + n * 16 + 4 * (lane >> 4)) >> 2;   // 8-byte granule 0..63
+        bf16x4 v;
+        v[0] = (__bf16)acc[m][n][0];
+        v[1] = (__bf16)acc[m][n][1];
+        v[2] = (__bf16)acc[m][n][2];
+        v[3] = (__bf16)acc[m][n][3];
+        *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
+      }
+    }
+    bar();
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < (BM * BN * 2) / (NTHREADS * 16); ++i) {      // 16 chunks per thread
+      const int r = i * (NTHREADS / 32) + (tid >> 5);
+      const int ch = tid & 31;                                        // 16-byte chunk in the row
+      const int s = r & 15;
+      const int pg = (2 * ch) ^ s;                                    // physical granule of the even half
+      const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
+      uint4 v = raw;
+      if (s & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+      *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+    }
+    return;
+  }
+
   const int row_base = tm * BM + wr * 128 + (lane & 15);
   const int col_base = tn * BN + wc * 64 + 4 * (lane >> 4);
 #pragma unroll
@@ -514,7 +553,6 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     __bf16* crow = C + (size_t)(row_base + m * 16) * N + col_base;
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
       bf16x4 v;
       v[0] = (__bf16)acc[m][n][0];
       v[1] = (__bf16)acc[m][n][1];
@@ -620,7 +658,7 @@ static int g_variant = -1;
 static int variant() {
   if (g_variant < 0) {
     const char* e = getenv("AMDGO_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 4;
+    g_variant = e ? atoi(e) : 5;
   }
   return g_variant;
 }
@@ -641,10 +679,13 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
       hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else if (v == 3 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL(gemm_bf16_256x256_pp<false>, dim3(nwg), dim3(NTHREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_pp<false, false>), dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else if (v == 4 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL(gemm_bf16_256x256_pp<true>, dim3(nwg), dim3(NTHREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, false>), dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v == 5 && K % (2 * BK) == 0)
+      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true>), dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else
       hipLaunchKernelGGL(gemm_bf16_256x256_v2, dim3(nwg), dim3(NTHREADS), 0, s,
