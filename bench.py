@@ -110,6 +110,19 @@ def main(argv=None) -> int:
         extras.update({"allreduce_bytes": r.nbytes, "allreduce_algbw_gbps": round(r.algbw_gbps, 2),
                        "allreduce_busbw_gbps": round(r.busbw_gbps, 2), "allreduce_ok": r.ok})
 
+    if n_gpus == 1 and not args.no_extras:
+        # node time-to-ready (driver -> validator) on this GPU, outside the timed region
+        try:
+            from gpu_operator_amd.validator import ttr
+            r = ttr.run_chain(gemm_shapes="8192", timeout=120)
+            if r["time_to_ready_s"] is not None:
+                extras["node_time_to_ready_s"] = round(r["time_to_ready_s"], 3)
+                extras["reference_model_time_to_ready_s"] = ttr.reference_model(r["steps_s"])["time_to_ready_s"]
+            else:
+                extras["node_time_to_ready_error"] = "; ".join(r["errors"])[:300]
+        except Exception as e:  # noqa: BLE001 - an extra must never fail the bench
+            extras["node_time_to_ready_error"] = str(e)[:300]
+
     if rank == 0:
         line = {
             "metric": "validator HIP GEMM TFLOPS (bf16 8192^3, aggregate over GPUs)",
