@@ -79,7 +79,7 @@ GPU_STATE_LABELS: Dict[str, Dict[str, str]] = {
 # Product families that support compute/memory partitioning (CDNA3/CDNA4 Instinct). The
 # labeller publishes amd.com/gpu.partition.capable from sysfs (available_compute_partition);
 # the family list is only a fallback for nodes labelled before the labeller ran.
-PARTITION_CAPABLE_FAMILIES = {"cdna3", "cdna4"}
+from ..models import PARTITION_CAPABLE_FAMILIES  # noqa: E402  (cdna3, cdna4)
 PARTITION_DISABLED_CONFIG = "spx-nps1"
 
 # --- operator namespace handling --------------------------------------------------------------

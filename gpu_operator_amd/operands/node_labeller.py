@@ -23,7 +23,7 @@ import sys
 import threading
 from typing import Dict, List, Optional
 
-from .. import devices
+from .. import devices, models
 from ..k8s import objects as o
 
 log = logging.getLogger("amd-node-labeller")
@@ -34,8 +34,7 @@ OWNED = re.compile(r"^amd\.com/gpu\.(product|family|gfx|device-id|count|cu-count
                    r"xgmi\.hive-id|xgmi\.links|xgmi\.fully-connected|driver-version)$")
 NFD_FEATURE_FILE = "/etc/kubernetes/node-feature-discovery/features.d/amd-gpu"
 
-FAMILIES = {"gfx950": "cdna4", "gfx942": "cdna3", "gfx941": "cdna3", "gfx940": "cdna3", "gfx90a": "cdna2",
-            "gfx908": "cdna1", "gfx1100": "rdna3", "gfx1101": "rdna3", "gfx1030": "rdna2"}
+FAMILIES = models.GFX_FAMILY
 
 
 def sanitize(v: str) -> str:

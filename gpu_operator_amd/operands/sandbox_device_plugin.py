@@ -24,19 +24,16 @@ from concurrent import futures
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
-from .. import devices
+from .. import devices, models
 from . import kubeletapi as K
 
 log = logging.getLogger("amd-sandbox-device-plugin")
 
-PRODUCTS = {0x75A3: "MI355X", 0x75A0: "MI350X", 0x74A1: "MI300X", 0x74A5: "MI325X", 0x74A2: "MI308X",
-            0x74A0: "MI300A", 0x740C: "MI250X", 0x740F: "MI210",
-            0x75B3: "MI355X_VF", 0x75B0: "MI350X_VF", 0x74B5: "MI300X_VF", 0x74B9: "MI325X_VF"}
-
 
 def resource_name(device_id: int, is_vf: bool) -> str:
-    name = PRODUCTS.get(device_id, f"DEVICE_{device_id:04X}")
-    if is_vf and not name.endswith("_VF"):
+    hit = models.by_device_id(device_id)
+    name = hit[0].name if hit else f"DEVICE_{device_id:04X}"
+    if is_vf or (hit and hit[1]):
         name += "_VF"
     return "amd.com/" + name
 
