@@ -338,7 +338,11 @@ __device__ __forceinline__ void bar() {
 // writes its bf16 128x64 sub-tile with ds_write_b64 (8-byte granules XOR-swizzled by row so the
 // 16 rows a lane group writes hit distinct banks), then every thread stores whole 16-byte
 // chunks, 32 lanes per 512-byte output row — fully coalesced global_store_dwordx4.
-template <bool BUF, bool EPI_LDS>
+// PH = 4: four 16-MFMA phases per K-tile (v3-v5). PH = 2 (v6): two 32-MFMA phases per K-tile
+// (P_a: A_lo x {B_lo,B_hi}, reads A_lo+B_lo+B_hi; P_b: A_hi x {B_hi,B_lo}, reads A_hi), halving
+// the group hand-offs. Staging: {A_lo,B_lo,B_hi} of a buffer 2 phases after their read, A_hi
+// likewise; every phase ends with a counted vmcnt (2 or 6) retiring what the next phase reads.
+template <bool BUF, bool EPI_LDS, int PH = 4>
 __global__ void __launch_bounds__(NTHREADS)
 gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
@@ -435,6 +439,156 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   char* const E = smem;
   char* const O = smem + BUF_BYTES;
 
+  if constexpr (PH == 2) {
+    stage(0, 0, 0, E + HB_A_LO);
+    stage(0, 1, 0, E + HB_A_HI);
+    stage(1, 0, 0, E + HB_B_LO);
+    stage(1, 1, 0, E + HB_B_HI);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (wr == 1) bar();
+    for (int t = 0; t < ktiles; t += 2) {
+      const bool more = t + 2 < ktiles;
+      const int k1 = (t + 1) * BK, k2 = (t + 2) * BK;
+      // P1: tile t (even), A_lo x {B_lo, B_hi}; stage odd {A_lo, B_lo, B_hi} <- t+1
+      read_b(E + HB_B_LO, 0);
+      read_b(E + HB_B_HI, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(E + HB_A_LO);
+      stage(0, 0, k1, O + HB_A_LO);
+      stage(1, 0, k1, O + HB_B_LO);
+      stage(1, 1, k1, O + HB_B_HI);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      bar();
+      mfma_q(0, 0);
+      mfma_q(0, 1);
+      bar();
+      // P2: A_hi x {B_hi, B_lo}; stage odd A_hi <- t+1
+      read_a(E + HB_A_HI);
+      stage(0, 1, k1, O + HB_A_HI);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      bar();
+      mfma_q(1, 1);
+      mfma_q(1, 0);
+      bar();
+      // P3: tile t+1 (odd); stage even {A_lo, B_lo, B_hi} <- t+2
+      read_b(O + HB_B_LO, 0);
+      read_b(O + HB_B_HI, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(O + HB_A_LO);
+      if (more) {
+        stage(0, 0, k2, E + HB_A_LO);
+        stage(1, 0, k2, E + HB_B_LO);
+        stage(1, 1, k2, E + HB_B_HI);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      bar();
+      mfma_q(0, 0);
+      mfma_q(0, 1);
+      bar();
+      // P4: stage even A_hi <- t+2
+      read_a(O + HB_A_HI);
+      if (more) {
+        stage(0, 1, k2, E + HB_A_HI);
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      bar();
+      mfma_q(1, 1);
+      mfma_q(1, 0);
+      bar();
+    }
+  } else if constexpr (PH == 8) {
+    // v7: v5's phases and staging order, but a counted wait before every phase that reads
+    // (vmcnt(8): four half-tiles in flight instead of two) — every half-tile gets >= 4
+    // phases between its DMA issue and the wait that retires it.
+#define VMWAIT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+    stage(0, 0, 0, E + HB_A_LO);
+    stage(1, 0, 0, E + HB_B_LO);
+    stage(1, 1, 0, E + HB_B_HI);
+    stage(0, 1, 0, E + HB_A_HI);
+    stage(0, 0, BK, O + HB_A_LO);
+    stage(1, 0, BK, O + HB_B_LO);
+    VMWAIT(8);
+    bar();
+    if (wr == 1) bar();
+    for (int t = 0; t < ktiles; t += 2) {
+      const bool more = t + 2 < ktiles;
+      const int k1 = (t + 1) * BK, k2 = (t + 2) * BK, k3 = (t + 3) * BK;
+      // P1
+      read_b(E + HB_B_LO, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(E + HB_A_LO);
+      stage(1, 1, k1, O + HB_B_HI);
+      VMWAIT(8);
+      bar();
+      mfma_q(0, 0);
+      bar();
+      // P2
+      read_b(E + HB_B_HI, 1);
+      stage(0, 1, k1, O + HB_A_HI);
+      VMWAIT(8);
+      bar();
+      mfma_q(0, 1);
+      bar();
+      // P3
+      read_a(E + HB_A_HI);
+      if (more) stage(0, 0, k2, E + HB_A_LO);
+      bar();
+      mfma_q(1, 1);
+      bar();
+      // P4
+      if (more) {
+        stage(1, 0, k2, E + HB_B_LO);
+        VMWAIT(8);
+      } else {
+        VMWAIT(4);
+      }
+      bar();
+      mfma_q(1, 0);
+      bar();
+      // P5
+      read_b(O + HB_B_LO, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(O + HB_A_LO);
+      if (more) {
+        stage(1, 1, k2, E + HB_B_HI);
+        VMWAIT(8);
+      } else {
+        VMWAIT(2);
+      }
+      bar();
+      mfma_q(0, 0);
+      bar();
+      // P6
+      read_b(O + HB_B_HI, 1);
+      if (more) {
+        stage(0, 1, k2, E + HB_A_HI);
+        VMWAIT(8);
+      } else {
+        VMWAIT(0);
+      }
+      bar();
+      mfma_q(0, 1);
+      bar();
+      // P7
+      read_a(O + HB_A_HI);
+      if (more) stage(0, 0, k3, O + HB_A_LO);
+      bar();
+      mfma_q(1, 1);
+      bar();
+      // P8
+      if (more) {
+        stage(1, 0, k3, O + HB_B_LO);
+        VMWAIT(8);
+      }
+      bar();
+      mfma_q(1, 0);
+      bar();
+    }
+#undef VMWAIT
+  } else {
   // prologue: even buffer <- tile 0 (complete), odd A_lo/B_lo <- tile 1 (in flight)
   stage(0, 0, 0, E + HB_A_LO);
   stage(0, 1, 0, E + HB_A_HI);
@@ -510,6 +664,7 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
     mfma_q(1, 0);
     bar();
   }
+  }  // PH
   if (wr == 0) bar();   // re-align the groups' barrier counts
 
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -686,6 +841,12 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else if (v == 5 && K % (2 * BK) == 0)
       hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true>), dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v == 6 && K % (2 * BK) == 0)
+      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 2>), dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v == 7 && K % (2 * BK) == 0)
+      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 8>), dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else
       hipLaunchKernelGGL(gemm_bf16_256x256_v2, dim3(nwg), dim3(NTHREADS), 0, s,
