@@ -31,10 +31,16 @@ def parse_args(argv=None):
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--k", type=int, default=8192)
+    ap.add_argument("--shape", default=None, help="MxNxK (overrides --m/--n/--k; safe under torchrun)")
     ap.add_argument("--allreduce-mib", type=int, default=256,
                     help="payload of the post-timing RCCL all-reduce probe (N>1)")
     ap.add_argument("--no-extras", action="store_true", help="skip the all-reduce/validation extras")
-    return ap.parse_args(argv)
+    ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
+                    help="cpu = rehearsal of the distributed plumbing (gloo, torch.matmul) for tests only")
+    a = ap.parse_args(argv)
+    if a.shape:
+        a.m, a.n, a.k = (int(x) for x in a.shape.lower().split("x"))
+    return a
 
 
 def main(argv=None) -> int:
@@ -51,22 +57,50 @@ def main(argv=None) -> int:
     if world != args.gpus and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     n_gpus = world
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    cpu = args.device == "cpu"
     distributed = world > 1
-    if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+    if cpu:
+        dev = torch.device("cpu")
+        if distributed:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        if distributed:
+            dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
         if distributed:
-            dist.barrier(device_ids=[local_rank])
+            if cpu:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local_rank])
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize(dev)
 
     m, n, k = args.m, args.n, args.k
     a = torch.empty((m, k), dtype=torch.bfloat16, device=dev)
     bt = torch.empty((n, k), dtype=torch.bfloat16, device=dev)
     c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
-    G.fill_uniform_(a, seed=1000 + rank)
-    G.fill_uniform_(bt, seed=2000 + rank)
+    if cpu:
+        g = torch.Generator().manual_seed(1000 + rank)
+        a.copy_(torch.rand((m, k), generator=g) * 2 - 1)
+        bt.copy_(torch.rand((n, k), generator=g) * 2 - 1)
+
+        def step():
+            torch.matmul(a, bt.t(), out=c)
+    else:
+        G.fill_uniform_(a, seed=1000 + rank)
+        G.fill_uniform_(bt, seed=2000 + rank)
+
+        def step():
+            G.gemm_bf16(a, bt, c)
+
+    if cpu:
+        return _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k,
+                                 {"device": "cpu-rehearsal"})
 
     # Validation chain (what the validator pod does before reporting ready).
     t_chain0 = time.perf_counter()
@@ -80,17 +114,23 @@ def main(argv=None) -> int:
         print(f"rank {rank}: validation FAILED smoke={smoke_ok} gemm={chk}", file=sys.stderr)
         return 2
 
+    extras = {"gemm_check_max_rel_err": chk.max_rel_err, "validation_chain_s": round(chain_s, 4)}
+    return _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k, extras)
+
+
+def _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k, extras):
+    from gpu_operator_amd.ops import gemm as G
     for _ in range(args.warmup):
-        G.gemm_bf16(a, bt, c)
-    torch.cuda.synchronize(dev)
+        step()
+    sync()
     barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        G.gemm_bf16(a, bt, c)
-    torch.cuda.synchronize(dev)
+        step()
+    sync()
     barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
 
     if distributed:
@@ -100,17 +140,17 @@ def main(argv=None) -> int:
     ms_per_step = elapsed / args.steps * 1e3
     per_gpu_tflops = G.tflops(m, n, k, elapsed / args.steps)
     total_tflops = per_gpu_tflops * n_gpus
-
-    extras = {"per_gpu_tflops": round(per_gpu_tflops, 2), "gemm_check_max_rel_err": chk.max_rel_err,
-              "validation_chain_s": round(chain_s, 4)}
+    extras = dict(extras, per_gpu_tflops=round(per_gpu_tflops, 2))
+    cpu = args.device == "cpu"
     if distributed and not args.no_extras:
         from gpu_operator_amd.parallel.allreduce import measure_allreduce
-        r = measure_allreduce(args.allreduce_mib * (1 << 20), dtype=torch.bfloat16, iters=10,
-                              warmup=3, device=dev)
+        nbytes = (64 << 10) if cpu else args.allreduce_mib * (1 << 20)
+        r = measure_allreduce(nbytes, dtype=torch.bfloat16, iters=3 if cpu else 10, warmup=1 if cpu else 3,
+                              device=dev)
         extras.update({"allreduce_bytes": r.nbytes, "allreduce_algbw_gbps": round(r.algbw_gbps, 2),
                        "allreduce_busbw_gbps": round(r.busbw_gbps, 2), "allreduce_ok": r.ok})
 
-    if n_gpus == 1 and not args.no_extras:
+    if n_gpus == 1 and not args.no_extras and not cpu:
         # node time-to-ready (driver -> validator) on this GPU, outside the timed region
         try:
             from gpu_operator_amd.validator import ttr
