@@ -264,7 +264,9 @@ class RestClient:
                                       params={"watch": "1", "resourceVersion": rv,
                                               "allowWatchBookmarks": "true", "timeoutSeconds": "300"},
                                       stream=True, timeout=(10, 330))
-                    for line in r.iter_lines():
+                    # chunk_size=None: yield each chunk as it arrives (the API server sends one
+                    # event per chunk); a fixed size would hold small events back
+                    for line in r.iter_lines(chunk_size=None):
                         if stop.is_set():
                             break
                         if not line:

@@ -1,0 +1,160 @@
+"""The production REST client and the operator process against an in-process HTTP API server
+(the envtest tier the reference never used)."""
+
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+
+import pytest
+import yaml
+
+from gpu_operator_amd.k8s import errors
+from gpu_operator_amd.k8s import objects as o
+from gpu_operator_amd.k8s.apiserver import FakeAPIServer, plural
+from gpu_operator_amd.k8s.fake import FakeClient
+from gpu_operator_amd.k8s.rest import Config, RestClient
+from gpu_operator_amd.k8s.sim import ClusterSim
+
+from k8s_helpers import NS, cluster, gpu_node, namespace, reconciler
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture
+def api():
+    srv = FakeAPIServer(FakeClient([namespace(), gpu_node("n1"), gpu_node("n2", gpu=False)]),
+                        unserved=("ServiceMonitor",)).start()
+    yield srv, RestClient(Config(srv.url, verify=False), timeout=10)
+    srv.stop()
+
+
+def _pod(name, node="n1", labels=None):
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": NS, "labels": labels or {}},
+            "spec": {"nodeName": node, "containers": [{"name": "c", "image": "x"}]}}
+
+
+def test_plural_rules():
+    assert [plural(k) for k in ("ClusterPolicy", "RuntimeClass", "SecurityContextConstraints", "Pod", "Ingress")] == \
+        ["clusterpolicies", "runtimeclasses", "securitycontextconstraints", "pods", "ingresses"]
+
+
+def test_crud_selectors_and_errors(api):
+    srv, c = api
+    assert c.server_version() == "v1.29.2"
+    assert c.has_kind("apps/v1", "DaemonSet") and not c.has_kind("monitoring.coreos.com/v1", "ServiceMonitor")
+    with pytest.raises(errors.NoKindMatch):
+        c.get("monitoring.coreos.com/v1", "ServiceMonitor", "x", NS)
+    p = c.create(_pod("a", labels={"app": "x"}))
+    assert p["metadata"]["uid"] and p["metadata"]["namespace"] == NS
+    c.create(_pod("b", node="n2", labels={"app": "y"}))
+    with pytest.raises(errors.AlreadyExists):
+        c.create(_pod("a"))
+    assert [o.name(x) for x in c.list("v1", "Pod", NS, label_selector="app in (x,z)")] == ["a"]
+    assert [o.name(x) for x in c.list("v1", "Pod", NS, label_selector={"app": "y"})] == ["b"]
+    assert [o.name(x) for x in c.list("v1", "Pod", field_selector="spec.nodeName=n2")] == ["b"]
+    assert {o.name(n) for n in c.list("v1", "Node")} == {"n1", "n2"}
+    # optimistic concurrency over the wire
+    cur = c.get("v1", "Pod", "a", NS)
+    cur["metadata"]["labels"]["v"] = "1"
+    c.update(cur)
+    cur["metadata"]["labels"]["v"] = "2"
+    with pytest.raises(errors.Conflict):
+        c.update(cur)                                   # stale resourceVersion
+    # merge patch + status subresource
+    c.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.present": "true", "gone": None}}})
+    assert o.get_labels(c.get("v1", "Node", "n1"))["amd.com/gpu.present"] == "true"
+    c.patch("v1", "Node", "n1", {"status": {"capacity": {"amd.com/gpu": "8"}}})
+    assert c.get("v1", "Node", "n1")["status"]["capacity"]["amd.com/gpu"] == "8"
+    c.delete("v1", "Pod", "b", NS)
+    with pytest.raises(errors.NotFound):
+        c.get("v1", "Pod", "b", NS)
+    c.evict("a", NS)
+    assert c.list("v1", "Pod", NS) == []
+    c.create_event(c.get("v1", "Node", "n1"), "Test", "hello")
+    evs = srv.client.objects("Event")
+    assert evs and evs[0]["reason"] == "Test" and o.name(evs[0]).startswith("n1.")
+    assert ("POST", f"/api/v1/namespaces/{NS}/pods/a/eviction") in srv.requests
+
+
+def test_watch_stream(api):
+    srv, c = api
+    seen = []
+    got = threading.Event()
+
+    def cb(ev):
+        seen.append((ev.type, o.name(ev.obj), o.get_labels(ev.old).get("x") if ev.old else None))
+        if ev.type == "DELETED":
+            got.set()
+    stop = c.watch("v1", "Pod", cb, NS)
+    try:
+        time.sleep(0.5)                                   # initial list + watch established
+        c.create(_pod("w"))
+        time.sleep(0.2)
+        c.patch("v1", "Pod", "w", {"metadata": {"labels": {"x": "1"}}}, NS)
+        time.sleep(0.2)
+        c.delete("v1", "Pod", "w", NS)
+        assert got.wait(10)
+    finally:
+        stop()
+    assert [s[:2] for s in seen] == [("ADDED", "w"), ("MODIFIED", "w"), ("DELETED", "w")]
+    assert seen[2][2] == "1"                              # DELETED carries the last known object
+
+
+def test_reconciler_over_http_reaches_ready():
+    backing = cluster([gpu_node(f"n{i}") for i in range(3)])
+    with FakeAPIServer(backing, unserved=("ServiceMonitor", "PrometheusRule")) as srv:
+        rc = RestClient(Config(srv.url, verify=False), timeout=10)
+        rec = reconciler(rc)
+        sim = ClusterSim(backing)
+        state = None
+        for _ in range(6):
+            rec.reconcile(("", "cluster-policy"))
+            sim.sync()
+            state = rc.get("amd.com/v1", "ClusterPolicy", "cluster-policy").get("status", {}).get("state")
+            if state == "ready":
+                break
+        assert state == "ready"
+        assert any(p.startswith("/apis/apps/v1/namespaces/") for _, p in srv.requests)
+
+
+def test_operator_process_end_to_end(tmp_path):
+    """`amd-gpu-operator` as a real process: kubeconfig -> HTTP API, leader election Lease,
+    watches, reconcile to ready while a simulated kubelet/DaemonSet controller runs."""
+    backing = cluster([gpu_node("n1"), gpu_node("n2")])
+    with FakeAPIServer(backing, unserved=("ServiceMonitor", "PrometheusRule")) as srv:
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "apiVersion": "v1", "kind": "Config", "current-context": "t",
+            "clusters": [{"name": "t", "cluster": {"server": srv.url}}],
+            "contexts": [{"name": "t", "context": {"cluster": "t", "user": "u"}}],
+            "users": [{"name": "u", "user": {}}]}))
+        env = dict(os.environ, OPERATOR_NAMESPACE=NS, PYTHONPATH=ROOT)
+        proc = subprocess.Popen([sys.executable, "-m", "gpu_operator_amd.cmd.operator", "--kubeconfig", str(kc),
+                                 "--leader-elect", "--metrics-bind-address", "127.0.0.1:0",
+                                 "--health-probe-bind-address", "127.0.0.1:0"],
+                                env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        sim = ClusterSim(backing)
+        state = None
+        try:
+            deadline = time.monotonic() + 90
+            while time.monotonic() < deadline and proc.poll() is None:
+                sim.sync()
+                state = (backing.get("amd.com/v1", "ClusterPolicy", "cluster-policy").get("status") or {}).get("state")
+                if state == "ready":
+                    break
+                time.sleep(0.5)
+            leases = backing.objects("Lease")
+        finally:
+            proc.send_signal(signal.SIGTERM)
+            try:
+                out, _ = proc.communicate(timeout=20)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+                out, _ = proc.communicate()
+        assert state == "ready", out[-3000:]
+        assert leases and o.name(leases[0]) == "53822513.amd.com"
+        labels = o.get_labels(backing.get("v1", "Node", "n1"))
+        assert labels.get("amd.com/gpu.present") == "true" and labels.get("amd.com/gpu.deploy.device-plugin") == "true"
