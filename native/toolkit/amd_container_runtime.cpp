@@ -377,11 +377,14 @@ void resolve_legacy(const std::vector<std::string>& req, const Config& cfg, Edit
 
 // ---- spec edits -----------------------------------------------------------------------------
 void apply(Value& spec, Edits& e, const Config& cfg) {
+  // Objects are vectors of members: create every key first, then take references (a later
+  // insertion into the same object would reallocate and dangle an earlier reference).
   Value& linux_ = spec["linux"];
-  Value& devs = linux_["devices"];
+  linux_["devices"];
+  linux_["resources"]["devices"];
+  Value& devs = *linux_.find("devices");
   if (devs.is_null()) devs = Value::array();
-  Value& res = linux_["resources"];
-  Value& allow = res["devices"];
+  Value& allow = (*linux_.find("resources"))["devices"];
   if (allow.is_null()) allow = Value::array();
   std::set<std::string> have;
   for (auto& d : devs.a) if (const Value* p = d.find("path")) have.insert(p->s);
