@@ -30,6 +30,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -342,7 +344,9 @@ __device__ __forceinline__ void bar() {
 // (P_a: A_lo x {B_lo,B_hi}, reads A_lo+B_lo+B_hi; P_b: A_hi x {B_hi,B_lo}, reads A_hi), halving
 // the group hand-offs. Staging: {A_lo,B_lo,B_hi} of a buffer 2 phases after their read, A_hi
 // likewise; every phase ends with a counted vmcnt (2 or 6) retiring what the next phase reads.
-template <bool BUF, bool EPI_LDS, int PH = 4>
+// KNOB (A/B experiments on the PH=4 schedule): 1 = no s_setprio around the MFMA blocks,
+// 2 = issue each phase's half-tile DMA before its ds_reads.
+template <bool BUF, bool EPI_LDS, int PH = 4, int KNOB = 0>
 __global__ void __launch_bounds__(NTHREADS)
 gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
@@ -423,7 +427,7 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
         bq[q][n][kk] = *reinterpret_cast<const bf16x8*>(half + b_off + n * 16 * ROW_BYTES + lane_off[kk]);
   };
   auto mfma_q = [&](int qm, int qn) {
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (KNOB != 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -432,7 +436,7 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
         for (int n = 0; n < 2; ++n)
           acc[qm * 4 + m][qn * 2 + n] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[qn][n][kk], af[m][kk], acc[qm * 4 + m][qn * 2 + n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (KNOB != 1) __builtin_amdgcn_s_setprio(0);
   };
 
   const int ktiles = K / BK;            // even (host guarantees K % 128 == 0)
@@ -588,6 +592,82 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
       bar();
     }
 #undef VMWAIT
+  } else if constexpr (KNOB == 2) {
+  // prologue: even buffer <- tile 0 (complete), odd A_lo/B_lo <- tile 1 (in flight)
+  stage(0, 0, 0, E + HB_A_LO);
+  stage(0, 1, 0, E + HB_A_HI);
+  stage(1, 0, 0, E + HB_B_LO);
+  stage(1, 1, 0, E + HB_B_HI);
+  stage(0, 0, BK, O + HB_A_LO);
+  stage(1, 0, BK, O + HB_B_LO);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  bar();
+  if (wr == 1) bar();   // stagger: group 1 runs one barrier behind group 0
+
+  for (int t = 0; t < ktiles; t += 2) {
+    const bool more = t + 2 < ktiles;
+    const int k1 = (t + 1) * BK, k2 = (t + 2) * BK, k3 = (t + 3) * BK;
+    // ---- even buffer (tile t) ----
+    // P1
+    stage(1, 1, k1, O + HB_B_HI);
+    read_b(E + HB_B_LO, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(E + HB_A_LO);
+    bar();
+    mfma_q(0, 0);
+    bar();
+    // P2
+    stage(0, 1, k1, O + HB_A_HI);
+    read_b(E + HB_B_HI, 1);
+    bar();
+    mfma_q(0, 1);
+    bar();
+    // P3
+    if (more) stage(0, 0, k2, E + HB_A_LO);
+    read_a(E + HB_A_HI);
+    bar();
+    mfma_q(1, 1);
+    bar();
+    // P4
+    if (more) {
+      stage(1, 0, k2, E + HB_B_LO);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    mfma_q(1, 0);
+    bar();
+    // ---- odd buffer (tile t+1) ----
+    // P5
+    if (more) stage(1, 1, k2, E + HB_B_HI);
+    read_b(O + HB_B_LO, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(O + HB_A_LO);
+    bar();
+    mfma_q(0, 0);
+    bar();
+    // P6
+    if (more) stage(0, 1, k2, E + HB_A_HI);
+    read_b(O + HB_B_HI, 1);
+    bar();
+    mfma_q(0, 1);
+    bar();
+    // P7
+    if (more) stage(0, 0, k3, O + HB_A_LO);
+    read_a(O + HB_A_HI);
+    bar();
+    mfma_q(1, 1);
+    bar();
+    // P8
+    if (more) {
+      stage(1, 0, k3, O + HB_B_LO);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    bar();
+    mfma_q(1, 0);
+    bar();
+  }
   } else {
   // prologue: even buffer <- tile 0 (complete), odd A_lo/B_lo <- tile 1 (in flight)
   stage(0, 0, 0, E + HB_A_LO);
@@ -718,6 +798,226 @@ gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   }
 }
 
+// v10: one wave per SIMD. 4 waves (2x2), each owning a 128x128 sub-tile: 8x8 MFMA 16x16x32
+// accumulators = the wave's 256 AGPRs; its fragments (2 x 16 x bf16x8 = 128 VGPRs) and addresses
+// fit the 256 VGPRs. A 128x128 wave tile halves the LDS bytes per MFMA against v5's 128x64
+// (256 B vs 384 B): per K-tile the CU reads 128 KiB of fragments + 64 KiB of DMA writes in 2048
+// MFMA cycles (96 B/clk of LDS's 128) where v5 needed 128 B/clk, i.e. sat on the LDS port.
+// Each SIMD's matrix pipe is fed by its single wave, which interleaves its own LDS fragment reads
+// (1 ds_read_b128 per 4 MFMAs) and LDS-DMA pieces (1 per 4 MFMAs) into the MFMA stream. Per K-tile:
+//   block(t, kk0): MFMA with R0, read R1 <- frags(t, kk1)
+//   wait lgkmcnt(0) + vmcnt(0) (tile t+1 landed) ; barrier (tile t fully read by every wave)
+//   block(t, kk1): MFMA with R1, read R0 <- frags(t+1, kk0), DMA tile t+2 into tile t's buffer
+// One barrier per K-tile; the DMA of a tile has a full K-tile (128 MFMAs) to land.
+//
+// The accumulators are pinned: hipcc's greedy allocator, given 64 tuples that fill all 256 AGPRs,
+// cannot keep them in place across the loop back-edge and shuffles them through a[0:3] with
+// ~600 v_accvgpr moves per K-tile. So the MFMAs are inline asm on literal a[4i:4i+3] (the kernel
+// owns every AGPR via W4_AGPR_CLOBBERS; the compiler has no AGPR values of its own -- audited in
+// tests/test_gemm_build.py: no compiler v_accvgpr_* outside the asm blocks). Hazards handled by
+// hand (cdna_hip_programming.md §5.7 item 2): zeroing writes -> first MFMA reading them as C are
+// separated by the prologue; the last MFMA's D -> v_accvgpr_read is covered by an explicit s_nop
+// pad; an accumulate chain MFMA -> MFMA (same C) needs none. A/B operands come from compiler
+// ds_reads whose lgkmcnt waits hipcc inserts before each asm statement that names them.
+constexpr int W4_THREADS = 256;
+
+struct W4Frags {
+  bf16x8 a[8];
+  bf16x8 b[8];
+};
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+#define W4_AGPR_CLOBBERS \
+  "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", \
+  "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", \
+  "a31", "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", \
+  "a46", "a47", "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", \
+  "a61", "a62", "a63", "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", \
+  "a76", "a77", "a78", "a79", "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", \
+  "a91", "a92", "a93", "a94", "a95", "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", \
+  "a105", "a106", "a107", "a108", "a109", "a110", "a111", "a112", "a113", "a114", "a115", "a116", "a117", \
+  "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127", "a128", "a129", "a130", \
+  "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143", \
+  "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", \
+  "a157", "a158", "a159", "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", \
+  "a170", "a171", "a172", "a173", "a174", "a175", "a176", "a177", "a178", "a179", "a180", "a181", "a182", \
+  "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", "a192", "a193", "a194", "a195", \
+  "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", "a208", \
+  "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", \
+  "a222", "a223", "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", \
+  "a235", "a236", "a237", "a238", "a239", "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", \
+  "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255"
+
+template <int I>
+__device__ __forceinline__ void w4_mfma(const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+               :: "i"(4 * I), "i"(4 * I + 3), "v"(b), "v"(a));
+}
+
+// fragment read order j -> (A or B, index): the order the next block consumes them
+// (i = 0..7 uses a0 with b0..b7, then a1 ...), so hipcc's lgkmcnt ladder releases MFMAs early.
+__device__ __forceinline__ constexpr int w4_isb(int j) { return j >= 1 && j <= 8; }
+__device__ __forceinline__ constexpr int w4_idx(int j) { return j == 0 ? 0 : (j <= 8 ? j - 1 : j - 8); }
+
+// RSPAN / DSPAN: the 16 fragment reads / DMA pieces of a block are spread over its first
+// RSPAN / DSPAN groups of 4 MFMAs (16 = evenly; smaller = earlier, more latency slack).
+template <int RSPAN = 16, int DSPAN = 16>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                     __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
+  // wave w issues pieces p = 4i + w (A row blocks 0..31, then B); every piece it issues has
+  // row-block parity w & 1, so one per-lane voffset serves all of them.
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, int k0, char* buf) {
+    const int p = i * 4 + wid;                     // 0..63
+    const int rblk = p & 31;
+    char* lds = buf + (p >= 32 ? PANEL_BYTES : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(p >= 32 ? rB : rA, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+  };
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * ROW_BYTES;
+  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  W4Frags R0, R1;
+  char* const buf0 = smem;
+  char* const buf1 = smem + BUF_BYTES;
+
+  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int x = w4_idx(j);
+    if constexpr (w4_isb(j))
+      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
+    else
+      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  // 64 MFMAs with Fc; optionally 16 fragment reads into Fn (from nbuf, step nkk) and 16 DMA
+  // pieces (tile at column dk into dbuf) placed after groups of 4 MFMAs; sched_barrier pins it.
+  auto block = [&](const W4Frags& Fc, W4Frags& Fn, const char* nbuf, int nkk, auto RD, char* dbuf, int dk,
+                   auto DM) {
+    static_for<0, 16>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      static_for<0, 4>([&](auto U) {
+        constexpr int i = q * 4 + decltype(U)::value;
+        w4_mfma<i>(Fc.b[i & 7], Fc.a[i >> 3]);
+      });
+      static_for<0, 16>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (decltype(RD)::value && j * RSPAN / 16 == q) read_frag(Fn, nbuf, nkk, J);
+      });
+      static_for<0, 16>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (decltype(DM)::value && j * DSPAN / 16 == q) dma_piece(j, dk, dbuf);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  auto sync_tile = [&]() {
+    __builtin_amdgcn_s_waitcnt(0x0070);             // vmcnt(0) lgkmcnt(0), visible to hipcc's counters
+    bar();
+  };
+
+  const int ktiles = K / BK;        // >= 2 (host guarantees)
+  // prologue: tile 0 -> buf0 (waited), tile 1 -> buf1 (in flight), R0 <- (0, kk0)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, 0, buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, BK, buf1);
+  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
+  bar();
+  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
+
+  char* cur = buf0;
+  char* nxt = buf1;
+  for (int t = 0; t < ktiles - 2; ++t) {
+    block(R0, R1, cur, 1, T_{}, nullptr, 0, F_{});
+    sync_tile();
+    block(R1, R0, nxt, 0, T_{}, cur, (t + 2) * BK, T_{});
+    char* tmp = cur; cur = nxt; nxt = tmp;
+  }
+  // second-to-last tile: prefetch fragments, no DMA; then the last tile
+  block(R0, R1, cur, 1, T_{}, nullptr, 0, F_{});
+  sync_tile();
+  block(R1, R0, nxt, 0, T_{}, nullptr, 0, F_{});
+  block(R0, R1, nxt, 1, T_{}, nullptr, 0, F_{});
+  block(R1, R0, nullptr, 0, F_{}, nullptr, 0, F_{});
+
+  // epilogue through LDS (every wave is past its last ds_read once all reach this barrier);
+  // pad the last MFMA's D before the accumulator reads.
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  bar();
+  constexpr int CROW = BN * 2;
+  static_for<0, 64>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int m = i >> 3, n = i & 7;
+    float x0, x1, x2, x3;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+    const int r = wr * 128 + m * 16 + (lane & 15);
+    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
+    bf16x4 v;
+    v[0] = (__bf16)x0;
+    v[1] = (__bf16)x1;
+    v[2] = (__bf16)x2;
+    v[3] = (__bf16)x3;
+    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
+  });
+  bar();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {      // 32 chunks per thread
+    const int r = i * (W4_THREADS / 32) + (tid >> 5);
+    const int ch = tid & 31;
+    const int sw = r & 15;
+    const int pg = (2 * ch) ^ sw;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
+    uint4 v = raw;
+    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+  }
+}
+
 // Generic bounds-checked MFMA kernel (64x64 tile, 4 waves of 32x32), register-staged.
 // Used for shapes that are not multiples of 256/256/64 and as a second, independent
 // implementation for cross-checking the fast path.
@@ -844,6 +1144,21 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else if (v == 6 && K % (2 * BK) == 0)
       hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 2>), dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v >= 10 && v <= 14 && K >= 2 * BK) {
+      auto kern = v == 10 ? gemm_bf16_256x256_w4<16, 16>
+                : v == 11 ? gemm_bf16_256x256_w4<12, 16>
+                : v == 12 ? gemm_bf16_256x256_w4<12, 8>
+                : v == 13 ? gemm_bf16_256x256_w4<8, 8>
+                          : gemm_bf16_256x256_w4<12, 4>;
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
+    else if (v == 8 && K % (2 * BK) == 0)
+      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 4, 1>), dim3(nwg), dim3(NTHREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v == 9 && K % (2 * BK) == 0)
+      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 4, 2>), dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     else if (v == 7 && K % (2 * BK) == 0)
       hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 8>), dim3(nwg), dim3(NTHREADS), 0, s,

@@ -1,0 +1,87 @@
+"""Static audit of the gfx950 GEMM code object (CPU-only: hipcc cross-compiles).
+
+The v10 kernel keeps its 256 accumulators in literal AGPRs written by inline-asm MFMAs
+(native/hip/gemm_bf16.hip, "v10" comment). That is only sound if hipcc never touches an AGPR
+itself, so every build is audited here: no compiler-emitted ``v_accvgpr_*`` outside the asm
+blocks, no scratch, occupancy 1, and the main loop carries exactly one barrier and no
+hipcc-inserted ``s_nop`` hazard padding (which would mean an unmodelled dependency)."""
+
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = "/opt/rocm/bin/hipcc"
+
+pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    out = tmp_path_factory.mktemp("gemm_asm") / "gemm.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/native/include",
+                    "--cuda-device-only", "-S", os.path.join(ROOT, "native/hip/gemm_bf16.hip"), "-o", str(out)],
+                   check=True, capture_output=True, timeout=600)
+    return out.read_text()
+
+
+def _kernels(asm: str, name: str):
+    starts = list(re.finditer(rf"^(_Z\w*{name}\w*):", asm, re.M))
+    assert starts, name
+    return [_kernel_at(asm, m) for m in starts]
+
+
+def _kernel_at(asm: str, start):
+    body = asm[start.start():asm.index(".end_amdhsa_kernel", start.start())]
+    tail = asm[start.start():]
+    stats = {k: int(v) for k, v in re.findall(r"^; (NumVgprs|NumAgprs|ScratchSize|Occupancy): (\d+)", tail,
+                                                re.M)[:4]}
+    return body, stats
+
+
+@pytest.fixture(scope="module")
+def w4(asm):
+    return _kernels(asm, "gemm_bf16_256x256_w4")
+
+
+def test_w4_accumulators_pinned(w4):
+    for body, st in w4:
+        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+        assert st["NumVgprs"] <= 256
+        outside = []
+        in_asm = False
+        for line in body.splitlines():
+            if ";;#ASMSTART" in line:
+                in_asm = True
+            elif ";;#ASMEND" in line:
+                in_asm = False
+            elif not in_asm and "v_accvgpr" in line:
+                outside.append(line.strip())
+        assert not outside, outside[:5]
+        assert len(re.findall(r"v_mfma_f32_16x16x32_bf16", body)) == 6 * 64
+
+
+def test_w4_main_loop_shape(w4):
+    for body, _ in w4:
+        loop = re.search(r"; =>This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
+        assert loop, "main loop not found"
+        text = loop.group(1)
+        assert text.count("v_mfma") == 128
+        assert text.count("ds_read_b128") == 32
+        assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
+        assert text.count("s_barrier") == 1
+        assert "scratch_" not in text
+        # the only padding hipcc may add is the M0 write -> LDS-DMA nop; anything else means it
+        # found a dependency the asm MFMAs hide from it
+        ins = [x.strip() for x in text.splitlines() if x.strip() and not x.strip().startswith((";", "."))]
+        for i, x in enumerate(ins):
+            if x.startswith("s_nop"):
+                assert ins[i + 1].startswith("buffer_load") and ins[i + 1].endswith(" lds"), ins[i - 3:i + 2]
+
+
+def test_no_kernel_spills(asm):
+    for m in re.finditer(r"^; ScratchSize: (\d+)", asm, re.M):
+        assert int(m.group(1)) == 0

@@ -15,6 +15,7 @@ def main():
     ap.add_argument("--variant", type=int, default=4)
     ap.add_argument("--size", default="8192")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--blas", action="store_true", help="run hipBLASLt (torch.matmul) instead")
     a = ap.parse_args()
     import torch
     from gpu_operator_amd.ops import gemm as G
@@ -27,7 +28,10 @@ def main():
     G.fill_uniform_(Bt, 2)
     G.set_variant(a.variant)
     for _ in range(a.iters):
-        G.gemm_bf16(A, Bt, C)
+        if a.blas:
+            torch.matmul(A, Bt.t(), out=C)
+        else:
+            G.gemm_bf16(A, Bt, C)
     torch.cuda.synchronize()
     print("ok", G.verify(A, Bt, C, nrows=8).ok)
 
