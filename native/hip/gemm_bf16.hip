@@ -868,7 +868,9 @@ __device__ __forceinline__ constexpr int w4_idx(int j) { return j == 0 ? 0 : (j 
 
 // RSPAN / DSPAN: the 16 fragment reads / DMA pieces of a block are spread over its first
 // RSPAN / DSPAN groups of 4 MFMAs (16 = evenly; smaller = earlier, more latency slack).
-template <int RSPAN = 16, int DSPAN = 16>
+// KO (profiling only, wrong results): bit0 drops the per-tile wait+barrier, bit1 the DMA, bit2
+// the fragment reads -- knock-out timings that price each component.
+template <int RSPAN = 16, int DSPAN = 16, int KO = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
@@ -939,11 +941,11 @@ gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
       });
       static_for<0, 16>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        if constexpr (decltype(RD)::value && j * RSPAN / 16 == q) read_frag(Fn, nbuf, nkk, J);
+        if constexpr (decltype(RD)::value && !(KO & 4) && j * RSPAN / 16 == q) read_frag(Fn, nbuf, nkk, J);
       });
       static_for<0, 16>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        if constexpr (decltype(DM)::value && j * DSPAN / 16 == q) dma_piece(j, dk, dbuf);
+        if constexpr (decltype(DM)::value && !(KO & 2) && j * DSPAN / 16 == q) dma_piece(j, dk, dbuf);
       });
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -951,8 +953,10 @@ gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   using T_ = std::true_type;
   using F_ = std::false_type;
   auto sync_tile = [&]() {
-    __builtin_amdgcn_s_waitcnt(0x0070);             // vmcnt(0) lgkmcnt(0), visible to hipcc's counters
-    bar();
+    if constexpr (!(KO & 1)) {
+      __builtin_amdgcn_s_waitcnt(0x0070);           // vmcnt(0) lgkmcnt(0), visible to hipcc's counters
+      bar();
+    }
   };
 
   const int ktiles = K / BK;        // >= 2 (host guarantees)
@@ -1007,6 +1011,312 @@ gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {      // 32 chunks per thread
+    const int r = i * (W4_THREADS / 32) + (tid >> 5);
+    const int ch = tid & 31;
+    const int sw = r & 15;
+    const int pg = (2 * ch) ^ sw;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
+    uint4 v = raw;
+    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+  }
+}
+
+// v18: v10's data layout with the schedule reshaped around the K-tile instead of two halves.
+// Knock-out cycle accounting of v10 (profiles/r1_gemm_v10/README.md) priced its DMA at 13 % of
+// the wave cycles and its wait+barrier at 4 %, with fragment reads nearly free. Here, in MFMA
+// slots 0..127 of iteration t (0..63 on R0 = tile t kk0, 64..127 on R1 = tile t kk1):
+//   slots 0..15      read R1 <- tile t kk1 (one per MFMA)
+//   slot B1          lgkmcnt(0) one MFMA earlier, then a barrier: every wave is done with tile t
+//   slots D0 + j*DS  DMA tile t+2 into tile t's buffer (16 pieces), starting ~40 slots earlier
+//                    than v10 so a piece has ~80 MFMAs to land
+//   slot B2          vmcnt(pieces issued so far this iteration) one MFMA earlier -- tile t+1 (last
+//                    iteration's pieces) landed, this iteration's stay in flight -- then a barrier
+//   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
+// Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                      __bf16* __restrict__ C, int M, int N, int K) {
+  static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, int k0, char* buf) {
+    const int p = i * 4 + wid;
+    const int rblk = p & 31;
+    char* lds = buf + (p >= 32 ? PANEL_BYTES : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(p >= 32 ? rB : rA, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+  };
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * ROW_BYTES;
+  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  W4Frags R0, R1;
+  char* const buf0 = smem;
+  char* const buf1 = smem + BUF_BYTES;
+  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int x = w4_idx(j);
+    if constexpr (w4_isb(j))
+      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
+    else
+      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  // DM: DMA tile t+2; NX: tile t+1 exists (wait for it, read its kk0 into R0); LAST_DMA: the
+  // previous iteration issued no DMA (vmcnt target 0 instead of this iteration's count)
+  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value;
+    static_for<0, 128>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
+      else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
+      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
+      if constexpr (dm && i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
+      if constexpr (nx && i == B2 - 1) {
+        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
+        // vmcnt(issued) lgkmcnt(0): vmcnt low 4 bits [3:0], high 2 bits [15:14]; expcnt 7
+        __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
+      }
+      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i > B2) {
+        static_for<0, 16>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  const int ktiles = K / BK;        // >= 2 (host guarantees)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, 0, buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, BK, buf1);
+  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
+  bar();
+  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
+
+  char* cur = buf0;
+  char* nxt = buf1;
+  for (int t = 0; t < ktiles - 2; ++t) {
+    iter(cur, nxt, (t + 2) * BK, T_{}, T_{});
+    char* tmp = cur; cur = nxt; nxt = tmp;
+  }
+  iter(cur, nxt, 0, F_{}, T_{});
+  iter(nxt, nullptr, 0, F_{}, F_{});
+
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  bar();
+  constexpr int CROW = BN * 2;
+  static_for<0, 64>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int m = i >> 3, n = i & 7;
+    float x0, x1, x2, x3;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+    const int r = wr * 128 + m * 16 + (lane & 15);
+    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
+    bf16x4 v;
+    v[0] = (__bf16)x0;
+    v[1] = (__bf16)x1;
+    v[2] = (__bf16)x2;
+    v[3] = (__bf16)x3;
+    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
+  });
+  bar();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {
+    const int r = i * (W4_THREADS / 32) + (tid >> 5);
+    const int ch = tid & 31;
+    const int sw = r & 15;
+    const int pg = (2 * ch) ^ sw;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
+    uint4 v = raw;
+    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+  }
+}
+
+// v15: v10's wave layout over a 5-slot ring of K-half-tiles (32 k-columns: A 16 KiB + B 16 KiB
+// per slot = all 160 KiB of LDS). v10 syncs once per K-tile but the DMA it waits for was issued
+// only one 64-MFMA block earlier (~1000 cycles: less than a loaded L2-miss round trip). Here block
+// h (64 MFMAs on half h) reads the fragments of half h+1 and DMAs half h+4 into the slot of half
+// h-1; its closing barrier needs half h+2, issued two blocks earlier (vmcnt(16): halves h+3, h+4
+// stay in flight). One barrier per 64 MFMAs instead of per 128.
+// Slot layout: 256 rows x 64 B per operand, 16-B chunk c of row r at ((c ^ ((r >> 2) & 3)) << 4):
+// the 16 lanes of a ds_read_b128 phase (16 rows, one chunk) cover all 64 banks. LDS-DMA writes a
+// 1-KiB piece (16 rows) lane-contiguous, so each lane fetches the global chunk its LDS slot holds.
+constexpr int RH_ROW = 64;                          // bytes per row per half
+constexpr int RH_OP = BM * RH_ROW;                  // 16 KiB per operand per half
+constexpr int RH_SLOT = 2 * RH_OP;                  // 32 KiB
+constexpr int RH_NSLOT = 5;                         // 160 KiB
+
+template <int RSPAN = 12, int DSPAN = 8>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+gemm_bf16_256x256_w4r(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                      __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[RH_NSLOT * RH_SLOT];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
+  // piece = 16 rows x 64 B; lane L -> row L>>2, LDS chunk L&3 holding global chunk (L&3)^((L>>4)&3)
+  const uint32_t voff = (uint32_t)(lane >> 2) * (uint32_t)K * 2u +
+                        (uint32_t)(((lane & 3) ^ ((lane >> 4) & 3)) * 16);
+  // half h: 32 pieces (A row blocks 0..15, B 0..15); wave w issues p = 4i + w, i = 0..7
+  // slot indices are carried incrementally (sl = h mod 5): no division in the loop
+  auto m5 = [](int x) { return x >= RH_NSLOT ? x - RH_NSLOT : x; };
+  auto dma_piece = [&](int i, int h, int sl) {
+    const int p = i * 4 + wid;
+    const int rblk = p & 15;
+    char* lds = smem + sl * RH_SLOT + (p >= 16 ? RH_OP : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(p >= 16 ? rB : rA, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 16u * (uint32_t)K * 2u + (uint32_t)h * 64u, 0, 0);
+  };
+  const int r16 = lane & 15;
+  const int lane_off = r16 * RH_ROW + (((lane >> 4) ^ ((r16 >> 2) & 3)) << 4);
+  const int a_off = wr * 128 * RH_ROW + lane_off;
+  const int b_off = RH_OP + wc * 128 * RH_ROW + lane_off;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  W4Frags R0, R1;
+  auto read_frag = [&](W4Frags& F, int sl, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int x = w4_idx(j);
+    const char* slot = smem + sl * RH_SLOT;
+    if constexpr (w4_isb(j))
+      F.b[x] = *reinterpret_cast<const bf16x8*>(slot + b_off + x * 16 * RH_ROW);
+    else
+      F.a[x] = *reinterpret_cast<const bf16x8*>(slot + a_off + x * 16 * RH_ROW);
+  };
+  // one block: 64 MFMAs on Fc; reads from slot rs into Fn; DMA of half dh into slot ds
+  auto block = [&](const W4Frags& Fc, W4Frags& Fn, int rs, auto RD, int dh, int ds, auto DM) {
+    static_for<0, 16>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      static_for<0, 4>([&](auto U) {
+        constexpr int i = q * 4 + decltype(U)::value;
+        w4_mfma<i>(Fc.b[i & 7], Fc.a[i >> 3]);
+      });
+      static_for<0, 16>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (decltype(RD)::value && j * RSPAN / 16 == q) read_frag(Fn, rs, J);
+      });
+      static_for<0, 8>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (decltype(DM)::value && j * DSPAN / 8 == q) dma_piece(j, dh, ds);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  const int H = K / 32;             // >= 4 (host guarantees K >= 128)
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma_piece(i, h, h);
+  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): halves 0, 1 landed
+  bar();
+  static_for<0, 16>([&](auto J) { read_frag(R0, 0, J); });
+
+  // steady state, two halves per trip so R0/R1 keep their roles
+  int h = 0, sl = 0;
+  for (; h + 5 < H; h += 2, sl = m5(sl + 2)) {
+    block(R0, R1, m5(sl + 1), T_{}, h + 4, m5(sl + 4), T_{});
+    __builtin_amdgcn_s_waitcnt(0x4070);             // vmcnt(16) lgkmcnt(0): half h+2 landed
+    bar();
+    block(R1, R0, m5(sl + 2), T_{}, h + 5, sl, T_{});
+    __builtin_amdgcn_s_waitcnt(0x4070);             // half h+3 landed
+    bar();
+  }
+  // H is even, so exactly 4 halves are left: h .. H-1
+  block(R0, R1, m5(sl + 1), T_{}, 0, 0, F_{});
+  __builtin_amdgcn_s_waitcnt(0x0078);             // vmcnt(8): half h+2 landed, h+3 in flight
+  bar();
+  block(R1, R0, m5(sl + 2), T_{}, 0, 0, F_{});
+  __builtin_amdgcn_s_waitcnt(0x0070);             // vmcnt(0): half h+3 landed
+  bar();
+  block(R0, R1, m5(sl + 3), T_{}, 0, 0, F_{});
+  block(R1, R0, 0, F_{}, 0, 0, F_{});
+
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  bar();
+  constexpr int CROW = BN * 2;
+  static_for<0, 64>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int m = i >> 3, n = i & 7;
+    float x0, x1, x2, x3;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+    const int r = wr * 128 + m * 16 + (lane & 15);
+    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
+    bf16x4 v;
+    v[0] = (__bf16)x0;
+    v[1] = (__bf16)x1;
+    v[2] = (__bf16)x2;
+    v[3] = (__bf16)x3;
+    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
+  });
+  bar();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {
     const int r = i * (W4_THREADS / 32) + (tid >> 5);
     const int ch = tid & 31;
     const int sw = r & 15;
@@ -1145,6 +1455,28 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
     else if (v == 6 && K % (2 * BK) == 0)
       hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 2>), dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    else if (v >= 18 && v <= 19 && K >= 2 * BK) {
+      auto kern = v == 18 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40>
+                          : gemm_bf16_256x256_w4s<17, 19, 4, 72, 48>;
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
+    else if (v >= 15 && v <= 17 && K >= 2 * BK) {
+      auto kern = v == 15 ? gemm_bf16_256x256_w4r<12, 8>
+                : v == 16 ? gemm_bf16_256x256_w4r<16, 16>
+                          : gemm_bf16_256x256_w4r<12, 4>;
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
+    else if (v >= 20 && v <= 24 && K >= 2 * BK) {    // knock-out timings (wrong results)
+      auto kern = v == 20 ? gemm_bf16_256x256_w4<16, 16, 1>
+                : v == 21 ? gemm_bf16_256x256_w4<16, 16, 2>
+                : v == 22 ? gemm_bf16_256x256_w4<16, 16, 4>
+                : v == 23 ? gemm_bf16_256x256_w4<16, 16, 7>
+                          : gemm_bf16_256x256_w4<16, 16, 3>;
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
     else if (v >= 10 && v <= 14 && K >= 2 * BK) {
       auto kern = v == 10 ? gemm_bf16_256x256_w4<16, 16>
                 : v == 11 ? gemm_bf16_256x256_w4<12, 16>

@@ -66,13 +66,19 @@ def test_w4_accumulators_pinned(w4):
 
 def test_w4_main_loop_shape(w4):
     for body, _ in w4:
+        ko = re.match(r"\w*w4ILi\d+ELi\d+ELi(\d+)E", body)
+        if ko and int(ko.group(1)):
+            continue                        # knock-out profiling builds drop parts on purpose
         loop = re.search(r"; =>This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
         assert loop, "main loop not found"
         text = loop.group(1)
         assert text.count("v_mfma") == 128
         assert text.count("ds_read_b128") == 32
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
-        assert text.count("s_barrier") == 1
+        # v10 syncs once per K-tile; the v15 half-tile ring once per 64-MFMA block; v18 twice per
+        # K-tile (buffer free for DMA, next tile landed)
+        name = body.split(":", 1)[0]
+        assert text.count("s_barrier") == (2 if ("w4r" in name or "w4s" in name) else 1)
         assert "scratch_" not in text
         # the only padding hipcc may add is the M0 write -> LDS-DMA nop; anything else means it
         # found a dependency the asm MFMAs hide from it
