@@ -118,6 +118,11 @@ def main(argv=None) -> int:
     return _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k, extras)
 
 
+def _r(x: float) -> float:
+    """2 decimals for real GPU numbers; keep significant digits for tiny CPU rehearsals."""
+    return round(x, 2) if abs(x) >= 1 else float(f"{x:.4g}")
+
+
 def _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k, extras):
     from gpu_operator_amd.ops import gemm as G
     for _ in range(args.warmup):
@@ -140,7 +145,7 @@ def _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier
     ms_per_step = elapsed / args.steps * 1e3
     per_gpu_tflops = G.tflops(m, n, k, elapsed / args.steps)
     total_tflops = per_gpu_tflops * n_gpus
-    extras = dict(extras, per_gpu_tflops=round(per_gpu_tflops, 2))
+    extras = dict(extras, per_gpu_tflops=_r(per_gpu_tflops))
     cpu = args.device == "cpu"
     if distributed and not args.no_extras:
         from gpu_operator_amd.parallel.allreduce import measure_allreduce
@@ -166,7 +171,7 @@ def _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier
     if rank == 0:
         line = {
             "metric": "validator HIP GEMM TFLOPS (bf16 8192^3, aggregate over GPUs)",
-            "value": round(total_tflops, 2),
+            "value": _r(total_tflops),
             "unit": "TFLOP/s",
             "n_gpus": n_gpus,
             "steps": args.steps,
