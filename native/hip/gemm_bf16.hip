@@ -22,8 +22,10 @@
 //
 // Variants (AMDGO_GEMM_VARIANT / amdgo_gemm_set_variant): 1 = double-buffered baseline, 2 = fragment
 // pipelined, 3 = ping-pong (two wave groups one barrier apart, half-tile LDS ring), 4 = v3 with
-// buffer_load...lds staging, 5 = v4 with an LDS-staged, fully coalesced epilogue (default;
-// K % 128 == 0, else v2). Measured: profiles/r1_gemm_v4/.
+// buffer_load...lds staging, 5 = v4 with an LDS-staged, fully coalesced epilogue (K % 128 == 0,
+// else v2); 10-19 = one wave per SIMD with a 128x128 wave tile (v18 = the K-tile schedule, the
+// default); 25/26 = v18 persistent; 30-35 = v18 barrier-placement sweep.
+// Measured: profiles/r1_gemm_v4/, profiles/r1_s2_gemm/.
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
 
 #include <hip/hip_runtime.h>
@@ -1060,10 +1062,10 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
                         (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
   auto dma_piece = [&](int i, int k0, char* buf) {
-    const int p = i * 4 + wid;
-    const int rblk = p & 31;
-    char* lds = buf + (p >= 32 ? PANEL_BYTES : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(p >= 32 ? rB : rA, (lds_void*)lds, 16, voff,
+    // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
+    const int rblk = ((i & 7) << 2) + wid;
+    char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
                                              (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
   };
 
@@ -1172,6 +1174,215 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
     *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+  }
+}
+
+// v25/v26: v18 made persistent. gridDim = one workgroup per CU; XCD x (= blockIdx % 8) owns a
+// contiguous run of output tiles (the bijective split of xcd_remap) that its gridDim/8
+// workgroups walk in strides. The K-tile stream runs on across tile boundaries: the last two
+// K-iterations of a tile DMA the NEXT tile's K-tiles 0 and 1 into the freed buffers and the last
+// one already reads its first fragments, so the next tile starts without a cold HBM prologue.
+// The epilogue no longer needs the K buffers: each wave stages its own 128x128 sub-tile through a
+// private 8 KiB slice of the 32 KiB of LDS the K buffers leave free (2 fragment rows = 32 C rows
+// per pass, XOR-swizzled, read back as full 256-B row segments), so it needs no workgroup barrier
+// and overlaps the in-flight DMA; the accumulators are zeroed as they are read.
+constexpr int W4P_EPI_WAVE = 8192;                       // 32 rows x 128 cols x bf16
+constexpr int W4P_LDS = LDS_BYTES + 4 * W4P_EPI_WAVE;     // 160 KiB
+
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                       __bf16* __restrict__ C, int M, int N, int K) {
+  static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[W4P_LDS];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int xcd = blockIdx.x % NXCD;
+  const int per = gridDim.x / NXCD;                       // workgroups per XCD (host: gridDim % 8 == 0)
+  const int q = nwg / NXCD, rem = nwg % NXCD;
+  const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+  const int t_end = t_begin + q + (xcd < rem ? 1 : 0);
+  int tile = t_begin + (int)(blockIdx.x / NXCD);
+  if (tile >= t_end) return;                              // uniform over the workgroup
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  auto rsrc = [&](const __bf16* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, panel_bytes, 0x00020000);
+  };
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, tm, tn);
+  __amdgpu_buffer_rsrc_t rA = rsrc(A + (size_t)tm * BM * K);
+  __amdgpu_buffer_rsrc_t rB = rsrc(Bt + (size_t)tn * BN * K);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int k0, char* buf) {
+    // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
+    const int rblk = ((i & 7) << 2) + wid;
+    char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+  };
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * ROW_BYTES;
+  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  W4Frags R0, R1;
+  char* const buf0 = smem;
+  char* const buf1 = smem + BUF_BYTES;
+  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int x = w4_idx(j);
+    if constexpr (w4_isb(j))
+      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
+    else
+      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  // The v18 iteration; the DMA target (operand panels and K offset) is a runtime argument so the
+  // same body serves this tile's K-tile t+2 and the next tile's K-tiles 0 and 1.
+  // FRESH: a tile's first iteration. The vmcnt(0) before it (prologue or previous epilogue) already
+  // retired this tile's K-tile 1, so its B2 does not wait again: the epilogue's C stores are older
+  // than this iteration's DMA, and a counted vmcnt would wait for them too.
+  auto iter = [&](char* cur, char* nxt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int dk, auto FR,
+                  auto DM, auto NX) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value, fresh = decltype(FR)::value;
+    static_for<0, 128>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
+      else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
+      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
+      if constexpr (dm && i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, ra, rb, dk, cur);
+      if constexpr (nx && i == B2 - 1) {
+        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
+        if constexpr (fresh) __builtin_amdgcn_s_waitcnt(0xC07F);             // lgkmcnt(0) only
+        else __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
+      }
+      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i > B2) {
+        static_for<0, 16>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  // Wave-private epilogue: 4 passes of 2 fragment rows (32 C rows x 128 cols).
+  char* const stg = smem + LDS_BYTES + wid * W4P_EPI_WAVE;
+  auto epilogue = [&](int tm_, int tn_) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA D -> accvgpr reads
+    static_for<0, 4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      static_for<0, 16>([&](auto I) {
+        constexpr int u = decltype(I)::value;
+        constexpr int mm = u >> 3, n = u & 7;
+        constexpr int i = (2 * s + mm) * 8 + n;                    // accumulator index m*8+n
+        float x0, x1, x2, x3;
+        asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                     "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
+                     "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
+                     "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
+                     : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                     : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+        const int r = mm * 16 + (lane & 15);                       // 0..31
+        const int g = n * 4 + (lane >> 4);                         // 8-byte group 0..31
+        bf16x4 v;
+        v[0] = (__bf16)x0;
+        v[1] = (__bf16)x1;
+        v[2] = (__bf16)x2;
+        v[3] = (__bf16)x3;
+        *reinterpret_cast<bf16x4*>(stg + r * 256 + ((g ^ (r & 15)) << 3)) = v;
+      });
+      asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
+      // retire the next tile's K-tile DMAs before the first C store (see `fresh`)
+      if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = k * 4 + (lane >> 4);
+        const int ch = lane & 15;
+        const int sw = r & 15;
+        const int pg = (2 * ch) ^ sw;
+        const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
+        uint4 v = raw;
+        if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * BM + wr * 128 + s * 32 + r) * N + tn_ * BN + wc * 128 + ch * 8) = v;
+      }
+      asm volatile("" ::: "memory");
+    });
+  };
+
+  const int ktiles = K / BK;        // >= 2 (host guarantees)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, 0, buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, BK, buf1);
+  __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0): K-tiles 0 and 1 landed (FRESH iteration)
+  bar();
+  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
+
+  char* cur = buf0;
+  char* nxt = buf1;
+  for (;;) {
+    const int next = tile + per;
+    const bool has_next = next < t_end;
+    int ntm = tm, ntn = tn;
+    __amdgpu_buffer_rsrc_t nA = rA, nB = rB;
+    if (has_next) {
+      tile_coords(next, tiles_m, tiles_n, ntm, ntn);
+      nA = rsrc(A + (size_t)ntm * BM * K);
+      nB = rsrc(Bt + (size_t)ntn * BN * K);
+    }
+    const int nsteady = has_next ? ktiles : ktiles - 2;
+    auto dma_of = [&](int t, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rb) {
+      const bool nt = t + 2 >= ktiles;               // DMA the next tile's K-tile t+2-ktiles
+      ra = nt ? nA : rA;
+      rb = nt ? nB : rB;
+      return (nt ? t + 2 - ktiles : t + 2) * BK;
+    };
+    __amdgpu_buffer_rsrc_t ra, rb;
+    if (nsteady > 0) {
+      const int dk = dma_of(0, ra, rb);
+      iter(cur, nxt, ra, rb, dk, T_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    for (int t = 1; t < nsteady; ++t) {
+      const int dk = dma_of(t, ra, rb);
+      iter(cur, nxt, ra, rb, dk, F_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    if (!has_next) {
+      iter(cur, nxt, rA, rB, 0, F_{}, F_{}, T_{});
+      iter(nxt, nullptr, rA, rB, 0, F_{}, F_{}, F_{});
+    }
+    epilogue(tm, tn);
+    if (!has_next) break;
+    tile = next;
+    tm = ntm;
+    tn = ntn;
+    rA = nA;
+    rB = nB;
   }
 }
 
@@ -1423,9 +1634,24 @@ static int g_variant = -1;
 static int variant() {
   if (g_variant < 0) {
     const char* e = getenv("AMDGO_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 5;
+    g_variant = e ? atoi(e) : 18;
   }
   return g_variant;
+}
+
+// Persistent grid: one workgroup per CU (the 160 KiB LDS admits one), a multiple of the 8 XCDs,
+// never more workgroups than tiles. 0 when the device or the tile count is too small.
+static int persistent_grid(int nwg) {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  const int g = nwg < cus[dev] ? nwg : cus[dev];
+  return (g / NXCD) * NXCD;
 }
 
 extern "C" {
@@ -1459,6 +1685,22 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
       auto kern = v == 18 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40>
                           : gemm_bf16_256x256_w4s<17, 19, 4, 72, 48>;
       hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
+    else if (v >= 30 && v <= 35 && K >= 2 * BK) {    // v18 schedule sweep: later B1 barrier
+      auto kern = v == 30 ? gemm_bf16_256x256_w4s<24, 26, 5, 80, 40>
+                : v == 31 ? gemm_bf16_256x256_w4s<32, 34, 5, 80, 40>
+                : v == 32 ? gemm_bf16_256x256_w4s<40, 42, 5, 96, 24>
+                : v == 33 ? gemm_bf16_256x256_w4s<32, 34, 5, 96, 24>
+                : v == 34 ? gemm_bf16_256x256_w4s<24, 26, 4, 72, 48>
+                          : gemm_bf16_256x256_w4s<48, 50, 4, 100, 24>;
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
+    else if (v >= 25 && v <= 26 && K >= 2 * BK && persistent_grid(nwg) >= NXCD) {
+      auto kern = v == 25 ? gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40>
+                          : gemm_bf16_256x256_w4sp<17, 19, 4, 72, 48>;
+      hipLaunchKernelGGL(kern, dim3(persistent_grid(nwg)), dim3(W4_THREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     }
     else if (v >= 15 && v <= 17 && K >= 2 * BK) {
