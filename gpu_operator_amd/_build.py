@@ -89,15 +89,16 @@ def _pyext_name(stem: str) -> str:
 
 TARGETS: List[Target] = [
     # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.
-    Target("libamdgo_hip.so", ["hip/gemm_bf16.hip", "hip/smoke.hip"], "hip-shared"),
+    Target("libamdgo_hip.so", ["hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/smoke.hip"], "hip-shared",
+           headers=["include/gemm_tile_common.h"]),
     # Node agent library (sysfs/KFD topology, partitions, telemetry, inotify barriers).
     Target(_pyext_name("_amdnode"), ["node/pybind.cpp", "node/amdnode.cpp"], "pyext",
            headers=["include/amdnode.h"]),
     Target("bin/amd-barrier-wait", ["node/barrier_wait.cpp", "node/amdnode.cpp"], "cxx-exe",
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
     # Validator workload binaries (run inside the validation pods).
-    Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip"], "hip-exe",
-           flags=["-x", "hip"]),
+    Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip", "hip/gemm_fp8.hip"],
+           "hip-exe", flags=["-x", "hip"], headers=["include/gemm_tile_common.h"]),
     Target("bin/amd-hip-smoke", ["hip/hip_smoke_main.cpp", "hip/smoke.hip"], "hip-exe", flags=["-x", "hip"]),
     Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp"], "hip-exe", flags=["-x", "hip"],
            libs=["-lrccl"]),

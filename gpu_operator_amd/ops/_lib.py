@@ -47,10 +47,22 @@ def load() -> ctypes.CDLL:
         lib.amdgo_fill_uniform_bf16.restype = i
         lib.amdgo_vector_add_f32.argtypes = [vp, vp, vp, sz, vp]
         lib.amdgo_vector_add_f32.restype = i
+        lib.amdgo_gemm_fp8.argtypes = [vp, vp, vp, i, i, i, vp]
+        lib.amdgo_gemm_fp8.restype = i
+        lib.amdgo_gemm_fp8_generic.argtypes = [vp, vp, vp, i, i, i, vp]
+        lib.amdgo_gemm_fp8_generic.restype = i
+        lib.amdgo_gemm_fp8_ref_rows.argtypes = [vp, vp, vp, i, vp, i, i, vp]
+        lib.amdgo_gemm_fp8_ref_rows.restype = i
+        lib.amdgo_fill_uniform_fp8.argtypes = [vp, sz, u32, vp]
+        lib.amdgo_fill_uniform_fp8.restype = i
+        lib.amdgo_gemm_fp8_set_variant.argtypes = [i]
+        lib.amdgo_gemm_fp8_set_variant.restype = None
+        lib.amdgo_gemm_fp8_get_variant.restype = i
         lib.amdgo_gemm_set_variant.argtypes = [i]
         lib.amdgo_gemm_set_variant.restype = None
         lib.amdgo_gemm_get_variant.restype = i
-        for f in ("amdgo_gemm_tile_m", "amdgo_gemm_tile_n", "amdgo_gemm_tile_k"):
+        for f in ("amdgo_gemm_tile_m", "amdgo_gemm_tile_n", "amdgo_gemm_tile_k",
+                  "amdgo_gemm_fp8_tile_m", "amdgo_gemm_fp8_tile_n", "amdgo_gemm_fp8_tile_k"):
             getattr(lib, f).restype = i
         _LIB = lib
         return lib

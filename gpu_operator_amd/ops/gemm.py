@@ -1,7 +1,11 @@
-"""Validator GEMM: hand-written CDNA4 MFMA bf16 kernel (``native/hip/gemm_bf16.hip``).
+"""Validator GEMMs: hand-written CDNA4 MFMA kernels.
 
-``C[M,N] = A[M,K] @ Bt[N,K].T`` with bf16 operands, fp32 accumulation and bf16 output.
-Both operands are K-major, the layout the MFMA 16x16x32 fragments read without a transpose.
+``C[M,N] = A[M,K] @ Bt[N,K].T`` with fp32 accumulation and bf16 output, both operands K-major
+(the layout the MFMA fragments read without a transpose):
+
+* bf16 operands: ``native/hip/gemm_bf16.hip`` (``gemm_bf16``);
+* fp8 OCP e4m3fn operands: ``native/hip/gemm_fp8.hip`` (``gemm_fp8``), the block-scaled
+  ``v_mfma_scale_f32_32x32x64_f8f6f4`` with unit scales, i.e. the matrix cores' fp8 rate.
 
 Replaces the reference validator's ``vectorAdd`` pass/fail probe
 (reference: validator/cuda-workload-validation.yaml:20) with a matrix-core
@@ -20,11 +24,12 @@ def _stream_ptr(torch, device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def _check_operand(t, name: str, rows: int, k: int) -> None:
+def _check_operand(t, name: str, rows: int, k: int, dtype=None) -> None:
     import torch
 
-    if t.dtype != torch.bfloat16:
-        raise TypeError(f"{name} must be bfloat16, got {t.dtype}")
+    dtype = dtype or torch.bfloat16
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
     if not t.is_cuda:
         raise ValueError(f"{name} must be a GPU tensor")
     if tuple(t.shape) != (rows, k) or not t.is_contiguous():
@@ -48,6 +53,42 @@ def gemm_bf16(a, bt, out=None, *, generic: bool = False):
     err = fn(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k, _stream_ptr(torch, a.device))
     _lib.check(err, "amdgo_gemm_bf16")
     return out
+
+
+def gemm_fp8(a, bt, out=None, *, generic: bool = False):
+    """Compute ``a @ bt.T`` with fp8 (``torch.float8_e4m3fn``) operands: [M,K] and [N,K], bf16 out."""
+    import torch
+
+    m, k = a.shape
+    n = bt.shape[0]
+    f8 = torch.float8_e4m3fn
+    _check_operand(a, "a", m, k, f8)
+    _check_operand(bt, "bt", n, k, f8)
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    else:
+        _check_operand(out, "out", m, n)
+    lib = _lib.load()
+    fn = lib.amdgo_gemm_fp8_generic if generic else lib.amdgo_gemm_fp8
+    err = fn(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k, _stream_ptr(torch, a.device))
+    _lib.check(err, "amdgo_gemm_fp8")
+    return out
+
+
+def set_fp8_variant(v: int) -> None:
+    """Select the fp8 fast-path schedule (1 = default, 2..4 placements; 0 = generic kernel)."""
+    _lib.load().amdgo_gemm_fp8_set_variant(int(v))
+
+
+def get_fp8_variant() -> int:
+    return _lib.load().amdgo_gemm_fp8_get_variant()
+
+
+def fp8_fast_path_supported(m: int, n: int, k: int) -> bool:
+    lib = _lib.load()
+    tk = lib.amdgo_gemm_fp8_tile_k()
+    return m % lib.amdgo_gemm_fp8_tile_m() == 0 and n % lib.amdgo_gemm_fp8_tile_n() == 0 \
+        and k % tk == 0 and k >= 2 * tk
 
 
 def set_variant(v: int) -> None:
@@ -77,17 +118,30 @@ def fill_uniform_(t, seed: int = 1234):
     return t
 
 
+def fill_uniform_fp8_(t, seed: int = 1234):
+    """Fill an e4m3fn GPU tensor with uniform [-1, 1) values rounded by the hardware converter."""
+    import torch
+
+    if t.dtype != torch.float8_e4m3fn or not t.is_cuda or not t.is_contiguous():
+        raise ValueError("fill_uniform_fp8_ needs a contiguous float8_e4m3fn GPU tensor")
+    lib = _lib.load()
+    _lib.check(lib.amdgo_fill_uniform_fp8(t.data_ptr(), t.numel(), seed & 0xFFFFFFFF,
+                                          _stream_ptr(torch, t.device)), "fill_uniform_fp8")
+    return t
+
+
 def reference_rows(a, bt, rows):
-    """fp32 reference of selected output rows, computed by an independent scalar HIP kernel."""
+    """fp32 reference of selected output rows, computed by an independent scalar HIP kernel
+    (software e4m3 decode for fp8 operands)."""
     import torch
 
     rows_t = torch.as_tensor(rows, dtype=torch.int32, device=a.device).contiguous()
     n, k = bt.shape
     out = torch.empty((rows_t.numel(), n), dtype=torch.float32, device=a.device)
     lib = _lib.load()
-    _lib.check(lib.amdgo_gemm_ref_rows(a.data_ptr(), bt.data_ptr(), rows_t.data_ptr(),
-                                       rows_t.numel(), out.data_ptr(), n, k,
-                                       _stream_ptr(torch, a.device)), "gemm_ref_rows")
+    fn = lib.amdgo_gemm_fp8_ref_rows if a.dtype == torch.float8_e4m3fn else lib.amdgo_gemm_ref_rows
+    _lib.check(fn(a.data_ptr(), bt.data_ptr(), rows_t.data_ptr(), rows_t.numel(), out.data_ptr(), n, k,
+                  _stream_ptr(torch, a.device)), "gemm_ref_rows")
     return out
 
 

@@ -184,7 +184,8 @@ def validate_hip(ctx: Context) -> Dict[str, Any]:
     mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
     if mode == "local":
         from .workload_main import run_hip
-        results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run)
+        results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run,
+                          dtype=ctx.env.get("GEMM_DTYPE", "bf16"))
     else:
         res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
                                  _validator_env(ctx), timeout=ctx.pod_timeout)

@@ -1,6 +1,6 @@
 """``amd-validator-workload``: what runs inside the spawned validation pods.
 
-    amd-validator-workload hip  [--gemm-shapes 8192,...] [--counters]
+    amd-validator-workload hip  [--gemm-shapes 8192,...] [--gemm-dtype bf16|fp8|both] [--counters]
     amd-validator-workload rccl [--max-bytes N] [--dtype float|bf16]
 
 Runs the native workload binaries (``amd-hip-smoke``, ``amd-gemm-validate``,
@@ -83,11 +83,16 @@ def collect_counters(shape: str, run: Callable = subprocess.run) -> List[Dict]:
 
 
 def run_hip(shapes: List[str], counters: bool = False, iters: int = 20,
-            run: Callable = subprocess.run) -> List[Dict]:
+            run: Callable = subprocess.run, dtype: str = "bf16") -> List[Dict]:
+    """hip-smoke, then the MFMA GEMM probe in ``dtype`` (bf16, fp8 e4m3fn on the block-scaled
+    matrix-core path, or both), then optionally one counter-collection pass."""
     results: List[Dict] = []
     rc, r = run_json([binary("amd-hip-smoke")], run)
     results += r or [{"event": "hip-smoke", "ok": False, "rc": rc}]
-    rc, r = run_json([binary("amd-gemm-validate"), "--shapes", ",".join(shapes), "--iters", str(iters)], run)
+    cmd = [binary("amd-gemm-validate"), "--shapes", ",".join(shapes), "--iters", str(iters)]
+    if dtype != "bf16":
+        cmd += ["--dtype", dtype]
+    rc, r = run_json(cmd, run)
     results += r
     if rc != 0 and not any(x.get("event") == "gemm" for x in r):
         results.append({"event": "gemm", "ok": False, "rc": rc})
@@ -127,12 +132,13 @@ def main(argv=None) -> int:
     h.add_argument("--gemm-shapes", default=os.environ.get("GEMM_SHAPES", "8192"))
     h.add_argument("--iters", type=int, default=20)
     h.add_argument("--counters", action="store_true")
+    h.add_argument("--gemm-dtype", choices=["bf16", "fp8", "both"], default=os.environ.get("GEMM_DTYPE", "bf16"))
     r = sub.add_parser("rccl")
     r.add_argument("--max-bytes", type=int, default=int(os.environ.get("RCCL_MAX_BYTES", 1 << 30)))
     r.add_argument("--dtype", default="float")
     a = ap.parse_args(argv)
     if a.what == "hip":
-        results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters)
+        results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters, dtype=a.gemm_dtype)
         ok = all(x.get("ok", True) for x in results if x.get("event") in ("gemm", "hip-smoke"))
     else:
         results = run_rccl(a.max_bytes, a.dtype)

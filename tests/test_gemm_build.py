@@ -19,13 +19,22 @@ HIPCC = "/opt/rocm/bin/hipcc"
 pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 
 
-@pytest.fixture(scope="module")
-def asm(tmp_path_factory):
+def _compile(tmp_path_factory, src: str) -> str:
     out = tmp_path_factory.mktemp("gemm_asm") / "gemm.s"
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/native/include",
-                    "--cuda-device-only", "-S", os.path.join(ROOT, "native/hip/gemm_bf16.hip"), "-o", str(out)],
+                    "--cuda-device-only", "-S", os.path.join(ROOT, "native/hip", src), "-o", str(out)],
                    check=True, capture_output=True, timeout=600)
     return out.read_text()
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    return _compile(tmp_path_factory, "gemm_bf16.hip")
+
+
+@pytest.fixture(scope="module")
+def asm_fp8(tmp_path_factory):
+    return _compile(tmp_path_factory, "gemm_fp8.hip")
 
 
 def _kernels(asm: str, name: str):
@@ -47,20 +56,44 @@ def w4(asm):
     return _kernels(asm, "gemm_bf16_256x256_w4")
 
 
+def _no_compiler_agpr_access(body: str):
+    outside = []
+    in_asm = False
+    for line in body.splitlines():
+        if ";;#ASMSTART" in line:
+            in_asm = True
+        elif ";;#ASMEND" in line:
+            in_asm = False
+        elif not in_asm and "v_accvgpr" in line:
+            outside.append(line.strip())
+    assert not outside, outside[:5]
+
+
+def test_fp8_kernel_audit(asm_fp8):
+    """fp8 w4s: 256 pinned AGPRs, no scratch, 32 scaled MFMAs per K-tile, 2 barriers, 16 DMA pieces."""
+    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4s")
+    assert len(kernels) == 4
+    for body, st in kernels:
+        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+        _no_compiler_agpr_access(body)
+        assert len(re.findall(r"v_mfma_scale_f32_32x32x64_f8f6f4", body)) == 3 * 32
+        assert "v_mfma_f32" not in body.replace("v_mfma_scale_f32", "")
+        loop = re.search(r"; =>\s*This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
+        assert loop, "main loop not found"
+        text = loop.group(1)
+        assert text.count("v_mfma_scale") == 32
+        assert text.count("ds_read_b128") == 32
+        assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
+        assert text.count("s_barrier") == 2
+        # fragments are loaded straight into the 8-VGPR operand tuples: no VALU copies before MFMAs
+        assert "v_mov_b32" not in text
+
+
 def test_w4_accumulators_pinned(w4):
     for body, st in w4:
         assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
         assert st["NumVgprs"] <= 256
-        outside = []
-        in_asm = False
-        for line in body.splitlines():
-            if ";;#ASMSTART" in line:
-                in_asm = True
-            elif ";;#ASMEND" in line:
-                in_asm = False
-            elif not in_asm and "v_accvgpr" in line:
-                outside.append(line.strip())
-        assert not outside, outside[:5]
+        _no_compiler_agpr_access(body)
         # 3 instances of the 128-MFMA iteration (steady, last-with-read, last); the persistent
         # w4sp adds its peeled first iteration of every tile
         name = body.split(":", 1)[0]

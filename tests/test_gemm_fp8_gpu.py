@@ -1,0 +1,114 @@
+"""Numerics of the hand-written CDNA4 fp8 (OCP e4m3fn) MFMA GEMM against a PyTorch fp32 reference.
+
+The reference decodes the same fp8 operands with PyTorch (``.float()``) and multiplies in fp32;
+the kernel accumulates in fp32 and rounds to bf16, so the tolerance is a bf16 ulp of the output
+plus accumulation-order slack.
+"""
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(a, bt):
+    return a.float() @ bt.float().t()
+
+
+def _rand_fp8(shape, gen, dev):
+    import torch
+
+    return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
+
+
+@pytest.fixture(params=[1, 2, 3, 4])
+def fp8_variant(request):
+    from gpu_operator_amd.ops import gemm as G
+
+    old = G.get_fp8_variant()
+    G.set_fp8_variant(request.param)
+    yield request.param
+    G.set_fp8_variant(old)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 512), (1024, 1024, 1024),
+                                   (2048, 512, 4096), (768, 2304, 640), (256, 512, 384)])
+def test_fp8_fast_path_matches_fp32_reference(cuda_device, fp8_variant, m, n, k):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    assert G.fp8_fast_path_supported(m, n, k)
+    g = torch.Generator(device=cuda_device).manual_seed(m + 3 * n + 7 * k)
+    a = _rand_fp8((m, k), g, cuda_device)
+    bt = _rand_fp8((n, k), g, cuda_device)
+    c = G.gemm_fp8(a, bt)
+    ref = _ref(a, bt)
+    torch.testing.assert_close(c.float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (17, 33, 70), (300, 129, 65), (256, 256, 128)])
+def test_fp8_generic_path_odd_shapes(cuda_device, m, n, k):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    g = torch.Generator(device=cuda_device).manual_seed(7)
+    a = _rand_fp8((m, k), g, cuda_device)
+    bt = _rand_fp8((n, k), g, cuda_device)
+    assert not G.fp8_fast_path_supported(m, n, k)
+    c = G.gemm_fp8(a, bt)
+    torch.testing.assert_close(c.float(), _ref(a, bt), atol=3e-2, rtol=1e-2)
+
+
+def test_fp8_identity_with_asymmetric_b_catches_transposes(cuda_device):
+    """A = I with an asymmetric B of small integers (exact in e4m3 and bf16): C must equal B."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    n = 512
+    a = torch.eye(n, device=cuda_device).to(torch.float8_e4m3fn)
+    idx = torch.arange(n, device=cuda_device)
+    b = ((idx[:, None] * 3 + idx[None, :] * 7) % 17 - 8).float()      # B[k][j]
+    bt = b.t().contiguous().to(torch.float8_e4m3fn)                     # Bt[j][k]
+    for generic in (False, True):
+        c = G.gemm_fp8(a, bt, generic=generic)
+        assert torch.equal(c.float(), b), f"generic={generic}"
+
+
+def test_fp8_fast_and_reference_rows_agree_on_8k_k(cuda_device):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    m, n, k = 1024, 2048, 8192
+    a = G.fill_uniform_fp8_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device=cuda_device), 1)
+    bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device=cuda_device), 2)
+    c = G.gemm_fp8(a, bt)
+    chk = G.verify(a, bt, c, nrows=64)
+    assert chk.ok, chk
+    torch.testing.assert_close(c.float(), _ref(a, bt), atol=0.15, rtol=1e-2)
+
+
+def test_fp8_software_decoder_matches_torch_on_every_code(cuda_device):
+    """The reference kernel's e4m3 decoder (A row x unit Bt) reproduces torch's decode of all codes."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    codes = torch.arange(256, dtype=torch.int32)
+    codes = codes[(codes & 0x7F) != 0x7F].to(torch.uint8)               # drop the two NaNs
+    k = codes.numel()
+    a = codes.view(torch.float8_e4m3fn).reshape(1, k).to(cuda_device)
+    bt = torch.eye(k, device=cuda_device).to(torch.float8_e4m3fn)
+    got = G.reference_rows(a, bt, [0])[0]
+    assert torch.equal(got, a.float()[0])
+
+
+def test_fill_uniform_fp8_range_and_determinism(cuda_device):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    f8 = torch.float8_e4m3fn
+    t1 = G.fill_uniform_fp8_(torch.empty(1 << 20, dtype=f8, device=cuda_device), 5)
+    t2 = G.fill_uniform_fp8_(torch.empty(1 << 20, dtype=f8, device=cuda_device), 5)
+    assert torch.equal(t1.view(torch.uint8), t2.view(torch.uint8))
+    f = t1.float()
+    assert float(f.min()) >= -1.0 and float(f.max()) <= 1.0
+    assert abs(float(f.mean())) < 0.01
+    assert torch.unique(t1.view(torch.uint8)).numel() > 100

@@ -30,7 +30,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8: e4m3fn operands on gemm_fp8 vs hipBLASLt through torch._scaled_mm")
     a = ap.parse_args()
+    if a.dtype == "fp8":
+        return sweep_fp8(a)
     import torch
     from gpu_operator_amd.ops import gemm as G
 
@@ -70,6 +74,58 @@ def main():
             rec[f"v{v}_tflops"] = round(G.tflops(m, n, k, t_o), 1)
             rec[f"v{v}_median_tflops"] = round(G.tflops(m, n, k, sorted(ours[v])[len(ours[v]) // 2]), 1)
             rec[f"v{v}_check_ok"] = checks[v].ok
+        print(json.dumps(rec), flush=True)
+        del A, Bt, C
+        torch.cuda.empty_cache()
+
+
+def sweep_fp8(a):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    dev = torch.device("cuda", 0)
+    one = torch.ones((), dtype=torch.float32, device=dev)
+    for s in a.shapes.split(","):
+        m, n, k = map(int, s.split("x")) if "x" in s else (int(s),) * 3
+        A = G.fill_uniform_fp8_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device=dev), 1)
+        Bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device=dev), 2)
+        C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+        variants = [int(v) for v in a.variants.split(",")]
+
+        def blas():
+            return torch._scaled_mm(A, Bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+
+        try:
+            blas()
+            blas_ok = True
+        except (RuntimeError, NotImplementedError) as e:          # no hipBLASLt fp8 path
+            print(json.dumps({"m": m, "n": n, "k": k, "hipblaslt_error": str(e)[:200]}), flush=True)
+            blas_ok = False
+        checks = {}
+        for v in variants:
+            G.set_fp8_variant(v)
+            C.zero_()
+            G.gemm_fp8(A, Bt, C)
+            checks[v] = G.verify(A, Bt, C, nrows=16)
+        ours = {v: [] for v in variants}
+        tb = []
+        for _ in range(a.rounds):
+            for v in variants:
+                G.set_fp8_variant(v)
+                for _ in range(3):
+                    G.gemm_fp8(A, Bt, C)
+                ours[v].append(time_fn(lambda: G.gemm_fp8(A, Bt, C), a.iters, torch))
+            if blas_ok:
+                for _ in range(3):
+                    blas()
+                tb.append(time_fn(blas, a.iters, torch))
+        rec = {"dtype": "fp8_e4m3fn", "m": m, "n": n, "k": k,
+               "hipblaslt_tflops": round(G.tflops(m, n, k, min(tb)), 1) if tb else None}
+        for v in variants:
+            rec[f"f8v{v}_tflops"] = round(G.tflops(m, n, k, min(ours[v])), 1)
+            rec[f"f8v{v}_median_tflops"] = round(G.tflops(m, n, k, sorted(ours[v])[len(ours[v]) // 2]), 1)
+            rec[f"f8v{v}_check_ok"] = checks[v].ok
+            rec[f"f8v{v}_max_rel_err"] = round(checks[v].max_rel_err, 5)
         print(json.dumps(rec), flush=True)
         del A, Bt, C
         torch.cuda.empty_cache()
