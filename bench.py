@@ -123,6 +123,38 @@ def _r(x: float) -> float:
     return round(x, 2) if abs(x) >= 1 else float(f"{x:.4g}")
 
 
+def _fp8_extra(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync):
+    """Same shape on the fp8 (OCP e4m3fn) block-scaled MFMA kernel, after and outside the timed
+    bf16 region: the matrix cores at their fp8 rate, reported as extra fields only."""
+    from gpu_operator_amd.ops import gemm as G
+    m, n, k = args.m, args.n, args.k
+    f8 = torch.float8_e4m3fn
+    a = G.fill_uniform_fp8_(torch.empty((m, k), dtype=f8, device=dev), seed=3000 + rank)
+    bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=f8, device=dev), seed=4000 + rank)
+    c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+    steps = max(1, min(args.steps, 100))
+    for _ in range(max(1, min(args.warmup, 50))):
+        G.gemm_fp8(a, bt, c)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        G.gemm_fp8(a, bt, c)
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    chk = G.verify(a, bt, c, nrows=16, seed=rank)
+    per_gpu = G.tflops(m, n, k, elapsed / steps)
+    return {"fp8_per_gpu_tflops": _r(per_gpu), "fp8_total_tflops": _r(per_gpu * n_gpus),
+            "fp8_check_ok": chk.ok, "fp8_steps": steps}
+
+
 def _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k, extras):
     from gpu_operator_amd.ops import gemm as G
     for _ in range(args.warmup):
@@ -147,6 +179,8 @@ def _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier
     total_tflops = per_gpu_tflops * n_gpus
     extras = dict(extras, per_gpu_tflops=_r(per_gpu_tflops))
     cpu = args.device == "cpu"
+    if not cpu and not args.no_extras:
+        extras.update(_fp8_extra(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync))
     if distributed and not args.no_extras:
         from gpu_operator_amd.parallel.allreduce import measure_allreduce
         nbytes = (64 << 10) if cpu else args.allreduce_mib * (1 << 20)

@@ -23,8 +23,10 @@
 // Variants (AMDGO_GEMM_VARIANT / amdgo_gemm_set_variant): 1 = double-buffered baseline, 2 = fragment
 // pipelined, 3 = ping-pong (two wave groups one barrier apart, half-tile LDS ring), 4 = v3 with
 // buffer_load...lds staging, 5 = v4 with an LDS-staged, fully coalesced epilogue (K % 128 == 0,
-// else v2); 10-19 = one wave per SIMD with a 128x128 wave tile (v18 = the K-tile schedule, the
-// default); 25/26 = v18 persistent; 30-35 = v18 barrier-placement sweep.
+// else v2); 10-19 = one wave per SIMD with a 128x128 wave tile (v18 = the K-tile schedule);
+// 25/26 = v18 persistent; 30-35 = v18 barrier-placement sweep; 40/41 = v18 + serpentine K,
+// 42/43 = v18/v19 with the loop rotated at the B1 barrier, 44 = v18 + both (the default; on a
+// device without 256 CUs the serpentine variants fall back to 42 / 18).
 // Measured: profiles/r1_gemm_v4/, profiles/r1_s2_gemm/.
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
 
@@ -977,7 +979,7 @@ gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 //                    iteration's pieces) landed, this iteration's stay in flight -- then a barrier
 //   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
 // Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
-template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40>
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -1036,14 +1038,15 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   };
   // DM: DMA tile t+2; NX: tile t+1 exists (wait for it, read its kk0 into R0); LAST_DMA: the
   // previous iteration issued no DMA (vmcnt target 0 instead of this iteration's count)
-  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX) {
+  // slots [LO, HI) of one K-tile iteration; the slots before B1 depend on no flag (ROT splits there)
+  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX, auto LO, auto HI) {
     constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value;
-    static_for<0, 128>([&](auto I) {
+    static_for<decltype(LO)::value, decltype(HI)::value>([&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
       else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
       if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
-      if constexpr (dm && i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
       if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
       if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
       if constexpr (nx && i == B2 - 1) {
@@ -1065,22 +1068,44 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   using F_ = std::false_type;
 
   const int ktiles = K / BK;        // >= 2 (host guarantees)
+  // SERP > 0 (serpentine K): with SERP co-resident workgroups per XCD, every other wave of tiles
+  // walks K backwards, so it starts on the K-slices of the A panels the previous wave just left
+  // in the XCD's L2.
+  const bool rev = SERP > 0 && (((int)blockIdx.x / NXCD) / (SERP > 0 ? SERP : 1)) & 1;
+  auto kof = [&](int kt) { return (rev ? ktiles - 1 - kt : kt) * BK; };
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, 0, buf0);
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(0), buf0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, BK, buf1);
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(1), buf1);
   __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
   bar();
   static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
 
+  using S0 = std::integral_constant<int, 0>;
+  using SB = std::integral_constant<int, B1>;
+  using SE = std::integral_constant<int, 128>;
   char* cur = buf0;
   char* nxt = buf1;
-  for (int t = 0; t < ktiles - 2; ++t) {
-    iter(cur, nxt, (t + 2) * BK, T_{}, T_{});
-    char* tmp = cur; cur = nxt; nxt = tmp;
+  if constexpr (ROT) {
+    // Loop rotation (v42/v43): an iteration runs slots B1..127 of tile t, then 0..B1-1 of tile
+    // t+1, so the back-edge follows the explicit lgkmcnt(0) at slot B1-1 instead of the R0 reads,
+    // where hipcc's merged loop-header state is a blanket lgkmcnt(0) before the first MFMA.
+    iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, SB{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+      iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, SB{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
+  } else {
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, S0{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, S0{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
   }
-  iter(cur, nxt, 0, F_{}, T_{});
-  iter(nxt, nullptr, 0, F_{}, F_{});
 
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -1575,7 +1600,7 @@ static int g_variant = -1;
 static int variant() {
   if (g_variant < 0) {
     const char* e = getenv("AMDGO_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 18;
+    g_variant = e ? atoi(e) : 44;
   }
   return g_variant;
 }
@@ -1583,15 +1608,8 @@ static int variant() {
 // Persistent grid: one workgroup per CU (the 160 KiB LDS admits one), a multiple of the 8 XCDs,
 // never more workgroups than tiles. 0 when the device or the tile count is too small.
 static int persistent_grid(int nwg) {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
-  }
-  const int g = nwg < cus[dev] ? nwg : cus[dev];
+  const int cus = device_cu_count();
+  const int g = nwg < cus ? nwg : cus;
   return (g / NXCD) * NXCD;
 }
 
@@ -1606,7 +1624,11 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   hipStream_t s = (hipStream_t)stream;
   if (M % BM == 0 && N % BN == 0 && K % BK == 0) {
     const int nwg = (M / BM) * (N / BN);
-    const int v = variant();
+    int v = variant();
+    // Short K (K-loop of <= 32 K-tiles) with several tiles per CU: the persistent v25 hides each
+    // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %).
+    if (v == 44 && K <= 32 * BK && nwg >= 2 * device_cu_count()) v = 25;
+    if ((v == 40 || v == 41 || v == 44) && device_cu_count() != 256) v = v == 44 ? 42 : 18;
     if (v == 1)
       hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
@@ -1625,6 +1647,15 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
     else if (v >= 18 && v <= 19 && K >= 2 * BK) {
       auto kern = v == 18 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40>
                           : gemm_bf16_256x256_w4s<17, 19, 4, 72, 48>;
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
+    else if (v >= 40 && v <= 44 && K >= 2 * BK) {    // v18 + serpentine K (32 / 64 co-resident per XCD)
+      auto kern = v == 40 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32>     // or v18/v19 + loop rotation
+                : v == 41 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 64>
+                : v == 42 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true>
+                : v == 43 ? gemm_bf16_256x256_w4s<17, 19, 4, 72, 48, 0, true>
+                          : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true>;
       hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     }

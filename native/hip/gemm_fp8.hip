@@ -71,7 +71,7 @@ __device__ __forceinline__ constexpr int f8_idx(int j) {
   return j < 3 ? j : (j < 6 ? j - 3 : 3);
 }
 
-template <int B1 = 5, int D0 = 5, int DSPAN = 16, int B2 = 20, int RS = 10>
+template <int B1 = 5, int D0 = 5, int DSPAN = 16, int B2 = 20, int RS = 10, int SERP = 0, bool ROT = false>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
@@ -137,9 +137,10 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
     if constexpr (f8_isb(j)) F.b[x] = v;
     else F.a[x] = v;
   };
-  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX) {
+  // slots [LO, HI) of one K-tile iteration; the slots before B1 depend on no flag (ROT splits there)
+  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX, auto LO, auto HI) {
     constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value;
-    static_for<0, SLOTS>([&](auto I) {
+    static_for<decltype(LO)::value, decltype(HI)::value>([&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i < 16) f8_mfma<i>(R0.b[i & 3], R0.a[i >> 2], scale);
       else f8_mfma<i - 16>(R1.b[i & 3], R1.a[(i - 16) >> 2], scale);
@@ -147,7 +148,7 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
         read_frag(R1, cur, 1, std::integral_constant<int, 2 * i>{});
         read_frag(R1, cur, 1, std::integral_constant<int, 2 * i + 1>{});
       }
-      if constexpr (dm && i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
       if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
       if constexpr (dm) {
         static_for<0, 16>([&](auto J) {
@@ -178,22 +179,44 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
   using F_ = std::false_type;
 
   const int ktiles = K / F8_BK;     // >= 2 (host guarantees)
+  // SERP > 0 (serpentine K): with SERP co-resident workgroups per XCD, every other wave of tiles
+  // walks K backwards, starting on the A-panel K-slices the previous wave left in the XCD's L2.
+  const bool rev = SERP > 0 && (((int)blockIdx.x / NXCD) / (SERP > 0 ? SERP : 1)) & 1;
+  auto kof = [&](int kt) { return (rev ? ktiles - 1 - kt : kt) * F8_BK; };
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, 0, buf0);
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(0), buf0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, F8_BK, buf1);
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(1), buf1);
   __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
   bar();
   static_for<0, 8>([&](auto J) { read_frag(R0, buf0, 0, J); });
 
+  using S0 = std::integral_constant<int, 0>;
+  using SB = std::integral_constant<int, B1>;
+  using SE = std::integral_constant<int, SLOTS>;
   char* cur = buf0;
   char* nxt = buf1;
-  for (int t = 0; t < ktiles - 2; ++t) {
-    iter(cur, nxt, (t + 2) * F8_BK, T_{}, T_{});
-    char* tmp = cur; cur = nxt; nxt = tmp;
+  if constexpr (ROT) {
+    // Loop rotation: an iteration runs slots B1..31 of tile t, then slots 0..B1-1 of tile t+1, so
+    // the back-edge sits right after the explicit lgkmcnt(0) at slot B1-1. Unrotated, the
+    // back-edge falls just after the R0 reads and hipcc's merged wait state at the loop header
+    // is a blanket lgkmcnt(0) before the first MFMA, which stalls on the newest read.
+    iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, SB{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+      iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, SB{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
+  } else {
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, S0{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, S0{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
   }
-  iter(cur, nxt, 0, F_{}, T_{});
-  iter(nxt, nullptr, 0, F_{}, F_{});
 
   // epilogue through LDS; pad the last MFMA's D before the accumulator reads
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -231,6 +254,230 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
     *reinterpret_cast<uint4*>(C + (size_t)(tm * F8_BM + r) * N + tn * F8_BN + ch * 8) = v;
+  }
+}
+
+// Persistent fp8 kernel (variants 10/11): the bf16 v25 structure (gemm_bf16.hip) on the fp8 body.
+// gridDim = one workgroup per CU (a multiple of 8); XCD x (= blockIdx % 8) owns the contiguous run
+// of tiles xcd_remap gives it and its gridDim/8 workgroups walk it in strides. The K-tile stream
+// runs across tile boundaries: a tile's last two K-iterations DMA the next tile's K-tiles 0 and 1
+// into the freed buffers, so the next tile starts without a cold HBM prologue. Each wave stages its
+// own 128x128 C sub-tile through a private 8 KiB LDS slice (32 rows per pass: one row of 32x32
+// accumulators), so the epilogue needs no workgroup barrier and overlaps the in-flight DMA; the
+// accumulators are zeroed as they are read. Pays off when the K-loop is short (16384x16384x1024).
+constexpr int F8P_EPI_WAVE = 8192;                        // 32 rows x 128 cols x bf16
+constexpr int F8P_LDS = F8_LDS + 4 * F8P_EPI_WAVE;        // 160 KiB
+
+template <int B1 = 6, int D0 = 7, int DSPAN = 16, int B2 = 24, int RS = 6>
+__global__ void __launch_bounds__(F8_THREADS, 1)
+gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
+                      __bf16* __restrict__ C, int M, int N, int K) {
+  constexpr int SLOTS = 32;
+  static_assert(B1 >= 4 && D0 >= B1 && D0 + DSPAN <= SLOTS && B2 >= 16 && B2 > B1 && B2 + RS < SLOTS,
+                "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[F8P_LDS];
+
+  const int tiles_m = M / F8_BM;
+  const int tiles_n = N / F8_BN;
+  const int nwg = tiles_m * tiles_n;
+  const int xcd = blockIdx.x % NXCD;
+  const int per = gridDim.x / NXCD;                       // workgroups per XCD (host: gridDim % 8 == 0)
+  const int q = nwg / NXCD, rem = nwg % NXCD;
+  const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+  const int t_end = t_begin + q + (xcd < rem ? 1 : 0);
+  int tile = t_begin + (int)(blockIdx.x / NXCD);
+  if (tile >= t_end) return;                              // uniform over the workgroup
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const uint32_t panel_bytes = (uint32_t)F8_BM * (uint32_t)K;
+  auto rsrc = [&](const uint8_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, panel_bytes, 0x00020000);
+  };
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, tm, tn);
+  __amdgpu_buffer_rsrc_t rA = rsrc(A + (size_t)tm * F8_BM * K);
+  __amdgpu_buffer_rsrc_t rB = rsrc(Bt + (size_t)tn * F8_BN * K);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int k0, char* buf) {
+    const int rblk = ((i & 7) << 2) + wid;
+    char* lds = buf + (i >= 8 ? F8_PANEL : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K + (uint32_t)k0, 0, 0);
+  };
+
+  int lane_off[2][2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r = lane & 31;
+      const int c = kh * 4 + 2 * (lane >> 5) + s;
+      lane_off[kh][s] = r * F8_ROW + ((c ^ ((r >> 1) & 7)) << 4);
+    }
+  const int a_off = wr * 128 * F8_ROW;
+  const int b_off = F8_PANEL + wc * 128 * F8_ROW;
+  const int scale = E8M0_ONE;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  F8Frags R0, R1;
+  char* const buf0 = smem;
+  char* const buf1 = smem + F8_BUF;
+  auto read_frag = [&](F8Frags& F, const char* buf, int kh, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int x = f8_idx(j);
+    const char* base = buf + (f8_isb(j) ? b_off : a_off) + x * 32 * F8_ROW;
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(base + lane_off[kh][0]);
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(base + lane_off[kh][1]);
+    const i32x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    if constexpr (f8_isb(j)) F.b[x] = v;
+    else F.a[x] = v;
+  };
+  // The w4s iteration with the DMA target (panels, K offset) a runtime argument. FRESH = a tile's
+  // first iteration: the vmcnt(0) before it (prologue or previous epilogue) already retired its
+  // K-tile 1, and a counted vmcnt would also wait for the epilogue's C stores.
+  auto iter = [&](char* cur, char* nxt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int dk, auto FR,
+                  auto DM, auto NX) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value, fresh = decltype(FR)::value;
+    static_for<0, SLOTS>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i < 16) f8_mfma<i>(R0.b[i & 3], R0.a[i >> 2], scale);
+      else f8_mfma<i - 16>(R1.b[i & 3], R1.a[(i - 16) >> 2], scale);
+      if constexpr (i < 4) {
+        read_frag(R1, cur, 1, std::integral_constant<int, 2 * i>{});
+        read_frag(R1, cur, 1, std::integral_constant<int, 2 * i + 1>{});
+      }
+      if constexpr (i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm) {
+        static_for<0, 16>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (D0 + (j * DSPAN) / 16 == i) dma_piece(j, ra, rb, dk, cur);
+        });
+      }
+      if constexpr (nx && i == B2 - 1) {
+        constexpr int issued = [] {
+          int n = 0;
+          for (int j = 0; j < 16; ++j) n += (dm && D0 + (j * DSPAN) / 16 <= B2 - 1) ? 1 : 0;
+          return n;
+        }();
+        if constexpr (fresh) __builtin_amdgcn_s_waitcnt(0xC07F);             // lgkmcnt(0) only
+        else __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
+      }
+      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i > B2) {
+        static_for<0, 8>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (B2 + 1 + (j * RS) / 8 == i) read_frag(R0, nxt, 0, J);
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  // Wave-private epilogue: 4 passes, one per accumulator row i_m (32 C rows x 128 cols).
+  char* const stg = smem + F8_LDS + wid * F8P_EPI_WAVE;
+  auto epilogue = [&](int tm_, int tn_) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // MFMA D -> reads
+    static_for<0, 4>([&](auto S) {
+      constexpr int im = decltype(S)::value;
+      static_for<0, 16>([&](auto I) {
+        constexpr int u = decltype(I)::value;
+        constexpr int in = u >> 2, g = u & 3;
+        constexpr int a0 = 16 * (4 * im + in) + 4 * g;
+        float x0, x1, x2, x3;
+        asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                     "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
+                     "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
+                     "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
+                     : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                     : "i"(a0), "i"(a0 + 1), "i"(a0 + 2), "i"(a0 + 3));
+        const int r = lane & 31;                                   // C row inside the pass
+        const int gi = 8 * in + 2 * g + (lane >> 5);               // 8-byte column group 0..31
+        bf16x4 v;
+        v[0] = (__bf16)x0;
+        v[1] = (__bf16)x1;
+        v[2] = (__bf16)x2;
+        v[3] = (__bf16)x3;
+        *reinterpret_cast<bf16x4*>(stg + r * 256 + ((gi ^ (r & 15)) << 3)) = v;
+      });
+      asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
+      if constexpr (im == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // see FRESH
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = k * 4 + (lane >> 4);
+        const int ch = lane & 15;
+        const int sw = r & 15;
+        const int pg = (2 * ch) ^ sw;
+        const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
+        uint4 v = raw;
+        if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * F8_BM + wr * 128 + im * 32 + r) * N + tn_ * F8_BN +
+                                  wc * 128 + ch * 8) = v;
+      }
+      asm volatile("" ::: "memory");
+    });
+  };
+
+  const int ktiles = K / F8_BK;     // >= 2 (host guarantees)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, 0, buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, F8_BK, buf1);
+  __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0): K-tiles 0 and 1 landed (FRESH iteration)
+  bar();
+  static_for<0, 8>([&](auto J) { read_frag(R0, buf0, 0, J); });
+
+  char* cur = buf0;
+  char* nxt = buf1;
+  for (;;) {
+    const int next = tile + per;
+    const bool has_next = next < t_end;
+    int ntm = tm, ntn = tn;
+    __amdgpu_buffer_rsrc_t nA = rA, nB = rB;
+    if (has_next) {
+      tile_coords(next, tiles_m, tiles_n, ntm, ntn);
+      nA = rsrc(A + (size_t)ntm * F8_BM * K);
+      nB = rsrc(Bt + (size_t)ntn * F8_BN * K);
+    }
+    const int nsteady = has_next ? ktiles : ktiles - 2;
+    auto dma_of = [&](int t, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rb) {
+      const bool nt = t + 2 >= ktiles;               // DMA the next tile's K-tile t+2-ktiles
+      ra = nt ? nA : rA;
+      rb = nt ? nB : rB;
+      return (nt ? t + 2 - ktiles : t + 2) * F8_BK;
+    };
+    __amdgpu_buffer_rsrc_t ra, rb;
+    if (nsteady > 0) {
+      const int dk = dma_of(0, ra, rb);
+      iter(cur, nxt, ra, rb, dk, T_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    for (int t = 1; t < nsteady; ++t) {
+      const int dk = dma_of(t, ra, rb);
+      iter(cur, nxt, ra, rb, dk, F_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    if (!has_next) {
+      iter(cur, nxt, rA, rB, 0, F_{}, F_{}, T_{});
+      iter(nxt, nullptr, rA, rB, 0, F_{}, F_{}, F_{});
+    }
+    epilogue(tm, tn);
+    if (!has_next) break;
+    tile = next;
+    tm = ntm;
+    tn = ntn;
+    rA = nA;
+    rB = nB;
   }
 }
 
@@ -321,7 +568,7 @@ static int g_fp8_variant = -1;
 static int fp8_variant() {
   if (g_fp8_variant < 0) {
     const char* e = getenv("AMDGO_GEMM_FP8_VARIANT");
-    g_fp8_variant = e ? atoi(e) : 1;
+    g_fp8_variant = e ? atoi(e) : 9;
   }
   return g_fp8_variant;
 }
@@ -332,21 +579,39 @@ void amdgo_gemm_fp8_set_variant(int v) { g_fp8_variant = v; }
 int amdgo_gemm_fp8_get_variant() { return fp8_variant(); }
 
 // Fast path: M % 256 == 0, N % 256 == 0, K % 128 == 0, K >= 256; otherwise the generic kernel.
-// Variant 0 forces the generic kernel; 1 (default) .. 4 are schedule placements of the fast path.
+// Variant 0 forces the generic kernel; 1 .. 4 are schedule placements of the fast path,
+// 5 / 6 = 4 / 3 with serpentine K, 7 / 8 = 4 / 3 with the loop rotated at slot B1, 9 = 4 with both
+// (the default; without 256 CUs the serpentine variants fall back to 7 / 4), 10 / 11 = persistent
+// with the schedules of 4 / 3 (the default switches to 10 for K <= 2048 and >= 2 tiles per CU).
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const int v = fp8_variant();
+  int v = fp8_variant();
+  const int nwg = (M / F8_BM) * (N / F8_BN);
+  const int cus = device_cu_count();
+  const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;     // persistent grid: one WG per CU
+  // Short K (<= 16 K-tiles) with several tiles per CU: the persistent kernel hides each tile's
+  // prologue and epilogue under the neighbouring K-loops.
+  if (v == 9 && K <= 16 * F8_BK && nwg >= 2 * cus) v = 10;
+  if ((v == 5 || v == 6 || v == 9) && cus != 256) v = v == 9 ? 7 : 4;
   const auto* a = (const uint8_t*)A;
   const auto* b = (const uint8_t*)Bt;
   auto* c = (__bf16*)C;
-  if (v >= 1 && v <= 4 && M % F8_BM == 0 && N % F8_BN == 0 && K % F8_BK == 0 && K >= 2 * F8_BK) {
-    const int nwg = (M / F8_BM) * (N / F8_BN);
+  const bool fast = M % F8_BM == 0 && N % F8_BN == 0 && K % F8_BK == 0 && K >= 2 * F8_BK;
+  if (fast && v >= 10 && v <= 11 && pgrid >= NXCD) {
+    auto kern = v == 10 ? gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6> : gemm_fp8_256x256_w4sp<4, 5, 20, 22, 8>;
+    hipLaunchKernelGGL(kern, dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+  } else if (fast && v >= 1 && v <= 9) {
     auto kern = v == 1 ? gemm_fp8_256x256_w4s<5, 5, 16, 20, 10>
               : v == 2 ? gemm_fp8_256x256_w4s<5, 6, 12, 18, 12>
               : v == 3 ? gemm_fp8_256x256_w4s<4, 5, 20, 22, 8>
-                       : gemm_fp8_256x256_w4s<6, 7, 16, 24, 6>;
+              : v == 4 ? gemm_fp8_256x256_w4s<6, 7, 16, 24, 6>
+              : v == 5 ? gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32>    // v4 + serpentine K
+              : v == 6 ? gemm_fp8_256x256_w4s<4, 5, 20, 22, 8, 32>    // v3 + serpentine K
+              : v == 7 ? gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 0, true>   // v4 + loop rotation
+              : v == 8 ? gemm_fp8_256x256_w4s<4, 5, 20, 22, 8, 0, true>   // v3 + loop rotation
+                       : gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true>; // v4 + both
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
   } else {
     dim3 grid((N + G8 - 1) / G8, (M + G8 - 1) / G8);

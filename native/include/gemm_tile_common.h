@@ -66,6 +66,20 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Host: compute units of the current device (cached per device; 256 on MI355X). The serpentine-K
+// variants assume NXCD x 32 co-resident workgroups (one per CU) and are only picked at 256.
+inline int device_cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (B < E) {

@@ -71,8 +71,8 @@ def _no_compiler_agpr_access(body: str):
 
 def test_fp8_kernel_audit(asm_fp8):
     """fp8 w4s: 256 pinned AGPRs, no scratch, 32 scaled MFMAs per K-tile, 2 barriers, 16 DMA pieces."""
-    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4s")
-    assert len(kernels) == 4
+    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4sI")
+    assert len(kernels) == 9
     for body, st in kernels:
         assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
         _no_compiler_agpr_access(body)
@@ -87,6 +87,16 @@ def test_fp8_kernel_audit(asm_fp8):
         assert text.count("s_barrier") == 2
         # fragments are loaded straight into the 8-VGPR operand tuples: no VALU copies before MFMAs
         assert "v_mov_b32" not in text
+
+
+def test_fp8_persistent_kernel_audit(asm_fp8):
+    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4spI")
+    assert len(kernels) == 2
+    for body, st in kernels:
+        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+        _no_compiler_agpr_access(body)
+        # fresh + steady iterations of every tile, plus the two tail iterations of the last one
+        assert len(re.findall(r"v_mfma_scale_f32_32x32x64_f8f6f4", body)) == 4 * 32
 
 
 def test_w4_accumulators_pinned(w4):

@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[1, 2, 3, 4])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
@@ -31,7 +31,8 @@ def fp8_variant(request):
 
 
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 512), (1024, 1024, 1024),
-                                   (2048, 512, 4096), (768, 2304, 640), (256, 512, 384)])
+                                   (2048, 512, 4096), (768, 2304, 640), (256, 512, 384),
+                                   (4608, 4608, 512)])   # > 256 tiles: serpentine waves reverse K
 def test_fp8_fast_path_matches_fp32_reference(cuda_device, fp8_variant, m, n, k):
     import torch
     from gpu_operator_amd.ops import gemm as G

@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 25, 26])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 25, 26, 40, 41, 42, 43, 44])
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -19,7 +19,8 @@ def variant(request):
 
 
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 256), (1024, 1024, 1024),
-                                   (2048, 512, 4096), (768, 2304, 640), (256, 512, 128)])
+                                   (2048, 512, 4096), (768, 2304, 640), (256, 512, 128),
+                                   (4608, 4608, 512)])   # > 256 tiles: serpentine waves reverse K
 def test_fast_path_matches_fp32_reference(cuda_device, variant, m, n, k):
     import torch
     from gpu_operator_amd.ops import gemm as G

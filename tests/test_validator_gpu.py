@@ -34,6 +34,17 @@ def test_gemm_validate_binary_checks_and_reports_tflops():
     assert agg["per_gpu_tflops"] > 900           # MI355X bf16 dense, random operands
 
 
+def test_gemm_validate_binary_fp8_and_both():
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "8192", "--dtype", "both", "--iters", "10")
+    assert rc == 0, err
+    gemms = [x for x in lines if x["event"] == "gemm"]
+    assert {g["dtype"] for g in gemms} == {"bf16", "fp8_e4m3fn"} and all(g["ok"] for g in gemms)
+    agg = {x["dtype"]: x["per_gpu_tflops"] for x in lines if x["event"] == "aggregate"}
+    assert agg["fp8_e4m3fn"] > 1.5 * agg["bf16"]   # the block-scaled fp8 MFMA runs at 2x the bf16 rate
+    rc, lines, err = run("amd-gemm-validate", "--dtype", "fp4")
+    assert rc == 2 and "unknown --dtype" in lines[0]["error"]
+
+
 def test_rccl_validate_binary():
     rc, lines, err = run("amd-rccl-validate", "--max-bytes", str(1 << 26), "--iters", "5", "--warmup", "2")
     assert rc == 0, err

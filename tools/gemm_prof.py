@@ -15,8 +15,11 @@ def main():
     ap.add_argument("--variant", type=int, default=4)
     ap.add_argument("--size", default="8192")
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--blas", action="store_true", help="run hipBLASLt (torch.matmul) instead")
+    ap.add_argument("--blas", action="store_true", help="run hipBLASLt (torch.matmul / _scaled_mm) instead")
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16")
     a = ap.parse_args()
+    if a.dtype == "fp8":
+        return main_fp8(a)
     import torch
     from gpu_operator_amd.ops import gemm as G
     m, n, k = (map(int, a.size.split("x")) if "x" in a.size else [int(a.size)] * 3)
@@ -32,6 +35,26 @@ def main():
             torch.matmul(A, Bt.t(), out=C)
         else:
             G.gemm_bf16(A, Bt, C)
+    torch.cuda.synchronize()
+    print("ok", G.verify(A, Bt, C, nrows=8).ok)
+
+
+def main_fp8(a):
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+    m, n, k = (map(int, a.size.split("x")) if "x" in a.size else [int(a.size)] * 3)
+    dev = torch.device("cuda", 0)
+    f8 = torch.float8_e4m3fn
+    A = G.fill_uniform_fp8_(torch.empty((m, k), dtype=f8, device=dev), 1)
+    Bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=f8, device=dev), 2)
+    C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+    one = torch.ones((), dtype=torch.float32, device=dev)
+    G.set_fp8_variant(a.variant)
+    for _ in range(a.iters):
+        if a.blas:
+            C = torch._scaled_mm(A, Bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+        else:
+            G.gemm_fp8(A, Bt, C)
     torch.cuda.synchronize()
     print("ok", G.verify(A, Bt, C, nrows=8).ok)
 

@@ -13,7 +13,8 @@ def summarise(d):
     agg = collections.defaultdict(float)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "gemm" not in r["Kernel_Name"] and "Cijk" not in r["Kernel_Name"]:
+            name = r["Kernel_Name"]
+            if ("gemm" not in name and "Cijk" not in name) or "ref_rows" in name:
                 continue
             agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     per = collections.defaultdict(list)
