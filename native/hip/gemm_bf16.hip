@@ -1155,7 +1155,7 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
 constexpr int W4P_EPI_WAVE = 8192;                       // 32 rows x 128 cols x bf16
 constexpr int W4P_LDS = LDS_BYTES + 4 * W4P_EPI_WAVE;     // 160 KiB
 
-template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40>
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, bool SERP = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
@@ -1300,10 +1300,14 @@ gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ 
   };
 
   const int ktiles = K / BK;        // >= 2 (host guarantees)
+  // SERP (v27): a workgroup's i-th tile belongs to wave i of its XCD; odd waves walk K backwards
+  // and start on the A-panel K-slices the previous wave left in the XCD's L2.
+  bool rev = false;
+  auto kof = [&](int kt, bool r) { return (r ? ktiles - 1 - kt : kt) * BK; };
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, 0, buf0);
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(0, rev), buf0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, BK, buf1);
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(1, rev), buf1);
   __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0): K-tiles 0 and 1 landed (FRESH iteration)
   bar();
   static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
@@ -1325,7 +1329,7 @@ gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ 
       const bool nt = t + 2 >= ktiles;               // DMA the next tile's K-tile t+2-ktiles
       ra = nt ? nA : rA;
       rb = nt ? nB : rB;
-      return (nt ? t + 2 - ktiles : t + 2) * BK;
+      return nt ? kof(t + 2 - ktiles, SERP && !rev) : kof(t + 2, rev);
     };
     __amdgpu_buffer_rsrc_t ra, rb;
     if (nsteady > 0) {
@@ -1345,6 +1349,7 @@ gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ 
     epilogue(tm, tn);
     if (!has_next) break;
     tile = next;
+    rev = SERP && !rev;
     tm = ntm;
     tn = ntn;
     rA = nA;
@@ -1669,9 +1674,10 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
       hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     }
-    else if (v >= 25 && v <= 26 && K >= 2 * BK && persistent_grid(nwg) >= NXCD) {
+    else if (v >= 25 && v <= 27 && K >= 2 * BK && persistent_grid(nwg) >= NXCD) {
       auto kern = v == 25 ? gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40>
-                          : gemm_bf16_256x256_w4sp<17, 19, 4, 72, 48>;
+                : v == 26 ? gemm_bf16_256x256_w4sp<17, 19, 4, 72, 48>
+                          : gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, true>;   // 25 + serpentine K
       hipLaunchKernelGGL(kern, dim3(persistent_grid(nwg)), dim3(W4_THREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     }

@@ -268,7 +268,7 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
 constexpr int F8P_EPI_WAVE = 8192;                        // 32 rows x 128 cols x bf16
 constexpr int F8P_LDS = F8_LDS + 4 * F8P_EPI_WAVE;        // 160 KiB
 
-template <int B1 = 6, int D0 = 7, int DSPAN = 16, int B2 = 24, int RS = 6>
+template <int B1 = 6, int D0 = 7, int DSPAN = 16, int B2 = 24, int RS = 6, bool SERP = false>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -429,10 +429,15 @@ gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__
   };
 
   const int ktiles = K / F8_BK;     // >= 2 (host guarantees)
+  // SERP: the workgroups of an XCD reach their i-th tile together, so tile i of every workgroup is
+  // one wave of co-resident tiles; odd waves walk K backwards and start on the A-panel K-slices
+  // the previous wave left in the XCD's L2.
+  bool rev = false;
+  auto kof = [&](int kt, bool r) { return (r ? ktiles - 1 - kt : kt) * F8_BK; };
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, 0, buf0);
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(0, rev), buf0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, F8_BK, buf1);
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(1, rev), buf1);
   __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0): K-tiles 0 and 1 landed (FRESH iteration)
   bar();
   static_for<0, 8>([&](auto J) { read_frag(R0, buf0, 0, J); });
@@ -454,7 +459,7 @@ gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__
       const bool nt = t + 2 >= ktiles;               // DMA the next tile's K-tile t+2-ktiles
       ra = nt ? nA : rA;
       rb = nt ? nB : rB;
-      return (nt ? t + 2 - ktiles : t + 2) * F8_BK;
+      return nt ? kof(t + 2 - ktiles, SERP && !rev) : kof(t + 2, rev);
     };
     __amdgpu_buffer_rsrc_t ra, rb;
     if (nsteady > 0) {
@@ -474,6 +479,7 @@ gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__
     epilogue(tm, tn);
     if (!has_next) break;
     tile = next;
+    rev = SERP && !rev;
     tm = ntm;
     tn = ntn;
     rA = nA;
@@ -582,7 +588,8 @@ int amdgo_gemm_fp8_get_variant() { return fp8_variant(); }
 // Variant 0 forces the generic kernel; 1 .. 4 are schedule placements of the fast path,
 // 5 / 6 = 4 / 3 with serpentine K, 7 / 8 = 4 / 3 with the loop rotated at slot B1, 9 = 4 with both
 // (the default; without 256 CUs the serpentine variants fall back to 7 / 4), 10 / 11 = persistent
-// with the schedules of 4 / 3 (the default switches to 10 for K <= 2048 and >= 2 tiles per CU).
+// with the schedules of 4 / 3, 12 = 10 with serpentine K (the default switches to 10 for K <= 2048
+// and >= 2 tiles per CU).
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
@@ -599,8 +606,10 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
   const auto* b = (const uint8_t*)Bt;
   auto* c = (__bf16*)C;
   const bool fast = M % F8_BM == 0 && N % F8_BN == 0 && K % F8_BK == 0 && K >= 2 * F8_BK;
-  if (fast && v >= 10 && v <= 11 && pgrid >= NXCD) {
-    auto kern = v == 10 ? gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6> : gemm_fp8_256x256_w4sp<4, 5, 20, 22, 8>;
+  if (fast && v >= 10 && v <= 12 && pgrid >= NXCD) {
+    auto kern = v == 10 ? gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>
+              : v == 11 ? gemm_fp8_256x256_w4sp<4, 5, 20, 22, 8>
+                        : gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6, true>;   // 10 + serpentine K
     hipLaunchKernelGGL(kern, dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
   } else if (fast && v >= 1 && v <= 9) {
     auto kern = v == 1 ? gemm_fp8_256x256_w4s<5, 5, 16, 20, 10>

@@ -91,7 +91,7 @@ def test_fp8_kernel_audit(asm_fp8):
 
 def test_fp8_persistent_kernel_audit(asm_fp8):
     kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4spI")
-    assert len(kernels) == 2
+    assert len(kernels) == 3
     for body, st in kernels:
         assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
         _no_compiler_agpr_access(body)

@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
