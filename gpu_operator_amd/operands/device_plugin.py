@@ -45,6 +45,14 @@ PARTITION_PREFIX = "amd.com/partition-"
 REPLICA_SEP = "::"
 
 
+def _unlink(path: str) -> None:
+    """Remove a unix socket path that grpc's ``server.stop()`` may be unlinking concurrently."""
+    try:
+        os.remove(path)
+    except FileNotFoundError:
+        pass
+
+
 @dataclass
 class Device:
     id: str
@@ -241,8 +249,7 @@ class ResourceServer:
     # -- lifecycle ----------------------------------------------------------------------------
     def serve(self) -> None:
         import grpc
-        if os.path.exists(self.socket):
-            os.remove(self.socket)
+        _unlink(self.socket)
         self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=8))
         self.server.add_generic_rpc_handlers((K.device_plugin_handler(self),))
         self.server.add_insecure_port("unix://" + self.socket)
@@ -261,8 +268,7 @@ class ResourceServer:
         self.notify()
         if self.server is not None:
             self.server.stop(grace=1)
-        if os.path.exists(self.socket):
-            os.remove(self.socket)
+        _unlink(self.socket)
 
 
 class DevicePlugin:

@@ -30,6 +30,14 @@ from . import kubeletapi as K
 log = logging.getLogger("amd-sandbox-device-plugin")
 
 
+def _unlink(path: str) -> None:
+    """Remove a unix socket path that grpc's ``server.stop()`` may be unlinking concurrently."""
+    try:
+        os.remove(path)
+    except FileNotFoundError:
+        pass
+
+
 def resource_name(device_id: int, is_vf: bool) -> str:
     hit = models.by_device_id(device_id)
     name = hit[0].name if hit else f"DEVICE_{device_id:04X}"
@@ -128,8 +136,7 @@ class VfioResourceServer:
 
     def serve(self) -> None:
         import grpc
-        if os.path.exists(self.socket):
-            os.remove(self.socket)
+        _unlink(self.socket)
         self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=4))
         self.server.add_generic_rpc_handlers((K.device_plugin_handler(self),))
         self.server.add_insecure_port("unix://" + self.socket)
@@ -147,8 +154,7 @@ class VfioResourceServer:
         self.notify()
         if self.server is not None:
             self.server.stop(grace=1)
-        if os.path.exists(self.socket):
-            os.remove(self.socket)
+        _unlink(self.socket)
 
 
 class SandboxDevicePlugin:
