@@ -979,7 +979,8 @@ gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
 //                    iteration's pieces) landed, this iteration's stay in flight -- then a barrier
 //   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
 // Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
-template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false>
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
+          bool SQ = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -990,7 +991,8 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   const int tiles_n = N / BN;
   const int nwg = tiles_m * tiles_n;
   int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+  if constexpr (SQ) tile_coords_sq(blockIdx.x, tiles_n, tm, tn);
+  else tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1633,7 +1635,14 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
     // Short K (K-loop of <= 32 K-tiles) with several tiles per CU: the persistent v25 hides each
     // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %).
     if (v == 44 && K <= 32 * BK && nwg >= 2 * device_cu_count()) v = 25;
-    if ((v == 40 || v == 41 || v == 44) && device_cu_count() != 256) v = v == 44 ? 42 : 18;
+    // Big grids (>= 8 dispatch waves) with long K: the square cross-XCD raster (v45) streams fewer
+    // distinct panels per wave (profiles/r1_s6_sq: 12288^3 +5.5 %, 16384x8192x8192 +2.9 %,
+    // 16384^3 +3.4 %; at 4 waves or K = 4096 it measured 1 % behind v44, so those stay on v44).
+    if (v == 44 && (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && nwg >= 8 * device_cu_count() && K >= 128 * BK)
+      v = 45;
+    if (v == 46) v = 44;                              // v44 pinned (no automatic switch), for A/B runs
+    if ((v == 40 || v == 41 || v == 44 || v == 45) && device_cu_count() != 256) v = (v == 44 || v == 45) ? 42 : 18;
+    if (v == 45 && ((M / BM) % 16 != 0 || (N / BN) % 16 != 0)) v = 44;   // square raster needs 16x16 super-tiles
     if (v == 1)
       hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
@@ -1654,6 +1663,10 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                           : gemm_bf16_256x256_w4s<17, 19, 4, 72, 48>;
       hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+    }
+    else if (v == 45 && K >= 2 * BK) {               // v44 + square cross-XCD raster
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
+                         0, s, (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
     }
     else if (v >= 40 && v <= 44 && K >= 2 * BK) {    // v18 + serpentine K (32 / 64 co-resident per XCD)
       auto kern = v == 40 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32>     // or v18/v19 + loop rotation

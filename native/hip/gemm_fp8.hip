@@ -71,7 +71,8 @@ __device__ __forceinline__ constexpr int f8_idx(int j) {
   return j < 3 ? j : (j < 6 ? j - 3 : 3);
 }
 
-template <int B1 = 5, int D0 = 5, int DSPAN = 16, int B2 = 20, int RS = 10, int SERP = 0, bool ROT = false>
+template <int B1 = 5, int D0 = 5, int DSPAN = 16, int B2 = 20, int RS = 10, int SERP = 0, bool ROT = false,
+          bool SQ = false>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
@@ -84,7 +85,8 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
   const int tiles_n = N / F8_BN;
   const int nwg = tiles_m * tiles_n;
   int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+  if constexpr (SQ) tile_coords_sq(blockIdx.x, tiles_n, tm, tn);   // square cross-XCD raster (v13)
+  else tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -589,7 +591,9 @@ int amdgo_gemm_fp8_get_variant() { return fp8_variant(); }
 // 5 / 6 = 4 / 3 with serpentine K, 7 / 8 = 4 / 3 with the loop rotated at slot B1, 9 = 4 with both
 // (the default; without 256 CUs the serpentine variants fall back to 7 / 4), 10 / 11 = persistent
 // with the schedules of 4 / 3, 12 = 10 with serpentine K (the default switches to 10 for K <= 2048
-// and >= 2 tiles per CU).
+// and >= 2 tiles per CU), 13 = 9 with the square cross-XCD raster (the default switches to 13 for
+// >= 16 dispatch waves with K >= 16384 when both tile counts are multiples of 16), 14 = 9 without
+// the automatic switches.
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
@@ -601,7 +605,13 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
   // Short K (<= 16 K-tiles) with several tiles per CU: the persistent kernel hides each tile's
   // prologue and epilogue under the neighbouring K-loops.
   if (v == 9 && K <= 16 * F8_BK && nwg >= 2 * cus) v = 10;
-  if ((v == 5 || v == 6 || v == 9) && cus != 256) v = v == 9 ? 7 : 4;
+  // The square cross-XCD raster (v13, as bf16 v45) only pays for fp8 on the biggest grids: at
+  // 16384^3 +4.3 %, but 12288^3, 16384x8192x8192 and 16384^2x8192 ran 1-3 % behind v9
+  // (profiles/r1_s6_sq). fp8 panels are half the bytes, so the panel traffic it saves matters less.
+  if (v == 9 && (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0 && nwg >= 16 * cus && K >= 128 * F8_BK) v = 13;
+  if (v == 13 && ((M / F8_BM) % 16 != 0 || (N / F8_BN) % 16 != 0)) v = 9;
+  if (v == 14) v = 9;                                   // v9 pinned (no automatic switch), for A/B runs
+  if ((v == 5 || v == 6 || v == 9 || v == 13) && cus != 256) v = (v == 9 || v == 13) ? 7 : 4;
   const auto* a = (const uint8_t*)A;
   const auto* b = (const uint8_t*)Bt;
   auto* c = (__bf16*)C;
@@ -611,6 +621,9 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
               : v == 11 ? gemm_fp8_256x256_w4sp<4, 5, 20, 22, 8>
                         : gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6, true>;   // 10 + serpentine K
     hipLaunchKernelGGL(kern, dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+  } else if (fast && v == 13) {
+    hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true, true>), dim3(nwg), dim3(F8_THREADS), 0, s,
+                       a, b, c, M, N, K);
   } else if (fast && v >= 1 && v <= 9) {
     auto kern = v == 1 ? gemm_fp8_256x256_w4s<5, 5, 16, 20, 10>
               : v == 2 ? gemm_fp8_256x256_w4s<5, 6, 12, 18, 12>

@@ -59,6 +59,25 @@ __device__ __forceinline__ void tile_coords(int wgid, int tiles_m, int tiles_n, 
   tn = in_group / gsize;
 }
 
+// Square cross-XCD raster (v45): one dispatch wave of 256 workgroups (32 per XCD, one per CU)
+// covers a 16x16-tile super-tile; XCD x owns its 8x4 sub-block (rows 8*(x&1), cols 4*(x>>1)).
+// Per wave the chip then streams 16 A + 16 B panels instead of 64 A + 4 B (16384^3) or
+// 32 A + 8 B (8192^3) for the XCD-contiguous raster, and XCD pairs / quads read the same B / A
+// panel K-slices at the same time (MALL hits). Consecutive waves walk N inside a super-row (an
+// XCD keeps its A panels, so serpentine K still finds their K-slices in L2); super-rows snake.
+// Host guarantees tiles_m % 16 == 0 and tiles_n % 16 == 0, so the map is a bijection.
+__device__ __forceinline__ void tile_coords_sq(int bid, int tiles_n, int& tm, int& tn) {
+  const int wave = bid >> 8;
+  const int xcd = bid & (NXCD - 1);
+  const int slot = (bid & 255) >> 3;
+  const int sn = tiles_n >> 4;
+  const int sr = wave / sn;
+  int sc = wave - sr * sn;
+  if (sr & 1) sc = sn - 1 - sc;
+  tm = (sr << 4) + ((xcd & 1) << 3) + (slot & 7);
+  tn = (sc << 4) + ((xcd >> 1) << 2) + (slot >> 3);
+}
+
 // Raw s_barrier pinned in place (no implicit vmcnt(0) as __syncthreads() would emit).
 __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);

@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
@@ -32,7 +32,8 @@ def fp8_variant(request):
 
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 512), (1024, 1024, 1024),
                                    (2048, 512, 4096), (768, 2304, 640), (256, 512, 384),
-                                   (4608, 4608, 512)])   # > 256 tiles: serpentine waves reverse K
+                                   (4608, 4608, 512),     # > 256 tiles: serpentine waves reverse K
+                                   (4096, 8192, 256), (8192, 4096, 384)])   # 16x16-tile super-tiles (v13)
 def test_fp8_fast_path_matches_fp32_reference(cuda_device, fp8_variant, m, n, k):
     import torch
     from gpu_operator_amd.ops import gemm as G
@@ -113,3 +114,29 @@ def test_fill_uniform_fp8_range_and_determinism(cuda_device):
     assert float(f.min()) >= -1.0 and float(f.max()) <= 1.0
     assert abs(float(f.mean())) < 0.01
     assert torch.unique(t1.view(torch.uint8)).numel() > 100
+
+
+def test_fp8_square_raster_covers_every_tile(cuda_device):
+    """The square cross-XCD raster (v13) over 12288x12288x8192 (48x48 tiles, 9 dispatch waves,
+    snaking super-rows); one checked row per tile row covers every output tile."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    old = G.get_fp8_variant()
+    G.set_fp8_variant(13)
+    try:
+        _check_square_raster_fp8(cuda_device, G, torch)
+    finally:
+        G.set_fp8_variant(old)
+
+
+def _check_square_raster_fp8(cuda_device, G, torch):
+    m = n = 12288
+    k = 8192
+    g = torch.Generator(device=cuda_device).manual_seed(99)
+    a = _rand_fp8((m, k), g, cuda_device)
+    bt = _rand_fp8((n, k), g, cuda_device)
+    c = G.gemm_fp8(a, bt)
+    rows = torch.tensor([tm * 256 + (tm * 53) % 256 for tm in range(m // 256)], device=cuda_device)
+    ref = a[rows].float() @ bt.float().t()
+    torch.testing.assert_close(c[rows].float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)

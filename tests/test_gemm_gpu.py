@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 25, 26, 27, 40, 41, 42, 43, 44])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 25, 26, 27, 40, 41, 42, 43, 44, 45])
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -20,7 +20,8 @@ def variant(request):
 
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 256), (1024, 1024, 1024),
                                    (2048, 512, 4096), (768, 2304, 640), (256, 512, 128),
-                                   (4608, 4608, 512)])   # > 256 tiles: serpentine waves reverse K
+                                   (4608, 4608, 512),     # > 256 tiles: serpentine waves reverse K
+                                   (4096, 8192, 256), (8192, 4096, 192)])   # 16x16-tile super-tiles (v45)
 def test_fast_path_matches_fp32_reference(cuda_device, variant, m, n, k):
     import torch
     from gpu_operator_amd.ops import gemm as G
@@ -91,3 +92,21 @@ def test_smoke_vector_add(cuda_device):
 
     assert smoke.smoke(n=50_000, device=str(cuda_device))
     assert smoke.smoke(n=1_000_003, device=str(cuda_device))
+
+
+def test_default_dispatch_square_raster_covers_every_tile(cuda_device):
+    """12288x12288x8192 (48x48 tiles, 9 dispatch waves) takes the square cross-XCD raster (v45)
+    under the default variant; one checked row per tile row covers every output tile."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    m = n = 12288
+    k = 8192
+    a = torch.empty((m, k), dtype=torch.bfloat16, device=cuda_device)
+    bt = torch.empty((n, k), dtype=torch.bfloat16, device=cuda_device)
+    G.fill_uniform_(a, 3)
+    G.fill_uniform_(bt, 4)
+    c = G.gemm_bf16(a, bt)
+    rows = torch.tensor([tm * 256 + (tm * 37) % 256 for tm in range(m // 256)], device=cuda_device)
+    ref = a[rows].float() @ bt.float().t()
+    torch.testing.assert_close(c[rows].float(), ref, atol=0.15, rtol=1e-2)
