@@ -7,11 +7,25 @@ null. One *step* is one validator GEMM probe per GPU: C = A @ Bt^T, bf16 8192x81
 hand-written CDNA4 MFMA kernel (native/hip/gemm_bf16.hip), uniform [-1,1) synthetic operands.
 Per-GPU work is fixed as N grows (weak scaling); ``value`` is the whole-job aggregate TFLOPS.
 
-Launch: ``python bench.py`` (1 GPU) or, for N>1, one rank per GPU under
-``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
-After the timed region (and outside it) the job also measures, and reports as extra fields:
-the RCCL all-reduce bus bandwidth over xGMI (N>1) and the node validation chain time
-(driver/device checks -> hip-smoke -> GEMM check) that gates the validator's readiness.
+Launch modes (both give one rank per GPU over RCCL):
+
+* ``python bench.py --gpus N`` with no ``WORLD_SIZE`` in the environment: this process never
+  touches the GPU; it checks that N devices are visible (exit 3 otherwise, never a silent
+  1-GPU run) and starts ``torch.distributed.run`` with N ranks as a child process.
+* ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``: the ranks read
+  RANK/LOCAL_RANK/WORLD_SIZE; ``--gpus`` must equal WORLD_SIZE.
+
+Timing protocol per rank: ``--warmup`` untimed steps, then a *clock-stabilisation* phase
+(outside the timed region) that keeps issuing GEMMs until the per-dispatch event times of the
+last 10 dispatches agree within 2 % (at least 50 dispatches, capped in time) -- MI355X
+ramps its clocks over the first ~25 back-to-back GEMMs (profiles/r1_s6_sq), and timing that
+transient under-reports steady-state throughput. Then exactly ``--steps`` steps are timed,
+bracketed by barrier + synchronize on both sides, MAX over ranks. Per-step event times give
+the median / p90. The same protocol is then applied, in the same process, to
+``torch.matmul`` on the same operands (hipBLASLt) so ``ratio_vs_hipblaslt`` is checkable.
+
+After the timed region the job also reports the fp8 kernel at the same shape, the RCCL
+all-reduce bus bandwidth over xGMI (N>1), and the validator's per-GPU check chain.
 """
 
 from __future__ import annotations
@@ -19,44 +33,91 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
 
 def parse_args(argv=None):
-    ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="number of GPUs/ranks (default: WORLD_SIZE if set, else 1)")
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--k", type=int, default=8192)
     ap.add_argument("--shape", default=None, help="MxNxK (overrides --m/--n/--k; safe under torchrun)")
     ap.add_argument("--allreduce-mib", type=int, default=256,
                     help="payload of the post-timing RCCL all-reduce probe (N>1)")
-    ap.add_argument("--no-extras", action="store_true", help="skip the all-reduce/validation extras")
+    ap.add_argument("--stabilise-max-s", type=float, default=6.0,
+                    help="time cap of the clock-stabilisation phase (outside the timed region)")
+    ap.add_argument("--no-extras", action="store_true", help="skip fp8/hipBLASLt/all-reduce/validation extras")
     ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
                     help="cpu = rehearsal of the distributed plumbing (gloo, torch.matmul) for tests only")
     a = ap.parse_args(argv)
     if a.shape:
         a.m, a.n, a.k = (int(x) for x in a.shape.lower().split("x"))
+    if a.gpus is None:
+        a.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
     return a
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _visible_gpus() -> int:
+    """Device count without initialising the GPU in this (launcher) process."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def launch(args, argv) -> int:
+    """Parent of an N-rank run: never initialises the GPU, starts torch.distributed.run as a child."""
+    if args.device == "gpu":
+        have = _visible_gpus()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) visible; "
+                  "refusing to run on fewer", file=sys.stderr)
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += list(sys.argv[1:] if argv is None else argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if args.device == "cpu":
+        env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args, argv)
+
     import torch
     import torch.distributed as dist
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, ROOT)
     from gpu_operator_amd.ops import gemm as G
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    n_gpus = world
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing a mismatched run", file=sys.stderr)
+        return 3
     cpu = args.device == "cpu"
     distributed = world > 1
     if cpu:
@@ -64,30 +125,26 @@ def main(argv=None) -> int:
         if distributed:
             dist.init_process_group("gloo")
     else:
+        if torch.cuda.device_count() <= local_rank:
+            print(f"rank {rank}: LOCAL_RANK {local_rank} but {torch.cuda.device_count()} GPU(s) visible",
+                  file=sys.stderr)
+            return 3
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
         if distributed:
             dist.init_process_group("nccl", device_id=dev)
-
-    def barrier():
-        if distributed:
-            if cpu:
-                dist.barrier()
-            else:
-                dist.barrier(device_ids=[local_rank])
-
-    def sync():
-        if not cpu:
-            torch.cuda.synchronize(dev)
+    ctx = Ctx(args, torch, dist, dev, rank, local_rank, world, distributed, cpu)
 
     m, n, k = args.m, args.n, args.k
     a = torch.empty((m, k), dtype=torch.bfloat16, device=dev)
     bt = torch.empty((n, k), dtype=torch.bfloat16, device=dev)
     c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+    extras = {}
     if cpu:
         g = torch.Generator().manual_seed(1000 + rank)
         a.copy_(torch.rand((m, k), generator=g) * 2 - 1)
         bt.copy_(torch.rand((n, k), generator=g) * 2 - 1)
+        extras["device"] = "cpu-rehearsal"
 
         def step():
             torch.matmul(a, bt.t(), out=c)
@@ -98,24 +155,58 @@ def main(argv=None) -> int:
         def step():
             G.gemm_bf16(a, bt, c)
 
-    if cpu:
-        return _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k,
-                                 {"device": "cpu-rehearsal"})
+        # Validation chain (what the validator pod does before reporting ready), untimed.
+        t_chain0 = time.perf_counter()
+        from gpu_operator_amd.ops import smoke as S
+        smoke_ok = S.smoke(device=str(dev))
+        G.gemm_bf16(a, bt, c)
+        chk = G.verify(a, bt, c, nrows=32, seed=rank)
+        torch.cuda.synchronize(dev)
+        if not (smoke_ok and chk.ok):
+            print(f"rank {rank}: validation FAILED smoke={smoke_ok} gemm={chk}", file=sys.stderr)
+            return 2
+        extras.update(gemm_check_max_rel_err=chk.max_rel_err,
+                      validation_chain_s=round(time.perf_counter() - t_chain0, 4))
 
-    # Validation chain (what the validator pod does before reporting ready).
-    t_chain0 = time.perf_counter()
-    from gpu_operator_amd.ops import smoke as S
-    smoke_ok = S.smoke(device=str(dev))
-    G.gemm_bf16(a, bt, c)
-    chk = G.verify(a, bt, c, nrows=32, seed=rank)
-    torch.cuda.synchronize(dev)
-    chain_s = time.perf_counter() - t_chain0
-    if not (smoke_ok and chk.ok):
-        print(f"rank {rank}: validation FAILED smoke={smoke_ok} gemm={chk}", file=sys.stderr)
-        return 2
+    res = ctx.timed(step, args.steps, args.warmup)
+    per_gpu = G.tflops(m, n, k, res["elapsed_s"] / args.steps)
+    extras.update(per_gpu_tflops=_r(per_gpu), stabilise_dispatches=res["stabilise_dispatches"],
+                  stabilise_spread=res["stabilise_spread"],
+                  step_ms_median=res["median_ms"], step_ms_p90=res["p90_ms"])
+    if res["median_ms"]:
+        extras["per_gpu_tflops_at_median"] = _r(G.tflops(m, n, k, res["median_ms"] / 1e3))
 
-    extras = {"gemm_check_max_rel_err": chk.max_rel_err, "validation_chain_s": round(chain_s, 4)}
-    return _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k, extras)
+    if not args.no_extras:
+        if not cpu:
+            extras.update(_hipblaslt_extra(ctx, a, bt, per_gpu))
+            extras.update(_fp8_extra(ctx))
+        if distributed:
+            extras.update(_allreduce_extra(ctx))
+
+    if rank == 0:
+        shape = f"{m}^3" if m == n == k else f"{m}x{n}x{k}"
+        line = {
+            "metric": f"validator HIP GEMM TFLOPS (bf16 {shape}, aggregate over GPUs)",
+            "value": _r(per_gpu * world),
+            "unit": "TFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(res["elapsed_s"] / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform [-1,1) bf16 operands, random init)",
+            "config": {"model": f"validator mfma-gemm bf16 M={m} N={n} K={k}",
+                       "global_batch": world, "seq_len": None,
+                       "parallelism": f"dp{world} (one GEMM per GPU, RCCL over xGMI)"},
+        }
+        line.update(extras)
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+    return 0
 
 
 def _r(x: float) -> float:
@@ -123,108 +214,145 @@ def _r(x: float) -> float:
     return round(x, 2) if abs(x) >= 1 else float(f"{x:.4g}")
 
 
-def _fp8_extra(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync):
+def _pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    i = min(len(xs) - 1, max(0, int(round(q * (len(xs) - 1)))))
+    return xs[i]
+
+
+class Ctx:
+    """Per-rank timing context: barriers, synchronisation, clock stabilisation and timed loops."""
+
+    def __init__(self, args, torch, dist, dev, rank, local_rank, world, distributed, cpu):
+        self.args, self.torch, self.dist, self.dev = args, torch, dist, dev
+        self.rank, self.local_rank, self.world = rank, local_rank, world
+        self.distributed, self.cpu = distributed, cpu
+
+    def barrier(self):
+        if self.distributed:
+            if self.cpu:
+                self.dist.barrier()
+            else:
+                self.dist.barrier(device_ids=[self.local_rank])
+
+    def sync(self):
+        if not self.cpu:
+            self.torch.cuda.synchronize(self.dev)
+
+    def max_over_ranks(self, x: float) -> float:
+        if not self.distributed:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def stabilise(self, step, min_dispatches=50, window=10, tol=0.02, batch=10):
+        """Issue back-to-back dispatches in batches of ``batch`` (event between each) until the
+        last ``window`` per-dispatch times spread by < ``tol`` of their median, with at least
+        ``min_dispatches`` and at most ``--stabilise-max-s`` seconds. Returns (count, spread)."""
+        if self.cpu:
+            return 0, None
+        torch = self.torch
+        t_end = time.perf_counter() + self.args.stabilise_max_s
+        times, count, spread = [], 0, None
+        while True:
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(batch + 1)]
+            evs[0].record()
+            for i in range(batch):
+                step()
+                evs[i + 1].record()
+            evs[-1].synchronize()
+            times += [evs[i].elapsed_time(evs[i + 1]) for i in range(batch)]
+            count += batch
+            last = sorted(times[-window:])
+            med = last[len(last) // 2]
+            spread = (last[-1] - last[0]) / med if med > 0 else 0.0
+            if (count >= min_dispatches and spread < tol) or time.perf_counter() > t_end:
+                return count, round(spread, 4)
+
+    def timed(self, step, steps, warmup):
+        torch = self.torch
+        for _ in range(warmup):
+            step()
+        self.sync()
+        n_stab, spread = self.stabilise(step)
+        self.sync()
+        self.barrier()
+        self.sync()
+        evs = None if self.cpu else [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        t0 = time.perf_counter()
+        if evs:
+            evs[0].record()
+        for i in range(steps):
+            step()
+            if evs:
+                evs[i + 1].record()
+        self.sync()
+        self.barrier()
+        self.sync()
+        elapsed = self.max_over_ranks(time.perf_counter() - t0)
+        per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else []
+        med, p90 = _pct(per, 0.5), _pct(per, 0.9)
+        return {"elapsed_s": elapsed, "stabilise_dispatches": n_stab, "stabilise_spread": spread,
+                "median_ms": round(med, 4) if med is not None else None,
+                "p90_ms": round(p90, 4) if p90 is not None else None}
+
+
+def _hipblaslt_extra(ctx, a, bt, ours_tflops):
+    """torch.matmul (hipBLASLt on ROCm) on the same operands, same protocol, same step count."""
+    torch = ctx.torch
+    from gpu_operator_amd.ops import gemm as G
+    m, k = a.shape
+    n = bt.shape[0]
+    c = torch.empty((m, n), dtype=torch.bfloat16, device=ctx.dev)
+    btt = bt.t()
+
+    def step():
+        torch.matmul(a, btt, out=c)
+
+    res = ctx.timed(step, ctx.args.steps, ctx.args.warmup)
+    blas = G.tflops(m, n, k, res["elapsed_s"] / ctx.args.steps)
+    out = {"hipblaslt_tflops": _r(blas), "ratio_vs_hipblaslt": round(ours_tflops / blas, 4),
+           "hipblaslt_step_ms_median": res["median_ms"]}
+    try:
+        out["blas_library"] = str(torch.backends.cuda.preferred_blas_library()).split(".")[-1]
+    except Exception:  # noqa: BLE001 - informational only
+        pass
+    return out
+
+
+def _fp8_extra(ctx):
     """Same shape on the fp8 (OCP e4m3fn) block-scaled MFMA kernel, after and outside the timed
     bf16 region: the matrix cores at their fp8 rate, reported as extra fields only."""
+    torch = ctx.torch
     from gpu_operator_amd.ops import gemm as G
-    m, n, k = args.m, args.n, args.k
+    m, n, k = ctx.args.m, ctx.args.n, ctx.args.k
     f8 = torch.float8_e4m3fn
-    a = G.fill_uniform_fp8_(torch.empty((m, k), dtype=f8, device=dev), seed=3000 + rank)
-    bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=f8, device=dev), seed=4000 + rank)
-    c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
-    steps = max(1, min(args.steps, 100))
-    for _ in range(max(1, min(args.warmup, 50))):
+    a = G.fill_uniform_fp8_(torch.empty((m, k), dtype=f8, device=ctx.dev), seed=3000 + ctx.rank)
+    bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=f8, device=ctx.dev), seed=4000 + ctx.rank)
+    c = torch.empty((m, n), dtype=torch.bfloat16, device=ctx.dev)
+
+    def step():
         G.gemm_fp8(a, bt, c)
-    sync()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        G.gemm_fp8(a, bt, c)
-    sync()
-    barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    chk = G.verify(a, bt, c, nrows=16, seed=rank)
-    per_gpu = G.tflops(m, n, k, elapsed / steps)
-    return {"fp8_per_gpu_tflops": _r(per_gpu), "fp8_total_tflops": _r(per_gpu * n_gpus),
-            "fp8_check_ok": chk.ok, "fp8_steps": steps}
+
+    steps = max(1, ctx.args.steps)
+    res = ctx.timed(step, steps, ctx.args.warmup)
+    chk = G.verify(a, bt, c, nrows=16, seed=ctx.rank)
+    per_gpu = G.tflops(m, n, k, res["elapsed_s"] / steps)
+    return {"fp8_per_gpu_tflops": _r(per_gpu), "fp8_total_tflops": _r(per_gpu * ctx.world),
+            "fp8_check_ok": chk.ok, "fp8_steps": steps, "fp8_step_ms_median": res["median_ms"]}
 
 
-def _timed_and_report(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync, step, m, n, k, extras):
-    from gpu_operator_amd.ops import gemm as G
-    for _ in range(args.warmup):
-        step()
-    sync()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed / args.steps * 1e3
-    per_gpu_tflops = G.tflops(m, n, k, elapsed / args.steps)
-    total_tflops = per_gpu_tflops * n_gpus
-    extras = dict(extras, per_gpu_tflops=_r(per_gpu_tflops))
-    cpu = args.device == "cpu"
-    if not cpu and not args.no_extras:
-        extras.update(_fp8_extra(args, torch, dist, dev, rank, n_gpus, distributed, barrier, sync))
-    if distributed and not args.no_extras:
-        from gpu_operator_amd.parallel.allreduce import measure_allreduce
-        nbytes = (64 << 10) if cpu else args.allreduce_mib * (1 << 20)
-        r = measure_allreduce(nbytes, dtype=torch.bfloat16, iters=3 if cpu else 10, warmup=1 if cpu else 3,
-                              device=dev)
-        extras.update({"allreduce_bytes": r.nbytes, "allreduce_algbw_gbps": round(r.algbw_gbps, 2),
-                       "allreduce_busbw_gbps": round(r.busbw_gbps, 2), "allreduce_ok": r.ok})
-
-    if n_gpus == 1 and not args.no_extras and not cpu:
-        # node time-to-ready (driver -> validator) on this GPU, outside the timed region
-        try:
-            from gpu_operator_amd.validator import ttr
-            r = ttr.run_chain(gemm_shapes="8192", timeout=120)
-            if r["time_to_ready_s"] is not None:
-                extras["node_time_to_ready_s"] = round(r["time_to_ready_s"], 3)
-                extras["reference_model_time_to_ready_s"] = ttr.reference_model(r["steps_s"])["time_to_ready_s"]
-            else:
-                extras["node_time_to_ready_error"] = "; ".join(r["errors"])[:300]
-        except Exception as e:  # noqa: BLE001 - an extra must never fail the bench
-            extras["node_time_to_ready_error"] = str(e)[:300]
-
-    if rank == 0:
-        line = {
-            "metric": "validator HIP GEMM TFLOPS (bf16 8192^3, aggregate over GPUs)",
-            "value": _r(total_tflops),
-            "unit": "TFLOP/s",
-            "n_gpus": n_gpus,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (uniform [-1,1) bf16 operands, random init)",
-            "config": {"model": f"validator mfma-gemm bf16 M={m} N={n} K={k}",
-                       "global_batch": n_gpus, "seq_len": None,
-                       "parallelism": f"dp{n_gpus} (one GEMM per GPU, RCCL over xGMI)"},
-        }
-        line.update(extras)
-        print(json.dumps(line), flush=True)
-    if distributed:
-        dist.destroy_process_group()
-    return 0
+def _allreduce_extra(ctx):
+    torch = ctx.torch
+    from gpu_operator_amd.parallel.allreduce import measure_allreduce
+    nbytes = (64 << 10) if ctx.cpu else ctx.args.allreduce_mib * (1 << 20)
+    r = measure_allreduce(nbytes, dtype=torch.bfloat16, iters=3 if ctx.cpu else 20,
+                          warmup=1 if ctx.cpu else 5, device=ctx.dev)
+    return {"allreduce_bytes": r.nbytes, "allreduce_algbw_gbps": round(r.algbw_gbps, 3),
+            "allreduce_busbw_gbps": round(r.busbw_gbps, 3), "allreduce_ok": r.ok}
 
 
 if __name__ == "__main__":

@@ -87,10 +87,12 @@ def _pyext_name(stem: str) -> str:
     return stem + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
 
 
+GEMM_HEADERS = ["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_fp8_kernels.h"]
+
 TARGETS: List[Target] = [
     # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.
     Target("libamdgo_hip.so", ["hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/smoke.hip"], "hip-shared",
-           headers=["include/gemm_tile_common.h"]),
+           headers=GEMM_HEADERS),
     # Node agent library (sysfs/KFD topology, partitions, telemetry, inotify barriers).
     Target(_pyext_name("_amdnode"), ["node/pybind.cpp", "node/amdnode.cpp"], "pyext",
            headers=["include/amdnode.h"]),
@@ -98,7 +100,7 @@ TARGETS: List[Target] = [
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
     # Validator workload binaries (run inside the validation pods).
     Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip", "hip/gemm_fp8.hip"],
-           "hip-exe", flags=["-x", "hip"], headers=["include/gemm_tile_common.h"]),
+           "hip-exe", flags=["-x", "hip"], headers=GEMM_HEADERS),
     Target("bin/amd-hip-smoke", ["hip/hip_smoke_main.cpp", "hip/smoke.hip"], "hip-exe", flags=["-x", "hip"]),
     Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp"], "hip-exe", flags=["-x", "hip"],
            libs=["-lrccl"]),
@@ -111,10 +113,18 @@ TARGETS: List[Target] = [
 ]
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> List[Path]:
+# Tools-only: superseded GEMM generations, placement sweeps and knock-out timings for A/B profiling
+# (tools/gemm_lab.py). Never loaded by the validator; built on request (`--lab`).
+LAB_TARGETS: List[Target] = [
+    Target("libamdgo_gemm_lab.so", ["hip/gemm_bf16_lab.hip", "hip/gemm_fp8_lab.hip"], "hip-shared",
+           headers=GEMM_HEADERS),
+]
+
+
+def build(force: bool = False, jobs: int = 4, verbose: bool = False, lab: bool = False) -> List[Path]:
     OUT.mkdir(parents=True, exist_ok=True)
     (OUT / "bin").mkdir(exist_ok=True)
-    todo = [t for t in TARGETS if force or t.stale()]
+    todo = [t for t in TARGETS + (LAB_TARGETS if lab else []) if force or t.stale()]
 
     def run(t: Target) -> Path:
         cmd = t.command()
@@ -136,11 +146,12 @@ def main(argv: Sequence[str] | None = None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=4)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--lab", action="store_true", help="also build the tools-only GEMM experiment library")
     a = ap.parse_args(argv)
     if shutil.which(hipcc()) is None and not Path(hipcc()).exists():
         print("hipcc not found", file=sys.stderr)
         return 1
-    built = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    built = build(force=a.force, jobs=a.jobs, verbose=a.verbose, lab=a.lab)
     for p in built:
         print(f"built {p.relative_to(REPO)}")
     return 0

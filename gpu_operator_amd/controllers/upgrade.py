@@ -13,7 +13,11 @@ hard-codes ``nvidia.com/``):
 
 All durable state is on the Node (state label, start-time annotations), so an operator
 restart resumes every upgrade where it stopped. Drains and pod evictions run on background
-workers guarded by a per-node in-flight set (the library's KeyedMutex + StringSet).
+workers guarded by a per-node in-flight set (the library's KeyedMutex + StringSet); like
+kubectl's drain helper (vendor/k8s.io/kubectl/pkg/drain/drain.go:248-353,410) a worker retries
+PDB-refused evictions and then waits until every evicted pod is gone, bounded by the policy's
+timeout. The wait's start time is a Node annotation, so an operator restart resumes the same
+deadline instead of starting a new one.
 """
 
 from __future__ import annotations
@@ -38,6 +42,7 @@ UPGRADE_SKIP_DRAIN_POD_LABEL = f"{C.PREFIX}/gpu-driver-upgrade-drain.skip"
 UPGRADE_INITIAL_STATE_ANNOTATION = f"{C.PREFIX}/gpu-driver-upgrade.node-initial-state.unschedulable"
 WAIT_FOR_POD_COMPLETION_START_ANNOTATION = f"{C.PREFIX}/gpu-driver-upgrade-wait-for-pod-completion-start-time"
 POD_EVICTION_START_ANNOTATION = f"{C.PREFIX}/gpu-driver-upgrade-pod-eviction-start-time"
+DRAIN_START_ANNOTATION = f"{C.PREFIX}/gpu-driver-upgrade-drain-start-time"
 VALIDATION_START_ANNOTATION = f"{C.PREFIX}/gpu-driver-upgrade-validation-start-time"
 EVENT_REASON = "AMDGPUDriverUpgrade"
 
@@ -60,6 +65,8 @@ IN_PROGRESS = {CORDON_REQUIRED, WAIT_FOR_JOBS_REQUIRED, POD_DELETION_REQUIRED, D
 
 VALIDATION_TIMEOUT_S = 600
 MAX_DRIVER_RESTARTS = 10
+EVICTION_RETRY_S = 5.0      # kubectl drain: an eviction refused by a PDB (429) is retried after 5 s
+DELETE_POLL_S = 1.0         # kubectl drain waitForDelete: poll interval
 
 
 def gpu_pod_filter(pod: Dict[str, Any]) -> bool:
@@ -95,8 +102,9 @@ class ClusterUpgradeState:
 class UpgradeStateManager:
     def __init__(self, client, namespace: str, pod_filter: Callable[[Dict], bool] = gpu_pod_filter,
                  validation_selector: Optional[str] = "app=amd-operator-validator",
-                 clock=time.time, run_async: bool = True, workers: int = 8):
+                 clock=time.time, run_async: bool = True, workers: int = 8, sleep=time.sleep):
         self.client = client
+        self.sleep = sleep
         self.namespace = namespace
         self.pod_filter = pod_filter
         self.validation_selector = validation_selector
@@ -283,44 +291,100 @@ class UpgradeStateManager:
         for ns in nodes:
             self._schedule(o.name(ns.node), lambda ns=ns: self._evict_gpu_pods(ns, policy, drain_enabled))
 
+    def _gpu_pods_on(self, node: str) -> List[Dict]:
+        return [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node}")
+                if self.pod_filter(p) and (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
+
+    def _drain_or_failed(self, ns: NodeState, drain_enabled: bool, why: str) -> None:
+        """reference: pod_manager.go:369-377 (updateNodeToDrainOrFailed)."""
+        self.client.create_event(ns.node, EVENT_REASON,
+                                 f"Failed to delete workload pods on the node for the driver upgrade, {why}",
+                                 "Warning")
+        self.set_state(ns.node, DRAIN_REQUIRED if drain_enabled else FAILED)
+
     def _evict_gpu_pods(self, ns: NodeState, policy: DriverUpgradePolicySpec, drain_enabled: bool) -> None:
+        """Delete the node's GPU pods and wait until they are gone (reference: pod_manager.go:117-223):
+        nothing to delete -> pod-restart-required; a pod the policy may not delete (emptyDir
+        without deleteEmptyDir, no controller without force) or an eviction error / timeout ->
+        drain-required when drain is enabled, else upgrade-failed."""
         pd = policy.podDeletion
         timeout = pd.timeout() if pd else 300
         node = o.name(ns.node)
-        pods = [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node}")
-                if self.pod_filter(p) and (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
+        pods = self._gpu_pods_on(node)
+        if not pods:
+            self.set_annotation(ns.node, POD_EVICTION_START_ANNOTATION, None)
+            self.set_state(ns.node, POD_RESTART_REQUIRED)
+            return
         blocked = []
         for p in pods:
-            owner = o.controller_of(p)
             uses_emptydir = any("emptyDir" in v for v in (p.get("spec") or {}).get("volumes") or [])
             if uses_emptydir and not (pd and pd.deleteEmptyDir):
                 blocked.append(f"{o.name(p)} (emptyDir)")
-                continue
-            if owner is None and not (pd and pd.force):
+            elif o.controller_of(p) is None and not (pd and pd.force):
                 blocked.append(f"{o.name(p)} (unmanaged)")
-                continue
-            try:
-                self.client.evict(o.name(p), o.namespace(p))
-            except errors.NotFound:
-                pass
-            except errors.ApiError as e:
-                blocked.append(f"{o.name(p)} ({e})")
-        if not blocked:
+        if blocked:
+            log.info("node %s: cannot delete all required pods: %s", node, blocked)
             self.set_annotation(ns.node, POD_EVICTION_START_ANNOTATION, None)
-            self.set_state(ns.node, POD_RESTART_REQUIRED if not drain_enabled else DRAIN_REQUIRED)
+            self._drain_or_failed(ns, drain_enabled, f"cannot delete {blocked}")
             return
-        start = o.get_annotations(ns.node).get(POD_EVICTION_START_ANNOTATION)
+        err = self._delete_or_evict(ns.node, pods, timeout, POD_EVICTION_START_ANNOTATION)
+        if err:
+            self._drain_or_failed(ns, drain_enabled, err)
+            return
+        self.client.create_event(ns.node, EVENT_REASON, "Deleted workload pods on the node for the driver upgrade")
+        self.set_state(ns.node, POD_RESTART_REQUIRED)
+
+    def _delete_or_evict(self, node: Dict, pods: List[Dict], timeout: int, start_key: str) -> Optional[str]:
+        """Evict ``pods`` and wait until every one of them is gone (kubectl drain's DeleteOrEvictPods
+        + waitForDelete, drain.go:248-353,410). A 429 (PodDisruptionBudget) is retried every
+        EVICTION_RETRY_S; a pod counts as gone when GET returns 404 or a different UID. ``timeout``
+        0 = no limit. The deadline runs from the ``start_key`` Node annotation, set on the first
+        attempt and cleared when the wait ends. Returns None on success, else the reason."""
+        start = o.get_annotations(node).get(start_key)
         if start is None:
-            self.set_annotation(ns.node, POD_EVICTION_START_ANNOTATION, str(int(self.clock())))
-            return
-        if timeout and self.clock() - int(start) >= timeout:
-            self.set_annotation(ns.node, POD_EVICTION_START_ANNOTATION, None)
-            if drain_enabled:
-                log.info("node %s: pod deletion failed (%s); falling back to drain", node, blocked)
-                self.set_state(ns.node, DRAIN_REQUIRED)
-            else:
-                self.client.create_event(ns.node, EVENT_REASON, f"pod deletion failed: {blocked}", "Warning")
-                self.set_state(ns.node, FAILED)
+            start = str(int(self.clock()))
+            self.set_annotation(node, start_key, start)
+        deadline = int(start) + timeout if timeout else None
+        pending = {(o.namespace(p), o.name(p)): p for p in pods}
+        evicted: Set[tuple] = set()
+        next_evict = 0.0
+        while True:
+            now = self.clock()
+            if now >= next_evict:
+                refused = False
+                for key, p in pending.items():
+                    if key in evicted or (p.get("metadata") or {}).get("deletionTimestamp"):
+                        evicted.add(key)
+                        continue
+                    try:
+                        self.client.evict(key[1], key[0])
+                        evicted.add(key)
+                    except errors.NotFound:
+                        evicted.add(key)
+                    except errors.TooManyRequests:
+                        refused = True          # PDB: retry after EVICTION_RETRY_S
+                    except errors.ApiError as e:
+                        self.set_annotation(node, start_key, None)
+                        return f"error when evicting pods/{key[1]} -n {key[0]}: {e}"
+                next_evict = now + EVICTION_RETRY_S if refused else float("inf")
+            for key in list(pending):
+                if key not in evicted:
+                    continue
+                try:
+                    cur = self.client.get("v1", "Pod", key[1], key[0])
+                except errors.NotFound:
+                    cur = None
+                if cur is None or cur["metadata"].get("uid") != pending[key]["metadata"].get("uid"):
+                    del pending[key]
+            if not pending:
+                self.set_annotation(node, start_key, None)
+                return None
+            if deadline is not None and self.clock() >= deadline:
+                self.set_annotation(node, start_key, None)
+                left = sorted(f"{ns_}/{n}" for ns_, n in pending)
+                what = "evicted but not yet deleted" if set(pending) <= evicted else "eviction refused"
+                return f"global timeout {timeout}s reached; pods {what}: {left}"
+            self.sleep(DELETE_POLL_S)
 
     def _drain(self, state: ClusterUpgradeState, policy: DriverUpgradePolicySpec) -> None:
         d = policy.drain
@@ -333,14 +397,14 @@ class UpgradeStateManager:
 
     def _drain_node(self, ns: NodeState, d) -> None:
         """Evict every pod on the node except DaemonSet pods, mirror pods and pods labelled
-        to skip drain (the operator itself), with the kubectl-drain options of the policy."""
+        to skip drain (the operator itself), with the kubectl-drain options of the policy, and
+        wait for them to be gone (reference: drain_manager.go:58-136)."""
         node = o.name(ns.node)
         sel = f"{UPGRADE_SKIP_DRAIN_POD_LABEL}!=true"
         if d.podSelector:
             sel = f"{d.podSelector},{sel}"
-        deadline = self.clock() + d.timeout() if d.timeout() else None
         pods = self.client.list("v1", "Pod", label_selector=sel, field_selector=f"spec.nodeName={node}")
-        errs = []
+        errs, victims = [], []
         for p in pods:
             owner = o.controller_of(p)
             if owner and owner.get("kind") == "DaemonSet":
@@ -356,24 +420,29 @@ class UpgradeStateManager:
             if owner is None and not d.force:
                 errs.append(f"{o.name(p)}: not managed by a controller")
                 continue
-            if deadline is not None and self.clock() > deadline:
-                errs.append("drain timed out")
-                break
-            try:
-                self.client.evict(o.name(p), o.namespace(p))
-            except errors.NotFound:
-                pass
-            except errors.ApiError as e:
-                errs.append(f"{o.name(p)}: {e}")
+            victims.append(p)
+        if not errs and victims:
+            err = self._delete_or_evict(ns.node, victims, d.timeout(), DRAIN_START_ANNOTATION)
+            if err:
+                errs.append(err)
         if errs:
-            self.client.create_event(ns.node, EVENT_REASON, f"drain failed: {errs}", "Warning")
+            self.set_annotation(ns.node, DRAIN_START_ANNOTATION, None)
+            self.client.create_event(ns.node, EVENT_REASON, f"Failed to drain the node, {errs}", "Warning")
             self.set_state(ns.node, FAILED)
         else:
+            self.client.create_event(ns.node, EVENT_REASON, "Successfully drained the node")
             self.set_state(ns.node, POD_RESTART_REQUIRED)
 
     def _pod_restart(self, state: ClusterUpgradeState) -> None:
         for ns in list(state.node_states.get(POD_RESTART_REQUIRED, [])):
             if self.pod_revision_hash(ns.driver_pod) != self.ds_revision_hash(ns.driver_ds):
+                if self.pod_filter is not None and self._gpu_pods_on(o.name(ns.node)):
+                    # never unload amdgpu under a pod that still holds /dev/kfd (one that started
+                    # after the eviction, e.g. with a toleration for the cordon): evict again
+                    log.info("node %s: GPU pods present again; back to pod deletion", o.name(ns.node))
+                    self.set_state(ns.node, POD_DELETION_REQUIRED)
+                    self._move(state, ns, POD_RESTART_REQUIRED, POD_DELETION_REQUIRED)
+                    continue
                 if not (ns.driver_pod.get("metadata") or {}).get("deletionTimestamp"):
                     try:
                         self.client.delete("v1", "Pod", o.name(ns.driver_pod), o.namespace(ns.driver_pod))

@@ -141,9 +141,22 @@ class FakeClient:
                 md["generation"] = gen
             if new.get("status") is None:
                 new.pop("status", None)
+            nmd = o.meta(new)
+            if nmd.get("deletionTimestamp") is None and cur["metadata"].get("deletionTimestamp"):
+                nmd["deletionTimestamp"] = cur["metadata"]["deletionTimestamp"]   # immutable once set
             self._bump(new)
-            self._store[k] = new
             out = copy.deepcopy(new)
+            if nmd.get("deletionTimestamp") and not nmd.get("finalizers"):
+                # the last finalizer of a terminating object is gone: the API server removes it
+                self._store.pop(k, None)
+                removed = [out] + self._gc(nmd["uid"])
+            else:
+                self._store[k] = new
+                removed = None
+        if removed is not None:
+            for r in removed:
+                self._notify(DELETED, r)
+            return out
         self._notify(MODIFIED, out, cur)
         return out
 
@@ -164,9 +177,24 @@ class FakeClient:
         with self._lock:
             self._intercept("delete", api_version, kind, name)
             k = self._k(api_version, kind, namespace, name)
-            obj = self._store.pop(k, None)
+            obj = self._store.get(k)
             if obj is None:
                 raise errors.NotFound(f'{kind} "{name}" not found')
+            if obj["metadata"].get("finalizers"):
+                # graceful: the object stays, terminating, until its finalizers are removed
+                if obj["metadata"].get("deletionTimestamp"):
+                    return
+                obj["metadata"]["deletionTimestamp"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+                self._bump(obj)
+                out = copy.deepcopy(obj)
+                mod = True
+            else:
+                mod = False
+                self._store.pop(k, None)
+        if mod:
+            self._notify(MODIFIED, out)
+            return
+        with self._lock:
             removed = [obj]
             if propagation != "Orphan":
                 removed += self._gc(obj["metadata"]["uid"])
@@ -183,8 +211,22 @@ class FakeClient:
         return gone
 
     def evict(self, name: str, namespace: str, grace_period_seconds: Optional[int] = None) -> None:
+        """The pods/eviction subresource: 429 when a PodDisruptionBudget selecting the pod allows no
+        disruption (status.disruptionsAllowed, kept up to date by the test), else a delete."""
         with self._lock:
             self._intercept("evict", "v1", "Pod", name)
+            pod = self._store.get(self._k("v1", "Pod", namespace, name))
+            if pod is None:
+                raise errors.NotFound(f'pods "{name}" not found')
+            if not pod["metadata"].get("deletionTimestamp"):
+                for (av, k, ns, _), pdb in self._store.items():
+                    if k != "PodDisruptionBudget" or ns != namespace:
+                        continue
+                    if not o.selector_matches((pdb.get("spec") or {}).get("selector"), o.get_labels(pod)):
+                        continue
+                    if int((pdb.get("status") or {}).get("disruptionsAllowed", 0)) <= 0:
+                        raise errors.TooManyRequests(
+                            "Cannot evict pod as it would violate the pod's disruption budget.")
         self.delete("v1", "Pod", name, namespace)
 
     # -- discovery / misc -----------------------------------------------------------------

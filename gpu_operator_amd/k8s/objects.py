@@ -28,7 +28,7 @@ CORE_KINDS = {
     "ServiceMonitor": "monitoring.coreos.com/v1", "PrometheusRule": "monitoring.coreos.com/v1",
     "SecurityContextConstraints": "security.openshift.io/v1",
     "CustomResourceDefinition": "apiextensions.k8s.io/v1",
-    "Job": "batch/v1",
+    "Job": "batch/v1", "PodDisruptionBudget": "policy/v1",
 }
 
 CLUSTER_SCOPED = {"Namespace", "Node", "ClusterRole", "ClusterRoleBinding", "RuntimeClass",

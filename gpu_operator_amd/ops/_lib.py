@@ -55,11 +55,13 @@ def load() -> ctypes.CDLL:
         lib.amdgo_gemm_fp8_ref_rows.restype = i
         lib.amdgo_fill_uniform_fp8.argtypes = [vp, sz, u32, vp]
         lib.amdgo_fill_uniform_fp8.restype = i
-        lib.amdgo_gemm_fp8_set_variant.argtypes = [i]
-        lib.amdgo_gemm_fp8_set_variant.restype = None
+        for f in ("amdgo_gemm_set_variant", "amdgo_gemm_fp8_set_variant"):
+            getattr(lib, f).argtypes = [i]
+            getattr(lib, f).restype = i
+        for f in ("amdgo_gemm_resolve_variant", "amdgo_gemm_fp8_resolve_variant"):
+            getattr(lib, f).argtypes = [i, i, i]
+            getattr(lib, f).restype = i
         lib.amdgo_gemm_fp8_get_variant.restype = i
-        lib.amdgo_gemm_set_variant.argtypes = [i]
-        lib.amdgo_gemm_set_variant.restype = None
         lib.amdgo_gemm_get_variant.restype = i
         for f in ("amdgo_gemm_tile_m", "amdgo_gemm_tile_n", "amdgo_gemm_tile_k",
                   "amdgo_gemm_fp8_tile_m", "amdgo_gemm_fp8_tile_n", "amdgo_gemm_fp8_tile_k"):

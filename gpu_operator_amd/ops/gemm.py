@@ -75,13 +75,39 @@ def gemm_fp8(a, bt, out=None, *, generic: bool = False):
     return out
 
 
+# Production variant sets (native/hip/gemm_bf16.hip, gemm_fp8.hip): 0 = automatic dispatch, any
+# other member pins that kernel. Everything else lives in the tools-only lab library.
+BF16_VARIANTS = (0, 18, 25, 42, 44, 45)
+FP8_VARIANTS = (0, 4, 7, 9, 10, 13)
+
+
+def set_variant(v: int) -> None:
+    """Pin a production bf16 kernel (see ``BF16_VARIANTS``; 0 restores automatic dispatch)."""
+    if _lib.load().amdgo_gemm_set_variant(int(v)) != 0:
+        raise ValueError(f"bf16 GEMM variant {v} is not in the production set {BF16_VARIANTS}")
+
+
+def get_variant() -> int:
+    return _lib.load().amdgo_gemm_get_variant()
+
+
+def resolve_variant(m: int, n: int, k: int) -> int:
+    """The bf16 kernel ``gemm_bf16`` runs for this shape on the current device (0 = generic)."""
+    return _lib.load().amdgo_gemm_resolve_variant(int(m), int(n), int(k))
+
+
 def set_fp8_variant(v: int) -> None:
-    """Select the fp8 fast-path schedule (1 = default, 2..4 placements; 0 = generic kernel)."""
-    _lib.load().amdgo_gemm_fp8_set_variant(int(v))
+    """Pin a production fp8 kernel (see ``FP8_VARIANTS``; 0 restores automatic dispatch)."""
+    if _lib.load().amdgo_gemm_fp8_set_variant(int(v)) != 0:
+        raise ValueError(f"fp8 GEMM variant {v} is not in the production set {FP8_VARIANTS}")
 
 
 def get_fp8_variant() -> int:
     return _lib.load().amdgo_gemm_fp8_get_variant()
+
+
+def resolve_fp8_variant(m: int, n: int, k: int) -> int:
+    return _lib.load().amdgo_gemm_fp8_resolve_variant(int(m), int(n), int(k))
 
 
 def fp8_fast_path_supported(m: int, n: int, k: int) -> bool:
@@ -91,19 +117,11 @@ def fp8_fast_path_supported(m: int, n: int, k: int) -> bool:
         and k % tk == 0 and k >= 2 * tk
 
 
-def set_variant(v: int) -> None:
-    """Select the fast-path kernel generation (1: baseline, 2: fragment-pipelined)."""
-    _lib.load().amdgo_gemm_set_variant(int(v))
-
-
-def get_variant() -> int:
-    return _lib.load().amdgo_gemm_get_variant()
-
-
 def fast_path_supported(m: int, n: int, k: int) -> bool:
     lib = _lib.load()
+    tk = lib.amdgo_gemm_tile_k()
     return m % lib.amdgo_gemm_tile_m() == 0 and n % lib.amdgo_gemm_tile_n() == 0 \
-        and k % lib.amdgo_gemm_tile_k() == 0
+        and k % tk == 0 and k >= 2 * tk
 
 
 def fill_uniform_(t, seed: int = 1234):

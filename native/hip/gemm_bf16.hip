@@ -1,4 +1,4 @@
-// CDNA4 (gfx950) bf16 GEMM for the node validator workload.
+// CDNA4 (gfx950) bf16 GEMM for the node validator workload -- the shipped dispatch.
 //
 //   C[M,N] (bf16) = A[M,K] (bf16, K-major) * Bt[N,K]^T (bf16, K-major), fp32 accumulation.
 //
@@ -7,1610 +7,27 @@
 // validator/cuda-workload-validation.yaml:20). There the kernel was a pass/fail
 // check; here it is a throughput probe that exercises the matrix cores, LDS and HBM.
 //
-// Design (MI355X-first, see docs/validator-gemm.md):
-//   * 256x256 output tile per 512-thread workgroup (8 wave64s laid out 2(M) x 4(N)),
-//     each wave owns a 128x64 sub-tile = 8x4 MFMA 16x16x32 accumulators (128 AGPR/VGPR).
-//   * K-step BK=64. Global->LDS staging with `global_load_lds_dwordx4` (LDS-DMA, no VGPR
-//     round trip). The LDS image is lane-linear (hardware rule) so the bank-conflict XOR
-//     swizzle is applied to the per-lane SOURCE address and again on the ds_read side.
-//   * Two LDS buffers (2 x 64 KiB); the next K-tile's DMA is issued before the current
-//     tile's ds_read+MFMA work so HBM latency hides behind 64 MFMAs per wave.
-//   * Operands are swapped in the MFMA (Bt fragment as "A") so every lane ends up holding
-//     4 consecutive N-columns of one output row: 8-byte packed bf16 stores in the epilogue.
-//   * XCD-aware, bijective blockIdx remap (8 XCDs, private 4 MiB L2 each) followed by a
-//     grouped (GROUP_M) raster so co-resident tiles on one XCD share A/B panels in L2.
+// Design (MI355X-first, see docs/validator-gemm.md; kernels in gemm_bf16_kernels.h):
+//   * 256x256 output tile per 256-thread workgroup: one wave64 per SIMD, each owning a 128x128
+//     sub-tile = 8x8 MFMA 16x16x32 accumulators pinned in all 256 AGPRs (inline-asm MFMAs).
+//   * K-step BK=64, two LDS buffers staged by `buffer_load ... lds` (LDS-DMA, no VGPR round trip),
+//     XOR-swizzled on the source address; the v18 K-tile schedule interleaves fragment reads,
+//     DMA pieces and two barriers into the 128-MFMA stream of each K-tile.
+//   * XCD-aware rasters (8 XCDs with private L2): a bijective XCD-contiguous remap plus grouped
+//     raster, serpentine K across dispatch waves, and a square cross-XCD super-tile raster.
 //
-// Variants (AMDGO_GEMM_VARIANT / amdgo_gemm_set_variant): 1 = double-buffered baseline, 2 = fragment
-// pipelined, 3 = ping-pong (two wave groups one barrier apart, half-tile LDS ring), 4 = v3 with
-// buffer_load...lds staging, 5 = v4 with an LDS-staged, fully coalesced epilogue (K % 128 == 0,
-// else v2); 10-19 = one wave per SIMD with a 128x128 wave tile (v18 = the K-tile schedule);
-// 25/26 = v18 persistent; 30-35 = v18 barrier-placement sweep; 40/41 = v18 + serpentine K,
-// 42/43 = v18/v19 with the loop rotated at the B1 barrier, 44 = v18 + both (the default; on a
-// device without 256 CUs the serpentine variants fall back to 42 / 18).
-// Measured: profiles/r1_gemm_v4/, profiles/r1_s2_gemm/.
+// Only numerically exact, measured production kernels are reachable from here. The variant is an
+// API argument (amdgo_gemm_set_variant), never read from the environment; superseded generations
+// and knock-out timings live in the tools-only gemm_bf16_lab.hip.
+//   0  = automatic (default): v44; v25 for short K with >= 2 tiles per CU; v45 for >= 8 dispatch
+//        waves with K >= 8192 on 16x16-tile multiples; v42 / v18 on devices without 256 CUs.
+//   18 / 25 / 42 / 44 / 45 = that kernel pinned (no automatic switch; still falls back to a kernel
+//        that can run the shape or the device).
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
 
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <stdlib.h>
+#include "gemm_bf16_kernels.h"
 
-#include "gemm_tile_common.h"
-
-namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int BM = 256;
-constexpr int BN = 256;
-constexpr int BK = 64;
-constexpr int NTHREADS = 512;
-constexpr int ROW_BYTES = BK * 2;             // 128 B per staged row
-constexpr int PANEL_BYTES = BM * ROW_BYTES;   // 32 KiB per operand per K-tile
-constexpr int BUF_BYTES = 2 * PANEL_BYTES;    // A + B
-constexpr int LDS_BYTES = 2 * BUF_BYTES;      // double buffered: 128 KiB
-
-// Stage one 256-row x 64-k panel (32 KiB) of a K-major operand into LDS.
-// 32 wave-instructions of 1 KiB (8 rows each); wave w issues rows blocks {w, w+8, w+16, w+24}.
-__device__ __forceinline__ void stage_panel(const __bf16* __restrict__ g, int ld, int k0,
-                                            char* lds_panel, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rblk = i * 8 + wid;           // 8-row block index 0..31
-    const int r = rblk * 8 + (lane >> 3);   // row inside the panel
-    const int pc = lane & 7;                // physical 16-B chunk this lane writes
-    const int c = pc ^ ((r >> 1) & 7);      // logical chunk it must fetch (XOR involution)
-    const __bf16* src = g + (size_t)r * ld + k0 + c * 8;
-    char* dst = lds_panel + rblk * 1024;    // wave-uniform base; HW adds lane*16
-    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
-  }
-}
-
-__global__ void __launch_bounds__(NTHREADS)
-gemm_bf16_256x256(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                  __bf16* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2;   // 0..1  -> 128-row half of the tile
-  const int wc = wid & 3;    // 0..3  -> 64-col quarter of the tile
-
-  const __bf16* gA = A + (size_t)tm * BM * K;
-  const __bf16* gB = Bt + (size_t)tn * BN * K;
-
-  // Per-lane LDS read offsets for the two 32-deep k-steps of a BK=64 tile.
-  // Row within a 16-row fragment = lane&15; logical chunk = kk*4 + (lane>>4);
-  // swizzle term ((row>>1)&7) only depends on lane because fragment bases are 16-row aligned.
-  int lane_off[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int r = lane & 15;
-    const int c = kk * 4 + (lane >> 4);
-    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-  const int a_row0 = wr * 128;   // first A row (panel-local) this wave reads
-  const int b_row0 = wc * 64;    // first Bt row (panel-local) this wave reads
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int ktiles = K / BK;
-
-  stage_panel(gA, K, 0, smem, wid, lane);
-  stage_panel(gB, K, 0, smem + PANEL_BYTES, wid, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int t = 0; t < ktiles; ++t) {
-    char* cur = smem + (t & 1) * BUF_BYTES;
-    if (t + 1 < ktiles) {
-      char* nxt = smem + ((t + 1) & 1) * BUF_BYTES;
-      stage_panel(gA, K, (t + 1) * BK, nxt, wid, lane);
-      stage_panel(gB, K, (t + 1) * BK, nxt + PANEL_BYTES, wid, lane);
-    }
-    const char* la = cur + a_row0 * ROW_BYTES;
-    const char* lb = cur + PANEL_BYTES + b_row0 * ROW_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[8], bfr[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        bfr[n] = *reinterpret_cast<const bf16x8*>(lb + n * 16 * ROW_BYTES + lane_off[kk]);
-#pragma unroll
-      for (int m = 0; m < 8; ++m)
-        af[m] = *reinterpret_cast<const bf16x8*>(la + m * 16 * ROW_BYTES + lane_off[kk]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int m = 0; m < 8; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n], af[m], acc[m][n], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // Epilogue: lane holds C[row = m*16 + (lane&15)][col = n*16 + 4*(lane>>4) + j], j = 0..3.
-  const int row_base = tm * BM + wr * 128 + (lane & 15);
-  const int col_base = tn * BN + wc * 64 + 4 * (lane >> 4);
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    __bf16* crow = C + (size_t)(row_base + m * 16) * N + col_base;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-      bf16x4 v;
-      v[0] = (__bf16)acc[m][n][0];
-      v[1] = (__bf16)acc[m][n][1];
-      v[2] = (__bf16)acc[m][n][2];
-      v[3] = (__bf16)acc[m][n][3];
-      *reinterpret_cast<bf16x4*>(crow + n * 16) = v;
-    }
-  }
-}
-
-// v2: same tile/LDS image as v1, software-pipelined at the fragment level.
-//   Two fragment register sets R0/R1 (k-steps kk=0/1 of a BK=64 tile). Per tile t:
-//     issue ds_read (t,kk1)->R1 ; MFMA R0 ; [vmcnt(0) lgkmcnt(0) ; barrier]
-//     issue LDS-DMA of tile t+2 into the buffer tile t used ; ds_read (t+1,kk0)->R0 ; MFMA R1
-//   The single barrier per tile sits mid-tile: the next tile's first fragment reads are
-//   in flight under the current tile's second MFMA cluster, and each LDS-DMA has a full
-//   tile of MFMAs (64 per wave) to land. WAR on the refilled buffer is covered by the
-//   lgkmcnt(0) + barrier (every wave's reads of tile t have completed).
-__global__ void __launch_bounds__(NTHREADS)
-gemm_bf16_256x256_v2(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                     __bf16* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2;
-  const int wc = wid & 3;
-
-  const __bf16* gA = A + (size_t)tm * BM * K;
-  const __bf16* gB = Bt + (size_t)tn * BN * K;
-
-  int lane_off[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int r = lane & 15;
-    const int c = kk * 4 + (lane >> 4);
-    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-  const int a_off = wr * 128 * ROW_BYTES;
-  const int b_off = PANEL_BYTES + wc * 64 * ROW_BYTES;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 a0[8], b0[4], a1[8], b1[4];
-  auto read_frags = [&](const char* buf, int kk, bf16x8 (&af)[8], bf16x8 (&bfr)[4]) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-      bfr[n] = *reinterpret_cast<const bf16x8*>(buf + b_off + n * 16 * ROW_BYTES + lane_off[kk]);
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-      af[m] = *reinterpret_cast<const bf16x8*>(buf + a_off + m * 16 * ROW_BYTES + lane_off[kk]);
-  };
-  auto mfma_all = [&](const bf16x8 (&af)[8], const bf16x8 (&bfr)[4]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n], af[m], acc[m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  const int ktiles = K / BK;
-
-  // prologue: tile 0 resident, tile 1 in flight, (0,kk0) fragments loaded
-  stage_panel(gA, K, 0, smem, wid, lane);
-  stage_panel(gB, K, 0, smem + PANEL_BYTES, wid, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (ktiles > 1) {
-    stage_panel(gA, K, BK, smem + BUF_BYTES, wid, lane);
-    stage_panel(gB, K, BK, smem + BUF_BYTES + PANEL_BYTES, wid, lane);
-  }
-  read_frags(smem, 0, a0, b0);
-
-  for (int t = 0; t < ktiles; ++t) {
-    char* cur = smem + (t & 1) * BUF_BYTES;
-    char* nxt = smem + ((t + 1) & 1) * BUF_BYTES;
-    read_frags(cur, 1, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_all(a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 2 < ktiles) {
-      stage_panel(gA, K, (t + 2) * BK, cur, wid, lane);
-      stage_panel(gB, K, (t + 2) * BK, cur + PANEL_BYTES, wid, lane);
-    }
-    if (t + 1 < ktiles) read_frags(nxt, 0, a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_all(a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-
-  const int row_base = tm * BM + wr * 128 + (lane & 15);
-  const int col_base = tn * BN + wc * 64 + 4 * (lane >> 4);
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    __bf16* crow = C + (size_t)(row_base + m * 16) * N + col_base;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-      bf16x4 v;
-      v[0] = (__bf16)acc[m][n][0];
-      v[1] = (__bf16)acc[m][n][1];
-      v[2] = (__bf16)acc[m][n][2];
-      v[3] = (__bf16)acc[m][n][3];
-      *reinterpret_cast<bf16x4*>(crow + n * 16) = v;
-    }
-  }
-}
-
-// v3: ping-pong schedule. Same 256x256x64 tile, 8 waves (2 groups of 4: one wave of each
-// group per SIMD), but the LDS image is cut into four 16 KiB half-tiles per K-tile that line
-// up with the waves' register quadrants:
-//     A_lo = A rows {0-63, 128-191}   A_hi = A rows {64-127, 192-255}
-//     B_lo = Bt rows {64w+0..31}      B_hi = Bt rows {64w+32..63}      (w = 0..3)
-// A K-tile is 4 phases, one output quadrant (4x2 fragments x K=64 = 16 MFMAs) each:
-//     P1 (lo,lo) reads A_lo+B_lo, P2 (lo,hi) reads B_hi, P3 (hi,hi) reads A_hi, P4 (hi,lo)
-//     reads nothing (B_lo kept in registers) — 24 ds_read_b128 per K-tile, the minimum.
-// Each phase: [ds_reads ; one half-tile of LDS-DMA prefetch] s_barrier [MFMA x16] s_barrier.
-// Group 1 runs one barrier behind group 0, so on every SIMD one wave issues MFMAs while the
-// other issues its reads and DMA: the matrix pipe never waits on LDS latency.
-// Two K-tile buffers (even/odd) = 128 KiB; a half-tile is restaged >= 2 phases after its last
-// read, and vmcnt(4) (two half-tiles in flight, never 0 in the steady loop) at P4/P8 retires
-// the buffer the next four phases read. See docs/validator-gemm.md for the full table.
-constexpr int HALF_BYTES = 128 * ROW_BYTES;   // 16 KiB
-constexpr int HB_A_LO = 0, HB_A_HI = HALF_BYTES, HB_B_LO = 2 * HALF_BYTES, HB_B_HI = 3 * HALF_BYTES;
-
-// LDS row r (0..127) of a half-tile -> row of the 256-row global panel.
-__device__ __forceinline__ int a_half_row(int r, int hi) { return (r & 63) + ((r >> 6) << 7) + (hi << 6); }
-__device__ __forceinline__ int b_half_row(int r, int hi) { return (r & 31) + ((r >> 5) << 6) + (hi << 5); }
-
-template <bool IS_A>
-__device__ __forceinline__ void stage_half(const __bf16* __restrict__ g, int ld, int k0, char* lds_half,
-                                           int hi, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int rblk = i * 8 + wid;            // 8-row block 0..15
-    const int r = rblk * 8 + (lane >> 3);    // LDS row 0..127
-    const int pc = lane & 7;
-    const int c = pc ^ ((r >> 1) & 7);
-    const int gr = IS_A ? a_half_row(r, hi) : b_half_row(r, hi);
-    const __bf16* src = g + (size_t)gr * ld + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds_half + rblk * 1024), 16, 0, 0);
-  }
-}
-
-// BUF=true (v4): the half-tile DMA is `buffer_load_dwordx4 ... lds` with a per-lane voffset fixed
-// for the whole kernel and the K offset in an SGPR — no per-load 64-bit VALU address math.
-// EPI_LDS (v5): the epilogue goes through LDS (the K loop's buffers are free by then): each wave
-// writes its bf16 128x64 sub-tile with ds_write_b64 (8-byte granules XOR-swizzled by row so the
-// 16 rows a lane group writes hit distinct banks), then every thread stores whole 16-byte
-// chunks, 32 lanes per 512-byte output row — fully coalesced global_store_dwordx4.
-// PH = 4: four 16-MFMA phases per K-tile (v3-v5). PH = 2 (v6): two 32-MFMA phases per K-tile
-// (P_a: A_lo x {B_lo,B_hi}, reads A_lo+B_lo+B_hi; P_b: A_hi x {B_hi,B_lo}, reads A_hi), halving
-// the group hand-offs. Staging: {A_lo,B_lo,B_hi} of a buffer 2 phases after their read, A_hi
-// likewise; every phase ends with a counted vmcnt (2 or 6) retiring what the next phase reads.
-// KNOB (A/B experiments on the PH=4 schedule): 1 = no s_setprio around the MFMA blocks,
-// 2 = issue each phase's half-tile DMA before its ds_reads.
-template <bool BUF, bool EPI_LDS, int PH = 4, int KNOB = 0>
-__global__ void __launch_bounds__(NTHREADS)
-gemm_bf16_256x256_pp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                     __bf16* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2;   // group: 0 or 1 (also the 128-row half of the output tile)
-  const int wc = wid & 3;
-
-  const __bf16* gA = A + (size_t)tm * BM * K;
-  const __bf16* gB = Bt + (size_t)tn * BN * K;
-  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
-  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
-  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
-  // per-lane byte offsets inside the panel: [A/B][hi][i]
-  uint32_t voff[2][2][2];
-#pragma unroll
-  for (int ab = 0; ab < 2; ++ab)
-#pragma unroll
-    for (int hi = 0; hi < 2; ++hi)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = (i * 8 + wid) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
-        const int gr = ab == 0 ? a_half_row(r, hi) : b_half_row(r, hi);
-        voff[ab][hi][i] = (uint32_t)gr * (uint32_t)K * 2u + (uint32_t)c * 16u;
-      }
-  auto stage = [&](int ab, int hi, int k0, char* lds_half) {
-    if constexpr (BUF) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ab == 0 ? rA : rB, (lds_void*)(lds_half + (i * 8 + wid) * 1024), 16,
-                                                 voff[ab][hi][i], k0 * 2, 0, 0);
-    } else {
-      if (ab == 0) stage_half<true>(gA, K, k0, lds_half, hi, wid, lane);
-      else stage_half<false>(gB, K, k0, lds_half, hi, wid, lane);
-    }
-  };
-
-  int lane_off[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int r = lane & 15;
-    const int c = kk * 4 + (lane >> 4);
-    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-  const int a_off = wr * 64 * ROW_BYTES;   // this wave's 64 rows inside A_lo / A_hi
-  const int b_off = wc * 32 * ROW_BYTES;   // this wave's 32 rows inside B_lo / B_hi
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 af[4][2];        // A quadrant: 4 fragments x 2 k-steps
-  bf16x8 bq[2][2][2];     // B: [lo/hi][2 fragments][2 k-steps]
-
-  auto read_a = [&](const char* half) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        af[m][kk] = *reinterpret_cast<const bf16x8*>(half + a_off + m * 16 * ROW_BYTES + lane_off[kk]);
-  };
-  auto read_b = [&](const char* half, int q) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-        bq[q][n][kk] = *reinterpret_cast<const bf16x8*>(half + b_off + n * 16 * ROW_BYTES + lane_off[kk]);
-  };
-  auto mfma_q = [&](int qm, int qn) {
-    if constexpr (KNOB != 1) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[qm * 4 + m][qn * 2 + n] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[qn][n][kk], af[m][kk], acc[qm * 4 + m][qn * 2 + n], 0, 0, 0);
-    if constexpr (KNOB != 1) __builtin_amdgcn_s_setprio(0);
-  };
-
-  const int ktiles = K / BK;            // even (host guarantees K % 128 == 0)
-  char* const E = smem;
-  char* const O = smem + BUF_BYTES;
-
-  if constexpr (PH == 2) {
-    stage(0, 0, 0, E + HB_A_LO);
-    stage(0, 1, 0, E + HB_A_HI);
-    stage(1, 0, 0, E + HB_B_LO);
-    stage(1, 1, 0, E + HB_B_HI);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (wr == 1) bar();
-    for (int t = 0; t < ktiles; t += 2) {
-      const bool more = t + 2 < ktiles;
-      const int k1 = (t + 1) * BK, k2 = (t + 2) * BK;
-      // P1: tile t (even), A_lo x {B_lo, B_hi}; stage odd {A_lo, B_lo, B_hi} <- t+1
-      read_b(E + HB_B_LO, 0);
-      read_b(E + HB_B_HI, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      read_a(E + HB_A_LO);
-      stage(0, 0, k1, O + HB_A_LO);
-      stage(1, 0, k1, O + HB_B_LO);
-      stage(1, 1, k1, O + HB_B_HI);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      bar();
-      mfma_q(0, 0);
-      mfma_q(0, 1);
-      bar();
-      // P2: A_hi x {B_hi, B_lo}; stage odd A_hi <- t+1
-      read_a(E + HB_A_HI);
-      stage(0, 1, k1, O + HB_A_HI);
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      bar();
-      mfma_q(1, 1);
-      mfma_q(1, 0);
-      bar();
-      // P3: tile t+1 (odd); stage even {A_lo, B_lo, B_hi} <- t+2
-      read_b(O + HB_B_LO, 0);
-      read_b(O + HB_B_HI, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      read_a(O + HB_A_LO);
-      if (more) {
-        stage(0, 0, k2, E + HB_A_LO);
-        stage(1, 0, k2, E + HB_B_LO);
-        stage(1, 1, k2, E + HB_B_HI);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      bar();
-      mfma_q(0, 0);
-      mfma_q(0, 1);
-      bar();
-      // P4: stage even A_hi <- t+2
-      read_a(O + HB_A_HI);
-      if (more) {
-        stage(0, 1, k2, E + HB_A_HI);
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      }
-      bar();
-      mfma_q(1, 1);
-      mfma_q(1, 0);
-      bar();
-    }
-  } else if constexpr (PH == 8) {
-    // v7: v5's phases and staging order, but a counted wait before every phase that reads
-    // (vmcnt(8): four half-tiles in flight instead of two) — every half-tile gets >= 4
-    // phases between its DMA issue and the wait that retires it.
-#define VMWAIT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
-    stage(0, 0, 0, E + HB_A_LO);
-    stage(1, 0, 0, E + HB_B_LO);
-    stage(1, 1, 0, E + HB_B_HI);
-    stage(0, 1, 0, E + HB_A_HI);
-    stage(0, 0, BK, O + HB_A_LO);
-    stage(1, 0, BK, O + HB_B_LO);
-    VMWAIT(8);
-    bar();
-    if (wr == 1) bar();
-    for (int t = 0; t < ktiles; t += 2) {
-      const bool more = t + 2 < ktiles;
-      const int k1 = (t + 1) * BK, k2 = (t + 2) * BK, k3 = (t + 3) * BK;
-      // P1
-      read_b(E + HB_B_LO, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      read_a(E + HB_A_LO);
-      stage(1, 1, k1, O + HB_B_HI);
-      VMWAIT(8);
-      bar();
-      mfma_q(0, 0);
-      bar();
-      // P2
-      read_b(E + HB_B_HI, 1);
-      stage(0, 1, k1, O + HB_A_HI);
-      VMWAIT(8);
-      bar();
-      mfma_q(0, 1);
-      bar();
-      // P3
-      read_a(E + HB_A_HI);
-      if (more) stage(0, 0, k2, E + HB_A_LO);
-      bar();
-      mfma_q(1, 1);
-      bar();
-      // P4
-      if (more) {
-        stage(1, 0, k2, E + HB_B_LO);
-        VMWAIT(8);
-      } else {
-        VMWAIT(4);
-      }
-      bar();
-      mfma_q(1, 0);
-      bar();
-      // P5
-      read_b(O + HB_B_LO, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      read_a(O + HB_A_LO);
-      if (more) {
-        stage(1, 1, k2, E + HB_B_HI);
-        VMWAIT(8);
-      } else {
-        VMWAIT(2);
-      }
-      bar();
-      mfma_q(0, 0);
-      bar();
-      // P6
-      read_b(O + HB_B_HI, 1);
-      if (more) {
-        stage(0, 1, k2, E + HB_A_HI);
-        VMWAIT(8);
-      } else {
-        VMWAIT(0);
-      }
-      bar();
-      mfma_q(0, 1);
-      bar();
-      // P7
-      read_a(O + HB_A_HI);
-      if (more) stage(0, 0, k3, O + HB_A_LO);
-      bar();
-      mfma_q(1, 1);
-      bar();
-      // P8
-      if (more) {
-        stage(1, 0, k3, O + HB_B_LO);
-        VMWAIT(8);
-      }
-      bar();
-      mfma_q(1, 0);
-      bar();
-    }
-#undef VMWAIT
-  } else if constexpr (KNOB == 2) {
-  // prologue: even buffer <- tile 0 (complete), odd A_lo/B_lo <- tile 1 (in flight)
-  stage(0, 0, 0, E + HB_A_LO);
-  stage(0, 1, 0, E + HB_A_HI);
-  stage(1, 0, 0, E + HB_B_LO);
-  stage(1, 1, 0, E + HB_B_HI);
-  stage(0, 0, BK, O + HB_A_LO);
-  stage(1, 0, BK, O + HB_B_LO);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  bar();
-  if (wr == 1) bar();   // stagger: group 1 runs one barrier behind group 0
-
-  for (int t = 0; t < ktiles; t += 2) {
-    const bool more = t + 2 < ktiles;
-    const int k1 = (t + 1) * BK, k2 = (t + 2) * BK, k3 = (t + 3) * BK;
-    // ---- even buffer (tile t) ----
-    // P1
-    stage(1, 1, k1, O + HB_B_HI);
-    read_b(E + HB_B_LO, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    read_a(E + HB_A_LO);
-    bar();
-    mfma_q(0, 0);
-    bar();
-    // P2
-    stage(0, 1, k1, O + HB_A_HI);
-    read_b(E + HB_B_HI, 1);
-    bar();
-    mfma_q(0, 1);
-    bar();
-    // P3
-    if (more) stage(0, 0, k2, E + HB_A_LO);
-    read_a(E + HB_A_HI);
-    bar();
-    mfma_q(1, 1);
-    bar();
-    // P4
-    if (more) {
-      stage(1, 0, k2, E + HB_B_LO);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    bar();
-    mfma_q(1, 0);
-    bar();
-    // ---- odd buffer (tile t+1) ----
-    // P5
-    if (more) stage(1, 1, k2, E + HB_B_HI);
-    read_b(O + HB_B_LO, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    read_a(O + HB_A_LO);
-    bar();
-    mfma_q(0, 0);
-    bar();
-    // P6
-    if (more) stage(0, 1, k2, E + HB_A_HI);
-    read_b(O + HB_B_HI, 1);
-    bar();
-    mfma_q(0, 1);
-    bar();
-    // P7
-    if (more) stage(0, 0, k3, O + HB_A_LO);
-    read_a(O + HB_A_HI);
-    bar();
-    mfma_q(1, 1);
-    bar();
-    // P8
-    if (more) {
-      stage(1, 0, k3, O + HB_B_LO);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    bar();
-    mfma_q(1, 0);
-    bar();
-  }
-  } else {
-  // prologue: even buffer <- tile 0 (complete), odd A_lo/B_lo <- tile 1 (in flight)
-  stage(0, 0, 0, E + HB_A_LO);
-  stage(0, 1, 0, E + HB_A_HI);
-  stage(1, 0, 0, E + HB_B_LO);
-  stage(1, 1, 0, E + HB_B_HI);
-  stage(0, 0, BK, O + HB_A_LO);
-  stage(1, 0, BK, O + HB_B_LO);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  bar();
-  if (wr == 1) bar();   // stagger: group 1 runs one barrier behind group 0
-
-  for (int t = 0; t < ktiles; t += 2) {
-    const bool more = t + 2 < ktiles;
-    const int k1 = (t + 1) * BK, k2 = (t + 2) * BK, k3 = (t + 3) * BK;
-    // ---- even buffer (tile t) ----
-    // P1
-    read_b(E + HB_B_LO, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    read_a(E + HB_A_LO);
-    stage(1, 1, k1, O + HB_B_HI);
-    bar();
-    mfma_q(0, 0);
-    bar();
-    // P2
-    read_b(E + HB_B_HI, 1);
-    stage(0, 1, k1, O + HB_A_HI);
-    bar();
-    mfma_q(0, 1);
-    bar();
-    // P3
-    read_a(E + HB_A_HI);
-    if (more) stage(0, 0, k2, E + HB_A_LO);
-    bar();
-    mfma_q(1, 1);
-    bar();
-    // P4
-    if (more) {
-      stage(1, 0, k2, E + HB_B_LO);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    bar();
-    mfma_q(1, 0);
-    bar();
-    // ---- odd buffer (tile t+1) ----
-    // P5
-    read_b(O + HB_B_LO, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    read_a(O + HB_A_LO);
-    if (more) stage(1, 1, k2, E + HB_B_HI);
-    bar();
-    mfma_q(0, 0);
-    bar();
-    // P6
-    read_b(O + HB_B_HI, 1);
-    if (more) stage(0, 1, k2, E + HB_A_HI);
-    bar();
-    mfma_q(0, 1);
-    bar();
-    // P7
-    read_a(O + HB_A_HI);
-    if (more) stage(0, 0, k3, O + HB_A_LO);
-    bar();
-    mfma_q(1, 1);
-    bar();
-    // P8
-    if (more) {
-      stage(1, 0, k3, O + HB_B_LO);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    bar();
-    mfma_q(1, 0);
-    bar();
-  }
-  }  // PH
-  if (wr == 0) bar();   // re-align the groups' barrier counts
-
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  if constexpr (EPI_LDS) {
-    bar();                // every wave is past its last ds_read of the K loop
-    constexpr int CROW = BN * 2;                     // 512-byte LDS row
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int r = wr * 128 + m * 16 + (lane & 15);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int g = (wc * 64 + n * 16 + 4 * (lane >> 4)) >> 2;   // 8-byte granule 0..63
-        bf16x4 v;
-        v[0] = (__bf16)acc[m][n][0];
-        v[1] = (__bf16)acc[m][n][1];
-        v[2] = (__bf16)acc[m][n][2];
-        v[3] = (__bf16)acc[m][n][3];
-        *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
-      }
-    }
-    bar();
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < (BM * BN * 2) / (NTHREADS * 16); ++i) {      // 16 chunks per thread
-      const int r = i * (NTHREADS / 32) + (tid >> 5);
-      const int ch = tid & 31;                                        // 16-byte chunk in the row
-      const int s = r & 15;
-      const int pg = (2 * ch) ^ s;                                    // physical granule of the even half
-      const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
-      uint4 v = raw;
-      if (s & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-      *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
-    }
-    return;
-  }
-
-  const int row_base = tm * BM + wr * 128 + (lane & 15);
-  const int col_base = tn * BN + wc * 64 + 4 * (lane >> 4);
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    __bf16* crow = C + (size_t)(row_base + m * 16) * N + col_base;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      bf16x4 v;
-      v[0] = (__bf16)acc[m][n][0];
-      v[1] = (__bf16)acc[m][n][1];
-      v[2] = (__bf16)acc[m][n][2];
-      v[3] = (__bf16)acc[m][n][3];
-      *reinterpret_cast<bf16x4*>(crow + n * 16) = v;
-    }
-  }
-}
-
-// v10: one wave per SIMD. 4 waves (2x2), each owning a 128x128 sub-tile: 8x8 MFMA 16x16x32
-// accumulators = the wave's 256 AGPRs; its fragments (2 x 16 x bf16x8 = 128 VGPRs) and addresses
-// fit the 256 VGPRs. A 128x128 wave tile halves the LDS bytes per MFMA against v5's 128x64
-// (256 B vs 384 B): per K-tile the CU reads 128 KiB of fragments + 64 KiB of DMA writes in 2048
-// MFMA cycles (96 B/clk of LDS's 128) where v5 needed 128 B/clk, i.e. sat on the LDS port.
-// Each SIMD's matrix pipe is fed by its single wave, which interleaves its own LDS fragment reads
-// (1 ds_read_b128 per 4 MFMAs) and LDS-DMA pieces (1 per 4 MFMAs) into the MFMA stream. Per K-tile:
-//   block(t, kk0): MFMA with R0, read R1 <- frags(t, kk1)
-//   wait lgkmcnt(0) + vmcnt(0) (tile t+1 landed) ; barrier (tile t fully read by every wave)
-//   block(t, kk1): MFMA with R1, read R0 <- frags(t+1, kk0), DMA tile t+2 into tile t's buffer
-// One barrier per K-tile; the DMA of a tile has a full K-tile (128 MFMAs) to land.
-//
-// The accumulators are pinned: hipcc's greedy allocator, given 64 tuples that fill all 256 AGPRs,
-// cannot keep them in place across the loop back-edge and shuffles them through a[0:3] with
-// ~600 v_accvgpr moves per K-tile. So the MFMAs are inline asm on literal a[4i:4i+3] (the kernel
-// owns every AGPR via W4_AGPR_CLOBBERS; the compiler has no AGPR values of its own -- audited in
-// tests/test_gemm_build.py: no compiler v_accvgpr_* outside the asm blocks). Hazards handled by
-// hand (cdna_hip_programming.md §5.7 item 2): zeroing writes -> first MFMA reading them as C are
-// separated by the prologue; the last MFMA's D -> v_accvgpr_read is covered by an explicit s_nop
-// pad; an accumulate chain MFMA -> MFMA (same C) needs none. A/B operands come from compiler
-// ds_reads whose lgkmcnt waits hipcc inserts before each asm statement that names them.
-constexpr int W4_THREADS = 256;
-
-struct W4Frags {
-  bf16x8 a[8];
-  bf16x8 b[8];
-};
-
-template <int I>
-__device__ __forceinline__ void w4_mfma(const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
-               :: "i"(4 * I), "i"(4 * I + 3), "v"(b), "v"(a));
-}
-
-// fragment read order j -> (A or B, index): the order the next block consumes them
-// (i = 0..7 uses a0 with b0..b7, then a1 ...), so hipcc's lgkmcnt ladder releases MFMAs early.
-__device__ __forceinline__ constexpr int w4_isb(int j) { return j >= 1 && j <= 8; }
-__device__ __forceinline__ constexpr int w4_idx(int j) { return j == 0 ? 0 : (j <= 8 ? j - 1 : j - 8); }
-
-// RSPAN / DSPAN: the 16 fragment reads / DMA pieces of a block are spread over its first
-// RSPAN / DSPAN groups of 4 MFMAs (16 = evenly; smaller = earlier, more latency slack).
-// KO (profiling only, wrong results): bit0 drops the per-tile wait+barrier, bit1 the DMA, bit2
-// the fragment reads -- knock-out timings that price each component.
-template <int RSPAN = 16, int DSPAN = 16, int KO = 0>
-__global__ void __launch_bounds__(W4_THREADS, 1)
-gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                     __bf16* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-
-  const __bf16* gA = A + (size_t)tm * BM * K;
-  const __bf16* gB = Bt + (size_t)tn * BN * K;
-  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
-  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
-  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
-  // wave w issues pieces p = 4i + w (A row blocks 0..31, then B); every piece it issues has
-  // row-block parity w & 1, so one per-lane voffset serves all of them.
-  const int par = wid & 1;
-  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
-                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
-  auto dma_piece = [&](int i, int k0, char* buf) {
-    const int p = i * 4 + wid;                     // 0..63
-    const int rblk = p & 31;
-    char* lds = buf + (p >= 32 ? PANEL_BYTES : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(p >= 32 ? rB : rA, (lds_void*)lds, 16, voff,
-                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
-  };
-
-  int lane_off[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int r = lane & 15;
-    const int c = kk * 4 + (lane >> 4);
-    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-  const int a_off = wr * 128 * ROW_BYTES;
-  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
-
-  asm volatile("" ::: W4_AGPR_CLOBBERS);
-  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
-
-  W4Frags R0, R1;
-  char* const buf0 = smem;
-  char* const buf1 = smem + BUF_BYTES;
-
-  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
-    constexpr int j = decltype(J)::value;
-    constexpr int x = w4_idx(j);
-    if constexpr (w4_isb(j))
-      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
-    else
-      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
-  };
-  // 64 MFMAs with Fc; optionally 16 fragment reads into Fn (from nbuf, step nkk) and 16 DMA
-  // pieces (tile at column dk into dbuf) placed after groups of 4 MFMAs; sched_barrier pins it.
-  auto block = [&](const W4Frags& Fc, W4Frags& Fn, const char* nbuf, int nkk, auto RD, char* dbuf, int dk,
-                   auto DM) {
-    static_for<0, 16>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      static_for<0, 4>([&](auto U) {
-        constexpr int i = q * 4 + decltype(U)::value;
-        w4_mfma<i>(Fc.b[i & 7], Fc.a[i >> 3]);
-      });
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(RD)::value && !(KO & 4) && j * RSPAN / 16 == q) read_frag(Fn, nbuf, nkk, J);
-      });
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(DM)::value && !(KO & 2) && j * DSPAN / 16 == q) dma_piece(j, dk, dbuf);
-      });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  auto sync_tile = [&]() {
-    if constexpr (!(KO & 1)) {
-      __builtin_amdgcn_s_waitcnt(0x0070);           // vmcnt(0) lgkmcnt(0), visible to hipcc's counters
-      bar();
-    }
-  };
-
-  const int ktiles = K / BK;        // >= 2 (host guarantees)
-  // prologue: tile 0 -> buf0 (waited), tile 1 -> buf1 (in flight), R0 <- (0, kk0)
-#pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, 0, buf0);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, BK, buf1);
-  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
-  bar();
-  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
-
-  char* cur = buf0;
-  char* nxt = buf1;
-  for (int t = 0; t < ktiles - 2; ++t) {
-    block(R0, R1, cur, 1, T_{}, nullptr, 0, F_{});
-    sync_tile();
-    block(R1, R0, nxt, 0, T_{}, cur, (t + 2) * BK, T_{});
-    char* tmp = cur; cur = nxt; nxt = tmp;
-  }
-  // second-to-last tile: prefetch fragments, no DMA; then the last tile
-  block(R0, R1, cur, 1, T_{}, nullptr, 0, F_{});
-  sync_tile();
-  block(R1, R0, nxt, 0, T_{}, nullptr, 0, F_{});
-  block(R0, R1, nxt, 1, T_{}, nullptr, 0, F_{});
-  block(R1, R0, nullptr, 0, F_{}, nullptr, 0, F_{});
-
-  // epilogue through LDS (every wave is past its last ds_read once all reach this barrier);
-  // pad the last MFMA's D before the accumulator reads.
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  bar();
-  constexpr int CROW = BN * 2;
-  static_for<0, 64>([&](auto I) {
-    constexpr int i = decltype(I)::value;
-    constexpr int m = i >> 3, n = i & 7;
-    float x0, x1, x2, x3;
-    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
-                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
-                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
-                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
-    const int r = wr * 128 + m * 16 + (lane & 15);
-    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
-    bf16x4 v;
-    v[0] = (__bf16)x0;
-    v[1] = (__bf16)x1;
-    v[2] = (__bf16)x2;
-    v[3] = (__bf16)x3;
-    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
-  });
-  bar();
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {      // 32 chunks per thread
-    const int r = i * (W4_THREADS / 32) + (tid >> 5);
-    const int ch = tid & 31;
-    const int sw = r & 15;
-    const int pg = (2 * ch) ^ sw;
-    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
-    uint4 v = raw;
-    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
-  }
-}
-
-// v18: v10's data layout with the schedule reshaped around the K-tile instead of two halves.
-// Knock-out cycle accounting of v10 (profiles/r1_gemm_v10/README.md) priced its DMA at 13 % of
-// the wave cycles and its wait+barrier at 4 %, with fragment reads nearly free. Here, in MFMA
-// slots 0..127 of iteration t (0..63 on R0 = tile t kk0, 64..127 on R1 = tile t kk1):
-//   slots 0..15      read R1 <- tile t kk1 (one per MFMA)
-//   slot B1          lgkmcnt(0) one MFMA earlier, then a barrier: every wave is done with tile t
-//   slots D0 + j*DS  DMA tile t+2 into tile t's buffer (16 pieces), starting ~40 slots earlier
-//                    than v10 so a piece has ~80 MFMAs to land
-//   slot B2          vmcnt(pieces issued so far this iteration) one MFMA earlier -- tile t+1 (last
-//                    iteration's pieces) landed, this iteration's stay in flight -- then a barrier
-//   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
-// Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
-template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
-          bool SQ = false>
-__global__ void __launch_bounds__(W4_THREADS, 1)
-gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                      __bf16* __restrict__ C, int M, int N, int K) {
-  static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  int tm, tn;
-  if constexpr (SQ) tile_coords_sq(blockIdx.x, tiles_n, tm, tn);
-  else tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-
-  const __bf16* gA = A + (size_t)tm * BM * K;
-  const __bf16* gB = Bt + (size_t)tn * BN * K;
-  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
-  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
-  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
-  const int par = wid & 1;
-  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
-                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
-  auto dma_piece = [&](int i, int k0, char* buf) {
-    // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
-    const int rblk = ((i & 7) << 2) + wid;
-    char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
-                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
-  };
-
-  int lane_off[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int r = lane & 15;
-    const int c = kk * 4 + (lane >> 4);
-    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-  const int a_off = wr * 128 * ROW_BYTES;
-  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
-
-  asm volatile("" ::: W4_AGPR_CLOBBERS);
-  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
-
-  W4Frags R0, R1;
-  char* const buf0 = smem;
-  char* const buf1 = smem + BUF_BYTES;
-  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
-    constexpr int j = decltype(J)::value;
-    constexpr int x = w4_idx(j);
-    if constexpr (w4_isb(j))
-      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
-    else
-      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
-  };
-  // DM: DMA tile t+2; NX: tile t+1 exists (wait for it, read its kk0 into R0); LAST_DMA: the
-  // previous iteration issued no DMA (vmcnt target 0 instead of this iteration's count)
-  // slots [LO, HI) of one K-tile iteration; the slots before B1 depend on no flag (ROT splits there)
-  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX, auto LO, auto HI) {
-    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value;
-    static_for<decltype(LO)::value, decltype(HI)::value>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
-      else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
-      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
-      if constexpr (i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
-      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
-      if constexpr (nx && i == B2 - 1) {
-        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
-        // vmcnt(issued) lgkmcnt(0): vmcnt low 4 bits [3:0], high 2 bits [15:14]; expcnt 7
-        __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
-      }
-      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
-      if constexpr (nx && i > B2) {
-        static_for<0, 16>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
-        });
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-
-  const int ktiles = K / BK;        // >= 2 (host guarantees)
-  // SERP > 0 (serpentine K): with SERP co-resident workgroups per XCD, every other wave of tiles
-  // walks K backwards, so it starts on the K-slices of the A panels the previous wave just left
-  // in the XCD's L2.
-  const bool rev = SERP > 0 && (((int)blockIdx.x / NXCD) / (SERP > 0 ? SERP : 1)) & 1;
-  auto kof = [&](int kt) { return (rev ? ktiles - 1 - kt : kt) * BK; };
-#pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, kof(0), buf0);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, kof(1), buf1);
-  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
-  bar();
-  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
-
-  using S0 = std::integral_constant<int, 0>;
-  using SB = std::integral_constant<int, B1>;
-  using SE = std::integral_constant<int, 128>;
-  char* cur = buf0;
-  char* nxt = buf1;
-  if constexpr (ROT) {
-    // Loop rotation (v42/v43): an iteration runs slots B1..127 of tile t, then 0..B1-1 of tile
-    // t+1, so the back-edge follows the explicit lgkmcnt(0) at slot B1-1 instead of the R0 reads,
-    // where hipcc's merged loop-header state is a blanket lgkmcnt(0) before the first MFMA.
-    iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
-    for (int t = 0; t < ktiles - 2; ++t) {
-      iter(cur, nxt, kof(t + 2), T_{}, T_{}, SB{}, SE{});
-      char* tmp = cur; cur = nxt; nxt = tmp;
-      iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
-    }
-    iter(cur, nxt, 0, F_{}, T_{}, SB{}, SE{});
-    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
-  } else {
-    for (int t = 0; t < ktiles - 2; ++t) {
-      iter(cur, nxt, kof(t + 2), T_{}, T_{}, S0{}, SE{});
-      char* tmp = cur; cur = nxt; nxt = tmp;
-    }
-    iter(cur, nxt, 0, F_{}, T_{}, S0{}, SE{});
-    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
-  }
-
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  bar();
-  constexpr int CROW = BN * 2;
-  static_for<0, 64>([&](auto I) {
-    constexpr int i = decltype(I)::value;
-    constexpr int m = i >> 3, n = i & 7;
-    float x0, x1, x2, x3;
-    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
-                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
-                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
-                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
-    const int r = wr * 128 + m * 16 + (lane & 15);
-    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
-    bf16x4 v;
-    v[0] = (__bf16)x0;
-    v[1] = (__bf16)x1;
-    v[2] = (__bf16)x2;
-    v[3] = (__bf16)x3;
-    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
-  });
-  bar();
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {
-    const int r = i * (W4_THREADS / 32) + (tid >> 5);
-    const int ch = tid & 31;
-    const int sw = r & 15;
-    const int pg = (2 * ch) ^ sw;
-    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
-    uint4 v = raw;
-    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
-  }
-}
-
-// v25/v26: v18 made persistent. gridDim = one workgroup per CU; XCD x (= blockIdx % 8) owns a
-// contiguous run of output tiles (the bijective split of xcd_remap) that its gridDim/8
-// workgroups walk in strides. The K-tile stream runs on across tile boundaries: the last two
-// K-iterations of a tile DMA the NEXT tile's K-tiles 0 and 1 into the freed buffers and the last
-// one already reads its first fragments, so the next tile starts without a cold HBM prologue.
-// The epilogue no longer needs the K buffers: each wave stages its own 128x128 sub-tile through a
-// private 8 KiB slice of the 32 KiB of LDS the K buffers leave free (2 fragment rows = 32 C rows
-// per pass, XOR-swizzled, read back as full 256-B row segments), so it needs no workgroup barrier
-// and overlaps the in-flight DMA; the accumulators are zeroed as they are read.
-constexpr int W4P_EPI_WAVE = 8192;                       // 32 rows x 128 cols x bf16
-constexpr int W4P_LDS = LDS_BYTES + 4 * W4P_EPI_WAVE;     // 160 KiB
-
-template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, bool SERP = false>
-__global__ void __launch_bounds__(W4_THREADS, 1)
-gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                       __bf16* __restrict__ C, int M, int N, int K) {
-  static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
-  __shared__ __attribute__((aligned(16))) char smem[W4P_LDS];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  const int xcd = blockIdx.x % NXCD;
-  const int per = gridDim.x / NXCD;                       // workgroups per XCD (host: gridDim % 8 == 0)
-  const int q = nwg / NXCD, rem = nwg % NXCD;
-  const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
-  const int t_end = t_begin + q + (xcd < rem ? 1 : 0);
-  int tile = t_begin + (int)(blockIdx.x / NXCD);
-  if (tile >= t_end) return;                              // uniform over the workgroup
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-
-  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
-  auto rsrc = [&](const __bf16* base) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, panel_bytes, 0x00020000);
-  };
-  int tm, tn;
-  tile_coords(tile, tiles_m, tiles_n, tm, tn);
-  __amdgpu_buffer_rsrc_t rA = rsrc(A + (size_t)tm * BM * K);
-  __amdgpu_buffer_rsrc_t rB = rsrc(Bt + (size_t)tn * BN * K);
-  const int par = wid & 1;
-  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
-                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
-  auto dma_piece = [&](int i, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int k0, char* buf) {
-    // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
-    const int rblk = ((i & 7) << 2) + wid;
-    char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff,
-                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
-  };
-
-  int lane_off[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int r = lane & 15;
-    const int c = kk * 4 + (lane >> 4);
-    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-  const int a_off = wr * 128 * ROW_BYTES;
-  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
-
-  asm volatile("" ::: W4_AGPR_CLOBBERS);
-  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
-
-  W4Frags R0, R1;
-  char* const buf0 = smem;
-  char* const buf1 = smem + BUF_BYTES;
-  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
-    constexpr int j = decltype(J)::value;
-    constexpr int x = w4_idx(j);
-    if constexpr (w4_isb(j))
-      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
-    else
-      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
-  };
-  // The v18 iteration; the DMA target (operand panels and K offset) is a runtime argument so the
-  // same body serves this tile's K-tile t+2 and the next tile's K-tiles 0 and 1.
-  // FRESH: a tile's first iteration. The vmcnt(0) before it (prologue or previous epilogue) already
-  // retired this tile's K-tile 1, so its B2 does not wait again: the epilogue's C stores are older
-  // than this iteration's DMA, and a counted vmcnt would wait for them too.
-  auto iter = [&](char* cur, char* nxt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int dk, auto FR,
-                  auto DM, auto NX) {
-    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value, fresh = decltype(FR)::value;
-    static_for<0, 128>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
-      else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
-      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
-      if constexpr (dm && i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
-      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, ra, rb, dk, cur);
-      if constexpr (nx && i == B2 - 1) {
-        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
-        if constexpr (fresh) __builtin_amdgcn_s_waitcnt(0xC07F);             // lgkmcnt(0) only
-        else __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
-      }
-      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
-      if constexpr (nx && i > B2) {
-        static_for<0, 16>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
-        });
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-
-  // Wave-private epilogue: 4 passes of 2 fragment rows (32 C rows x 128 cols).
-  char* const stg = smem + LDS_BYTES + wid * W4P_EPI_WAVE;
-  auto epilogue = [&](int tm_, int tn_) {
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA D -> accvgpr reads
-    static_for<0, 4>([&](auto S) {
-      constexpr int s = decltype(S)::value;
-      static_for<0, 16>([&](auto I) {
-        constexpr int u = decltype(I)::value;
-        constexpr int mm = u >> 3, n = u & 7;
-        constexpr int i = (2 * s + mm) * 8 + n;                    // accumulator index m*8+n
-        float x0, x1, x2, x3;
-        asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
-                     "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
-                     "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
-                     "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
-                     : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
-                     : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
-        const int r = mm * 16 + (lane & 15);                       // 0..31
-        const int g = n * 4 + (lane >> 4);                         // 8-byte group 0..31
-        bf16x4 v;
-        v[0] = (__bf16)x0;
-        v[1] = (__bf16)x1;
-        v[2] = (__bf16)x2;
-        v[3] = (__bf16)x3;
-        *reinterpret_cast<bf16x4*>(stg + r * 256 + ((g ^ (r & 15)) << 3)) = v;
-      });
-      asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
-      // retire the next tile's K-tile DMAs before the first C store (see `fresh`)
-      if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int r = k * 4 + (lane >> 4);
-        const int ch = lane & 15;
-        const int sw = r & 15;
-        const int pg = (2 * ch) ^ sw;
-        const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
-        uint4 v = raw;
-        if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * BM + wr * 128 + s * 32 + r) * N + tn_ * BN + wc * 128 + ch * 8) = v;
-      }
-      asm volatile("" ::: "memory");
-    });
-  };
-
-  const int ktiles = K / BK;        // >= 2 (host guarantees)
-  // SERP (v27): a workgroup's i-th tile belongs to wave i of its XCD; odd waves walk K backwards
-  // and start on the A-panel K-slices the previous wave left in the XCD's L2.
-  bool rev = false;
-  auto kof = [&](int kt, bool r) { return (r ? ktiles - 1 - kt : kt) * BK; };
-#pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(0, rev), buf0);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(1, rev), buf1);
-  __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0): K-tiles 0 and 1 landed (FRESH iteration)
-  bar();
-  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
-
-  char* cur = buf0;
-  char* nxt = buf1;
-  for (;;) {
-    const int next = tile + per;
-    const bool has_next = next < t_end;
-    int ntm = tm, ntn = tn;
-    __amdgpu_buffer_rsrc_t nA = rA, nB = rB;
-    if (has_next) {
-      tile_coords(next, tiles_m, tiles_n, ntm, ntn);
-      nA = rsrc(A + (size_t)ntm * BM * K);
-      nB = rsrc(Bt + (size_t)ntn * BN * K);
-    }
-    const int nsteady = has_next ? ktiles : ktiles - 2;
-    auto dma_of = [&](int t, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rb) {
-      const bool nt = t + 2 >= ktiles;               // DMA the next tile's K-tile t+2-ktiles
-      ra = nt ? nA : rA;
-      rb = nt ? nB : rB;
-      return nt ? kof(t + 2 - ktiles, SERP && !rev) : kof(t + 2, rev);
-    };
-    __amdgpu_buffer_rsrc_t ra, rb;
-    if (nsteady > 0) {
-      const int dk = dma_of(0, ra, rb);
-      iter(cur, nxt, ra, rb, dk, T_{}, T_{}, T_{});
-      char* tmp = cur; cur = nxt; nxt = tmp;
-    }
-    for (int t = 1; t < nsteady; ++t) {
-      const int dk = dma_of(t, ra, rb);
-      iter(cur, nxt, ra, rb, dk, F_{}, T_{}, T_{});
-      char* tmp = cur; cur = nxt; nxt = tmp;
-    }
-    if (!has_next) {
-      iter(cur, nxt, rA, rB, 0, F_{}, F_{}, T_{});
-      iter(nxt, nullptr, rA, rB, 0, F_{}, F_{}, F_{});
-    }
-    epilogue(tm, tn);
-    if (!has_next) break;
-    tile = next;
-    rev = SERP && !rev;
-    tm = ntm;
-    tn = ntn;
-    rA = nA;
-    rB = nB;
-  }
-}
-
-// v15: v10's wave layout over a 5-slot ring of K-half-tiles (32 k-columns: A 16 KiB + B 16 KiB
-// per slot = all 160 KiB of LDS). v10 syncs once per K-tile but the DMA it waits for was issued
-// only one 64-MFMA block earlier (~1000 cycles: less than a loaded L2-miss round trip). Here block
-// h (64 MFMAs on half h) reads the fragments of half h+1 and DMAs half h+4 into the slot of half
-// h-1; its closing barrier needs half h+2, issued two blocks earlier (vmcnt(16): halves h+3, h+4
-// stay in flight). One barrier per 64 MFMAs instead of per 128.
-// Slot layout: 256 rows x 64 B per operand, 16-B chunk c of row r at ((c ^ ((r >> 2) & 3)) << 4):
-// the 16 lanes of a ds_read_b128 phase (16 rows, one chunk) cover all 64 banks. LDS-DMA writes a
-// 1-KiB piece (16 rows) lane-contiguous, so each lane fetches the global chunk its LDS slot holds.
-constexpr int RH_ROW = 64;                          // bytes per row per half
-constexpr int RH_OP = BM * RH_ROW;                  // 16 KiB per operand per half
-constexpr int RH_SLOT = 2 * RH_OP;                  // 32 KiB
-constexpr int RH_NSLOT = 5;                         // 160 KiB
-
-template <int RSPAN = 12, int DSPAN = 8>
-__global__ void __launch_bounds__(W4_THREADS, 1)
-gemm_bf16_256x256_w4r(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                      __bf16* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char smem[RH_NSLOT * RH_SLOT];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-
-  const __bf16* gA = A + (size_t)tm * BM * K;
-  const __bf16* gB = Bt + (size_t)tn * BN * K;
-  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
-  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
-  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
-  // piece = 16 rows x 64 B; lane L -> row L>>2, LDS chunk L&3 holding global chunk (L&3)^((L>>4)&3)
-  const uint32_t voff = (uint32_t)(lane >> 2) * (uint32_t)K * 2u +
-                        (uint32_t)(((lane & 3) ^ ((lane >> 4) & 3)) * 16);
-  // half h: 32 pieces (A row blocks 0..15, B 0..15); wave w issues p = 4i + w, i = 0..7
-  // slot indices are carried incrementally (sl = h mod 5): no division in the loop
-  auto m5 = [](int x) { return x >= RH_NSLOT ? x - RH_NSLOT : x; };
-  auto dma_piece = [&](int i, int h, int sl) {
-    const int p = i * 4 + wid;
-    const int rblk = p & 15;
-    char* lds = smem + sl * RH_SLOT + (p >= 16 ? RH_OP : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(p >= 16 ? rB : rA, (lds_void*)lds, 16, voff,
-                                             (uint32_t)rblk * 16u * (uint32_t)K * 2u + (uint32_t)h * 64u, 0, 0);
-  };
-  const int r16 = lane & 15;
-  const int lane_off = r16 * RH_ROW + (((lane >> 4) ^ ((r16 >> 2) & 3)) << 4);
-  const int a_off = wr * 128 * RH_ROW + lane_off;
-  const int b_off = RH_OP + wc * 128 * RH_ROW + lane_off;
-
-  asm volatile("" ::: W4_AGPR_CLOBBERS);
-  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
-
-  W4Frags R0, R1;
-  auto read_frag = [&](W4Frags& F, int sl, auto J) {
-    constexpr int j = decltype(J)::value;
-    constexpr int x = w4_idx(j);
-    const char* slot = smem + sl * RH_SLOT;
-    if constexpr (w4_isb(j))
-      F.b[x] = *reinterpret_cast<const bf16x8*>(slot + b_off + x * 16 * RH_ROW);
-    else
-      F.a[x] = *reinterpret_cast<const bf16x8*>(slot + a_off + x * 16 * RH_ROW);
-  };
-  // one block: 64 MFMAs on Fc; reads from slot rs into Fn; DMA of half dh into slot ds
-  auto block = [&](const W4Frags& Fc, W4Frags& Fn, int rs, auto RD, int dh, int ds, auto DM) {
-    static_for<0, 16>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      static_for<0, 4>([&](auto U) {
-        constexpr int i = q * 4 + decltype(U)::value;
-        w4_mfma<i>(Fc.b[i & 7], Fc.a[i >> 3]);
-      });
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(RD)::value && j * RSPAN / 16 == q) read_frag(Fn, rs, J);
-      });
-      static_for<0, 8>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(DM)::value && j * DSPAN / 8 == q) dma_piece(j, dh, ds);
-      });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-
-  const int H = K / 32;             // >= 4 (host guarantees K >= 128)
-#pragma unroll
-  for (int h = 0; h < 4; ++h)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) dma_piece(i, h, h);
-  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): halves 0, 1 landed
-  bar();
-  static_for<0, 16>([&](auto J) { read_frag(R0, 0, J); });
-
-  // steady state, two halves per trip so R0/R1 keep their roles
-  int h = 0, sl = 0;
-  for (; h + 5 < H; h += 2, sl = m5(sl + 2)) {
-    block(R0, R1, m5(sl + 1), T_{}, h + 4, m5(sl + 4), T_{});
-    __builtin_amdgcn_s_waitcnt(0x4070);             // vmcnt(16) lgkmcnt(0): half h+2 landed
-    bar();
-    block(R1, R0, m5(sl + 2), T_{}, h + 5, sl, T_{});
-    __builtin_amdgcn_s_waitcnt(0x4070);             // half h+3 landed
-    bar();
-  }
-  // H is even, so exactly 4 halves are left: h .. H-1
-  block(R0, R1, m5(sl + 1), T_{}, 0, 0, F_{});
-  __builtin_amdgcn_s_waitcnt(0x0078);             // vmcnt(8): half h+2 landed, h+3 in flight
-  bar();
-  block(R1, R0, m5(sl + 2), T_{}, 0, 0, F_{});
-  __builtin_amdgcn_s_waitcnt(0x0070);             // vmcnt(0): half h+3 landed
-  bar();
-  block(R0, R1, m5(sl + 3), T_{}, 0, 0, F_{});
-  block(R1, R0, 0, F_{}, 0, 0, F_{});
-
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  bar();
-  constexpr int CROW = BN * 2;
-  static_for<0, 64>([&](auto I) {
-    constexpr int i = decltype(I)::value;
-    constexpr int m = i >> 3, n = i & 7;
-    float x0, x1, x2, x3;
-    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
-                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
-                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
-                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
-    const int r = wr * 128 + m * 16 + (lane & 15);
-    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
-    bf16x4 v;
-    v[0] = (__bf16)x0;
-    v[1] = (__bf16)x1;
-    v[2] = (__bf16)x2;
-    v[3] = (__bf16)x3;
-    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
-  });
-  bar();
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {
-    const int r = i * (W4_THREADS / 32) + (tid >> 5);
-    const int ch = tid & 31;
-    const int sw = r & 15;
-    const int pg = (2 * ch) ^ sw;
-    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
-    uint4 v = raw;
-    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
-  }
-}
-
-// Generic bounds-checked MFMA kernel (64x64 tile, 4 waves of 32x32), register-staged.
-// Used for shapes that are not multiples of 256/256/64 and as a second, independent
-// implementation for cross-checking the fast path.
-constexpr int GBM = 64, GBN = 64, GBK = 32;
-
-__global__ void __launch_bounds__(256)
-gemm_bf16_generic(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                  __bf16* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) __bf16 sa[GBM][GBK + 8];
-  __shared__ __attribute__((aligned(16))) __bf16 sb[GBN][GBK + 8];
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
-
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // 256 threads x 8 elements = 64 rows x 32 k per operand.
-  const int lr = threadIdx.x >> 2;        // row 0..63
-  const int lk = (threadIdx.x & 3) * 8;   // k offset 0,8,16,24
-  for (int k0 = 0; k0 < K; k0 += GBK) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = k0 + lk + e;
-      const int ra = m0 + lr, rb = n0 + lr;
-      sa[lr][lk + e] = (ra < M && k < K) ? A[(size_t)ra * K + k] : (__bf16)0.f;
-      sb[lr][lk + e] = (rb < N && k < K) ? Bt[(size_t)rb * K + k] : (__bf16)0.f;
-    }
-    __syncthreads();
-    bf16x8 af[2], bfr[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        af[i][e] = sa[wr * 32 + i * 16 + (lane & 15)][8 * (lane >> 4) + e];
-        bfr[i][e] = sb[wc * 32 + i * 16 + (lane & 15)][8 * (lane >> 4) + e];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wr * 32 + i * 16 + (lane & 15);
-        const int col = n0 + wc * 32 + j * 16 + 4 * (lane >> 4) + e;
-        if (row < M && col < N) C[(size_t)row * N + col] = (__bf16)acc[i][j][e];
-      }
-}
-
-// fp32-accumulating reference (one thread per output element; sampled rows only).
-__global__ void gemm_ref_rows(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                              const int* __restrict__ rows, int nrows, float* __restrict__ out,
-                              int N, int K) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ri = blockIdx.y;
-  if (col >= N || ri >= nrows) return;
-  const __bf16* a = A + (size_t)rows[ri] * K;
-  const __bf16* b = Bt + (size_t)col * K;
-  float s = 0.f;
-  for (int k = 0; k < K; ++k) s += (float)a[k] * (float)b[k];
-  out[(size_t)ri * N + col] = s;
-}
-
-// Deterministic uniform [-1,1) bf16 fill (counter-based hash), so validator runs on
-// random data (zero-filled operands inflate MFMA clocks and hide layout bugs).
-__global__ void fill_uniform_bf16(__bf16* p, size_t n, uint32_t seed) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (; i < n; i += stride) {
-    uint32_t x = (uint32_t)i * 0x9E3779B1u ^ seed;
-    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-    const float u = (float)(x >> 8) * (1.0f / 16777216.0f);
-    p[i] = (__bf16)(2.0f * u - 1.0f);
-  }
-}
-
-}  // namespace
-
-static int g_variant = -1;
-
-static int variant() {
-  if (g_variant < 0) {
-    const char* e = getenv("AMDGO_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 44;
-  }
-  return g_variant;
-}
+static int g_variant = 0;
 
 // Persistent grid: one workgroup per CU (the 160 KiB LDS admits one), a multiple of the 8 XCDs,
 // never more workgroups than tiles. 0 when the device or the tile count is too small.
@@ -1620,121 +37,73 @@ static int persistent_grid(int nwg) {
   return (g / NXCD) * NXCD;
 }
 
+// The kernel amdgo_gemm_bf16 runs for this shape on this device (0 = generic).
+static int resolve_variant(int M, int N, int K) {
+  if (M % BM || N % BN || K % BK || K < 2 * BK) return 0;
+  const int nwg = (M / BM) * (N / BN);
+  const int cus = device_cu_count();
+  const bool sq = (M / BM) % 16 == 0 && (N / BN) % 16 == 0;
+  int v = g_variant;
+  if (v == 0) {
+    v = 44;
+    // Short K (K-loop of <= 32 K-tiles) with several tiles per CU: the persistent v25 hides each
+    // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %).
+    if (K <= 32 * BK && nwg >= 2 * cus) v = 25;
+    // Big grids (>= 8 dispatch waves) with long K: the square cross-XCD raster (v45) streams fewer
+    // distinct panels per wave (profiles/r1_s6_sq: 12288^3 +5.5 %, 16384x8192x8192 +2.9 %,
+    // 16384^3 +3.4 %; at 4 waves or K = 4096 it measured 1 % behind v44, so those stay on v44).
+    else if (sq && nwg >= 8 * cus && K >= 128 * BK) v = 45;
+  }
+  if (v == 45 && !sq) v = 44;                           // square raster needs 16x16 super-tiles
+  if (v == 25 && persistent_grid(nwg) < NXCD) v = 44;
+  if ((v == 44 || v == 45) && cus != 256) v = 42;       // serpentine K assumes 32 co-resident WGs / XCD
+  return v;
+}
+
 extern "C" {
 
-void amdgo_gemm_set_variant(int v) { g_variant = v; }
-int amdgo_gemm_get_variant() { return variant(); }
+// 0 on success; hipErrorInvalidValue for a variant outside the production set.
+int amdgo_gemm_set_variant(int v) {
+  if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45) return (int)hipErrorInvalidValue;
+  g_variant = v;
+  return 0;
+}
+int amdgo_gemm_get_variant() { return g_variant; }
+int amdgo_gemm_resolve_variant(int M, int N, int K) { return resolve_variant(M, N, K); }
 
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if (M % BM == 0 && N % BN == 0 && K % BK == 0) {
-    const int nwg = (M / BM) * (N / BN);
-    int v = variant();
-    // Short K (K-loop of <= 32 K-tiles) with several tiles per CU: the persistent v25 hides each
-    // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %).
-    if (v == 44 && K <= 32 * BK && nwg >= 2 * device_cu_count()) v = 25;
-    // Big grids (>= 8 dispatch waves) with long K: the square cross-XCD raster (v45) streams fewer
-    // distinct panels per wave (profiles/r1_s6_sq: 12288^3 +5.5 %, 16384x8192x8192 +2.9 %,
-    // 16384^3 +3.4 %; at 4 waves or K = 4096 it measured 1 % behind v44, so those stay on v44).
-    if (v == 44 && (M / BM) % 16 == 0 && (N / BN) % 16 == 0 && nwg >= 8 * device_cu_count() && K >= 128 * BK)
-      v = 45;
-    if (v == 46) v = 44;                              // v44 pinned (no automatic switch), for A/B runs
-    if ((v == 40 || v == 41 || v == 44 || v == 45) && device_cu_count() != 256) v = (v == 44 || v == 45) ? 42 : 18;
-    if (v == 45 && ((M / BM) % 16 != 0 || (N / BN) % 16 != 0)) v = 44;   // square raster needs 16x16 super-tiles
-    if (v == 1)
-      hipLaunchKernelGGL(gemm_bf16_256x256, dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else if (v == 3 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL((gemm_bf16_256x256_pp<false, false>), dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else if (v == 4 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, false>), dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else if (v == 5 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true>), dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else if (v == 6 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 2>), dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else if (v >= 18 && v <= 19 && K >= 2 * BK) {
-      auto kern = v == 18 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40>
-                          : gemm_bf16_256x256_w4s<17, 19, 4, 72, 48>;
-      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    }
-    else if (v == 45 && K >= 2 * BK) {               // v44 + square cross-XCD raster
+  const auto* a = (const __bf16*)A;
+  const auto* b = (const __bf16*)Bt;
+  auto* c = (__bf16*)C;
+  const int nwg = (M / BM) * (N / BN);
+  switch (resolve_variant(M, N, K)) {
+    case 18:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40>), dim3(nwg), dim3(W4_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 25:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40>), dim3(persistent_grid(nwg)),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 42:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 44:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 45:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
-                         0, s, (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+                         0, s, a, b, c, M, N, K);
+      break;
+    default: {
+      dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
+      hipLaunchKernelGGL(gemm_bf16_generic, grid, dim3(256), 0, s, a, b, c, M, N, K);
     }
-    else if (v >= 40 && v <= 44 && K >= 2 * BK) {    // v18 + serpentine K (32 / 64 co-resident per XCD)
-      auto kern = v == 40 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32>     // or v18/v19 + loop rotation
-                : v == 41 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 64>
-                : v == 42 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true>
-                : v == 43 ? gemm_bf16_256x256_w4s<17, 19, 4, 72, 48, 0, true>
-                          : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true>;
-      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    }
-    else if (v >= 30 && v <= 35 && K >= 2 * BK) {    // v18 schedule sweep: later B1 barrier
-      auto kern = v == 30 ? gemm_bf16_256x256_w4s<24, 26, 5, 80, 40>
-                : v == 31 ? gemm_bf16_256x256_w4s<32, 34, 5, 80, 40>
-                : v == 32 ? gemm_bf16_256x256_w4s<40, 42, 5, 96, 24>
-                : v == 33 ? gemm_bf16_256x256_w4s<32, 34, 5, 96, 24>
-                : v == 34 ? gemm_bf16_256x256_w4s<24, 26, 4, 72, 48>
-                          : gemm_bf16_256x256_w4s<48, 50, 4, 100, 24>;
-      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    }
-    else if (v >= 25 && v <= 27 && K >= 2 * BK && persistent_grid(nwg) >= NXCD) {
-      auto kern = v == 25 ? gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40>
-                : v == 26 ? gemm_bf16_256x256_w4sp<17, 19, 4, 72, 48>
-                          : gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, true>;   // 25 + serpentine K
-      hipLaunchKernelGGL(kern, dim3(persistent_grid(nwg)), dim3(W4_THREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    }
-    else if (v >= 15 && v <= 17 && K >= 2 * BK) {
-      auto kern = v == 15 ? gemm_bf16_256x256_w4r<12, 8>
-                : v == 16 ? gemm_bf16_256x256_w4r<16, 16>
-                          : gemm_bf16_256x256_w4r<12, 4>;
-      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    }
-    else if (v >= 20 && v <= 24 && K >= 2 * BK) {    // knock-out timings (wrong results)
-      auto kern = v == 20 ? gemm_bf16_256x256_w4<16, 16, 1>
-                : v == 21 ? gemm_bf16_256x256_w4<16, 16, 2>
-                : v == 22 ? gemm_bf16_256x256_w4<16, 16, 4>
-                : v == 23 ? gemm_bf16_256x256_w4<16, 16, 7>
-                          : gemm_bf16_256x256_w4<16, 16, 3>;
-      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    }
-    else if (v >= 10 && v <= 14 && K >= 2 * BK) {
-      auto kern = v == 10 ? gemm_bf16_256x256_w4<16, 16>
-                : v == 11 ? gemm_bf16_256x256_w4<12, 16>
-                : v == 12 ? gemm_bf16_256x256_w4<12, 8>
-                : v == 13 ? gemm_bf16_256x256_w4<8, 8>
-                          : gemm_bf16_256x256_w4<12, 4>;
-      hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    }
-    else if (v == 8 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 4, 1>), dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else if (v == 9 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 4, 2>), dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else if (v == 7 && K % (2 * BK) == 0)
-      hipLaunchKernelGGL((gemm_bf16_256x256_pp<true, true, 8>), dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-    else
-      hipLaunchKernelGGL(gemm_bf16_256x256_v2, dim3(nwg), dim3(NTHREADS), 0, s,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-  } else {
-    dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
-    hipLaunchKernelGGL(gemm_bf16_generic, grid, dim3(256), 0, s,
-                       (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
   }
   return (int)hipGetLastError();
 }

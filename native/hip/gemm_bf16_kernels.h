@@ -1,0 +1,544 @@
+// Production gfx950 bf16 GEMM kernels of the node validator (shared by the validator library
+// gemm_bf16.hip and the tools-only experiment library gemm_bf16_lab.hip):
+//
+//   C[M,N] (bf16) = A[M,K] (bf16, K-major) * Bt[N,K]^T (bf16, K-major), fp32 accumulation.
+//
+//   * gemm_bf16_256x256_w4s  -- v18 schedule; v44 = + serpentine K + loop rotation (the default),
+//                               v45 = v44 + square cross-XCD raster, v42 = rotation only (devices
+//                               without 256 CUs), v18 = neither;
+//   * gemm_bf16_256x256_w4sp -- v25: v18 made persistent (short K, several tiles per CU);
+//   * gemm_bf16_generic      -- bounds-checked 64x64-tile MFMA kernel for every other shape;
+//   * gemm_ref_rows / fill_uniform_bf16 -- scalar fp32 reference rows and the operand filler.
+// Design notes and measurements: docs/validator-gemm.md, profiles/r1_*.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gemm_tile_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 256;
+constexpr int BN = 256;
+constexpr int BK = 64;
+constexpr int NTHREADS = 512;
+constexpr int ROW_BYTES = BK * 2;             // 128 B per staged row
+constexpr int PANEL_BYTES = BM * ROW_BYTES;   // 32 KiB per operand per K-tile
+constexpr int BUF_BYTES = 2 * PANEL_BYTES;    // A + B
+constexpr int LDS_BYTES = 2 * BUF_BYTES;      // double buffered: 128 KiB
+
+// The accumulators are pinned: hipcc's greedy allocator, given 64 tuples that fill all 256 AGPRs,
+// cannot keep them in place across the loop back-edge and shuffles them through a[0:3] with
+// ~600 v_accvgpr moves per K-tile. So the MFMAs are inline asm on literal a[4i:4i+3] (the kernel
+// owns every AGPR via W4_AGPR_CLOBBERS; the compiler has no AGPR values of its own -- audited in
+// tests/test_gemm_build.py: no compiler v_accvgpr_* outside the asm blocks). Hazards handled by
+// hand (cdna_hip_programming.md §5.7 item 2): zeroing writes -> first MFMA reading them as C are
+// separated by the prologue; the last MFMA's D -> v_accvgpr_read is covered by an explicit s_nop
+// pad; an accumulate chain MFMA -> MFMA (same C) needs none. A/B operands come from compiler
+// ds_reads whose lgkmcnt waits hipcc inserts before each asm statement that names them.
+constexpr int W4_THREADS = 256;
+
+struct W4Frags {
+  bf16x8 a[8];
+  bf16x8 b[8];
+};
+
+template <int I>
+__device__ __forceinline__ void w4_mfma(const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+               :: "i"(4 * I), "i"(4 * I + 3), "v"(b), "v"(a));
+}
+
+// fragment read order j -> (A or B, index): the order the next block consumes them
+// (i = 0..7 uses a0 with b0..b7, then a1 ...), so hipcc's lgkmcnt ladder releases MFMAs early.
+__device__ __forceinline__ constexpr int w4_isb(int j) { return j >= 1 && j <= 8; }
+__device__ __forceinline__ constexpr int w4_idx(int j) { return j == 0 ? 0 : (j <= 8 ? j - 1 : j - 8); }
+
+// RSPAN / DSPAN: the 16 fragment reads / DMA pieces of a block are spread over its first
+// RSPAN / DSPAN groups of 4 MFMAs (16 = evenly; smaller = earlier, more latency slack).
+// KO (profiling only, wrong results): bit0 drops the per-tile wait+barrier, bit1 the DMA, bit2
+// the fragment reads -- knock-out timings that price each component.
+
+// v18: v10's data layout with the schedule reshaped around the K-tile instead of two halves.
+// Knock-out cycle accounting of v10 (profiles/r1_gemm_v10/README.md) priced its DMA at 13 % of
+// the wave cycles and its wait+barrier at 4 %, with fragment reads nearly free. Here, in MFMA
+// slots 0..127 of iteration t (0..63 on R0 = tile t kk0, 64..127 on R1 = tile t kk1):
+//   slots 0..15      read R1 <- tile t kk1 (one per MFMA)
+//   slot B1          lgkmcnt(0) one MFMA earlier, then a barrier: every wave is done with tile t
+//   slots D0 + j*DS  DMA tile t+2 into tile t's buffer (16 pieces), starting ~40 slots earlier
+//                    than v10 so a piece has ~80 MFMAs to land
+//   slot B2          vmcnt(pieces issued so far this iteration) one MFMA earlier -- tile t+1 (last
+//                    iteration's pieces) landed, this iteration's stay in flight -- then a barrier
+//   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
+// Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
+          bool SQ = false>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                      __bf16* __restrict__ C, int M, int N, int K) {
+  static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  if constexpr (SQ) tile_coords_sq(blockIdx.x, tiles_n, tm, tn);
+  else tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, int k0, char* buf) {
+    // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
+    const int rblk = ((i & 7) << 2) + wid;
+    char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+  };
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * ROW_BYTES;
+  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  W4Frags R0, R1;
+  char* const buf0 = smem;
+  char* const buf1 = smem + BUF_BYTES;
+  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int x = w4_idx(j);
+    if constexpr (w4_isb(j))
+      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
+    else
+      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  // DM: DMA tile t+2; NX: tile t+1 exists (wait for it, read its kk0 into R0); LAST_DMA: the
+  // previous iteration issued no DMA (vmcnt target 0 instead of this iteration's count)
+  // slots [LO, HI) of one K-tile iteration; the slots before B1 depend on no flag (ROT splits there)
+  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX, auto LO, auto HI) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value;
+    static_for<decltype(LO)::value, decltype(HI)::value>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
+      else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
+      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
+      if constexpr (i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
+      if constexpr (nx && i == B2 - 1) {
+        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
+        // vmcnt(issued) lgkmcnt(0): vmcnt low 4 bits [3:0], high 2 bits [15:14]; expcnt 7
+        __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
+      }
+      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i > B2) {
+        static_for<0, 16>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  const int ktiles = K / BK;        // >= 2 (host guarantees)
+  // SERP > 0 (serpentine K): with SERP co-resident workgroups per XCD, every other wave of tiles
+  // walks K backwards, so it starts on the K-slices of the A panels the previous wave just left
+  // in the XCD's L2.
+  const bool rev = SERP > 0 && (((int)blockIdx.x / NXCD) / (SERP > 0 ? SERP : 1)) & 1;
+  auto kof = [&](int kt) { return (rev ? ktiles - 1 - kt : kt) * BK; };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(0), buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(1), buf1);
+  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
+  bar();
+  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
+
+  using S0 = std::integral_constant<int, 0>;
+  using SB = std::integral_constant<int, B1>;
+  using SE = std::integral_constant<int, 128>;
+  char* cur = buf0;
+  char* nxt = buf1;
+  if constexpr (ROT) {
+    // Loop rotation (v42/v43): an iteration runs slots B1..127 of tile t, then 0..B1-1 of tile
+    // t+1, so the back-edge follows the explicit lgkmcnt(0) at slot B1-1 instead of the R0 reads,
+    // where hipcc's merged loop-header state is a blanket lgkmcnt(0) before the first MFMA.
+    iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, SB{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+      iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, SB{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
+  } else {
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, S0{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, S0{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
+  }
+
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  bar();
+  constexpr int CROW = BN * 2;
+  static_for<0, 64>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int m = i >> 3, n = i & 7;
+    float x0, x1, x2, x3;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+    const int r = wr * 128 + m * 16 + (lane & 15);
+    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
+    bf16x4 v;
+    v[0] = (__bf16)x0;
+    v[1] = (__bf16)x1;
+    v[2] = (__bf16)x2;
+    v[3] = (__bf16)x3;
+    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
+  });
+  bar();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {
+    const int r = i * (W4_THREADS / 32) + (tid >> 5);
+    const int ch = tid & 31;
+    const int sw = r & 15;
+    const int pg = (2 * ch) ^ sw;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
+    uint4 v = raw;
+    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+  }
+}
+// v25/v26: v18 made persistent. gridDim = one workgroup per CU; XCD x (= blockIdx % 8) owns a
+// contiguous run of output tiles (the bijective split of xcd_remap) that its gridDim/8
+// workgroups walk in strides. The K-tile stream runs on across tile boundaries: the last two
+// K-iterations of a tile DMA the NEXT tile's K-tiles 0 and 1 into the freed buffers and the last
+// one already reads its first fragments, so the next tile starts without a cold HBM prologue.
+// The epilogue no longer needs the K buffers: each wave stages its own 128x128 sub-tile through a
+// private 8 KiB slice of the 32 KiB of LDS the K buffers leave free (2 fragment rows = 32 C rows
+// per pass, XOR-swizzled, read back as full 256-B row segments), so it needs no workgroup barrier
+// and overlaps the in-flight DMA; the accumulators are zeroed as they are read.
+constexpr int W4P_EPI_WAVE = 8192;                       // 32 rows x 128 cols x bf16
+constexpr int W4P_LDS = LDS_BYTES + 4 * W4P_EPI_WAVE;     // 160 KiB
+
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, bool SERP = false>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                       __bf16* __restrict__ C, int M, int N, int K) {
+  static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[W4P_LDS];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int xcd = blockIdx.x % NXCD;
+  const int per = gridDim.x / NXCD;                       // workgroups per XCD (host: gridDim % 8 == 0)
+  const int q = nwg / NXCD, rem = nwg % NXCD;
+  const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+  const int t_end = t_begin + q + (xcd < rem ? 1 : 0);
+  int tile = t_begin + (int)(blockIdx.x / NXCD);
+  if (tile >= t_end) return;                              // uniform over the workgroup
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  auto rsrc = [&](const __bf16* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, panel_bytes, 0x00020000);
+  };
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, tm, tn);
+  __amdgpu_buffer_rsrc_t rA = rsrc(A + (size_t)tm * BM * K);
+  __amdgpu_buffer_rsrc_t rB = rsrc(Bt + (size_t)tn * BN * K);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int k0, char* buf) {
+    // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
+    const int rblk = ((i & 7) << 2) + wid;
+    char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+  };
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * ROW_BYTES;
+  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  W4Frags R0, R1;
+  char* const buf0 = smem;
+  char* const buf1 = smem + BUF_BYTES;
+  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int x = w4_idx(j);
+    if constexpr (w4_isb(j))
+      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
+    else
+      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  // The v18 iteration; the DMA target (operand panels and K offset) is a runtime argument so the
+  // same body serves this tile's K-tile t+2 and the next tile's K-tiles 0 and 1.
+  // FRESH: a tile's first iteration. The vmcnt(0) before it (prologue or previous epilogue) already
+  // retired this tile's K-tile 1, so its B2 does not wait again: the epilogue's C stores are older
+  // than this iteration's DMA, and a counted vmcnt would wait for them too.
+  auto iter = [&](char* cur, char* nxt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int dk, auto FR,
+                  auto DM, auto NX) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value, fresh = decltype(FR)::value;
+    static_for<0, 128>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
+      else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
+      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
+      if constexpr (dm && i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, ra, rb, dk, cur);
+      if constexpr (nx && i == B2 - 1) {
+        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
+        if constexpr (fresh) __builtin_amdgcn_s_waitcnt(0xC07F);             // lgkmcnt(0) only
+        else __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
+      }
+      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i > B2) {
+        static_for<0, 16>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  // Wave-private epilogue: 4 passes of 2 fragment rows (32 C rows x 128 cols).
+  char* const stg = smem + LDS_BYTES + wid * W4P_EPI_WAVE;
+  auto epilogue = [&](int tm_, int tn_) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA D -> accvgpr reads
+    static_for<0, 4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      static_for<0, 16>([&](auto I) {
+        constexpr int u = decltype(I)::value;
+        constexpr int mm = u >> 3, n = u & 7;
+        constexpr int i = (2 * s + mm) * 8 + n;                    // accumulator index m*8+n
+        float x0, x1, x2, x3;
+        asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                     "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
+                     "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
+                     "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
+                     : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                     : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+        const int r = mm * 16 + (lane & 15);                       // 0..31
+        const int g = n * 4 + (lane >> 4);                         // 8-byte group 0..31
+        bf16x4 v;
+        v[0] = (__bf16)x0;
+        v[1] = (__bf16)x1;
+        v[2] = (__bf16)x2;
+        v[3] = (__bf16)x3;
+        *reinterpret_cast<bf16x4*>(stg + r * 256 + ((g ^ (r & 15)) << 3)) = v;
+      });
+      asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
+      // retire the next tile's K-tile DMAs before the first C store (see `fresh`)
+      if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = k * 4 + (lane >> 4);
+        const int ch = lane & 15;
+        const int sw = r & 15;
+        const int pg = (2 * ch) ^ sw;
+        const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
+        uint4 v = raw;
+        if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * BM + wr * 128 + s * 32 + r) * N + tn_ * BN + wc * 128 + ch * 8) = v;
+      }
+      asm volatile("" ::: "memory");
+    });
+  };
+
+  const int ktiles = K / BK;        // >= 2 (host guarantees)
+  // SERP (v27): a workgroup's i-th tile belongs to wave i of its XCD; odd waves walk K backwards
+  // and start on the A-panel K-slices the previous wave left in the XCD's L2.
+  bool rev = false;
+  auto kof = [&](int kt, bool r) { return (r ? ktiles - 1 - kt : kt) * BK; };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(0, rev), buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(1, rev), buf1);
+  __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0): K-tiles 0 and 1 landed (FRESH iteration)
+  bar();
+  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
+
+  char* cur = buf0;
+  char* nxt = buf1;
+  for (;;) {
+    const int next = tile + per;
+    const bool has_next = next < t_end;
+    int ntm = tm, ntn = tn;
+    __amdgpu_buffer_rsrc_t nA = rA, nB = rB;
+    if (has_next) {
+      tile_coords(next, tiles_m, tiles_n, ntm, ntn);
+      nA = rsrc(A + (size_t)ntm * BM * K);
+      nB = rsrc(Bt + (size_t)ntn * BN * K);
+    }
+    const int nsteady = has_next ? ktiles : ktiles - 2;
+    auto dma_of = [&](int t, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rb) {
+      const bool nt = t + 2 >= ktiles;               // DMA the next tile's K-tile t+2-ktiles
+      ra = nt ? nA : rA;
+      rb = nt ? nB : rB;
+      return nt ? kof(t + 2 - ktiles, SERP && !rev) : kof(t + 2, rev);
+    };
+    __amdgpu_buffer_rsrc_t ra, rb;
+    if (nsteady > 0) {
+      const int dk = dma_of(0, ra, rb);
+      iter(cur, nxt, ra, rb, dk, T_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    for (int t = 1; t < nsteady; ++t) {
+      const int dk = dma_of(t, ra, rb);
+      iter(cur, nxt, ra, rb, dk, F_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    if (!has_next) {
+      iter(cur, nxt, rA, rB, 0, F_{}, F_{}, T_{});
+      iter(nxt, nullptr, rA, rB, 0, F_{}, F_{}, F_{});
+    }
+    epilogue(tm, tn);
+    if (!has_next) break;
+    tile = next;
+    rev = SERP && !rev;
+    tm = ntm;
+    tn = ntn;
+    rA = nA;
+    rB = nB;
+  }
+}
+// Generic bounds-checked MFMA kernel (64x64 tile, 4 waves of 32x32), register-staged.
+// Used for shapes that are not multiples of 256/256/64 and as a second, independent
+// implementation for cross-checking the fast path.
+constexpr int GBM = 64, GBN = 64, GBK = 32;
+
+__global__ void __launch_bounds__(256)
+gemm_bf16_generic(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                  __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) __bf16 sa[GBM][GBK + 8];
+  __shared__ __attribute__((aligned(16))) __bf16 sb[GBN][GBK + 8];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // 256 threads x 8 elements = 64 rows x 32 k per operand.
+  const int lr = threadIdx.x >> 2;        // row 0..63
+  const int lk = (threadIdx.x & 3) * 8;   // k offset 0,8,16,24
+  for (int k0 = 0; k0 < K; k0 += GBK) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = k0 + lk + e;
+      const int ra = m0 + lr, rb = n0 + lr;
+      sa[lr][lk + e] = (ra < M && k < K) ? A[(size_t)ra * K + k] : (__bf16)0.f;
+      sb[lr][lk + e] = (rb < N && k < K) ? Bt[(size_t)rb * K + k] : (__bf16)0.f;
+    }
+    __syncthreads();
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        af[i][e] = sa[wr * 32 + i * 16 + (lane & 15)][8 * (lane >> 4) + e];
+        bfr[i][e] = sb[wc * 32 + i * 16 + (lane & 15)][8 * (lane >> 4) + e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wr * 32 + i * 16 + (lane & 15);
+        const int col = n0 + wc * 32 + j * 16 + 4 * (lane >> 4) + e;
+        if (row < M && col < N) C[(size_t)row * N + col] = (__bf16)acc[i][j][e];
+      }
+}
+
+// fp32-accumulating reference (one thread per output element; sampled rows only).
+__global__ void gemm_ref_rows(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                              const int* __restrict__ rows, int nrows, float* __restrict__ out,
+                              int N, int K) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ri = blockIdx.y;
+  if (col >= N || ri >= nrows) return;
+  const __bf16* a = A + (size_t)rows[ri] * K;
+  const __bf16* b = Bt + (size_t)col * K;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += (float)a[k] * (float)b[k];
+  out[(size_t)ri * N + col] = s;
+}
+
+// Deterministic uniform [-1,1) bf16 fill (counter-based hash), so validator runs on
+// random data (zero-filled operands inflate MFMA clocks and hide layout bugs).
+__global__ void fill_uniform_bf16(__bf16* p, size_t n, uint32_t seed) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t x = (uint32_t)i * 0x9E3779B1u ^ seed;
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    const float u = (float)(x >> 8) * (1.0f / 16777216.0f);
+    p[i] = (__bf16)(2.0f * u - 1.0f);
+  }
+}
+
+}  // namespace

@@ -1,0 +1,45 @@
+// Tools-only fp8 experiment dispatch (libamdgo_gemm_lab.so; see gemm_bf16_lab.hip): every schedule
+// placement of the fp8 kernels under its variant number, without automatic switches.
+//   1 .. 4 = schedule placements, 5 / 6 = 4 / 3 with serpentine K, 7 / 8 = 4 / 3 with the loop
+//   rotated at slot B1, 9 = 4 with both, 10 / 11 = persistent with the schedules of 4 / 3,
+//   12 = 10 with serpentine K, 13 = 9 with the square cross-XCD raster.
+#include "gemm_fp8_kernels.h"
+
+extern "C" {
+
+int amdgo_lab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % F8_BM || N % F8_BN || K % F8_BK || K < 2 * F8_BK)
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const auto* a = (const uint8_t*)A;
+  const auto* b = (const uint8_t*)Bt;
+  auto* c = (__bf16*)C;
+  const int nwg = (M / F8_BM) * (N / F8_BN);
+  const int cus = device_cu_count();
+  const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;
+  if (v >= 10 && v <= 12 && pgrid >= NXCD) {
+    auto kern = v == 10 ? gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>
+              : v == 11 ? gemm_fp8_256x256_w4sp<4, 5, 20, 22, 8>
+                        : gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6, true>;
+    hipLaunchKernelGGL(kern, dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+  } else if (v == 13 && (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0) {
+    hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true, true>), dim3(nwg), dim3(F8_THREADS), 0, s,
+                       a, b, c, M, N, K);
+  } else if (v >= 1 && v <= 9) {
+    auto kern = v == 1 ? gemm_fp8_256x256_w4s<5, 5, 16, 20, 10>
+              : v == 2 ? gemm_fp8_256x256_w4s<5, 6, 12, 18, 12>
+              : v == 3 ? gemm_fp8_256x256_w4s<4, 5, 20, 22, 8>
+              : v == 4 ? gemm_fp8_256x256_w4s<6, 7, 16, 24, 6>
+              : v == 5 ? gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32>
+              : v == 6 ? gemm_fp8_256x256_w4s<4, 5, 20, 22, 8, 32>
+              : v == 7 ? gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 0, true>
+              : v == 8 ? gemm_fp8_256x256_w4s<4, 5, 20, 22, 8, 0, true>
+                       : gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

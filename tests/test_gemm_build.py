@@ -52,8 +52,30 @@ def _kernel_at(asm: str, start):
 
 
 @pytest.fixture(scope="module")
-def w4(asm):
+def asm_lab(tmp_path_factory):
+    return _compile(tmp_path_factory, "gemm_bf16_lab.hip")
+
+
+@pytest.fixture(scope="module", params=["production", "lab"])
+def w4(request):
+    asm = request.getfixturevalue("asm" if request.param == "production" else "asm_lab")
     return _kernels(asm, "gemm_bf16_256x256_w4")
+
+
+def test_production_library_kernel_set(asm):
+    """The shipped code object holds exactly the production kernels: w4s for v18/v42/v44/v45, the
+    persistent w4sp (v25) and the generic kernel -- no superseded generation, no knock-out build."""
+    names = re.findall(r"^(_Z\w+):", asm, re.M)
+    assert len([x for x in names if "w4sI" in x]) == 4
+    assert len([x for x in names if "w4spI" in x]) == 1
+    assert not [x for x in names if re.search(r"w4I|w4rI|_ppI|256x256_v2|256x256P", x)], names
+    assert "AMDGO_GEMM" not in asm
+
+
+def test_production_sources_read_no_environment():
+    for f in ("gemm_bf16.hip", "gemm_fp8.hip", "gemm_bf16_kernels.h", "gemm_fp8_kernels.h"):
+        text = open(os.path.join(ROOT, "native/hip", f)).read()
+        assert "getenv" not in text, f
 
 
 def _no_compiler_agpr_access(body: str):
@@ -72,7 +94,7 @@ def _no_compiler_agpr_access(body: str):
 def test_fp8_kernel_audit(asm_fp8):
     """fp8 w4s: 256 pinned AGPRs, no scratch, 32 scaled MFMAs per K-tile, 2 barriers, 16 DMA pieces."""
     kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4sI")
-    assert len(kernels) == 10   # v1-v9 + v13 (square raster)
+    assert len(kernels) == 4    # production: v4, v7, v9, v13 (square raster)
     for body, st in kernels:
         assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
         _no_compiler_agpr_access(body)
@@ -91,7 +113,7 @@ def test_fp8_kernel_audit(asm_fp8):
 
 def test_fp8_persistent_kernel_audit(asm_fp8):
     kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4spI")
-    assert len(kernels) == 3
+    assert len(kernels) == 1    # production: v10
     for body, st in kernels:
         assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
         _no_compiler_agpr_access(body)
@@ -137,3 +159,23 @@ def test_w4_main_loop_shape(w4):
 def test_no_kernel_spills(asm):
     for m in re.finditer(r"^; ScratchSize: (\d+)", asm, re.M):
         assert int(m.group(1)) == 0
+
+
+def test_shipped_library_exports_no_lab_entry_points():
+    """libamdgo_hip.so (validator + ops) carries only the production dispatch: no lab symbols, no
+    environment switch, and the variant API refuses everything outside the production set."""
+    lib = os.path.join(ROOT, "gpu_operator_amd", "_native", "libamdgo_hip.so")
+    if not os.path.exists(lib):
+        pytest.skip("native library not built")
+    syms = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    assert "amdgo_gemm_bf16" in syms and "lab" not in syms
+    assert b"AMDGO_GEMM" not in open(lib, "rb").read()
+    from gpu_operator_amd.ops import gemm as G
+    for bad in (1, 20, 24, 46, 14):
+        with pytest.raises(ValueError):
+            G.set_variant(bad)
+    for bad in (1, 5, 11, 14):
+        with pytest.raises(ValueError):
+            G.set_fp8_variant(bad)
+    G.set_variant(0)
+    G.set_fp8_variant(0)

@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.fixture(params=[0, 4, 7, 9, 10, 13])   # the production set (gemm.FP8_VARIANTS)
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
@@ -140,3 +140,15 @@ def _check_square_raster_fp8(cuda_device, G, torch):
     rows = torch.tensor([tm * 256 + (tm * 53) % 256 for tm in range(m // 256)], device=cuda_device)
     ref = a[rows].float() @ bt.float().t()
     torch.testing.assert_close(c[rows].float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+
+
+def test_fp8_production_variant_set_is_closed(cuda_device):
+    from gpu_operator_amd.ops import gemm as G
+
+    for bad in (1, 2, 3, 5, 6, 8, 11, 12, 14, 99):
+        with pytest.raises(ValueError):
+            G.set_fp8_variant(bad)
+    assert G.get_fp8_variant() == 0
+    assert G.resolve_fp8_variant(8192, 8192, 8192) in (9, 7)
+    assert G.resolve_fp8_variant(16384, 16384, 1024) == 10
+    assert G.resolve_fp8_variant(300, 256, 256) == 0

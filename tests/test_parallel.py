@@ -69,3 +69,35 @@ def test_bench_cpu_rehearsal_two_ranks():
     assert d["value"] == pytest.approx(d["per_gpu_tflops"] * 2, rel=1e-3, abs=0.02) and d["value"] > 0
     assert d["allreduce_ok"] and d["device"] == "cpu-rehearsal"
     assert d["config"]["parallelism"].startswith("dp2")
+
+
+def test_bench_self_launches_n_ranks_without_torchrun():
+    """`bench.py --gpus 4` with no WORLD_SIZE must run 4 ranks itself (never a silent 1-rank run)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "2", "--warmup", "1",
+           "--device", "cpu", "--shape", "64x64x128"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1                                   # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"].startswith("dp4")
+    assert "allreduce_busbw_gbps" in d and d["allreduce_ok"]
+    assert d["metric"].startswith("validator HIP GEMM TFLOPS (bf16 64x64x128")
+
+
+def test_bench_refuses_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--device", "cpu", "--shape", "64x64x64"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert p.returncode == 3 and "WORLD_SIZE" in p.stderr
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    # This container has no GPU: an 8-GPU request must fail loudly instead of running on fewer.
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "0"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert p.returncode == 3 and "visible" in p.stderr

@@ -198,3 +198,211 @@ def test_metrics_published():
     up.reconcile(("", "cluster-policy"))
     assert rec.metrics.upgrades_done._value.get() == 2
     assert rec.metrics.driver_auto_upgrade_enabled._value.get() == 1
+
+
+# -- eviction waits for deletion, PDB 429 retries (kubectl drain semantics) -------------------------
+
+def _fake_time(up, hook=None):
+    clock = [1000.0]
+    up.mgr.clock = lambda: clock[0]
+
+    def sleep(dt):
+        clock[0] += dt
+        if hook:
+            hook(clock[0])
+    up.mgr.sleep = sleep
+    return clock
+
+
+def _guard_driver_restart(c):
+    """Fail the test if a driver pod is deleted while a GPU pod still exists on its node."""
+    def hook(verb, av, kind, arg):
+        if verb != "delete" or kind != "Pod" or not isinstance(arg, str) or not arg.startswith(C.DS_DRIVER):
+            return
+        drv = [p for p in c.list("v1", "Pod", NS) if o.name(p) == arg]
+        if not drv:
+            return
+        node = drv[0]["spec"]["nodeName"]
+        gpu = [o.name(p) for p in c.list("v1", "Pod", field_selector=f"spec.nodeName={node}") if U.gpu_pod_filter(p)]
+        assert not gpu, f"driver pod {arg} deleted while GPU pods {gpu} remain on {node}"
+    c.interceptors.append(hook)
+
+
+def _start_upgrade(n_nodes=1, **policy):
+    c, rec, sim, up = setup(n_nodes=n_nodes, **policy)
+    up.reconcile(("", "cluster-policy"))
+    return c, rec, sim, up
+
+
+def test_pod_stuck_terminating_holds_pod_deletion_then_fails_at_timeout():
+    c, rec, sim, up = _start_upgrade(podDeletion={"timeoutSeconds": 30})
+    seen = []
+    clock = _fake_time(up, lambda t: seen.append(states(c)["n0"]))
+    stuck = gpu_workload("n0", "stuck")
+    stuck["metadata"]["finalizers"] = ["example.com/hold"]
+    c.create(stuck)
+    _guard_driver_restart(c)
+    drv_before = {o.name(p) for p in c.list("v1", "Pod", NS, label_selector={"app": C.DS_DRIVER})}
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    for _ in range(8):
+        step(c, rec, sim, up)
+        if states(c)["n0"] == U.FAILED:
+            break
+    assert states(c)["n0"] == U.FAILED
+    assert seen and set(seen) == {U.POD_DELETION_REQUIRED}           # held there while waiting
+    assert 30 <= clock[0] - 1000.0 <= 32                              # bounded by timeoutSeconds
+    assert c.get("v1", "Pod", "stuck", "default")["metadata"].get("deletionTimestamp")
+    assert U.POD_EVICTION_START_ANNOTATION not in o.get_annotations(c.get("v1", "Node", "n0"))
+    assert any("global timeout 30s" in e["message"] for e in c.events if e["type"] == "Warning")
+    drv_after = {o.name(p) for p in c.list("v1", "Pod", NS, label_selector={"app": C.DS_DRIVER})}
+    assert drv_after == drv_before                                    # driver never restarted
+
+
+def test_pod_stuck_terminating_falls_back_to_drain_then_fails():
+    c, rec, sim, up = _start_upgrade(podDeletion={"timeoutSeconds": 20},
+                                     drain={"enable": True, "force": True, "timeoutSeconds": 20})
+    _fake_time(up)
+    stuck = gpu_workload("n0", "stuck")
+    stuck["metadata"]["finalizers"] = ["example.com/hold"]
+    c.create(stuck)
+    _guard_driver_restart(c)
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    visited = []
+    for _ in range(10):
+        step(c, rec, sim, up)
+        visited.append(states(c)["n0"])
+        if visited[-1] == U.FAILED:
+            break
+    assert U.DRAIN_REQUIRED in visited and visited[-1] == U.FAILED, visited
+
+
+def test_terminating_pod_that_finishes_lets_the_upgrade_complete():
+    c, rec, sim, up = _start_upgrade(podDeletion={"timeoutSeconds": 60})
+    slow = gpu_workload("n0", "slow")
+    slow["metadata"]["finalizers"] = ["example.com/hold"]
+    c.create(slow)
+
+    def release(t):
+        if t >= 1010:          # the workload finishes its shutdown after ~10 s
+            try:
+                p = c.get("v1", "Pod", "slow", "default")
+            except errors.NotFound:
+                return
+            p["metadata"]["finalizers"] = []
+            c.update(p)
+    _fake_time(up, release)
+    _guard_driver_restart(c)
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    for _ in range(40):
+        step(c, rec, sim, up)
+        if states(c)["n0"] == U.DONE:
+            break
+    assert states(c)["n0"] == U.DONE
+    assert not [p for p in c.list("v1", "Pod", "default") if o.name(p) == "slow"]
+
+
+def test_pdb_refused_eviction_is_retried_until_allowed():
+    c, rec, sim, up = _start_upgrade(podDeletion={"timeoutSeconds": 120})
+    w = gpu_workload("n0", "guarded")
+    w["metadata"]["labels"] = {"app": "trainer"}
+    c.create(w)
+    c.create({"apiVersion": "policy/v1", "kind": "PodDisruptionBudget",
+              "metadata": {"name": "trainer-pdb", "namespace": "default"},
+              "spec": {"selector": {"matchLabels": {"app": "trainer"}}, "minAvailable": 1},
+              "status": {"disruptionsAllowed": 0}})
+    evictions = []
+    c.interceptors.append(lambda v, av, k, a: evictions.append(a) if v == "evict" else None)
+
+    def allow(t):
+        if t >= 1012:
+            pdb = c.get("policy/v1", "PodDisruptionBudget", "trainer-pdb", "default")
+            if pdb["status"]["disruptionsAllowed"] == 0:
+                pdb["status"]["disruptionsAllowed"] = 1
+                c.update_status(pdb)
+    clock = _fake_time(up, allow)
+    _guard_driver_restart(c)
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    for _ in range(40):
+        step(c, rec, sim, up)
+        if states(c)["n0"] == U.DONE:
+            break
+    assert states(c)["n0"] == U.DONE
+    assert evictions.count("guarded") >= 3                # refused (429) at least twice, then allowed
+    assert clock[0] - 1000.0 < 120
+
+
+def test_pdb_that_never_allows_fails_the_node_at_timeout():
+    c, rec, sim, up = _start_upgrade(podDeletion={"timeoutSeconds": 15})
+    w = gpu_workload("n0", "guarded")
+    w["metadata"]["labels"] = {"app": "trainer"}
+    c.create(w)
+    c.create({"apiVersion": "policy/v1", "kind": "PodDisruptionBudget",
+              "metadata": {"name": "trainer-pdb", "namespace": "default"},
+              "spec": {"selector": {"matchLabels": {"app": "trainer"}}}, "status": {"disruptionsAllowed": 0}})
+    _fake_time(up)
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    for _ in range(8):
+        step(c, rec, sim, up)
+    assert states(c)["n0"] == U.FAILED
+    assert c.get("v1", "Pod", "guarded", "default")                     # never deleted
+    assert any("eviction refused" in e["message"] for e in c.events if e["type"] == "Warning")
+
+
+def test_eviction_deadline_survives_operator_restart():
+    """The wait's start time is a Node annotation: a restarted operator keeps the old deadline."""
+    c, rec, sim, up = _start_upgrade(podDeletion={"timeoutSeconds": 50})
+    stuck = gpu_workload("n0", "stuck")
+    stuck["metadata"]["finalizers"] = ["example.com/hold"]
+    c.create(stuck)
+    clock = [1000.0]
+    # the "previous operator" started waiting 40 s ago and died
+    c.patch("v1", "Node", "n0", {"metadata": {"annotations": {U.POD_EVICTION_START_ANNOTATION: "960"}}})
+    up.mgr.clock = lambda: clock[0]
+
+    def sleep(dt):
+        clock[0] += dt
+    up.mgr.sleep = sleep
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    for _ in range(8):
+        step(c, rec, sim, up)
+        if states(c)["n0"] == U.FAILED:
+            break
+    assert states(c)["n0"] == U.FAILED
+    assert clock[0] <= 1012          # ~10 s left of the 50 s budget, not a fresh 50 s
+
+
+def test_gpu_pod_reappearing_before_driver_restart_is_evicted_first():
+    c, rec, sim, up = _start_upgrade(podDeletion={"timeoutSeconds": 60})
+    _fake_time(up)
+    _guard_driver_restart(c)
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    for _ in range(10):
+        step(c, rec, sim, up)
+        if states(c)["n0"] == U.POD_RESTART_REQUIRED:
+            break
+    assert states(c)["n0"] == U.POD_RESTART_REQUIRED
+    # a tolerating GPU pod lands on the cordoned node between eviction and the driver restart;
+    # the worker pass below must evict it before the driver pod goes
+    c.create(gpu_workload("n0", "late"))
+    seen = []
+    for _ in range(40):
+        step(c, rec, sim, up)
+        seen.append(states(c)["n0"])
+        if seen[-1] == U.DONE:
+            break
+    assert states(c)["n0"] == U.DONE and seen[0] == U.POD_DELETION_REQUIRED, seen
+    assert not [p for p in c.list("v1", "Pod", "default") if o.name(p) == "late"]

@@ -1,18 +1,23 @@
 #!/usr/bin/env python3
 """Run one GEMM variant repeatedly on random bf16 data (a target for rocprofv3 --pmc / --stats).
 
-    rocprofv3 --pmc SQ_WAVE_CYCLES ... -- python3 tools/gemm_prof.py --variant 4 --size 8192 --iters 50
+    rocprofv3 --pmc SQ_WAVE_CYCLES ... -- python3 tools/gemm_prof.py --variant p0 --size 8192 --iters 50
+
+``--variant p<v>`` runs the shipped library (p0 = automatic dispatch); a plain number runs that
+variant of the tools-only lab library (tools/gemm_lab.py).
 """
 import argparse
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gemm_sweep import runner  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", type=int, default=4)
+    ap.add_argument("--variant", default="p0")
     ap.add_argument("--size", default="8192")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--blas", action="store_true", help="run hipBLASLt (torch.matmul / _scaled_mm) instead")
@@ -29,12 +34,12 @@ def main():
     C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
     G.fill_uniform_(A, 1)
     G.fill_uniform_(Bt, 2)
-    G.set_variant(a.variant)
+    run = runner(G, a.variant, "bf16")
     for _ in range(a.iters):
         if a.blas:
             torch.matmul(A, Bt.t(), out=C)
         else:
-            G.gemm_bf16(A, Bt, C)
+            run(A, Bt, C)
     torch.cuda.synchronize()
     print("ok", G.verify(A, Bt, C, nrows=8).ok)
 
@@ -49,12 +54,12 @@ def main_fp8(a):
     Bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=f8, device=dev), 2)
     C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
     one = torch.ones((), dtype=torch.float32, device=dev)
-    G.set_fp8_variant(a.variant)
+    run = runner(G, a.variant, "fp8")
     for _ in range(a.iters):
         if a.blas:
             C = torch._scaled_mm(A, Bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
         else:
-            G.gemm_fp8(A, Bt, C)
+            run(A, Bt, C)
     torch.cuda.synchronize()
     print("ok", G.verify(A, Bt, C, nrows=8).ok)
 

@@ -3,7 +3,9 @@
 
 Shapes follow SURVEY.md §7.5: M=N=K in {1024, 4096, 8192, 16384} plus skinny 16384x16384x1024.
 Interleaves the two implementations in one process (methodology rule: A/B in one process).
-Prints one JSON line per shape.
+Prints one JSON line per shape. ``--variants`` takes production numbers (``p0`` = automatic
+dispatch of the shipped library, ``p44`` = pinned) or lab numbers (plain integers: the tools-only
+experiment library, tools/gemm_lab.py; build it with ``python -m gpu_operator_amd._build --lab``).
 """
 import argparse
 import json
@@ -11,6 +13,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def time_fn(fn, iters, torch):
@@ -24,12 +27,25 @@ def time_fn(fn, iters, torch):
     return start.elapsed_time(end) / iters / 1e3
 
 
+def runner(G, spec: str, dtype: str):
+    """A callable (A, Bt, C) for a production ('p<v>') or lab ('<v>') variant."""
+    if spec.startswith("p"):
+        v = int(spec[1:])
+        if dtype == "bf16":
+            return lambda A, Bt, C: (G.set_variant(v), G.gemm_bf16(A, Bt, C))
+        return lambda A, Bt, C: (G.set_fp8_variant(v), G.gemm_fp8(A, Bt, C))
+    import gemm_lab
+    v = int(spec)
+    return (lambda A, Bt, C: gemm_lab.gemm_bf16(v, A, Bt, C)) if dtype == "bf16" else \
+        (lambda A, Bt, C: gemm_lab.gemm_fp8(v, A, Bt, C))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="1024,4096,8192,16384,16384x16384x1024")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--variants", default="p0,44,45")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: e4m3fn operands on gemm_fp8 vs hipBLASLt through torch._scaled_mm")
     a = ap.parse_args()
@@ -49,21 +65,20 @@ def main():
         G.fill_uniform_(A, 1)
         G.fill_uniform_(Bt, 2)
         C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
-        variants = [int(v) for v in a.variants.split(",")]
+        variants = a.variants.split(",")
+        run = {v: runner(G, v, "bf16") for v in variants}
         checks = {}
         for v in variants:
-            G.set_variant(v)
             C.zero_()
-            G.gemm_bf16(A, Bt, C)
+            run[v](A, Bt, C)
             checks[v] = G.verify(A, Bt, C, nrows=16)
         ours = {v: [] for v in variants}
         blas = []
         for _ in range(a.rounds):
             for v in variants:
-                G.set_variant(v)
                 for _ in range(3):
-                    G.gemm_bf16(A, Bt, C)
-                ours[v].append(time_fn(lambda: G.gemm_bf16(A, Bt, C), a.iters, torch))
+                    run[v](A, Bt, C)
+                ours[v].append(time_fn(lambda: run[v](A, Bt, C), a.iters, torch))
             for _ in range(3):
                 torch.matmul(A, Bt.t())
             blas.append(time_fn(lambda: torch.matmul(A, Bt.t(), out=C), a.iters, torch))
@@ -90,7 +105,8 @@ def sweep_fp8(a):
         A = G.fill_uniform_fp8_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device=dev), 1)
         Bt = G.fill_uniform_fp8_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device=dev), 2)
         C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
-        variants = [int(v) for v in a.variants.split(",")]
+        variants = a.variants.split(",")
+        run = {v: runner(G, v, "fp8") for v in variants}
 
         def blas():
             return torch._scaled_mm(A, Bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
@@ -103,18 +119,16 @@ def sweep_fp8(a):
             blas_ok = False
         checks = {}
         for v in variants:
-            G.set_fp8_variant(v)
             C.zero_()
-            G.gemm_fp8(A, Bt, C)
+            run[v](A, Bt, C)
             checks[v] = G.verify(A, Bt, C, nrows=16)
         ours = {v: [] for v in variants}
         tb = []
         for _ in range(a.rounds):
             for v in variants:
-                G.set_fp8_variant(v)
                 for _ in range(3):
-                    G.gemm_fp8(A, Bt, C)
-                ours[v].append(time_fn(lambda: G.gemm_fp8(A, Bt, C), a.iters, torch))
+                    run[v](A, Bt, C)
+                ours[v].append(time_fn(lambda: run[v](A, Bt, C), a.iters, torch))
             if blas_ok:
                 for _ in range(3):
                     blas()
