@@ -18,7 +18,7 @@ def variant(request):
     G.set_variant(old)
 
 
-@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 256), (1024, 1024, 1024),
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 768, 256), (1024, 1024, 1024),
                                    (2048, 512, 4096), (768, 2304, 640), (256, 512, 128),
                                    (4608, 4608, 512),     # > 256 tiles: serpentine waves reverse K
                                    (4096, 8192, 256), (8192, 4096, 192)])   # 16x16-tile super-tiles (v45)
