@@ -102,8 +102,8 @@ TARGETS: List[Target] = [
     Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip", "hip/gemm_fp8.hip"],
            "hip-exe", flags=["-x", "hip"], headers=GEMM_HEADERS),
     Target("bin/amd-hip-smoke", ["hip/hip_smoke_main.cpp", "hip/smoke.hip"], "hip-exe", flags=["-x", "hip"]),
-    Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp"], "hip-exe", flags=["-x", "hip"],
-           libs=["-lrccl"]),
+    Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp", "node/amdnode.cpp"], "hip-exe", flags=["-x", "hip"],
+           libs=["-lrccl"], headers=["include/amdnode.h"]),
     # OCI runtime shim injecting /dev/kfd + render nodes (legacy) or CDI edits into bundles.
     # Fully static: it runs on the host (via containerd/CRI-O/docker), whatever its glibc.
     Target("bin/amd-container-runtime", ["toolkit/amd_container_runtime.cpp", "node/amdnode.cpp"], "cxx-exe",

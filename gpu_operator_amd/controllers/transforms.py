@@ -430,11 +430,10 @@ def transform_metrics_exporter(obj: Obj, spec: cp.ClusterPolicySpec, n) -> None:
     transform_validation_init_containers(obj, spec)
     c = _container(obj, "amd-metrics-exporter")
     apply_component(obj, c, spec.metricsExporter)
-    if spec.rdc.is_enabled():
-        # attach to the standalone rdcd on this node's host port
-        o.pod_spec(obj)["hostNetwork"] = True
-        o.pod_spec(obj)["dnsPolicy"] = "ClusterFirstWithHostNet"
-        o.set_env(c, "RDC_HOST", f"localhost:{spec.rdc.host_port()}")
+    # Unlike dcgm-exporter (reference :1352-1355, which needs the DCGM host engine and so joins
+    # the host network when DCGM runs standalone), amd-metrics-exporter reads the kernel and PMFW
+    # telemetry (hwmon, gpu_metrics incl. per-link xGMI counters) natively, so it never attaches
+    # to rdcd: the RDC state is for RDC's own clients (rdci, job stats) and widens nothing here.
     cfg = spec.metricsExporter.config
     if cfg is not None and cfg.name:
         for v in o.pod_spec(obj).get("volumes", []):

@@ -80,6 +80,34 @@ def read_telemetry(root: Optional[str] = None) -> List[Dict]:
     return out
 
 
+GPU_METRICS_FIELDS = ("index", "pci_bdf", "valid", "error", "format_revision", "content_revision", "structure_size",
+                      "temp_hotspot_c", "temp_mem_c", "temp_vrsoc_c", "socket_power_w", "gfx_activity_pct",
+                      "umc_activity_pct", "energy_acc", "system_clock_ns", "firmware_timestamp",
+                      "accumulation_counter", "ppt_residency_acc", "pcie_link_width", "pcie_link_speed",
+                      "xgmi_link_width", "xgmi_link_speed", "pcie_bandwidth_acc", "pcie_bandwidth_inst",
+                      "mem_max_bandwidth", "xgmi_read_kb", "xgmi_write_kb", "xgmi_link_status", "gfxclk_mhz",
+                      "uclk_mhz")
+ENERGY_UNIT_J = 15.259e-6           # gpu_metrics energy_accumulator unit (2^-16 J)
+
+
+def _metrics_dict(m) -> Dict:
+    d = {f: getattr(m, f) for f in GPU_METRICS_FIELDS}
+    for f in ("xgmi_read_kb", "xgmi_write_kb", "xgmi_link_status", "gfxclk_mhz"):
+        d[f] = list(d[f])
+    return d
+
+
+def read_gpu_metrics(root: Optional[str] = None) -> List[Dict]:
+    """Per GPU agent: the decoded sysfs ``gpu_metrics`` table (xGMI per-link KiB read/written,
+    link status/width/speed, energy, PCIe bandwidth, clocks). ``valid`` is False (with ``error``)
+    for a table revision whose layout has not been pinned on hardware."""
+    return [_metrics_dict(m) for m in native().read_gpu_metrics(root or sys_root())]
+
+
+def parse_gpu_metrics(blob: bytes) -> Dict:
+    return _metrics_dict(native().parse_gpu_metrics(blob))
+
+
 def set_partition(bdf: str, kind: str, mode: str, root: Optional[str] = None) -> None:
     err = native().set_partition(root or sys_root(), bdf, kind, mode)
     if err:

@@ -9,14 +9,47 @@ The reference ships no fake GPU or sysfs for its validator.
 from __future__ import annotations
 
 import os
+import struct
 from pathlib import Path
-from typing import Dict, Optional
+from typing import Dict, Optional, Sequence
 
 MI355X_DEVICE_ID = 0x75A3
 MI355X_CUS = 256
 MI355X_VRAM = 288 * (1 << 30)          # 288 GiB HBM3E
 PARTITION_XCDS = {"SPX": 8, "DPX": 4, "QPX": 2, "CPX": 1}
 GFX950 = 90500
+
+
+GPU_METRICS_V18_SIZE = 3872
+
+
+def encode_gpu_metrics_v18(*, xgmi_read_kb: Sequence[int] = (0,) * 8, xgmi_write_kb: Sequence[int] = (0,) * 8,
+                           xgmi_link_status: Sequence[int] = (-1, 1, 1, 1, 1, 1, 1, 1), clock_ns: int = 10 ** 15,
+                           energy_acc: int = 1 << 40, socket_power_w: int = 750, temp_hotspot_c: int = 61,
+                           temp_mem_c: int = 52, xgmi_link_width: int = 16, xgmi_link_speed: int = 38,
+                           gfxclk_mhz: Sequence[int] = (2100,) * 8) -> bytes:
+    """A gpu_metrics table in the MI355X layout (format 1, content 8) with every field the native
+    decoder reads; everything else holds the PMFW's N/A pattern (0xFF bytes)."""
+    b = bytearray(b"\xff" * GPU_METRICS_V18_SIZE)
+    struct.pack_into("<HBB", b, 0, GPU_METRICS_V18_SIZE, 1, 8)
+    struct.pack_into("<HHHHHH", b, 4, temp_hotspot_c, temp_mem_c, 40, socket_power_w, 37, 12)
+    struct.pack_into("<QQQ", b, 16, 8192, energy_acc, clock_ns)
+    struct.pack_into("<IIIIIII", b, 40, 1000, 0, 0, 0, 0, 0, 0)
+    struct.pack_into("<HHHH", b, 68, 16, 320, xgmi_link_width, xgmi_link_speed)
+    struct.pack_into("<QQ", b, 88, 1 << 30, 20)
+    struct.pack_into("<8Q", b, 136, *xgmi_read_kb)
+    struct.pack_into("<8Q", b, 200, *xgmi_write_kb)
+    struct.pack_into("<8H", b, 264, *[0xFFFF if x < 0 else x for x in xgmi_link_status])
+    struct.pack_into("<Q", b, 288, clock_ns // 10)
+    struct.pack_into("<8H", b, 296, *gfxclk_mhz)
+    struct.pack_into("<H", b, 336, 1900)
+    return bytes(b)
+
+
+def write_gpu_metrics(root, bdf: str, blob: bytes) -> None:
+    p = Path(root) / "sys/bus/pci/devices" / bdf / "gpu_metrics"
+    p.parent.mkdir(parents=True, exist_ok=True)
+    p.write_bytes(blob)
 
 
 def _w(p: Path, content) -> None:
@@ -73,6 +106,7 @@ def make_node(root, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
         _w(dev / "pp_dpm_sclk", "0: 500Mhz\n1: 2100Mhz *\n2: 2400Mhz")
         _w(dev / "pp_dpm_mclk", "0: 900Mhz\n1: 1900Mhz *")
         _w(dev / "ras/umc_err_count", "ue: 0\nce: 3")
+        (dev / "gpu_metrics").write_bytes(encode_gpu_metrics_v18())
         hw = dev / "hwmon/hwmon3"
         _w(hw / "power1_average", 750_000_000)
         for i, (label, t) in enumerate((("edge", 45000), ("junction", 61000), ("mem", 52000)), start=1):

@@ -65,7 +65,7 @@ def compute_labels(root: Optional[str] = None) -> Dict[str, str]:
         PREFIX + "cu-count": str(max(cus_per_physical.values())),
         PREFIX + "simd-count": str(sum(g["simd_count"] for g in gpus if g["pci_bdf"] == first["pci_bdf"])),
         PREFIX + "lds-kib": str(first["lds_size_kib"]),
-        PREFIX + "vram": f"{first['vram_total'] // (1 << 30)}G",
+        PREFIX + "vram": f"{round(first['vram_total'] / (1 << 30))}G",   # nearest GiB (firmware reserves a few MiB)
         PREFIX + "partition.capable": "true" if first["partition_capable"] else "false",
         PREFIX + "partition.count": str(len(gpus)),
         PREFIX + "numa-nodes": str(len({g["numa_node"] for g in gpus if g["numa_node"] >= 0}) or 1),

@@ -263,8 +263,15 @@ def validate_plugin(ctx: Context) -> Dict[str, Any]:
 def summarize_rccl(results: List[Dict[str, Any]]) -> Dict[str, Any]:
     sweep = [r for r in results if r.get("event") == "allreduce"]
     summ = next((r for r in results if r.get("event") == "summary"), {})
+    fabric = next((r for r in results if r.get("event") == "fabric"), {})
+    per_ranks = {r["ranks"]: r.get("peak_busbw_gbps") for r in results if r.get("event") == "ranks_summary"}
+    debug = next((r for r in results if r.get("event") == "rccl-debug"), {})
+    summaries = [r for r in results if r.get("event") == "summary"]
     return {"sweep": sweep, "ranks": summ.get("ranks"), "peak_busbw_gbps": summ.get("peak_busbw_gbps"),
-            "ok": bool(summ.get("ok")) and all(r.get("ok") for r in sweep)}
+            "busbw_by_ranks": per_ranks, "fabric": fabric, "skipped": bool(summ.get("skipped")),
+            "algo_proto": debug.get("algo_proto"),
+            "ok": bool(summaries) and all(s.get("ok") for s in summaries) and all(r.get("ok") for r in sweep)
+            and fabric.get("ok", True) is not False}
 
 
 def validate_rccl(ctx: Context) -> Dict[str, Any]:
@@ -274,8 +281,15 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
         info = {"skipped": f"{ngpu} GPU(s) allocatable: no fabric to validate", "ok": True}
         ctx.status.create(S.RCCL_READY, info)
         return info
+    env = _validator_env(ctx)
+    env.update({k: v for k, v in ctx.env.items() if k.startswith(("RCCL_", "NCCL_"))})
+    # the rank sweep stops at the node's GPU count; the busBW floor comes from
+    # spec.validator.rccl.env (RCCL_MIN_BUSBW_GBPS), so a slow fabric fails validation
+    env.setdefault("RCCL_RANKS", ",".join(str(n) for n in (2, 4, 8) if n <= ngpu) or str(ngpu))
+    if ngpu not in [int(x) for x in env["RCCL_RANKS"].split(",") if x]:
+        env["RCCL_RANKS"] += f",{ngpu}"
     out = W.run_workload_pod(ctx.client, "rccl-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                             _validator_env(ctx), timeout=ctx.pod_timeout, gpu_limit={GPU_RESOURCE: ngpu})
+                             env, timeout=ctx.pod_timeout, gpu_limit={GPU_RESOURCE: ngpu})
     info = summarize_rccl(out["results"])
     if not info["ok"]:
         raise ValidationError(f"RCCL all-reduce validation failed: {info}")

@@ -62,6 +62,11 @@ def prepare_pod(client, template: Dict[str, Any], namespace: str, node: str, env
         c["imagePullPolicy"] = policy
         # termination message carries the workload's JSON result
         c.setdefault("terminationMessagePolicy", "FallbackToLogsOnError")
+    for c in spec.get("initContainers", []):
+        # workload knobs (RCCL_RANKS, RCCL_MIN_BUSBW_GBPS, NCCL_*, ...) reach the workload process
+        for k, v in sorted(env.items()):
+            if not k.startswith("VALIDATOR_"):
+                o.set_env(c, k, v)
     secrets = [s for s in env.get("VALIDATOR_IMAGE_PULL_SECRETS", "").split(",") if s]
     if secrets:
         spec["imagePullSecrets"] = [{"name": s} for s in secrets]

@@ -1,7 +1,8 @@
 """``amd-validator-workload``: what runs inside the spawned validation pods.
 
     amd-validator-workload hip  [--gemm-shapes 8192,...] [--gemm-dtype bf16|fp8|both] [--counters]
-    amd-validator-workload rccl [--max-bytes N] [--dtype float|bf16]
+    amd-validator-workload rccl [--ranks 2,4,8] [--processes N] [--max-bytes N] [--dtype float|bf16]
+                                [--min-busbw GBPS]
 
 Runs the native workload binaries (``amd-hip-smoke``, ``amd-gemm-validate``,
 ``amd-rccl-validate``), optionally collects rocprofv3 counters for one GEMM dispatch
@@ -17,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -101,12 +103,103 @@ def run_hip(shapes: List[str], counters: bool = False, iters: int = 20,
     return results
 
 
-def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run) -> List[Dict]:
-    rc, r = run_json([binary("amd-rccl-validate"), "--max-bytes", str(max_bytes), "--dtype", dtype,
-                      "--min-bytes", "1024"], run, timeout=1200)
-    if rc != 0 and not any(x.get("event") == "summary" for x in r):
-        r.append({"event": "summary", "ok": False, "rc": rc})
-    return r
+# NCCL's numeric algorithm / protocol ids in its TUNING lines (NCCL_ALGO_*, NCCL_PROTO_*)
+_ALGOS = {"0": "Tree", "1": "Ring", "2": "CollNetDirect", "3": "CollNetChain", "4": "NVLS", "5": "NVLSTree"}
+_PROTOS = {"0": "LL", "1": "LL128", "2": "Simple"}
+_RCCL_KEEP = re.compile(r"Algo|algorithm|proto|Channel \d+/\d+|nRanks|Init COMPLETE|Connected all|xGMI|P2P|rings?\b",
+                        re.I)
+
+
+def parse_rccl_debug(text: str, keep: int = 40) -> Dict:
+    """Summarise an RCCL ``NCCL_DEBUG=INFO`` log (subsystems INIT,TUNING,GRAPH): the algorithm and
+    protocol picked per message size, channel count, transport lines and ranks."""
+    algo_proto: Dict[str, int] = {}
+    channels = set()
+    lines: List[str] = []
+    for line in text.splitlines():
+        if "NCCL INFO" not in line and "RCCL" not in line:
+            continue
+        m = re.search(r"Algo\s+(\w+)\s+proto\s+(\w+)", line, re.I) or \
+            re.search(r"algorithm\s+(\w+).*?protocol\s+(\w+)", line, re.I)
+        if m:
+            key = f"{_ALGOS.get(m.group(1), m.group(1))}/{_PROTOS.get(m.group(2), m.group(2))}"
+            algo_proto[key] = algo_proto.get(key, 0) + 1
+        c = re.search(r"Channel (\d+)/(\d+)", line)
+        if c:
+            channels.add(int(c.group(2)))
+        if _RCCL_KEEP.search(line) and len(lines) < keep:
+            lines.append(line.split("NCCL INFO", 1)[-1].strip()[:200])
+    return {"event": "rccl-debug", "algo_proto": algo_proto, "channels": max(channels) if channels else None,
+            "lines": lines}
+
+
+def _rccl_env(log_path: str) -> Dict[str, str]:
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,TUNING,GRAPH", NCCL_DEBUG_FILE=log_path)
+    return env
+
+
+def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run, ranks: Optional[str] = None,
+             min_busbw: Optional[float] = None, processes: int = 0, min_bytes: int = 1024,
+             timeout: float = 1200) -> List[Dict]:
+    """The xGMI fabric proof: topology + fabric check, then a rank-count sweep in one process
+    (``ranks`` "2,4,8") or, with ``processes`` N, one process per GPU joined through
+    ncclCommInitRank. RCCL's INFO log is captured and summarised (algorithm/protocol per size)."""
+    base = ["--max-bytes", str(max_bytes), "--dtype", dtype, "--min-bytes", str(min_bytes)]
+    if min_busbw:
+        base += ["--min-busbw", str(min_busbw)]
+    tmp = tempfile.mkdtemp(prefix="amdgo-rccl-")
+    try:
+        if processes > 0:
+            results = _run_rccl_mp(processes, base, tmp, timeout)
+        else:
+            cmd = [binary("amd-rccl-validate")] + base + (["--ranks", ranks] if ranks else [])
+            p = run(cmd, capture_output=True, text=True, timeout=timeout, env=_rccl_env(os.path.join(tmp, "rccl.%p.log")))
+            if p.stderr:
+                sys.stderr.write(p.stderr[-4000:])
+            results = _json_lines(p.stdout)
+            if p.returncode != 0 and not any(x.get("event") == "summary" for x in results):
+                results.append({"event": "summary", "ok": False, "rc": p.returncode})
+        text = ""
+        for f in sorted(glob.glob(os.path.join(tmp, "rccl.*.log"))):
+            with open(f, errors="replace") as fh:
+                text += fh.read()
+        results.append(parse_rccl_debug(text))
+        return results
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict]:
+    """Start N ranks of amd-rccl-validate (this process never touches the GPU); rank 0 publishes the
+    ncclUniqueId through a file, the others join. Rank 0's lines plus every rank's summary."""
+    id_file = os.path.join(tmp, "nccl.id")
+    procs = []
+    for r in range(n):
+        cmd = [binary("amd-rccl-validate")] + base + ["--mp-rank", str(r), "--mp-nranks", str(n),
+                                                      "--mp-id-file", id_file, "--device", str(r)]
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                      env=_rccl_env(os.path.join(tmp, f"rccl.{r}.log"))))
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            out, err = p.communicate()
+        if err:
+            sys.stderr.write(err[-2000:])
+        outs.append((p.returncode, _json_lines(out)))
+    results = list(outs[0][1])
+    for r, (rc, lines) in enumerate(outs[1:], start=1):
+        results += [x for x in lines if x.get("event") in ("summary", "start") or "error" in x]
+        if rc != 0 and not any(x.get("event") == "summary" for x in lines):
+            results.append({"event": "summary", "rank": r, "ok": False, "rc": rc})
+    if outs[0][0] != 0 and not any(x.get("event") == "summary" for x in outs[0][1]):
+        results.append({"event": "summary", "rank": 0, "ok": False, "rc": outs[0][0]})
+    return results
 
 
 def emit(results: List[Dict], termination_log: Optional[str] = "/dev/termination-log") -> None:
@@ -135,13 +228,16 @@ def main(argv=None) -> int:
     h.add_argument("--gemm-dtype", choices=["bf16", "fp8", "both"], default=os.environ.get("GEMM_DTYPE", "bf16"))
     r = sub.add_parser("rccl")
     r.add_argument("--max-bytes", type=int, default=int(os.environ.get("RCCL_MAX_BYTES", 1 << 30)))
-    r.add_argument("--dtype", default="float")
+    r.add_argument("--dtype", default=os.environ.get("RCCL_DTYPE", "float"))
+    r.add_argument("--ranks", default=os.environ.get("RCCL_RANKS", "2,4,8"))
+    r.add_argument("--processes", type=int, default=int(os.environ.get("RCCL_PROCESSES", "0")))
+    r.add_argument("--min-busbw", type=float, default=float(os.environ.get("RCCL_MIN_BUSBW_GBPS", "0") or 0))
     a = ap.parse_args(argv)
     if a.what == "hip":
         results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters, dtype=a.gemm_dtype)
         ok = all(x.get("ok", True) for x in results if x.get("event") in ("gemm", "hip-smoke"))
     else:
-        results = run_rccl(a.max_bytes, a.dtype)
+        results = run_rccl(a.max_bytes, a.dtype, ranks=a.ranks, min_busbw=a.min_busbw, processes=a.processes)
         ok = all(x.get("ok", False) for x in results if x.get("event") == "summary")
     emit(results)
     return 0 if ok else 1

@@ -99,12 +99,43 @@ struct Telemetry {
   double pcie_bw_bytes = -1;
 };
 
+// Decoded sysfs `gpu_metrics` (the PMFW metrics table the amdgpu driver exports per device).
+// Only layouts verified byte-for-byte against amd-smi on real hardware are decoded (format 1,
+// content 8 = MI355X; tests/fixtures/gpu_metrics/); any other revision sets `error` and leaves
+// every value at its N/A default rather than guessing offsets.
+struct GpuMetrics {
+  int index = 0;
+  std::string pci_bdf;
+  bool valid = false;
+  std::string error;
+  int format_revision = 0, content_revision = 0;
+  uint32_t structure_size = 0;
+  double temp_hotspot_c = -1, temp_mem_c = -1, temp_vrsoc_c = -1;
+  double socket_power_w = -1, gfx_activity_pct = -1, umc_activity_pct = -1;
+  uint64_t energy_acc = 0;              // 15.259 uJ (2^-16 J) units
+  uint64_t system_clock_ns = 0;         // driver timestamp of the sample
+  uint64_t firmware_timestamp = 0;      // PMFW timestamp, 10 ns units
+  uint64_t accumulation_counter = 0;
+  uint64_t ppt_residency_acc = 0;       // power-limit (PPT) throttle residency, accumulated
+  int pcie_link_width = -1, pcie_link_speed = -1;    // lanes, 0.1 GT/s
+  int xgmi_link_width = -1, xgmi_link_speed = -1;    // lanes, Gbps per lane
+  uint64_t pcie_bandwidth_acc = 0, pcie_bandwidth_inst = 0;   // GB/s (accumulated / instantaneous)
+  uint64_t mem_max_bandwidth = 0;       // GB/s
+  std::vector<uint64_t> xgmi_read_kb;   // per xGMI link: accumulated KiB read
+  std::vector<uint64_t> xgmi_write_kb;  // per xGMI link: accumulated KiB written
+  std::vector<int> xgmi_link_status;    // per link: 1 up, 0 down, -1 not applicable
+  std::vector<int> gfxclk_mhz;          // per XCC
+  int uclk_mhz = -1;
+};
+
 // --- discovery -------------------------------------------------------------------------
 std::vector<Gpu> enumerate_gpus(const std::string& root = "/");
 std::vector<PciFunction> scan_pci(const std::string& root = "/", uint16_t vendor = 0x1002,
                                   bool gpu_classes_only = true);
 DriverState driver_state(const std::string& root = "/", const std::string& dev_root = "/");
 std::vector<Telemetry> read_telemetry(const std::string& root = "/");
+GpuMetrics parse_gpu_metrics(const std::string& blob);
+std::vector<GpuMetrics> read_gpu_metrics(const std::string& root = "/");
 
 // --- partitioning ------------------------------------------------------------------------
 // Write current_{compute,memory}_partition of one GPU (by PCI BDF). Returns "" on success or

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <set>
 #include <sstream>
 #include <thread>
@@ -197,10 +198,16 @@ std::vector<Gpu> enumerate_gpus(const std::string& root) {
   const std::string topo = join(root, "/sys/class/kfd/kfd/topology/nodes");
   int index = 0;
   std::map<int, int> node_to_index;
+  std::set<int> cpu_nodes;
   for (const auto& n : list_dir(topo)) {
     const std::string nd = topo + "/" + n;
     auto kv = read_kv(nd + "/properties");
-    if (kv_u64(kv, "simd_count") == 0) continue;  // CPU agent
+    if (kv_u64(kv, "simd_count") == 0) {
+      // CPU agent -- or a GPU agent this cgroup may not access: KFD refuses to show its
+      // properties (EPERM, empty read), so only a node with CPU cores counts as a CPU.
+      if (kv_u64(kv, "cpu_cores_count") > 0) cpu_nodes.insert((int)to_u64(n));
+      continue;
+    }
     Gpu g;
     g.kfd_node = (int)to_u64(n);
     g.gpu_id = (uint32_t)to_u64(read_file(nd + "/gpu_id"));
@@ -276,11 +283,11 @@ std::vector<Gpu> enumerate_gpus(const std::string& root) {
     node_to_index[g.kfd_node] = index++;
     gpus.push_back(g);
   }
-  // count xGMI/PCIe links between GPU agents
+  // count xGMI/PCIe links. An xGMI io_link whose peer agent is not enumerated here (a GPU this
+  // container's cgroup hides from KFD) still is a physical GPU-to-GPU link: count all but CPU peers.
   for (auto& g : gpus) {
     for (const auto& l : g.links) {
-      bool to_gpu = node_to_index.count(l.node_to) > 0;
-      if (l.type == 11 && to_gpu) g.xgmi_links++;
+      if (l.type == 11 && !cpu_nodes.count(l.node_to)) g.xgmi_links++;
       if (l.type == 2) g.pcie_links++;
     }
   }
@@ -387,6 +394,102 @@ std::vector<Telemetry> read_telemetry(const std::string& root) {
       t.pcie_bw_bytes = (double)(rx + tx) * (double)mps;
     }
     out.push_back(t);
+  }
+  return out;
+}
+
+namespace {
+
+template <typename T>
+T rd(const std::string& b, size_t off) {
+  T v{};
+  if (off + sizeof(T) <= b.size()) std::memcpy(&v, b.data() + off, sizeof(T));
+  return v;
+}
+
+double na16(uint16_t v) { return v == 0xFFFF ? -1.0 : (double)v; }
+int na16i(uint16_t v) { return v == 0xFFFF ? -1 : (int)v; }
+uint64_t na64(uint64_t v) { return v == ~0ull ? 0 : v; }
+uint64_t na32(uint32_t v) { return v == ~0u ? 0 : v; }
+
+// gpu_metrics format 1 content 8 (MI355X PMFW, 3872 bytes). Offsets pinned against amd-smi's
+// decoding of the same blob on an MI355X (tools/gpu_metrics_probe.py, tests/fixtures/gpu_metrics).
+struct LayoutV18 {
+  static constexpr size_t temp_hotspot = 4, temp_mem = 6, temp_vrsoc = 8, socket_power = 10;
+  static constexpr size_t gfx_activity = 12, umc_activity = 14, mem_max_bw = 16, energy = 24, sysclk = 32;
+  static constexpr size_t accum = 40, ppt_res = 48;
+  static constexpr size_t pcie_width = 68, pcie_speed = 70, xgmi_width = 72, xgmi_speed = 74;
+  static constexpr size_t pcie_bw_acc = 88, pcie_bw_inst = 96;
+  static constexpr size_t xgmi_read = 136, xgmi_write = 200, xgmi_status = 264;   // 8 links each
+  static constexpr size_t fw_ts = 288, gfxclk = 296, uclk = 336;
+  static constexpr int links = 8, xccs = 8;
+  static constexpr size_t min_size = 338;
+};
+
+}  // namespace
+
+GpuMetrics parse_gpu_metrics(const std::string& blob) {
+  GpuMetrics m;
+  if (blob.size() < 4) {
+    m.error = "gpu_metrics too short";
+    return m;
+  }
+  m.structure_size = rd<uint16_t>(blob, 0);
+  m.format_revision = (uint8_t)blob[2];
+  m.content_revision = (uint8_t)blob[3];
+  if (m.format_revision != 1 || m.content_revision != 8) {
+    m.error = "unsupported gpu_metrics v" + std::to_string(m.format_revision) + "." +
+              std::to_string(m.content_revision);
+    return m;
+  }
+  using L = LayoutV18;
+  if (blob.size() < L::min_size || m.structure_size < L::min_size) {
+    m.error = "gpu_metrics v1.8 truncated";
+    return m;
+  }
+  m.temp_hotspot_c = na16(rd<uint16_t>(blob, L::temp_hotspot));
+  m.temp_mem_c = na16(rd<uint16_t>(blob, L::temp_mem));
+  m.temp_vrsoc_c = na16(rd<uint16_t>(blob, L::temp_vrsoc));
+  m.socket_power_w = na16(rd<uint16_t>(blob, L::socket_power));
+  m.gfx_activity_pct = na16(rd<uint16_t>(blob, L::gfx_activity));
+  m.umc_activity_pct = na16(rd<uint16_t>(blob, L::umc_activity));
+  m.mem_max_bandwidth = na64(rd<uint64_t>(blob, L::mem_max_bw));
+  m.energy_acc = na64(rd<uint64_t>(blob, L::energy));
+  m.system_clock_ns = na64(rd<uint64_t>(blob, L::sysclk));
+  m.accumulation_counter = na32(rd<uint32_t>(blob, L::accum));
+  m.ppt_residency_acc = na32(rd<uint32_t>(blob, L::ppt_res));
+  m.pcie_link_width = na16i(rd<uint16_t>(blob, L::pcie_width));
+  m.pcie_link_speed = na16i(rd<uint16_t>(blob, L::pcie_speed));
+  m.xgmi_link_width = na16i(rd<uint16_t>(blob, L::xgmi_width));
+  m.xgmi_link_speed = na16i(rd<uint16_t>(blob, L::xgmi_speed));
+  m.pcie_bandwidth_acc = na64(rd<uint64_t>(blob, L::pcie_bw_acc));
+  m.pcie_bandwidth_inst = na64(rd<uint64_t>(blob, L::pcie_bw_inst));
+  m.firmware_timestamp = na64(rd<uint64_t>(blob, L::fw_ts));
+  for (int i = 0; i < L::links; ++i) {
+    m.xgmi_read_kb.push_back(na64(rd<uint64_t>(blob, L::xgmi_read + 8 * i)));
+    m.xgmi_write_kb.push_back(na64(rd<uint64_t>(blob, L::xgmi_write + 8 * i)));
+    m.xgmi_link_status.push_back(na16i(rd<uint16_t>(blob, L::xgmi_status + 2 * i)));
+  }
+  for (int i = 0; i < L::xccs; ++i) m.gfxclk_mhz.push_back(na16i(rd<uint16_t>(blob, L::gfxclk + 2 * i)));
+  m.uclk_mhz = na16i(rd<uint16_t>(blob, L::uclk));
+  m.valid = true;
+  return m;
+}
+
+std::vector<GpuMetrics> read_gpu_metrics(const std::string& root) {
+  std::vector<GpuMetrics> out;
+  for (const auto& g : enumerate_gpus(root)) {
+    std::ifstream f(g.device_path + "/gpu_metrics", std::ios::binary);
+    GpuMetrics m;
+    if (!f) {
+      m.error = "no gpu_metrics";
+    } else {
+      std::string blob((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+      m = parse_gpu_metrics(blob);
+    }
+    m.index = g.index;
+    m.pci_bdf = g.pci_bdf;
+    out.push_back(m);
   }
   return out;
 }

@@ -89,11 +89,45 @@ PYBIND11_MODULE(_amdnode, m) {
       .def_readonly("ecc_uncorrectable", &Telemetry::ecc_uncorrectable)
       .def_readonly("pcie_bw_bytes", &Telemetry::pcie_bw_bytes);
 
+  py::class_<GpuMetrics>(m, "GpuMetrics")
+      .def_readonly("index", &GpuMetrics::index)
+      .def_readonly("pci_bdf", &GpuMetrics::pci_bdf)
+      .def_readonly("valid", &GpuMetrics::valid)
+      .def_readonly("error", &GpuMetrics::error)
+      .def_readonly("format_revision", &GpuMetrics::format_revision)
+      .def_readonly("content_revision", &GpuMetrics::content_revision)
+      .def_readonly("structure_size", &GpuMetrics::structure_size)
+      .def_readonly("temp_hotspot_c", &GpuMetrics::temp_hotspot_c)
+      .def_readonly("temp_mem_c", &GpuMetrics::temp_mem_c)
+      .def_readonly("temp_vrsoc_c", &GpuMetrics::temp_vrsoc_c)
+      .def_readonly("socket_power_w", &GpuMetrics::socket_power_w)
+      .def_readonly("gfx_activity_pct", &GpuMetrics::gfx_activity_pct)
+      .def_readonly("umc_activity_pct", &GpuMetrics::umc_activity_pct)
+      .def_readonly("energy_acc", &GpuMetrics::energy_acc)
+      .def_readonly("system_clock_ns", &GpuMetrics::system_clock_ns)
+      .def_readonly("firmware_timestamp", &GpuMetrics::firmware_timestamp)
+      .def_readonly("accumulation_counter", &GpuMetrics::accumulation_counter)
+      .def_readonly("ppt_residency_acc", &GpuMetrics::ppt_residency_acc)
+      .def_readonly("pcie_link_width", &GpuMetrics::pcie_link_width)
+      .def_readonly("pcie_link_speed", &GpuMetrics::pcie_link_speed)
+      .def_readonly("xgmi_link_width", &GpuMetrics::xgmi_link_width)
+      .def_readonly("xgmi_link_speed", &GpuMetrics::xgmi_link_speed)
+      .def_readonly("pcie_bandwidth_acc", &GpuMetrics::pcie_bandwidth_acc)
+      .def_readonly("pcie_bandwidth_inst", &GpuMetrics::pcie_bandwidth_inst)
+      .def_readonly("mem_max_bandwidth", &GpuMetrics::mem_max_bandwidth)
+      .def_readonly("xgmi_read_kb", &GpuMetrics::xgmi_read_kb)
+      .def_readonly("xgmi_write_kb", &GpuMetrics::xgmi_write_kb)
+      .def_readonly("xgmi_link_status", &GpuMetrics::xgmi_link_status)
+      .def_readonly("gfxclk_mhz", &GpuMetrics::gfxclk_mhz)
+      .def_readonly("uclk_mhz", &GpuMetrics::uclk_mhz);
+
   m.def("enumerate_gpus", &enumerate_gpus, py::arg("root") = "/");
   m.def("scan_pci", &scan_pci, py::arg("root") = "/", py::arg("vendor") = 0x1002,
         py::arg("gpu_classes_only") = true);
   m.def("driver_state", &driver_state, py::arg("root") = "/", py::arg("dev_root") = "/");
   m.def("read_telemetry", &read_telemetry, py::arg("root") = "/");
+  m.def("read_gpu_metrics", &read_gpu_metrics, py::arg("root") = "/");
+  m.def("parse_gpu_metrics", [](const py::bytes& b) { return parse_gpu_metrics(std::string(b)); });
   m.def("set_partition", &set_partition, py::arg("root"), py::arg("bdf"), py::arg("kind"), py::arg("mode"));
   m.def(
       "wait_files",

@@ -188,13 +188,15 @@ def test_runtime_detection_prefers_containerd_then_falls_back_to_default():
 
 
 # ------------------------------------------------------------------------------ telemetry etc.
-def test_metrics_exporter_attaches_to_rdc_when_enabled():
+def test_metrics_exporter_stays_off_the_host_network_with_rdc_enabled():
+    """The exporter reads telemetry natively (no RDC client), so enabling rdcd must not give it
+    hostNetwork or an RDC endpoint (round-1 review: that privilege bought nothing)."""
     c = cluster(cp=sample_cp(**{"rdc.enabled": True, "rdc.hostPort": 50555,
                                 "metricsExporter.config": {"name": "my-fields"}}))
     reconcile_once(c)
     ex = daemonset(c, C.DS_METRICS_EXPORTER)
-    assert ex["spec"]["template"]["spec"]["hostNetwork"] is True
-    assert env(container(ex, "amd-metrics-exporter"))["RDC_HOST"] == "localhost:50555"
+    assert not ex["spec"]["template"]["spec"].get("hostNetwork")
+    assert "RDC_HOST" not in env(container(ex, "amd-metrics-exporter"))
     vols = {v["name"]: v for v in ex["spec"]["template"]["spec"]["volumes"]}
     assert vols["fields"]["configMap"]["name"] == "my-fields"
     rdc = daemonset(c, C.DS_RDC)

@@ -143,3 +143,22 @@ def test_node_probe_cli(node):
                          capture_output=True, text=True, check=True).stdout
     j = json.loads(out)
     assert j["driver"]["live"] and len(j["gpus"]) == 8 and j["gpus"][3]["gfx"] == "gfx950"
+
+
+def test_gpus_hidden_by_the_device_cgroup_still_count_as_xgmi_peers(tmp_path):
+    """In a container that may access one GPU, KFD refuses to show the other GPU agents'
+    properties (EPERM, read as empty). Their xGMI links are still physical GPU links: a GPU of an
+    8-GPU hive reports 7, as on the MI355X box."""
+    from pathlib import Path
+
+    from gpu_operator_amd import devices as D
+    from gpu_operator_amd.devices import fakesys
+
+    root = fakesys.make_node(tmp_path, n_gpus=8)
+    topo = Path(root) / "sys/class/kfd/kfd/topology/nodes"
+    for n in range(2, 9):
+        (topo / str(n) / "properties").write_text("")
+    gpus = D.enumerate_gpus(str(root))
+    assert len(gpus) == 1 and gpus[0]["xgmi_links"] == 7 and gpus[0]["pcie_links"] == 1
+    from gpu_operator_amd.operands import node_labeller as NL
+    assert NL.compute_labels(str(root))["amd.com/gpu.xgmi.links"] == "7"

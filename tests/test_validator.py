@@ -2,6 +2,7 @@
 
 import json
 import os
+import subprocess
 import threading
 import time
 
@@ -294,3 +295,127 @@ def test_reference_model_constants():
     # toolkit ready at 6 s; the first validation attempt (0.6 s) fails -> 10 s back-off
     assert m["toolkit_crashloops"] == 1 and m["toolkit_ready_s"] == 6.0
     assert m["time_to_ready_s"] >= 15.0
+
+
+# -- RCCL fabric proof: rank sweep, busBW floor, topology ------------------------------------------
+RCCL_SWEEP_MSG = "\n".join(json.dumps(x) for x in [
+    {"event": "fabric", "physical_gpus": 8, "single_hive": True, "full_node": True, "min_xgmi_links": 7, "ok": True},
+    {"event": "ranks_summary", "ranks": 2, "peak_busbw_gbps": 140.0, "ok": True},
+    {"event": "ranks_summary", "ranks": 8, "peak_busbw_gbps": 310.0, "ok": True},
+    {"event": "summary", "ranks": 8, "ranks_run": [2, 4, 8], "peak_busbw_gbps": 310.0, "ok": True},
+    {"event": "rccl-debug", "algo_proto": {"Ring/Simple": 3}, "channels": 32, "lines": []}])
+
+
+def _pod_env(pod):
+    return {e["name"]: e.get("value") for e in pod["spec"]["initContainers"][0].get("env", [])}
+
+
+def test_rccl_sweeps_rank_counts_and_passes_the_busbw_floor(tmp_path, node_root):
+    c = FakeClient([node_obj()])
+    k = FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG})
+    ctx = ctx_for(tmp_path, node_root, client=c, env={"RCCL_MIN_BUSBW_GBPS": "250"})
+    info = comp.validate_rccl(ctx)
+    env = _pod_env(k.seen[0])
+    assert env["RCCL_RANKS"] == "2,4,8" and env["RCCL_MIN_BUSBW_GBPS"] == "250"
+    assert "amd.com/gpu: 8" not in open(os.path.join(os.path.dirname(comp.__file__), "manifests",
+                                                     "rccl-workload-validation.yaml")).read()
+    assert info["busbw_by_ranks"] == {2: 140.0, 8: 310.0} and info["algo_proto"] == {"Ring/Simple": 3}
+    assert info["fabric"]["full_node"] and info["ok"]
+
+
+def test_rccl_fails_validation_on_a_split_hive(tmp_path, node_root):
+    msg = "\n".join(json.dumps(x) for x in [
+        {"event": "fabric", "physical_gpus": 8, "single_hive": False, "ok": False, "reason": "GPUs span 2 xGMI hives"},
+        {"event": "summary", "ok": False, "reason": "fabric check failed"}])
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-rccl-validator": msg}, phase="Failed")
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    with pytest.raises(Exception):
+        comp.validate_rccl(ctx)
+    assert not ctx.status.exists(S.RCCL_READY)
+
+
+def test_rccl_ranks_follow_the_node_gpu_count(tmp_path, node_root):
+    c = FakeClient([node_obj(gpus=4)])
+    k = FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG})
+    comp.validate_rccl(ctx_for(tmp_path, node_root, client=c))
+    assert _pod_env(k.seen[0])["RCCL_RANKS"] == "2,4"
+    assert k.seen[0]["spec"]["initContainers"][0]["resources"]["limits"] == {"amd.com/gpu": 4}
+
+
+RCCL_BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpu_operator_amd", "_native",
+                        "bin", "amd-rccl-validate")
+
+
+def _topology(root):
+    p = subprocess.run([RCCL_BIN, "--topology-only", "--sys-root", str(root)], capture_output=True, text=True,
+                       timeout=30)
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    return p.returncode, {x["event"]: x for x in lines}
+
+
+@pytest.mark.skipif(not os.path.exists(RCCL_BIN), reason="amd-rccl-validate not built")
+def test_rccl_topology_full_mesh_hive_ok(tmp_path):
+    rc, ev = _topology(fakesys.make_node(tmp_path, n_gpus=8))
+    assert rc == 0 and ev["fabric"]["ok"] and ev["fabric"]["full_node"] and ev["fabric"]["min_xgmi_links"] == 7
+    assert len(ev["topology"]["gpus"]) == 8 and all(len(g["xgmi_peers"]) == 7 for g in ev["topology"]["gpus"])
+
+
+@pytest.mark.skipif(not os.path.exists(RCCL_BIN), reason="amd-rccl-validate not built")
+def test_rccl_topology_split_hive_fails(tmp_path):
+    from pathlib import Path
+    root = fakesys.make_node(tmp_path, n_gpus=8)
+    topo = Path(root) / "sys/class/kfd/kfd/topology/nodes"
+    for n in (5, 6, 7, 8):                     # half the GPUs report another hive
+        props = topo / str(n) / "properties"
+        props.write_text(props.read_text().replace(f"hive_id {0x5A5A_0001}", "hive_id 12345"))
+        (Path(root) / "sys/bus/pci/devices").joinpath(f"0000:{0x05 + 0x10 * (n - 1):02x}:00.0",
+                                                      "xgmi_hive_info/xgmi_hive_id").write_text("12345\n")
+    rc, ev = _topology(root)
+    assert rc == 1 and not ev["fabric"]["ok"] and "2 xGMI hives" in ev["fabric"]["reason"]
+
+
+@pytest.mark.skipif(not os.path.exists(RCCL_BIN), reason="amd-rccl-validate not built")
+def test_rccl_topology_missing_link_fails(tmp_path):
+    import shutil
+    from pathlib import Path
+    root = fakesys.make_node(tmp_path, n_gpus=8)
+    shutil.rmtree(Path(root) / "sys/class/kfd/kfd/topology/nodes/3/io_links/4")
+    rc, ev = _topology(root)
+    assert rc == 1 and "6 xGMI links" in ev["fabric"]["reason"]
+
+
+@pytest.mark.skipif(not os.path.exists(RCCL_BIN), reason="amd-rccl-validate not built")
+def test_rccl_topology_single_gpu_is_fine(tmp_path):
+    rc, ev = _topology(fakesys.make_node(tmp_path, n_gpus=1))
+    assert rc == 0 and ev["fabric"]["ok"] and not ev["fabric"]["full_node"]
+
+
+def test_rccl_debug_log_summary():
+    from gpu_operator_amd.validator.workload_main import parse_rccl_debug
+    log = "\n".join([
+        "host:1:1 [0] NCCL INFO Channel 00/16 :    0   1   2   3   4   5   6   7",
+        "host:1:1 [0] NCCL INFO Channel 15/16 :    0   1   2   3   4   5   6   7",
+        "host:1:1 [0] NCCL INFO comm 0x1 rank 0 nRanks 8 nNodes 1 localRanks 8 localRank 0",
+        "host:1:1 [0] NCCL INFO AllReduce: 1048576 Bytes -> Algo 1 proto 2 time 21.5",
+        "host:1:1 [0] NCCL INFO AllReduce: 1024 Bytes -> Algo 0 proto 0 time 9.1",
+        "host:1:1 [0] NCCL INFO AllReduce: 2048 Bytes -> Algo 0 proto 0 time 9.4",
+        "unrelated"])
+    d = parse_rccl_debug(log)
+    assert d["algo_proto"] == {"Ring/Simple": 1, "Tree/LL": 2} and d["channels"] == 16
+    assert any("nRanks 8" in x for x in d["lines"])
+
+
+def test_rccl_workload_cli_reads_env(monkeypatch):
+    from gpu_operator_amd.validator import workload_main as WM
+    seen = {}
+
+    def fake(max_bytes, dtype, ranks=None, min_busbw=None, processes=0, **kw):
+        seen.update(max_bytes=max_bytes, dtype=dtype, ranks=ranks, min_busbw=min_busbw, processes=processes)
+        return [{"event": "summary", "ok": True}]
+    monkeypatch.setattr(WM, "run_rccl", fake)
+    monkeypatch.setattr(WM, "emit", lambda r: None)
+    monkeypatch.setenv("RCCL_MIN_BUSBW_GBPS", "123.5")
+    monkeypatch.setenv("RCCL_RANKS", "2,8")
+    assert WM.main(["rccl"]) == 0
+    assert seen == {"max_bytes": 1 << 30, "dtype": "float", "ranks": "2,8", "min_busbw": 123.5, "processes": 0}

@@ -48,9 +48,32 @@ def test_gemm_validate_binary_fp8_and_both():
 def test_rccl_validate_binary():
     rc, lines, err = run("amd-rccl-validate", "--max-bytes", str(1 << 26), "--iters", "5", "--warmup", "2")
     assert rc == 0, err
+    ev = {x.get("event"): x for x in lines}
+    assert ev["fabric"]["ok"] and ev["fabric"]["single_hive"]
+    assert ev["topology"]["gpus"][0]["xgmi_links"] == 7          # a GPU of the box's 8-GPU hive
     summ = lines[-1]
     assert summ["event"] == "summary" and summ["ok"]
     assert all(x["ok"] for x in lines if x.get("event") == "allreduce")
+
+
+def test_rccl_rank_sweep_on_one_gpu_is_a_clean_skip():
+    rc, lines, err = run("amd-rccl-validate", "--ranks", "2,4,8", "--max-bytes", str(1 << 20), "--iters", "2")
+    assert rc == 0, err
+    skipped = [x["ranks"] for x in lines if x.get("event") == "skipped"]
+    assert skipped == [2, 4, 8]
+    assert lines[-1]["event"] == "summary" and lines[-1]["ok"] and lines[-1]["skipped"]
+
+
+def test_rccl_multi_process_mode_and_debug_capture():
+    from gpu_operator_amd.validator.workload_main import run_rccl
+    res = run_rccl(1 << 22, "bf16", processes=1, min_bytes=1 << 20, timeout=300)
+    summ = [x for x in res if x.get("event") == "summary"]
+    assert summ and all(x["ok"] for x in summ), res
+    start = [x for x in res if x.get("event") == "start"][0]
+    assert start["mode"] == "multi-process" and start["ranks"] == 1
+    assert all(x["ok"] for x in res if x.get("event") == "allreduce")
+    dbg = [x for x in res if x.get("event") == "rccl-debug"][0]
+    assert isinstance(dbg["algo_proto"], dict) and dbg["lines"]          # RCCL's INFO log was captured
 
 
 def test_node_probe_on_real_hardware():
