@@ -12,12 +12,16 @@ agents and render nodes. This agent:
 2. if the node differs: state ``pending``; pauses the GPU clients by flipping their deploy
    labels to ``paused-for-partition-change`` (their DaemonSet pods leave the node) and waits
    for those pods to be gone; stops listed host services;
-3. applies memory then compute modes (validated against ``available_*_partition``);
+3. applies the memory (NPS) modes; an NPS change only takes effect once amdgpu reloads, so the
+   node goes ``reload-required`` -> ``reloading``: ``modprobe -r amdgpu && modprobe amdgpu`` on
+   the host (or DRIVER_RELOAD_CMD, e.g. through the driver container), then a bounded wait for
+   ``initstate=live``; then the compute modes (validated against ``available_*_partition``);
 4. waits (bounded) until the KFD agent count matches the new layout — the re-enumeration;
 5. restores the deploy labels (the device plugin comes back and re-registers the new
    devices), writes the ``partition-applied`` barrier (relabels the node), records
    ``state=success`` and the applied config on the node. Any failure -> ``state=failed``
-   with the reason in an event; labels are always restored.
+   with the reason in an event; labels are always restored (also labels a crashed agent left
+   paused: the next reconcile restores them).
 
 All state lives on the Node, so a restarted agent resumes or re-verifies.
 """
@@ -27,6 +31,7 @@ from __future__ import annotations
 import argparse
 import logging
 import os
+import shlex
 import subprocess
 import sys
 import threading
@@ -92,7 +97,9 @@ class PartitionManager:
                  default_config: str = "", barrier_dir: str = "/run/amd/validations",
                  reenumerate: Optional[Callable[[], None]] = None, enum_timeout: float = 120.0,
                  pods_timeout: float = 300.0, host_services: Optional[List[str]] = None,
-                 run: Callable = subprocess.run, namespace: str = ""):
+                 run: Callable = subprocess.run, namespace: str = "",
+                 reload_driver: Optional[Callable[[], None]] = None, reload_cmd: str = "",
+                 reload_timeout: float = 600.0):
         self.client = client
         self.node = node
         self.config_file = config_file
@@ -105,6 +112,9 @@ class PartitionManager:
         self.host_services = host_services or []
         self.run = run
         self.namespace = namespace
+        self.reload_driver = reload_driver or self._reload_driver   # tests inject the driver's reload
+        self.reload_cmd = reload_cmd
+        self.reload_timeout = reload_timeout
 
     # -- node state -----------------------------------------------------------------------------
     def _node(self) -> Dict:
@@ -138,6 +148,7 @@ class PartitionManager:
         todo = [(i, g, want[i]) for i, g in enumerate(gpus) if i in want and
                 (g["compute_partition"], g["memory_partition"]) != want[i]]
         if not todo:
+            self.resume_clients(self._left_paused(labels))      # a crashed agent's pause
             if labels.get(STATE_LABEL) != "success" or o.get_annotations(node).get(APPLIED_ANNOTATION) != selected:
                 self.set_state("success", selected)
                 self._barrier(selected)
@@ -146,14 +157,22 @@ class PartitionManager:
         self.set_state("pending")
         paused: List[str] = []
         try:
-            paused = self.pause_clients()
+            # the relabel is recorded before the wait, so the finally below always restores it
+            paused = self.pause_clients(labels)
+            self.wait_clients_gone()
             self.stop_host_services()
-            for i, g, (compute, memory) in todo:
-                if g["memory_partition"] and g["memory_partition"] != memory:
-                    self._set(g, "memory", memory)
-            for i, g, (compute, memory) in todo:
-                if g["compute_partition"] != compute:
-                    self._set(g, "compute", compute)
+            mem = [(g, m) for _, g, (_, m) in todo if g["memory_partition"] and g["memory_partition"] != m]
+            for g, memory in mem:
+                self._set(g, "memory", memory)
+            if mem:
+                self.set_state("reload-required")
+                self.set_state("reloading")
+                self.reload_driver()
+                self.wait_driver_live()
+                gpus = physical_gpus(self.root)                 # re-read: the reload re-enumerated
+            for i, g in enumerate(gpus):
+                if i in want and g["compute_partition"] != want[i][0]:
+                    self._set(g, "compute", want[i][0])
             if self.reenumerate:
                 self.reenumerate()
             self.wait_reenumerated(want, len(gpus))
@@ -166,6 +185,28 @@ class PartitionManager:
         self.set_state("success", selected)
         self._barrier(selected)
         return "applied"
+
+    # -- driver reload (memory partition) ----------------------------------------------------------
+    def _reload_driver(self) -> None:
+        """Unload and reload amdgpu so a new NPS mode takes effect. The GPU clients
+        are paused and the host services stopped by now; a failing step is a PartitionError."""
+        cmds = [shlex.split(c) for c in self.reload_cmd.split(";") if c.strip()] if self.reload_cmd else \
+            [["chroot", "/host", "modprobe", "-r", "amdgpu"], ["chroot", "/host", "modprobe", "amdgpu"]]
+        for cmd in cmds:
+            try:
+                p = self.run(cmd, capture_output=True, text=True, timeout=self.reload_timeout)
+            except (OSError, subprocess.TimeoutExpired) as e:
+                raise PartitionError(f"driver reload: {' '.join(cmd)}: {e}") from e
+            if getattr(p, "returncode", 0) != 0:
+                err = (getattr(p, "stderr", "") or "").strip()[-300:]
+                raise PartitionError(f"driver reload: {' '.join(cmd)} exited {p.returncode}: {err}")
+
+    def wait_driver_live(self) -> None:
+        deadline = time.monotonic() + self.reload_timeout
+        while not devices.driver_state(self.root)["live"]:
+            if time.monotonic() > deadline:
+                raise PartitionError("amdgpu did not come back live after the reload")
+            time.sleep(0.5)
 
     def _set(self, g: Dict, kind: str, mode: str) -> None:
         avail = g[f"available_{kind}_partitions"]
@@ -192,18 +233,27 @@ class PartitionManager:
             time.sleep(0.5)
 
     # -- GPU clients -----------------------------------------------------------------------------
-    def pause_clients(self) -> List[str]:
-        labels = o.get_labels(self._node())
-        paused = [k for k in CLIENT_DEPLOY_LABELS if labels.get(k) == "true"]
+    @staticmethod
+    def _left_paused(labels: Dict[str, str]) -> List[str]:
+        return [k for k in CLIENT_DEPLOY_LABELS if labels.get(k) == PAUSED]
+
+    def pause_clients(self, labels: Optional[Dict[str, str]] = None) -> List[str]:
+        """Flip the enabled GPU clients' deploy labels to PAUSED (their DaemonSet pods leave the node);
+        returns what it paused (including labels an earlier, crashed run left paused)."""
+        labels = labels if labels is not None else o.get_labels(self._node())
+        paused = [k for k in CLIENT_DEPLOY_LABELS if labels.get(k) in ("true", PAUSED)]
         if paused:
             self.client.patch("v1", "Node", self.node, {"metadata": {"labels": {k: PAUSED for k in paused}}})
+        return paused
+
+    def wait_clients_gone(self) -> None:
         deadline = time.monotonic() + self.pods_timeout
         while True:
             left = [p for p in self.client.list("v1", "Pod", self.namespace,
                                                 field_selector=f"spec.nodeName={self.node}")
                     if o.get_labels(p).get("app") in CLIENT_APPS]
             if not left:
-                return paused
+                return
             if time.monotonic() > deadline:
                 raise PartitionError(f"GPU clients still running: {[o.name(p) for p in left]}")
             time.sleep(1.0)
@@ -258,12 +308,14 @@ def main(argv=None, client=None) -> int:
     ap.add_argument("--default", default=os.environ.get("DEFAULT_PARTITION_CONFIG", ""))
     ap.add_argument("--namespace", default=os.environ.get("OPERATOR_NAMESPACE", ""))
     ap.add_argument("--resync", type=float, default=300.0)
+    ap.add_argument("--reload-cmd", default=os.environ.get("DRIVER_RELOAD_CMD", ""),
+                    help="';'-separated commands that reload amdgpu (default: modprobe -r/modprobe via /host)")
     a = ap.parse_args(argv)
     if client is None:
         from ..k8s.rest import RestClient
         client = RestClient()
     pm = PartitionManager(client, a.node_name, a.config_file, default_config=a.default, namespace=a.namespace,
-                          host_services=load_clients(a.gpu_clients_file))
+                          host_services=load_clients(a.gpu_clients_file), reload_cmd=a.reload_cmd)
     kick = threading.Event()
 
     def on_node(ev):

@@ -128,8 +128,9 @@ def _cluster(config_label=None):
 
 
 def _mgr(c, spx, cfg, tmp_path, **kw):
+    kw.setdefault("reload_driver", lambda: None)        # the fake driver applies NPS writes at once
     return pm.PartitionManager(c, "n1", cfg, root=spx, barrier_dir=str(tmp_path / "barriers"),
-                               enum_timeout=3.0, pods_timeout=3.0, **kw)
+                               enum_timeout=3.0, pods_timeout=3.0, reload_timeout=3.0, **kw)
 
 
 def test_desired_layout():
@@ -214,6 +215,111 @@ def test_partition_host_services(spx, cfg, tmp_path):
              reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS2"))
     assert m.reconcile() == "applied"
     assert calls == [["stop", "amd-smi-exporter"], ["start", "amd-smi-exporter"]]
+
+
+def test_partition_client_pod_that_never_exits_restores_labels(spx, cfg, tmp_path):
+    """a timed-out wait for a client pod must still restore the paused deploy labels."""
+    c = _cluster("all-cpx")
+    c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "dp-stuck", "namespace": "gpu",
+                                                               "labels": {"app": "amd-device-plugin-daemonset"}},
+              "spec": {"nodeName": "n1"}})
+    m = _mgr(c, spx, cfg, tmp_path)
+    m.pods_timeout = 0.3
+    assert m.reconcile() == "failed"
+    labels = o.get_labels(c.get("v1", "Node", "n1"))
+    assert labels["amd.com/gpu.deploy.device-plugin"] == "true"
+    assert labels["amd.com/gpu.deploy.metrics-exporter"] == "true"
+    assert labels["amd.com/gpu.deploy.rdc"] == "false"
+    assert "still running" in [e for e in c.events if e["reason"] == "PartitionFailed"][0]["message"]
+
+
+def test_partition_restores_labels_a_crashed_run_left_paused(spx, cfg, tmp_path):
+    c = _cluster("all-spx")
+    c.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.deploy.device-plugin": pm.PAUSED}}})
+    assert _mgr(c, spx, cfg, tmp_path).reconcile() == "in-sync"
+    assert o.get_labels(c.get("v1", "Node", "n1"))["amd.com/gpu.deploy.device-plugin"] == "true"
+
+
+def test_partition_nps_change_reloads_the_driver(spx, cfg, tmp_path):
+    """NPS1 -> NPS2: memory modes written, then amdgpu reloaded (reload-required -> reloading),
+    then the compute modes, then re-enumeration; clients paused throughout and restored."""
+    c = _cluster("all-cpx")
+    order, states = [], []
+    c.watch("v1", "Node", lambda ev: states.append(o.get_labels(ev.obj).get(pm.STATE_LABEL)))
+    real_set = D.set_partition
+
+    def spy_set(bdf, kind, mode, root=None):
+        order.append(kind)
+        real_set(bdf, kind, mode, root=root)
+
+    def reload():
+        order.append("reload")
+        dp = o.get_labels(c.get("v1", "Node", "n1"))["amd.com/gpu.deploy.device-plugin"]
+        assert dp == pm.PAUSED                         # no GPU client across the reload
+    import unittest.mock as um
+    with um.patch.object(pm.devices, "set_partition", spy_set):
+        m = _mgr(c, spx, cfg, tmp_path, reload_driver=reload,
+                 reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS2"))
+        assert m.reconcile() == "applied"
+    assert order.index("reload") > max(i for i, k in enumerate(order) if k == "memory")
+    assert order.index("reload") < min(i for i, k in enumerate(order) if k == "compute")
+    assert order.count("reload") == 1 and order.count("memory") == 8
+    seen = [s for i, s in enumerate(states) if s and (i == 0 or states[i - 1] != s)]
+    assert seen[:4] == ["pending", "reload-required", "reloading", "success"], seen
+    assert o.get_labels(c.get("v1", "Node", "n1"))["amd.com/gpu.deploy.device-plugin"] == "true"
+
+
+def test_partition_compute_only_change_needs_no_reload(spx, cfg, tmp_path):
+    cfgd = yaml.safe_load(open(cfg))
+    cfgd["partition-configs"]["cpx-nps1"] = [{"devices": "all", "compute": "CPX", "memory": "NPS1"}]
+    open(cfg, "w").write(yaml.safe_dump(cfgd))
+    reloads = []
+    m = _mgr(_cluster("cpx-nps1"), spx, cfg, tmp_path, reload_driver=lambda: reloads.append(1),
+             reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS1"))
+    assert m.reconcile() == "applied" and reloads == []
+
+
+def test_partition_reload_failure_fails_and_restores_clients(spx, cfg, tmp_path):
+    c = _cluster("all-cpx")
+    calls = []
+
+    def run(argv, **kw):
+        calls.append(argv)
+        import subprocess as sp
+        return sp.CompletedProcess(argv, 1 if "-r" in argv else 0, "", "modprobe: FATAL: Module amdgpu is in use.")
+    m = _mgr(c, spx, cfg, tmp_path, run=run)
+    m.reload_driver = m._reload_driver                   # the real modprobe sequence, faked run()
+    assert m.reconcile() == "failed"
+    assert calls[0] == ["chroot", "/host", "modprobe", "-r", "amdgpu"] and len(calls) == 1
+    labels = o.get_labels(c.get("v1", "Node", "n1"))
+    assert labels[pm.STATE_LABEL] == "failed" and labels["amd.com/gpu.deploy.device-plugin"] == "true"
+    msg = [e for e in c.events if e["reason"] == "PartitionFailed"][0]["message"]
+    assert "in use" in msg and "modprobe -r amdgpu" in msg
+
+
+def test_partition_reload_cmd_override(spx, cfg, tmp_path):
+    calls = []
+    import subprocess as sp
+    m = _mgr(_cluster("all-cpx"), spx, cfg, tmp_path, run=lambda argv, **kw: (calls.append(argv),
+                                                                             sp.CompletedProcess(argv, 0))[1],
+             reload_cmd="chroot /host /usr/local/bin/amdgpu-reload --nps; true",
+             reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS2"))
+    m.reload_driver = m._reload_driver
+    assert m.reconcile() == "applied"
+    assert calls == [["chroot", "/host", "/usr/local/bin/amdgpu-reload", "--nps"], ["true"]]
+
+
+def test_partition_driver_not_live_after_reload_fails(spx, cfg, tmp_path):
+    from pathlib import Path
+    c = _cluster("all-cpx")
+
+    def reload_broken():
+        (Path(spx) / "sys/module/amdgpu/initstate").write_text("coming\n")
+    m = _mgr(c, spx, cfg, tmp_path, reload_driver=reload_broken)
+    m.reload_timeout = 0.5
+    assert m.reconcile() == "failed"
+    assert "did not come back live" in [e for e in c.events if e["reason"] == "PartitionFailed"][0]["message"]
+    assert o.get_labels(c.get("v1", "Node", "n1"))["amd.com/gpu.deploy.device-plugin"] == "true"
 
 
 # -- metrics exporter ------------------------------------------------------------------------------
