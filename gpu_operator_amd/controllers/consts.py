@@ -85,6 +85,14 @@ PARTITION_DISABLED_CONFIG = "spx-nps1"
 # --- operator namespace handling --------------------------------------------------------------
 OCP_SUGGESTED_NAMESPACE = "amd-gpu-operator"
 OCP_MONITORING_LABEL = "openshift.io/cluster-monitoring"
+# OpenShift cluster proxy with a user CA bundle (reference: object_controls.go:53-60, 931-961):
+# the Cluster Network Operator fills a ConfigMap labelled inject-trusted-cabundle, which the
+# driver container mounts where RHEL's ca-trust looks for the extracted PEM bundle.
+TRUSTED_CA_CONFIGMAP = "amd-gpu-operator-trusted-ca"
+TRUSTED_CA_INJECT_LABEL = "config.openshift.io/inject-trusted-cabundle"
+TRUSTED_CA_BUNDLE_KEY = "ca-bundle.crt"
+TRUSTED_CA_MOUNT_DIR = "/etc/pki/ca-trust/extracted/pem"
+TRUSTED_CA_CERT_FILE = "tls-ca-bundle.pem"
 POD_SECURITY_PREFIX = "pod-security.kubernetes.io/"
 POD_SECURITY_MODES = ("enforce", "audit", "warn")
 

@@ -190,6 +190,7 @@ class StateManager:
         self.dtk_requested = False
         self._dtk_enabled = False
         self._proxy: Dict[str, str] = {}
+        self._proxy_trusted_ca = ""
         # current fan-out variant
         self.current_kernel: Optional[str] = None
         self.current_rhcos: Optional[str] = None
@@ -287,8 +288,12 @@ class StateManager:
             self._proxy = {k: v for k, v in (("HTTP_PROXY", spec.get("httpProxy")),
                                               ("HTTPS_PROXY", spec.get("httpsProxy")),
                                               ("NO_PROXY", spec.get("noProxy"))) if v}
+            self._proxy_trusted_ca = ((spec.get("trustedCA") or {}).get("name") or "") if self.openshift else ""
         except (errors.NotFound, errors.NoKindMatch):
             self._proxy = {}
+            self._proxy_trusted_ca = ""
+        if self._proxy_trusted_ca:
+            self.ensure_trusted_ca_configmap()
         if self.namespace == C.OCP_SUGGESTED_NAMESPACE:
             ns = self.client.get("v1", "Namespace", self.namespace)
             if C.OCP_MONITORING_LABEL not in o.get_labels(ns):
@@ -417,6 +422,30 @@ class StateManager:
 
     def cluster_proxy(self) -> Dict[str, str]:
         return dict(self._proxy)
+
+    def trusted_ca_configmap(self) -> str:
+        """Name of the CA-bundle ConfigMap the driver container mounts ("" without a proxy CA)."""
+        return C.TRUSTED_CA_CONFIGMAP if self._proxy_trusted_ca else ""
+
+    def ensure_trusted_ca_configmap(self) -> None:
+        """Get-or-create the ConfigMap the cluster network operator injects the proxy's CA bundle
+        into (reference: getOrCreateTrustedCAConfigMap, object_controls.go:971-1010). Never
+        updated afterwards: its data belongs to the injector."""
+        try:
+            self.client.get("v1", "ConfigMap", C.TRUSTED_CA_CONFIGMAP, self.namespace)
+            return
+        except errors.NotFound:
+            pass
+        cm = {"apiVersion": "v1", "kind": "ConfigMap",
+              "metadata": {"name": C.TRUSTED_CA_CONFIGMAP, "namespace": self.namespace,
+                           "labels": {C.TRUSTED_CA_INJECT_LABEL: "true"}},
+              "data": {C.TRUSTED_CA_BUNDLE_KEY: ""}}
+        o.set_controller_reference(self.owner, cm)
+        try:
+            self.client.create(cm)
+            log.info("created trusted CA bundle ConfigMap %s/%s", self.namespace, C.TRUSTED_CA_CONFIGMAP)
+        except errors.AlreadyExists:
+            pass
 
     def node_os_tag(self) -> str:
         if self.current_os:

@@ -254,6 +254,12 @@ def transform_driver(obj: Obj, spec: cp.ClusterPolicySpec, n) -> None:
         proxy = n.cluster_proxy()
         for k, v in proxy.items():
             o.set_env(c, k, v)
+        ca = n.trusted_ca_configmap() if hasattr(n, "trusted_ca_configmap") else ""
+        if ca:
+            # the proxy's user CA bundle, where the driver container's package manager trusts it
+            o.add_volume(obj, {"name": ca, "configMap": {"name": ca, "items": [
+                {"key": C.TRUSTED_CA_BUNDLE_KEY, "path": C.TRUSTED_CA_CERT_FILE}]}})
+            o.add_volume_mount(c, {"name": ca, "mountPath": C.TRUSTED_CA_MOUNT_DIR, "readOnly": True})
     apply_variant_identity(obj, n)
 
 

@@ -517,3 +517,50 @@ def test_watch_driven_controller_converges_without_timers():
         sim.sync()
     ctl.drain()
     assert c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")["status"]["state"] == "ready"
+
+
+# ------------------------------------------------------------------------------ OpenShift proxy CA
+def _ocp_cluster(trusted_ca="user-ca-bundle"):
+    c = cluster([gpu_node("a", os_id="rhel", os_ver="9.4")])
+    c.create({"apiVersion": "config.openshift.io/v1", "kind": "ClusterVersion", "metadata": {"name": "version"},
+              "status": {"desired": {"version": "4.16.3"}}})
+    px = {"apiVersion": "config.openshift.io/v1", "kind": "Proxy", "metadata": {"name": "cluster"},
+          "spec": {"httpsProxy": "http://proxy.corp:3128", "noProxy": ".cluster.local"}}
+    if trusted_ca:
+        px["spec"]["trustedCA"] = {"name": trusted_ca}
+    c.create(px)
+    return c
+
+
+def test_ocp_proxy_trusted_ca_configmap_and_driver_mount():
+    """reference: object_controls.go:908-1010 (applyOCPProxySpec, getOrCreateTrustedCAConfigMap)."""
+    c = _ocp_cluster()
+    reconcile_once(c)
+    cm = c.get("v1", "ConfigMap", C.TRUSTED_CA_CONFIGMAP, NS)
+    assert o.get_labels(cm)[C.TRUSTED_CA_INJECT_LABEL] == "true"
+    assert cm["data"] == {C.TRUSTED_CA_BUNDLE_KEY: ""}
+    cpol = c.get("amd.com/v1", "ClusterPolicy", "cluster-policy")
+    assert o.owned_by(cm, cpol["metadata"]["uid"])
+    ds = [d for d in c.list("apps/v1", "DaemonSet", NS) if o.name(d).startswith(C.DS_DRIVER)][0]
+    drv = container(ds, "amdgpu-driver-ctr")
+    e = env(drv)
+    assert e["HTTPS_PROXY"] == "http://proxy.corp:3128" and e["NO_PROXY"] == ".cluster.local"
+    mounts = {m["name"]: m for m in drv["volumeMounts"]}
+    assert mounts[C.TRUSTED_CA_CONFIGMAP]["mountPath"] == C.TRUSTED_CA_MOUNT_DIR
+    vols = {v["name"]: v for v in ds["spec"]["template"]["spec"]["volumes"]}
+    assert vols[C.TRUSTED_CA_CONFIGMAP]["configMap"]["items"] == [{"key": "ca-bundle.crt", "path": "tls-ca-bundle.pem"}]
+    # the injector owns the data: a filled bundle survives further reconciles
+    cm["data"][C.TRUSTED_CA_BUNDLE_KEY] = "-----BEGIN CERTIFICATE-----\n..."
+    c.update(cm)
+    reconcile_once(c)
+    assert c.get("v1", "ConfigMap", C.TRUSTED_CA_CONFIGMAP, NS)["data"][C.TRUSTED_CA_BUNDLE_KEY].startswith("-----BEGIN")
+
+
+def test_ocp_proxy_without_trusted_ca_sets_env_only():
+    c = _ocp_cluster(trusted_ca=None)
+    reconcile_once(c)
+    assert not [x for x in c.list("v1", "ConfigMap", NS) if o.name(x) == C.TRUSTED_CA_CONFIGMAP]
+    ds = [d for d in c.list("apps/v1", "DaemonSet", NS) if o.name(d).startswith(C.DS_DRIVER)][0]
+    drv = container(ds, "amdgpu-driver-ctr")
+    assert env(drv)["HTTPS_PROXY"] == "http://proxy.corp:3128"
+    assert C.TRUSTED_CA_CONFIGMAP not in {m["name"] for m in drv.get("volumeMounts", [])}
