@@ -37,6 +37,7 @@ def main(argv=None) -> int:
     ap.add_argument("--zap-time-encoding", default="iso8601")
     ap.add_argument("--zap-devel", action="store_true")
     ap.add_argument("--kubeconfig", default=None)
+    ap.add_argument("--no-cache", action="store_true", help="read from the API server on every access (debugging)")
     a = ap.parse_args(argv)
 
     level = {"debug": logging.DEBUG, "info": logging.INFO, "error": logging.ERROR}.get(a.zap_log_level, logging.INFO)
@@ -55,12 +56,16 @@ def main(argv=None) -> int:
     from ..controllers.state_manager import SnapshotHolder
     from ..controllers.upgrade_controller import UpgradeReconciler
     from ..k8s.rest import Config, RestClient
+    from ..runtime.cache import CachedClient
     from ..runtime.manager import Manager
 
     cfg = Config.from_kubeconfig(a.kubeconfig) if a.kubeconfig else Config.auto()
-    client = RestClient(cfg)
+    api = RestClient(cfg)
+    # reconcilers read through informers (reference: main.go:104, the manager's cached client);
+    # leader election keeps reading Leases from the API server itself
+    client = api if a.no_cache else CachedClient(api)
     metrics = OperatorMetrics()
-    mgr = Manager(client, namespace, registry=metrics.registry, metrics_addr=a.metrics_bind_address,
+    mgr = Manager(api, namespace, registry=metrics.registry, metrics_addr=a.metrics_bind_address,
                   probe_addr=a.health_probe_bind_address, leader_elect=a.leader_elect,
                   lease_duration=parse_duration(a.leader_lease_duration),
                   renew_deadline=parse_duration(a.leader_lease_renew_deadline),

@@ -62,7 +62,11 @@ def spec_hash(obj: Obj) -> str:
 
 
 def _delete(n, obj: Obj) -> None:
+    """Delete the object of a disabled state if it exists. The existence check is a cache read
+    under the informer cache (runtime/cache.py), so a steady pass over disabled states writes
+    nothing, where the reference issues a blind DELETE per object per pass."""
     try:
+        n.client.get(obj["apiVersion"], obj["kind"], o.name(obj), o.namespace(obj))
         n.client.delete(obj["apiVersion"], obj["kind"], o.name(obj), o.namespace(obj))
         log.info("deleted %s/%s (state disabled)", obj["kind"], o.name(obj))
     except errors.NotFound:
