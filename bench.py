@@ -25,7 +25,9 @@ the median / p90. The same protocol is then applied, in the same process, to
 ``torch.matmul`` on the same operands (hipBLASLt) so ``ratio_vs_hipblaslt`` is checkable.
 
 After the timed region the job also reports the fp8 kernel at the same shape, the RCCL
-all-reduce bus bandwidth over xGMI (N>1), and the validator's per-GPU check chain.
+all-reduce bus bandwidth over xGMI (N>1), the validator's per-GPU check chain and (N=1) the
+node time-to-ready measured on real processes for this framework's operand chain and for the
+reference's protocol constants in the same harness (gpu_operator_amd/validator/ttr.py).
 """
 
 from __future__ import annotations
@@ -182,6 +184,8 @@ def main(argv=None) -> int:
             extras.update(_fp8_extra(ctx))
         if distributed:
             extras.update(_allreduce_extra(ctx))
+        if world == 1 and not cpu:
+            extras.update(_time_to_ready_extra())
 
     if rank == 0:
         shape = f"{m}^3" if m == n == k else f"{m}x{n}x{k}"
@@ -343,6 +347,29 @@ def _fp8_extra(ctx):
     per_gpu = G.tflops(m, n, k, res["elapsed_s"] / steps)
     return {"fp8_per_gpu_tflops": _r(per_gpu), "fp8_total_tflops": _r(per_gpu * ctx.world),
             "fp8_check_ok": chk.ok, "fp8_steps": steps, "fp8_step_ms_median": res["median_ms"]}
+
+
+def _time_to_ready_extra():
+    """Node time-to-ready on real processes (validator/ttr.py), outside the timed region: this
+    framework's operand chain vs the reference's protocol constants executed in the same
+    harness (host driver, HIP GEMM validation on this GPU)."""
+    try:
+        from gpu_operator_amd.validator import ttr
+        r = ttr.run_both(hip_mode="local", gemm_shapes="8192", timeout=180)
+    except Exception as e:  # noqa: BLE001 - an extra must never fail the bench
+        return {"time_to_ready_error": str(e)[:300]}
+    ours, ref = r["ours"], r["reference"]
+    out = {"agent_chain_time_to_ready_s": r["agent_chain_time_to_ready_s"],
+           "reference_protocol_time_to_ready_s": r["reference_protocol_time_to_ready_s"],
+           "time_to_ready_barriers_s": ours["barriers_s"],
+           "reference_protocol_barriers_s": ref["barriers_s"]}
+    if out["agent_chain_time_to_ready_s"] and out["reference_protocol_time_to_ready_s"]:
+        out["time_to_ready_speedup"] = round(out["reference_protocol_time_to_ready_s"]
+                                             / out["agent_chain_time_to_ready_s"], 2)
+    errs = ours["errors"] + ref["errors"]
+    if errs:
+        out["time_to_ready_errors"] = "; ".join(errs)[:300]
+    return out
 
 
 def _allreduce_extra(ctx):

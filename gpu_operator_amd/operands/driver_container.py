@@ -227,7 +227,8 @@ def main(argv=None, stop: Optional[threading.Event] = None, dc: Optional[DriverC
     ap = argparse.ArgumentParser(prog="amdgpu-driver")
     ap.add_argument("command", choices=["init", "probe", "load-only"])
     a = ap.parse_args(argv)
-    dc = dc or DriverContainer(sys_root=os.environ.get("AMD_SYSFS_ROOT", "/"))
+    dc = dc or DriverContainer(sys_root=os.environ.get("AMD_SYSFS_ROOT", "/"),
+                               dev_root=os.environ.get("AMD_DEV_ROOT", "/"))
     if a.command == "probe":
         ok, why = dc.ready()
         print(why)

@@ -60,12 +60,21 @@ class Context:
     env: Dict[str, str] = field(default_factory=lambda: dict(os.environ))
     run: Callable[..., subprocess.CompletedProcess] = subprocess.run
     clock: Callable[[], float] = time.monotonic
+    # VALIDATOR_WAIT_MODE=poll: wait the way the reference validator does -- fixed
+    # sleep_interval polls for barriers, node capacity and workload pods
+    # (reference validator/main.go:127,556-572,1042-1059,1102-1122). Used by the node bring-up
+    # harness (ttr.py) to execute the reference protocol; production waits are event-driven.
+    poll_mode: bool = False
+
+    def __post_init__(self):
+        if self.env.get("VALIDATOR_WAIT_MODE", "") == "poll":
+            self.poll_mode = True
 
 
 def retry(ctx: Context, what: str, fn: Callable[[], Any]) -> Any:
     """Run ``fn`` once, or until it stops raising (bounded by ctx.wait_timeout) in wait mode."""
     deadline = ctx.clock() + ctx.wait_timeout
-    delay = 0.2
+    delay = ctx.sleep_interval if ctx.poll_mode else 0.2
     while True:
         try:
             return fn()
@@ -75,6 +84,18 @@ def retry(ctx: Context, what: str, fn: Callable[[], Any]) -> Any:
             log.info("%s not ready (%s); retrying in %.1fs", what, e, delay)
             time.sleep(delay)
             delay = min(ctx.sleep_interval, delay * 2)
+
+
+def wait_barriers(ctx: Context, names, timeout: Optional[float]) -> bool:
+    """Event-driven (inotify) barrier wait; a fixed-period stat loop in poll mode."""
+    if not ctx.poll_mode:
+        return bool(ctx.status.wait(names, timeout=timeout))
+    deadline = None if timeout is None else ctx.clock() + timeout
+    while not all(ctx.status.exists(n) for n in names):
+        if deadline is not None and ctx.clock() >= deadline:
+            return False
+        time.sleep(ctx.sleep_interval)
+    return True
 
 
 # ---------------------------------------------------------------------------------------------
@@ -122,7 +143,7 @@ def validate_driver(ctx: Context) -> Dict[str, Any]:
         if not ctx.status.exists(S.DRIVER_CTR_READY):
             if not ctx.with_wait:
                 raise ValidationError("driver container not ready (.driver-ctr-ready missing)")
-            if not ctx.status.wait([S.DRIVER_CTR_READY], timeout=t):
+            if not wait_barriers(ctx, [S.DRIVER_CTR_READY], t):
                 raise ValidationError("timed out waiting for the driver container")
     info = retry(ctx, "driver", lambda: check_driver(ctx))
     info["mode"] = "host" if host else "container"
@@ -180,12 +201,38 @@ def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
     return out
 
 
+def _run_local_hip(ctx: Context) -> List[Dict[str, Any]]:
+    """The HIP workload in this process's container (HIP_VALIDATION_MODE=local)."""
+    from .workload_main import run_hip
+    t0 = ctx.clock()
+    results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run,
+                      dtype=ctx.env.get("GEMM_DTYPE", "bf16"))
+    if ctx.poll_mode:
+        # the reference spawns the workload pod and polls its phase every sleep_interval, first
+        # right after creating it (validator/main.go:1042-1059): it sees the result at the
+        # first tick after completion
+        ticks = max(1, int(-(-(ctx.clock() - t0) // ctx.sleep_interval)))
+        time.sleep(max(0.0, t0 + ticks * ctx.sleep_interval - ctx.clock()))
+    return results
+
+
+def _local_workload(ctx: Context, mode: str) -> Dict[str, Any]:
+    if mode == "skip":
+        return {"skipped": True}
+    info = summarize_gemm(_run_local_hip(ctx))
+    if [r for r in info["gemm"] if not r.get("ok")] or info.get("smoke_ok") is False:
+        raise ValidationError(f"plugin workload failed: {info}")
+    return info
+
+
 def validate_hip(ctx: Context) -> Dict[str, Any]:
     mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
+    if mode == "skip":                  # no GPU work (CPU rehearsals of the node bring-up)
+        info = {"skipped": True}
+        ctx.status.create(S.HIP_READY, info)
+        return info
     if mode == "local":
-        from .workload_main import run_hip
-        results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run,
-                          dtype=ctx.env.get("GEMM_DTYPE", "bf16"))
+        results = _run_local_hip(ctx)
     else:
         res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
                                  _validator_env(ctx), timeout=ctx.pod_timeout)
@@ -217,6 +264,15 @@ def gpu_resources(node: Dict[str, Any], strategy: str) -> Dict[str, int]:
 
 def wait_gpu_resources(ctx: Context) -> Dict[str, int]:
     """Watch the Node (event-driven) until it advertises GPU resources, bounded."""
+    if ctx.poll_mode:
+        deadline = ctx.clock() + ctx.resource_timeout
+        while True:
+            r = gpu_resources(ctx.client.get("v1", "Node", ctx.node_name), ctx.partition_strategy)
+            if r:
+                return r
+            if ctx.clock() >= deadline:
+                raise ValidationError(f"no {GPU_RESOURCE} resources on node {ctx.node_name}")
+            time.sleep(ctx.sleep_interval)
     done = threading.Event()
     found: Dict[str, int] = {}
 
@@ -248,11 +304,15 @@ def validate_plugin(ctx: Context) -> Dict[str, Any]:
     res = wait_gpu_resources(ctx)
     info: Dict[str, Any] = {"resources": res, "devices": sum(res.values())}
     if ctx.with_workload:
-        # prefer a partition resource (like the reference prefers MIG), else one whole GPU
-        name = next((k for k in sorted(res) if k.startswith(PARTITION_RESOURCE_PREFIX)), GPU_RESOURCE)
-        out = W.run_workload_pod(ctx.client, "plugin-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                                 _validator_env(ctx), timeout=ctx.pod_timeout, gpu_limit={name: 1})
-        info["workload"] = summarize_gemm(out["results"])
+        mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
+        if mode in ("local", "skip"):
+            info["workload"] = _local_workload(ctx, mode)
+        else:
+            # prefer a partition resource (like the reference prefers MIG), else one whole GPU
+            name = next((k for k in sorted(res) if k.startswith(PARTITION_RESOURCE_PREFIX)), GPU_RESOURCE)
+            out = W.run_workload_pod(ctx.client, "plugin-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                                     _validator_env(ctx), timeout=ctx.pod_timeout, gpu_limit={name: 1})
+            info["workload"] = summarize_gemm(out["results"])
     ctx.status.create(S.PLUGIN_READY, info)
     return info
 
@@ -274,11 +334,26 @@ def summarize_rccl(results: List[Dict[str, Any]]) -> Dict[str, Any]:
             and fabric.get("ok", True) is not False}
 
 
+def _run_rccl_local(ctx: Context, ngpu: int) -> List[Dict[str, Any]]:
+    from .workload_main import run_rccl
+    ranks = ctx.env.get("RCCL_RANKS") or ",".join(str(n) for n in (2, 4, 8) if n <= ngpu) or str(ngpu)
+    mb = float(ctx.env.get("RCCL_MIN_BUSBW_GBPS", "0") or 0)
+    return run_rccl(int(ctx.env.get("RCCL_MAX_BYTES", 1 << 26)), ctx.env.get("RCCL_DTYPE", "bf16"), ranks=ranks,
+                    min_busbw=mb or None)
+
+
 def validate_rccl(ctx: Context) -> Dict[str, Any]:
     node = ctx.client.get("v1", "Node", ctx.node_name)
     ngpu = int(((node.get("status") or {}).get("allocatable") or {}).get(GPU_RESOURCE, 0) or 0)
     if ngpu < 2:
         info = {"skipped": f"{ngpu} GPU(s) allocatable: no fabric to validate", "ok": True}
+        ctx.status.create(S.RCCL_READY, info)
+        return info
+    if ctx.env.get("HIP_VALIDATION_MODE", "pod") in ("local", "skip"):
+        info = {"skipped": f"{ngpu} GPU(s); local mode"} if ctx.env.get("HIP_VALIDATION_MODE") == "skip" else \
+            summarize_rccl(_run_rccl_local(ctx, ngpu))
+        if not info.get("skipped") and not info["ok"]:
+            raise ValidationError(f"RCCL all-reduce validation failed: {info}")
         ctx.status.create(S.RCCL_READY, info)
         return info
     env = _validator_env(ctx)

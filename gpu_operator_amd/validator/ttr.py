@@ -1,53 +1,111 @@
-"""Node time-to-ready: the bring-up chain of one GPU node, measured end to end.
+"""Node time-to-ready, measured on real processes: the bring-up of one GPU node from "operand
+pods scheduled" to "validator Ready", run twice in the same harness -- once with this
+framework's protocol and once with the reference's protocol constants executed.
 
-BASELINE.json's metric is "node time-to-ready (driver -> validator)". This harness runs the
-REAL node-side components of this framework concurrently, the way their DaemonSet pods start
-together on a fresh node, and wires them only through what they use in production — the
-barrier directory (inotify waits), a Kubernetes API (in-process fake), the kubelet device-plugin
-gRPC API (an in-process fake kubelet that registers plugins and mirrors ListAndWatch into the
-Node's capacity) and the GPUs themselves:
+BASELINE.json's metric is "node time-to-ready (driver -> validator)"; the reference's timing
+envelope is the sum of its fixed sleeps, 5 s polls and crash-loop back-offs.
 
-    validator      driver check -> toolkit check -> HIP smoke + MFMA GEMM (real GPU) -> plugin
-                   (event-driven wait for amd.com/gpu capacity) -> rccl (>=2 GPUs) -> ready
-    toolkit        waits driver-ready -> amd-ctk install (runtime shim + config edit)
-    device plugin  waits toolkit-ready -> discovers KFD agents -> registers -> ListAndWatch
-    labeller       waits toolkit-ready -> labels the Node
-    exporter       waits toolkit-ready -> first scrape
+What is real
+  * every container is its own OS process started through its console-script name
+    (``amd-validator``, ``amd-ctk``, ``amd-device-plugin``, ``amd-node-labeller``,
+    ``amd-metrics-exporter``: one-line wrappers on PATH around cmd/entry.py), init containers
+    run in order, main containers concurrently;
+  * the entrypoint scripts are the ConfigMap scripts of this repo's assets, run by ``sh`` with
+    their hostPath volumes mapped to the harness's directories; init gates are the native
+    ``amd-barrier-wait`` binary (inotify);
+  * the agents talk to a Kubernetes API over HTTP (the in-process API server of k8s/apiserver.py,
+    through RestClient and a kubeconfig) and to a kubelet device-plugin gRPC endpoint (a fake
+    kubelet that registers plugins and mirrors ListAndWatch into the Node's capacity, as kubelet
+    does); the device plugin, labeller and exporter read the GPUs through libamdnode, and the
+    validator's HIP check runs the MFMA GEMM probe on the GPU (``HIP_VALIDATION_MODE=local``;
+    ``skip`` on CPU-only rehearsals).
 
-The host's amdgpu driver is used (the reference's host-driver mode); the
-driver container's own load time is not part of this measurement.
+What is simulated (identically for both protocols)
+  * the container runtime: pods with ``runtimeClassName`` (validator, device plugin, labeller,
+    exporter) cannot start until ``amd-ctk install`` has put the runtime handler into the
+    (harness-local) containerd config -- the kubelet retries sandbox creation every
+    KUBELET_SYNC_S; a failing init container restarts with kubelet's crash-loop back-off;
+  * the host driver is already live (the box's preinstalled amdgpu: the reference's host-driver
+    mode), so the driver DaemonSet's module load is not part of the measurement; its startup
+    probe ``amdgpu-driver probe`` still gates ``.driver-ctr-ready`` in the ``driver-container``
+    scenario.
 
-The same measured step durations are then fed to a model of the reference's chain with its
-fixed constants: 5 s barrier polling in init containers, the 5 s
-toolkit sleep, toolkit validation by crash-loop back-off (10 s, 20 s, ...), 5 s polls for the
-CUDA workload pod and for GPU capacity, the device plugin's 5 s poll for toolkit-ready.
+The reference protocol (host driver), from its assets and validator: init gates poll every 5 s
+(assets/state-device-plugin/0500_daemonset.yaml:31), the toolkit entrypoint sleeps 5 s
+(assets/state-container-toolkit/0400_configmap.yaml:34), the device-plugin entrypoint polls for
+the driver barrier every 5 s (assets/state-device-plugin/0400_configmap.yaml:9-36), the validator
+retries with 5 s sleeps and polls workload pods and node capacity every 5 s
+(validator/main.go:127,556-572,1042-1059,1102-1122), toolkit validation runs without wait
+(crash-loop back-off), and plugin validation runs a second workload (WITH_WORKLOAD=true). The
+driver container's startup probe starts after 60 s and repeats every 10 s
+(assets/state-driver/0500_daemonset.yaml:132-140). Here those constants are executed by our own
+agents in the reference's wait mode (``VALIDATOR_WAIT_MODE=poll``), not modelled.
 """
 
 from __future__ import annotations
 
 import json
 import logging
-import math
 import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
 import tempfile
 import threading
 import time
 from concurrent import futures
+from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
-from .. import devices
-from ..k8s.fake import FakeClient
-from . import components as Cm
+import yaml
+
 from . import status as S
 
 log = logging.getLogger("amd-ttr")
 
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ASSETS = os.path.join(REPO, "gpu_operator_amd", "assets")
+NATIVE_BIN = os.path.join(REPO, "gpu_operator_amd", "_native", "bin")
 
+KUBELET_SYNC_S = 1.0                              # harness kubelet: sandbox-creation retry period
+CRASHLOOP_BACKOFF_S = [10.0, 20.0, 40.0, 80.0, 160.0, 300.0]   # kubelet container restart back-off
+NODE = "ttr-node"
+NAMESPACE = "amd-gpu-operator"
+
+
+@dataclass
+class Ctr:
+    name: str
+    argv: List[str]
+    env: Dict[str, str] = field(default_factory=dict)
+
+
+@dataclass
+class Probe:
+    argv: List[str]
+    initial_delay: float
+    period: float
+
+
+@dataclass
+class Pod:
+    name: str
+    inits: List[Ctr]
+    mains: List[Ctr]
+    runtime_class: bool = False
+    startup_probe: Optional[Probe] = None
+
+
+# ---------------------------------------------------------------------------------------------
+# kubelet-side fakes
+# ---------------------------------------------------------------------------------------------
 class FakeKubelet:
-    """Registration server + a ListAndWatch client per registered plugin that mirrors the
-    healthy device count into the Node's capacity/allocatable (what kubelet does)."""
+    """Device-plugin registration server + a ListAndWatch client per registered plugin that
+    mirrors the healthy device count into the Node's capacity/allocatable (what kubelet does)."""
 
-    def __init__(self, plugin_dir: str, client, node: str):
+    def __init__(self, plugin_dir: str, client, node: str, on_event=None):
         import grpc
         from ..operands import kubeletapi as K
         self.K = K
@@ -55,233 +113,386 @@ class FakeKubelet:
         self.plugin_dir = plugin_dir
         self.client = client
         self.node = node
+        self.on_event = on_event or (lambda name: None)
         self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=4))
         self.server.add_generic_rpc_handlers((K.registration_handler(self._on_register),))
         self.server.add_insecure_port("unix://" + os.path.join(plugin_dir, "kubelet.sock"))
-        self.threads: List[threading.Thread] = []
         self._stop = threading.Event()
 
     def start(self):
         self.server.start()
 
     def _on_register(self, req):
-        t = threading.Thread(target=self._watch, args=(req.endpoint, req.resource_name), daemon=True)
-        t.start()
-        self.threads.append(t)
+        self.on_event(f"kubelet:registered:{req.resource_name}")
+        threading.Thread(target=self._watch, args=(req.endpoint, req.resource_name), daemon=True).start()
 
     def _watch(self, endpoint: str, resource: str):
         K = self.K
-        with self.grpc.insecure_channel("unix://" + os.path.join(self.plugin_dir, endpoint)) as ch:
-            stream = K.device_plugin_stub(ch)["ListAndWatch"](K.DP["Empty"]())
-            for resp in stream:
-                n = sum(1 for d in resp.devices if d.health == K.HEALTHY)
-                self.client.patch("v1", "Node", self.node, {"status": {"capacity": {resource: str(n)},
-                                                                       "allocatable": {resource: str(n)}}})
-                if self._stop.is_set():
-                    stream.cancel()
-                    break
+        try:
+            with self.grpc.insecure_channel("unix://" + os.path.join(self.plugin_dir, endpoint)) as ch:
+                stream = K.device_plugin_stub(ch)["ListAndWatch"](K.DP["Empty"]())
+                for resp in stream:
+                    n = sum(1 for d in resp.devices if d.health == K.HEALTHY)
+                    self.client.patch("v1", "Node", self.node, {"status": {"capacity": {resource: str(n)},
+                                                                           "allocatable": {resource: str(n)}}})
+                    self.on_event(f"kubelet:capacity:{resource}={n}")
+                    if self._stop.is_set():
+                        stream.cancel()
+                        break
+        except Exception as e:  # noqa: BLE001 - the plugin went away at teardown
+            if not self._stop.is_set():
+                log.warning("ListAndWatch %s ended: %s", resource, e)
 
     def stop(self):
         self._stop.set()
         self.server.stop(0)
 
 
-def _node(name: str) -> Dict:
-    return {"apiVersion": "v1", "kind": "Node",
-            "metadata": {"name": name, "labels": {"feature.node.kubernetes.io/pci-1002.present": "true",
-                                                   "amd.com/gpu.present": "true"}},
-            "status": {"capacity": {}, "allocatable": {}}}
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def run_chain(workdir: Optional[str] = None, gemm_shapes: str = "8192", sys_root: str = "/",
-              dev_root: str = "/", hip_mode: str = "local", timeout: float = 300.0) -> Dict:
-    """Run the node chain once; returns timestamps relative to t0 and the step durations."""
-    from ..operands.device_plugin import Config as DPConfig, DevicePlugin
-    from ..operands.metrics_exporter import build_registry, load_fields
-    from ..operands.node_labeller import apply_node, compute_labels
-    from ..toolkit.ctk import Installer
-
-    wd = workdir or tempfile.mkdtemp(prefix="amd-ttr-")
-    vdir = os.path.join(wd, "validations")
-    pdir = os.path.join(wd, "device-plugins")
-    os.makedirs(pdir, exist_ok=True)
-    sd = S.StatusDir(vdir)
-    sd.ensure()
-    node = "ttr-node"
-    client = FakeClient([_node(node)])
-    kubelet = FakeKubelet(pdir, client, node)
-    kubelet.start()
-    marks: Dict[str, float] = {}
-    steps: Dict[str, float] = {}
-    errors: List[str] = []
-    lock = threading.Lock()
-
-    def mark(name: str, t: float):
-        with lock:
-            marks[name] = t
-
-    env = dict(os.environ, HIP_VALIDATION_MODE=hip_mode, GEMM_SHAPES=gemm_shapes, DRIVER_ROOT_MODE="host",
-               DRIVER_VALIDATION_STRICT="false")
-    ctx = Cm.Context(status=sd, node_name=node, namespace="amd-gpu-operator", client=client, host_root="/",
-                     sys_root=sys_root, dev_root=dev_root, with_wait=True, wait_timeout=timeout,
-                     resource_timeout=timeout, env=env)
-    plugin: Dict[str, DevicePlugin] = {}
-    t0 = time.monotonic()
-
-    def timed(name, fn):
-        s = time.monotonic()
-        r = fn()
-        steps[name] = time.monotonic() - s
-        mark(name, time.monotonic() - t0)
-        return r
-
-    def validator():
-        try:
-            timed("driver", lambda: Cm.validate_driver(ctx))
-            timed("toolkit_validation", lambda: (sd.wait([".toolkit-installed"], timeout=timeout),
-                                                 Cm.validate_toolkit(ctx)))
-            if hip_mode == "skip":      # CPU tests: no GPU work
-                timed("hip", lambda: sd.create(S.HIP_READY, {"skipped": True}))
-            else:
-                timed("hip", lambda: Cm.validate_hip(ctx))
-            timed("plugin_validation", lambda: Cm.validate_plugin(ctx))
-            ngpu = len({g["pci_bdf"] for g in devices.enumerate_gpus(sys_root)})   # KFD-visible GPUs
-            if ngpu >= 2 and hip_mode == "local":
-                from .workload_main import run_rccl
-                timed("rccl", lambda: run_rccl(64 << 20, "bf16"))
-            sd.create("validator-ready", {"ok": True})
-            mark("ready", time.monotonic() - t0)
-        except Exception as e:  # noqa: BLE001
-            errors.append(f"validator: {e}")
-            sd.create(".abort")
-
-    def toolkit():
-        try:
-            got = sd.wait([S.DRIVER_READY, S.HOST_DRIVER_READY, ".abort"], any_of=True, timeout=timeout)
-            if ".abort" in got or not got:
-                return
-            cfgf = os.path.join(wd, "containerd", "config.toml")
-            inst = Installer(root=os.path.join(wd, "usr-local-amd"), runtime="containerd", runtime_config=cfgf,
-                             runtime_socket=os.path.join(wd, "containerd.sock"), restart_mode="none",
-                             sys_root=sys_root, dev_root=dev_root)
-            timed("toolkit_install", inst.install)
-            sd.create(".toolkit-installed")
-        except Exception as e:  # noqa: BLE001
-            errors.append(f"toolkit: {e}")
-
-    def device_plugin():
-        try:
-            got = sd.wait([S.TOOLKIT_READY, ".abort"], any_of=True, timeout=timeout)
-            if S.TOOLKIT_READY not in got:
-                return
-
-            def start():
-                p = DevicePlugin(DPConfig.load(None, {}), root=sys_root, plugin_dir=pdir)
-                p.start(register=True)
-                plugin["p"] = p
-            timed("device_plugin_start", start)
-        except Exception as e:  # noqa: BLE001
-            errors.append(f"device-plugin: {e}")
-
-    def labeller():
-        try:
-            got = sd.wait([S.TOOLKIT_READY, ".abort"], any_of=True, timeout=timeout)
-            if S.TOOLKIT_READY not in got:
-                return
-            timed("labeller", lambda: apply_node(client, node, compute_labels(sys_root)))
-        except Exception as e:  # noqa: BLE001
-            errors.append(f"labeller: {e}")
-
-    def exporter():
-        try:
-            got = sd.wait([S.TOOLKIT_READY, ".abort"], any_of=True, timeout=timeout)
-            if S.TOOLKIT_READY not in got:
-                return
-            from prometheus_client import generate_latest
-            timed("exporter_first_scrape", lambda: generate_latest(build_registry(load_fields(None), sys_root)))
-        except Exception as e:  # noqa: BLE001
-            errors.append(f"exporter: {e}")
-
-    threads = [threading.Thread(target=f, daemon=True) for f in (validator, toolkit, device_plugin, labeller, exporter)]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join(timeout + 10)
-    if "p" in plugin:
-        plugin["p"].stop()
-    kubelet.stop()
-    barriers = {}
-    for b in (S.HOST_DRIVER_READY, S.DRIVER_READY, S.TOOLKIT_READY, S.HIP_READY, S.PLUGIN_READY, "validator-ready"):
-        p = sd.read(b)
-        if p and "ts" in p:
-            barriers[b] = p["ts"]
-    hip = sd.read(S.HIP_READY) or {}
-    return {"time_to_ready_s": marks.get("ready"), "marks_s": {k: round(v, 4) for k, v in sorted(marks.items(),
-                                                                                             key=lambda kv: kv[1])},
-            "steps_s": {k: round(v, 4) for k, v in steps.items()}, "errors": errors,
-            "gemm_tflops_per_gpu": hip.get("gemm_tflops_per_gpu"), "gpus": hip.get("gpus"),
-            "capacity": (client.get("v1", "Node", node).get("status") or {}).get("capacity")}
+def _asset_script(state: str, fname: str) -> str:
+    with open(os.path.join(ASSETS, state, fname)) as f:
+        return yaml.safe_load(f)["data"]["entrypoint.sh"]
 
 
 # ---------------------------------------------------------------------------------------------
-# the reference's chain, same step durations, its fixed delays and polling periods
+# the harness
 # ---------------------------------------------------------------------------------------------
-POLL = 5.0                 # init containers / --with-wait / capacity / workload pod (validator/main.go:127,159,163)
-TOOLKIT_SLEEP = 5.0        # assets/state-container-toolkit/0400_configmap.yaml:34
-BACKOFF = [10.0, 20.0, 40.0, 80.0, 160.0, 300.0]   # kubelet crash-loop back-off (toolkit validation)
-POD_START = 1.0            # container start of a spawned workload pod (image cached)
+class Harness:
+    def __init__(self, workdir: Optional[str] = None, sys_root: str = "/", dev_root: str = "/",
+                 hip_mode: str = "local", gemm_shapes: str = "8192", timeout: float = 240.0,
+                 scenario: str = "host-driver"):
+        if scenario not in ("host-driver", "driver-container"):
+            raise ValueError(f"unknown scenario {scenario!r}")
+        self.wd = workdir or tempfile.mkdtemp(prefix="amd-ttr-")
+        self.sys_root, self.dev_root = sys_root, dev_root
+        self.hip_mode, self.gemm_shapes, self.timeout, self.scenario = hip_mode, gemm_shapes, timeout, scenario
+        self.marks: Dict[str, float] = {}
+        self.restarts: Dict[str, int] = {}
+        self.errors: List[str] = []
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._procs: List[subprocess.Popen] = []
+
+    # -- bookkeeping -----------------------------------------------------------------------------
+    def mark(self, name: str) -> None:
+        with self._lock:
+            self.marks.setdefault(name, round(time.monotonic() - self.t0, 4))
+
+    def _setup(self, tag: str) -> None:
+        base = os.path.join(self.wd, tag)
+        shutil.rmtree(base, ignore_errors=True)
+        self.base = base
+        self.vdir = os.path.join(base, "validations")
+        self.pdir = os.path.join(base, "device-plugins")
+        self.amd_root = os.path.join(base, "usr-local-amd")
+        self.cfg = os.path.join(base, "containerd", "config.toml")
+        self.bin = os.path.join(base, "bin")
+        self.logs = os.path.join(base, "logs")
+        for d in (self.vdir, self.pdir, self.amd_root, os.path.dirname(self.cfg), self.bin, self.logs,
+                  os.path.join(base, "cdi")):
+            os.makedirs(d, exist_ok=True)
+        from ..cmd.entry import SCRIPTS
+        for name in SCRIPTS:
+            p = os.path.join(self.bin, name)
+            with open(p, "w") as f:
+                f.write(f'#!/bin/sh\nexec "{sys.executable}" -m gpu_operator_amd.cmd.entry {name} "$@"\n')
+            os.chmod(p, 0o755)
+        for name in ("amd-barrier-wait", "amd-hip-smoke", "amd-gemm-validate", "amd-rccl-validate"):
+            if os.path.exists(os.path.join(NATIVE_BIN, name)):
+                os.symlink(os.path.join(NATIVE_BIN, name), os.path.join(self.bin, name))
+        # the API server (HTTP) with this node, and a kubeconfig for the agents
+        from ..k8s.apiserver import FakeAPIServer
+        from ..k8s.fake import FakeClient
+        node = {"apiVersion": "v1", "kind": "Node",
+                "metadata": {"name": NODE, "labels": {"feature.node.kubernetes.io/pci-1002.present": "true",
+                                                      "amd.com/gpu.present": "true"}},
+                "status": {"capacity": {}, "allocatable": {}}}
+        ns = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NAMESPACE}}
+        self.backing = FakeClient([ns, node])
+        self.api = FakeAPIServer(self.backing).start()
+        self.kubeconfig = os.path.join(base, "kubeconfig")
+        with open(self.kubeconfig, "w") as f:
+            yaml.safe_dump({"apiVersion": "v1", "kind": "Config", "current-context": "ttr",
+                            "clusters": [{"name": "ttr", "cluster": {"server": self.api.url}}],
+                            "contexts": [{"name": "ttr", "context": {"cluster": "ttr", "user": "ttr"}}],
+                            "users": [{"name": "ttr", "user": {}}]}, f)
+        from ..k8s.rest import Config, RestClient
+        self.client = RestClient(Config.from_kubeconfig(self.kubeconfig))
+        self.kubelet = FakeKubelet(self.pdir, self.client, NODE, on_event=self.mark)
+        self.kubelet.start()
+
+        from ..k8s import objects as o
+
+        def on_node(ev):
+            if o.get_labels(ev.obj).get("amd.com/gpu.gfx"):
+                self.mark("node:labelled")
+        self.backing.watch("v1", "Node", on_node)
+        self.env = dict(os.environ)
+        self.env.update({
+            "PATH": f"{self.bin}:{os.environ.get('PATH', '/usr/bin:/bin')}",
+            "PYTHONPATH": REPO + (os.pathsep + os.environ["PYTHONPATH"] if os.environ.get("PYTHONPATH") else ""),
+            "KUBECONFIG": self.kubeconfig, "NODE_NAME": NODE, "OPERATOR_NAMESPACE": NAMESPACE,
+            "OUTPUT_DIR": self.vdir, "AMD_SYSFS_ROOT": self.sys_root, "AMD_DEV_ROOT": self.dev_root,
+            "HIP_VALIDATION_MODE": self.hip_mode, "GEMM_SHAPES": self.gemm_shapes,
+            "DRIVER_ROOT_MODE": "host" if self.scenario == "host-driver" else "container",
+            "DRIVER_VALIDATION_STRICT": "false", "WAIT_TIMEOUT_SECONDS": str(int(self.timeout)),
+            "ROOT": self.amd_root, "RUNTIME": "containerd", "RUNTIME_CONFIG": self.cfg,
+            "RUNTIME_SOCKET": os.path.join(base, "containerd.sock"), "RESTART_MODE": "none",
+            "CDI_SPEC_DIR": os.path.join(base, "cdi"), "NO_CLEANUP": "true", "PYTHONUNBUFFERED": "1",
+            "HSA_ENABLE_IPC_MODE_LEGACY": "0", "LABELLER_OUTPUT": "node",
+        })
+
+    def _teardown(self) -> None:
+        self._stop.set()
+        for p in self._procs:          # every container is its own process group (its session)
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+        deadline = time.monotonic() + 5
+        for p in self._procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                p.wait()
+        self.kubelet.stop()
+        self.api.stop()
+
+    # -- pod runtime ------------------------------------------------------------------------------
+    def _map(self, text: str) -> str:
+        """hostPath volumes -> harness directories."""
+        return (text.replace("/run/amd/validations", self.vdir).replace("/run/amd/driver", os.path.join(self.base, "driver"))
+                .replace("/var/lib/kubelet/device-plugins", self.pdir))
+
+    def runtime_ready(self) -> bool:
+        shim = os.path.join(self.amd_root, "toolkit", "amd-container-runtime")
+        try:
+            with open(self.cfg) as f:
+                cfg = f.read()
+        except OSError:
+            return False
+        return os.path.exists(shim) and "amd-container-runtime" in cfg
+
+    def _spawn(self, pod: Pod, c: Ctr) -> subprocess.Popen:
+        env = dict(self.env)
+        env.update(c.env)
+        logf = open(os.path.join(self.logs, f"{pod.name}.{c.name}.log"), "ab")
+        p = subprocess.Popen([self._map(a) for a in c.argv], env=env, stdout=logf, stderr=subprocess.STDOUT,
+                             start_new_session=True)
+        logf.close()
+        with self._lock:
+            self._procs.append(p)
+        return p
+
+    def _sleep(self, s: float) -> bool:
+        return not self._stop.wait(s)
+
+    def _run_pod(self, pod: Pod) -> None:
+        try:
+            if pod.runtime_class:
+                while not self.runtime_ready():
+                    if not self._sleep(KUBELET_SYNC_S):
+                        return
+            self.mark(f"{pod.name}:started")
+            for c in pod.inits:
+                attempt = 0
+                while True:
+                    p = self._spawn(pod, c)
+                    while p.poll() is None:
+                        if self._stop.wait(0.02):
+                            return
+                    if p.returncode == 0:
+                        break
+                    key = f"{pod.name}:{c.name}"
+                    self.restarts[key] = self.restarts.get(key, 0) + 1
+                    if not self._sleep(CRASHLOOP_BACKOFF_S[min(attempt, len(CRASHLOOP_BACKOFF_S) - 1)]):
+                        return
+                    attempt += 1
+                self.mark(f"{pod.name}:{c.name}:done")
+            for c in pod.mains:
+                self._spawn(pod, c)
+                self.mark(f"{pod.name}:{c.name}:started")
+            if pod.startup_probe is not None:
+                pr = pod.startup_probe
+                if not self._sleep(pr.initial_delay):
+                    return
+                while True:
+                    env = dict(self.env)
+                    if subprocess.run([self._map(a) for a in pr.argv], env=env, capture_output=True,
+                                      timeout=60).returncode == 0:
+                        self.mark(f"{pod.name}:startup-probe:ok")
+                        break
+                    if not self._sleep(pr.period):
+                        return
+        except Exception as e:  # noqa: BLE001
+            self.errors.append(f"{pod.name}: {e}")
+
+    def _scrape_exporter(self, port: int) -> None:
+        import urllib.request
+        while not self._stop.is_set():
+            try:
+                with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=2) as r:
+                    if r.status == 200 and b"amd_gpu_" in r.read():
+                        self.mark("exporter:first-scrape")
+                        return
+            except OSError:
+                pass
+            self._stop.wait(0.05)
+
+    # -- protocols --------------------------------------------------------------------------------
+    def pods_ours(self, port: int) -> List[Pod]:
+        """This framework's operand pods (gpu_operator_amd/assets, container workload)."""
+        gate = ["amd-barrier-wait", "--dir", "/run/amd/validations", "--all", "toolkit-ready", "--timeout", "3600"]
+        v = lambda comp, **e: Ctr(f"{comp}-validation", ["amd-validator"], dict({"COMPONENT": comp}, **e))  # noqa: E731
+        pods = [
+            Pod("toolkit", [v("driver", WITH_WAIT="true")],
+                [Ctr("amd-container-toolkit-ctr",
+                     ["sh", "-c", self._map(_asset_script("state-container-toolkit", "0400_configmap.yaml"))])]),
+            Pod("validator", [v("driver", WITH_WAIT="true"), v("toolkit", WITH_WAIT="true"), v("hip"),
+                              v("plugin", WITH_WORKLOAD="false"), v("rccl")],
+                [Ctr("amd-operator-validator", ["amd-validator", "--component", "ready"])], runtime_class=True),
+            Pod("device-plugin", [Ctr("toolkit-validation", gate)],
+                [Ctr("amd-device-plugin", ["sh", "-c", self._map(_asset_script("state-device-plugin",
+                                                                                "0400_configmap.yaml")),
+                                           "entrypoint", "--plugin-dir", self.pdir])], runtime_class=True),
+            Pod("node-labeller", [Ctr("toolkit-validation", gate)],
+                [Ctr("amd-node-labeller", ["amd-node-labeller", "--output", "node", "--barrier-dir", self.vdir])],
+                runtime_class=True),
+            Pod("metrics-exporter", [Ctr("toolkit-validation", gate)],
+                [Ctr("amd-metrics-exporter", ["amd-metrics-exporter", "--listen", f"127.0.0.1:{port}"])],
+                runtime_class=True),
+        ]
+        if self.scenario == "driver-container":
+            pods.insert(0, Pod("driver", [], [Ctr("amdgpu-driver-ctr", ["sleep", "infinity"])],
+                               startup_probe=Probe(["sh", "-c", "amdgpu-driver probe && touch "
+                                                    "/run/amd/validations/.driver-ctr-ready"], 0.0, 2.0)))
+        return pods
+
+    def pods_reference(self, port: int) -> List[Pod]:
+        """The reference's operand protocol executed with our agents (see module doc)."""
+        poll = lambda f: f"until [ -f /run/amd/validations/{f} ]; do sleep 5; done"  # noqa: E731
+        gate = ["sh", "-c", poll("toolkit-ready")]
+        ref = {"VALIDATOR_WAIT_MODE": "poll", "SLEEP_INTERVAL_SECONDS": "5"}
+        v = lambda comp, **e: Ctr(f"{comp}-validation", ["amd-validator"], dict(ref, COMPONENT=comp, **e))  # noqa: E731
+        toolkit = ("driver_root=/run/amd/driver; if [ -f /run/amd/validations/host-driver-ready ]; then "
+                   "driver_root=/; fi; export AMD_DRIVER_ROOT=$driver_root; sleep 5; exec amd-ctk install --daemon")
+        plugin = ("while true; do if [ -f /run/amd/validations/host-driver-ready ] || "
+                  "[ -f /run/amd/validations/driver-ready ]; then break; fi; sleep 5; done; "
+                  "exec amd-device-plugin \"$@\"")
+        pods = [
+            Pod("toolkit", [v("driver", WITH_WAIT="true")], [Ctr("toolkit-ctr", ["sh", "-c", self._map(toolkit)])]),
+            Pod("validator", [v("driver", WITH_WAIT="true"), v("toolkit", WITH_WAIT="false"), v("hip"),
+                              v("plugin", WITH_WORKLOAD="true")],
+                [Ctr("validator", ["amd-validator", "--component", "ready"])], runtime_class=True),
+            Pod("device-plugin", [Ctr("toolkit-validation", gate)],
+                [Ctr("device-plugin", ["sh", "-c", self._map(plugin), "entrypoint", "--plugin-dir", self.pdir])],
+                runtime_class=True),
+            Pod("node-labeller", [Ctr("toolkit-validation", gate)],
+                [Ctr("gfd", ["amd-node-labeller", "--output", "node", "--barrier-dir", self.vdir])], runtime_class=True),
+            Pod("metrics-exporter", [Ctr("toolkit-validation", gate)],
+                [Ctr("dcgm-exporter", ["amd-metrics-exporter", "--listen", f"127.0.0.1:{port}"])], runtime_class=True),
+        ]
+        if self.scenario == "driver-container":
+            pods.insert(0, Pod("driver", [], [Ctr("driver-ctr", ["sleep", "infinity"])],
+                               startup_probe=Probe(["sh", "-c", "amdgpu-driver probe && touch "
+                                                    "/run/amd/validations/.driver-ctr-ready"], 60.0, 10.0)))
+        return pods
+
+    def run(self, protocol: str = "ours") -> Dict:
+        self._stop.clear()
+        self._procs = []
+        self.marks, self.restarts, self.errors = {}, {}, []
+        self._setup(protocol)
+        port = _free_port()
+        pods = self.pods_ours(port) if protocol == "ours" else self.pods_reference(port)
+        self.t0 = time.monotonic()
+        self.t0_wall = time.time()
+        threads = [threading.Thread(target=self._run_pod, args=(p,), daemon=True) for p in pods]
+        threads.append(threading.Thread(target=self._scrape_exporter, args=(port,), daemon=True))
+        for t in threads:
+            t.start()
+        ready_key = "validator:amd-operator-validator:started" if protocol == "ours" else "validator:validator:started"
+        deadline = self.t0 + self.timeout
+        while time.monotonic() < deadline and ready_key not in self.marks and not self.errors:
+            if any(self.restarts.get(f"validator:{c}", 0) > 5 for c in ("hip-validation", "plugin-validation")):
+                break
+            time.sleep(0.02)
+        # let the concurrent operands finish their first action (bounded) for the breakdown
+        settle = time.monotonic() + 15
+        while time.monotonic() < settle and not {"node:labelled", "exporter:first-scrape"} <= set(self.marks):
+            time.sleep(0.05)
+        self._teardown()
+        barriers = {}
+        sd = S.StatusDir(self.vdir)
+        for b in (S.DRIVER_CTR_READY, S.HOST_DRIVER_READY, S.DRIVER_READY, S.TOOLKIT_READY, S.HIP_READY,
+                  S.PLUGIN_READY, S.RCCL_READY):
+            d = sd.read(b)
+            if d is not None:
+                ts = d.get("ts") if isinstance(d, dict) else None
+                barriers[b] = round((ts if ts else os.path.getmtime(sd.file(b))) - self.t0_wall, 4)
+        hip = sd.read(S.HIP_READY) or {}
+        ttr = self.marks.get(ready_key)
+        if ttr is None and not self.errors:
+            self.errors.append(f"validator not ready within {self.timeout:.0f}s; logs in {self.logs}")
+        return {"protocol": protocol, "scenario": self.scenario, "time_to_ready_s": ttr,
+                "barriers_s": dict(sorted(barriers.items(), key=lambda kv: kv[1])),
+                "marks_s": dict(sorted(self.marks.items(), key=lambda kv: kv[1])),
+                "restarts": self.restarts, "errors": self.errors,
+                "gemm_tflops_per_gpu": hip.get("gemm_tflops_per_gpu"), "processes": len(self._procs)}
 
 
-def _next_poll(t_ready: float, t_start: float, period: float = POLL) -> float:
-    """First poll tick (start + k*period, k>=0) at or after t_ready."""
-    if t_ready <= t_start:
-        return t_start
-    return t_start + math.ceil((t_ready - t_start) / period) * period
-
-
-def reference_model(steps: Dict[str, float]) -> Dict[str, float]:
-    d = steps.get("driver", 0.5)
-    tk_install = steps.get("toolkit_install", 0.5)
-    tk_check = max(steps.get("toolkit_validation", 0.1) - 0.0, 0.05)
-    hip = steps.get("hip", 2.0)
-    dp_start = steps.get("device_plugin_start", 0.2)
-    # toolkit DaemonSet: driver-validation (first check immediate) -> sleep 5 -> install
-    toolkit_ready_at = d + TOOLKIT_SLEEP + tk_install
-    # validator: driver (d) -> toolkit validation without wait: crash-loops until the hook works
-    t = d
-    attempt = 0
-    while t + tk_check < toolkit_ready_at:
-        t = t + tk_check + BACKOFF[min(attempt, len(BACKOFF) - 1)] + d   # restart reruns driver-validation
-        attempt += 1
-    t_toolkit_ok = t + tk_check
-    # device plugin: init container polls toolkit-ready every 5 s from pod start (t=0)
-    dp_registered = _next_poll(t_toolkit_ok, 0.0) + dp_start
-    # cuda validation: spawn pod, poll its phase every 5 s
-    t_cuda_start = t_toolkit_ok
-    t_cuda_done = _next_poll(t_cuda_start + POD_START + hip, t_cuda_start)
-    # plugin validation: poll node capacity every 5 s (first check immediately)
-    t_plugin = _next_poll(max(dp_registered, t_cuda_done), t_cuda_done)
-    return {"time_to_ready_s": round(t_plugin, 3), "toolkit_crashloops": attempt,
-            "toolkit_ready_s": round(toolkit_ready_at, 3), "device_plugin_registered_s": round(dp_registered, 3),
-            "cuda_validation_done_s": round(t_cuda_done, 3)}
+def run_both(hip_mode: str = "local", gemm_shapes: str = "8192", sys_root: str = "/", dev_root: str = "/",
+             scenario: str = "host-driver", timeout: float = 240.0, keep: bool = False) -> Dict:
+    h = Harness(sys_root=sys_root, dev_root=dev_root, hip_mode=hip_mode, gemm_shapes=gemm_shapes,
+                timeout=timeout, scenario=scenario)
+    try:
+        ours = h.run("ours")
+        ref = h.run("reference")
+    finally:
+        if not keep:
+            shutil.rmtree(h.wd, ignore_errors=True)
+    return {"agent_chain_time_to_ready_s": ours["time_to_ready_s"],
+            "reference_protocol_time_to_ready_s": ref["time_to_ready_s"], "ours": ours, "reference": ref}
 
 
 def main(argv=None) -> int:
     import argparse
     logging.basicConfig(level=logging.WARNING)
-    ap = argparse.ArgumentParser(prog="amd-ttr")
+    ap = argparse.ArgumentParser(prog="amd-ttr", description=__doc__.split("\n\n")[0])
+    ap.add_argument("--protocol", choices=["ours", "reference", "both"], default="both")
+    ap.add_argument("--scenario", choices=["host-driver", "driver-container"], default="host-driver")
+    ap.add_argument("--hip-mode", choices=["local", "skip"], default="local")
     ap.add_argument("--gemm-shapes", default="8192")
-    ap.add_argument("--runs", type=int, default=3)
-    ap.add_argument("--timeout", type=float, default=120.0)
+    ap.add_argument("--sys-root", default=os.environ.get("AMD_SYSFS_ROOT", "/"))
+    ap.add_argument("--dev-root", default=os.environ.get("AMD_DEV_ROOT", "/"))
+    ap.add_argument("--timeout", type=float, default=240.0)
+    ap.add_argument("--keep", action="store_true", help="keep the work dir (logs of every container)")
     a = ap.parse_args(argv)
-    for i in range(a.runs):
-        r = run_chain(gemm_shapes=a.gemm_shapes, timeout=a.timeout)
-        r["reference_model"] = reference_model(r["steps_s"])
-        r["run"] = i
+    h = Harness(sys_root=a.sys_root, dev_root=a.dev_root, hip_mode=a.hip_mode, gemm_shapes=a.gemm_shapes,
+                timeout=a.timeout, scenario=a.scenario)
+    protos = ["ours", "reference"] if a.protocol == "both" else [a.protocol]
+    ok = True
+    for p in protos:
+        r = h.run(p)
+        ok = ok and r["time_to_ready_s"] is not None
         print(json.dumps(r), flush=True)
-    return 0
+    if not a.keep:
+        shutil.rmtree(h.wd, ignore_errors=True)
+    else:
+        print(json.dumps({"workdir": h.wd}), flush=True)
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":
-    import sys
     sys.exit(main())

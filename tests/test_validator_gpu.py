@@ -101,3 +101,15 @@ def test_validator_hip_component_local_mode(tmp_path):
                                                                       "GEMM_SHAPES": "4096"})
     info = comp.validate_hip(ctx)
     assert info["gemm_tflops_per_gpu"] > 500 and ctx.status.exists(S.HIP_READY)
+
+
+def test_node_time_to_ready_both_protocols_on_the_gpu():
+    """Real processes, real GPU validation: our chain must reach Ready and beat the reference's
+    protocol constants executed in the same harness."""
+    from gpu_operator_amd.validator import ttr
+    r = ttr.run_both(hip_mode="local", gemm_shapes="4096", timeout=120)
+    ours, ref = r["ours"], r["reference"]
+    assert ours["errors"] == [] and ref["errors"] == [], (ours["errors"], ref["errors"])
+    assert ours["gemm_tflops_per_gpu"] and ours["gemm_tflops_per_gpu"] > 300
+    assert r["agent_chain_time_to_ready_s"] < r["reference_protocol_time_to_ready_s"]
+    assert ours["marks_s"]["kubelet:capacity:amd.com/gpu=1"] < ours["barriers_s"]["plugin-ready"]
