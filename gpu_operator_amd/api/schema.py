@@ -30,6 +30,11 @@ class ValidationError(ValueError):
     """A CR field violates its schema (path-qualified message)."""
 
 
+class IntOrString:
+    """Type marker for Kubernetes ``intstr.IntOrString`` / quantity fields: the value is kept as
+    given (int or str) and the schema carries ``x-kubernetes-int-or-string``."""
+
+
 def field(json: Optional[str] = None, *, doc: str = "", enum: Optional[List[Any]] = None,
           pattern: Optional[str] = None, minimum: Optional[int] = None,
           maximum: Optional[int] = None, aliases: Tuple[str, ...] = (),
@@ -173,6 +178,10 @@ def _coerce(tp, val, strict: bool, path: str):
     origin = get_origin(tp)
     if tp is Any:
         return copy.deepcopy(val)
+    if tp is IntOrString:
+        if isinstance(val, bool) or not isinstance(val, (int, str)):
+            raise ValidationError(f"{path}: expected integer or string, got {val!r}")
+        return val
     if isinstance(tp, type) and issubclass(tp, Spec):
         return tp.from_dict(val, strict=strict, path=path)
     if origin in (list, List):
@@ -220,6 +229,8 @@ def _type_schema(tp) -> Dict[str, Any]:
     origin = get_origin(tp)
     if tp is Any:
         return {"x-kubernetes-preserve-unknown-fields": True}
+    if tp is IntOrString:
+        return {"x-kubernetes-int-or-string": True, "anyOf": [{"type": "integer"}, {"type": "string"}]}
     if isinstance(tp, type) and issubclass(tp, Spec):
         return tp.openapi()
     if origin in (list, List):

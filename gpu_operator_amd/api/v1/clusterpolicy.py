@@ -25,7 +25,7 @@ import os
 from dataclasses import dataclass
 from typing import Any, ClassVar, Dict, List, Optional
 
-from ..schema import Spec, ValidationError, field
+from ..schema import IntOrString, Spec, ValidationError, field
 from .upgrade import DriverUpgradePolicySpec
 
 GROUP = "amd.com"
@@ -62,8 +62,8 @@ class EnvVar(Spec):
 class ResourceRequirements(Spec):
     """Compute resources of an operand container."""
 
-    limits: Optional[Dict[str, Any]] = field("limits", doc="Maximum resources allowed.")
-    requests: Optional[Dict[str, Any]] = field("requests", doc="Minimum resources required.")
+    limits: Optional[Dict[str, IntOrString]] = field("limits", doc="Maximum resources allowed.")
+    requests: Optional[Dict[str, IntOrString]] = field("requests", doc="Minimum resources required.")
 
 
 @dataclass

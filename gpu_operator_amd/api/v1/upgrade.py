@@ -8,7 +8,7 @@ import math
 from dataclasses import dataclass
 from typing import Optional, Union
 
-from ..schema import Spec, field
+from ..schema import IntOrString, Spec, field
 
 
 @dataclass
@@ -54,7 +54,7 @@ class DriverUpgradePolicySpec(Spec):
 
     autoUpgrade: Optional[bool] = field("autoUpgrade", schema_default=False)
     maxParallelUpgrades: Optional[int] = field("maxParallelUpgrades", minimum=0, schema_default=1)
-    maxUnavailable: Optional[str] = field("maxUnavailable", schema_default="25%",
+    maxUnavailable: Optional[IntOrString] = field("maxUnavailable", schema_default="25%",
                                           doc="Absolute number (e.g. 5) or percentage (e.g. 10%).")
     podDeletion: Optional[PodDeletionSpec] = field("podDeletion")
     waitForCompletion: Optional[WaitForCompletionSpec] = field("waitForCompletion")

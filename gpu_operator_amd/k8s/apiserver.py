@@ -23,7 +23,7 @@ from urllib.parse import parse_qs, urlparse
 
 from . import errors
 from . import objects as o
-from .client import ADDED, DELETED, MODIFIED
+from .client import ADDED, DELETED, MODIFIED, merge_patch
 from .fake import FakeClient
 
 EXTRA_KINDS = {"ClusterPolicy": "amd.com/v1", "NodeFeatureRule": "nfd.k8s-sigs.io/v1alpha1",
@@ -111,6 +111,42 @@ class FakeAPIServer:
             raise errors.NotFound(f"no resources for {av}")
         return {"kind": "APIResourceList", "groupVersion": av, "resources": res}
 
+    # -- CRD schema admission (k8s/openapi.py) -------------------------------------------------
+    def _crd_schema(self, av: str, kind: str):
+        version = av.split("/")[-1]
+        for crd in self.client.list("apiextensions.k8s.io/v1", "CustomResourceDefinition"):
+            names = (crd.get("spec") or {}).get("names") or {}
+            if names.get("kind") != kind:
+                continue
+            for v in (crd.get("spec") or {}).get("versions") or []:
+                if v.get("name") == version:
+                    return ((v.get("schema") or {}).get("openAPIV3Schema"))
+        return None
+
+    def _admit(self, av: str, kind: str, obj: Dict) -> None:
+        """What kube-apiserver does before storing: a v1 CRD must be structural; a custom
+        resource is pruned, defaulted and validated against its CRD's schema."""
+        from . import openapi
+        if kind == "CustomResourceDefinition":
+            errs = []
+            for v in (obj.get("spec") or {}).get("versions") or []:
+                sch = (v.get("schema") or {}).get("openAPIV3Schema")
+                if sch is None:
+                    errs.append(f"spec.versions[{v.get('name')}].schema.openAPIV3Schema: Required value")
+                else:
+                    errs += [f"spec.versions[{v.get('name')}].schema.openAPIV3Schema.{e}"
+                             for e in openapi.structural_errors(sch)]
+            if errs:
+                raise errors.Invalid(f'CustomResourceDefinition "{o.name(obj)}" is invalid: ' + "; ".join(errs[:20]))
+            return
+        sch = self._crd_schema(av, kind)
+        if sch is None:
+            return
+        errs = openapi.admit(obj, sch)
+        if errs:
+            group = av.split("/")[0] if "/" in av else ""
+            raise errors.Invalid(f'{kind}.{group} "{o.name(obj)}" is invalid: ' + "; ".join(errs[:20]))
+
     def _current_rv(self) -> int:
         rvs = [int((x.get("metadata") or {}).get("resourceVersion", 0) or 0) for x in self.client.objects()]
         return max(rvs, default=0)
@@ -173,14 +209,24 @@ class FakeAPIServer:
                         if ns and kind not in o.CLUSTER_SCOPED:
                             body["metadata"]["namespace"] = ns
                         body.setdefault("apiVersion", av)
+                        body.setdefault("kind", kind)
+                        srv._admit(av, kind, body)
                         return self._send(201, c.create(body))
                     if verb == "PUT":
                         body.setdefault("apiVersion", av)
+                        body.setdefault("kind", kind)
+                        if sub != "status":
+                            srv._admit(av, kind, body)
                         return self._send(200, c.update_status(body) if sub == "status" else c.update(body))
                     if verb == "PATCH":
                         ct = self.headers.get("Content-Type", "")
                         if "merge-patch" not in ct and "strategic" not in ct:
                             raise errors.ApiError(f"unsupported patch type {ct}", 415, "UnsupportedMediaType")
+                        if sub != "status" and (kind == "CustomResourceDefinition" or srv._crd_schema(av, kind)):
+                            cur = c.get(av, kind, name, ns)
+                            new = merge_patch(cur, body)
+                            srv._admit(av, kind, new)
+                            return self._send(200, c.update(new))
                         return self._send(200, c.patch(av, kind, name, body, ns))
                     if verb == "DELETE":
                         c.delete(av, kind, name, ns, propagation=(body or {}).get("propagationPolicy"))
