@@ -57,6 +57,13 @@ def _w(p: Path, content) -> None:
     p.write_text(f"{content}\n")
 
 
+def _group_member(grp: Path, dev: Path) -> None:
+    link = grp / "devices" / dev.name
+    link.parent.mkdir(parents=True, exist_ok=True)
+    if not link.is_symlink():
+        os.symlink(os.path.relpath(dev, link.parent), link)
+
+
 def _props(p: Path, kv: Dict[str, int]) -> None:
     _w(p, "\n".join(f"{k} {v}" for k, v in kv.items()))
 
@@ -64,7 +71,7 @@ def _props(p: Path, kv: Dict[str, int]) -> None:
 def make_node(root, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", driver: str = "amdgpu",
               live: bool = True, kfd: bool = True, hive_id: int = 0x5A5A_0001, device_id: int = MI355X_DEVICE_ID,
               driver_version: str = "6.12.12", sriov_totalvfs: int = 0, vfio_bound: bool = False,
-              product: Optional[str] = "AMD Instinct MI355X") -> Path:
+              product: Optional[str] = "AMD Instinct MI355X", companion_audio: bool = False) -> Path:
     """Create a fake node under ``root``; returns the root path."""
     root = Path(root)
     nparts = 8 // PARTITION_XCDS[compute]
@@ -125,6 +132,20 @@ def make_node(root, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
         ig = dev / "iommu_group"
         if not ig.exists():
             os.symlink(os.path.relpath(grp, dev), ig)
+        _group_member(grp, dev)
+        if companion_audio:
+            # a second endpoint in the GPU's IOMMU group (HD-audio class), bound to snd_hda_intel
+            adev = root / "sys/bus/pci/devices" / f"0000:{bus:02x}:00.1"
+            _w(adev / "vendor", "0x1002")
+            _w(adev / "device", "0xab38")
+            _w(adev / "class", "0x040300")
+            adrv = root / "sys/bus/pci/drivers/snd_hda_intel"
+            adrv.mkdir(parents=True, exist_ok=True)
+            if not (adev / "driver").is_symlink():
+                os.symlink(os.path.relpath(adrv, adev), adev / "driver")
+            if not (adev / "iommu_group").exists():
+                os.symlink(os.path.relpath(grp, adev), adev / "iommu_group")
+            _group_member(grp, adev)
         if sriov_totalvfs:
             _w(dev / "sriov_totalvfs", sriov_totalvfs)
             _w(dev / "sriov_numvfs", 0)

@@ -287,3 +287,82 @@ def test_kata_manager_pull_command_and_errors(tmp_path):
     with pytest.raises(km.KataError):
         km.KataManager({"runtimeClasses": [{"name": "y", "artifacts": {}}]}, str(tmp_path / "c.toml"),
                        artifacts_dir=str(tmp_path / "a")).handlers()
+
+
+# -- vfio-manage.sh executed against a fake sysfs with a simulated PCI core ------------------------
+def _vfio_script():
+    import yaml
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(here, "gpu_operator_amd/assets/state-vfio-manager/0400_configmap.yaml")) as f:
+        return yaml.safe_load(f)["data"]["vfio-manage.sh"]
+
+
+class _FakePciCore:
+    """Serves sysfs bus/pci/drivers_probe as a FIFO: binds a device to its driver_override, or
+    back to its original driver when the override is cleared (what the kernel's probe does)."""
+
+    def __init__(self, root):
+        import threading
+        self.root = root
+        self.pci = os.path.join(root, "sys/bus/pci")
+        self.orig = {b: os.path.basename(os.readlink(os.path.join(self.pci, "devices", b, "driver")))
+                     for b in os.listdir(os.path.join(self.pci, "devices"))
+                     if os.path.islink(os.path.join(self.pci, "devices", b, "driver"))}
+        self.fifo = os.path.join(self.pci, "drivers_probe")
+        os.mkfifo(self.fifo)
+        self.stop = False
+        self.t = threading.Thread(target=self.run, daemon=True)
+        self.t.start()
+
+    def run(self):
+        while not self.stop:
+            with open(self.fifo) as f:
+                data = f.read()
+            for bdf in data.split():
+                dev = os.path.join(self.pci, "devices", bdf)
+                try:
+                    ov = open(os.path.join(dev, "driver_override")).read().strip()
+                except OSError:
+                    ov = ""
+                drv = ov or self.orig.get(bdf, "")
+                link = os.path.join(dev, "driver")
+                if os.path.islink(link):
+                    os.unlink(link)
+                if drv:
+                    d = os.path.join(self.pci, "drivers", drv)
+                    os.makedirs(d, exist_ok=True)
+                    os.symlink(os.path.relpath(d, dev), link)
+
+    def close(self):
+        self.stop = True
+        with open(self.fifo, "w") as f:
+            f.write("\n")
+        self.t.join(5)
+
+
+def _driver(root, bdf):
+    return os.path.basename(os.readlink(os.path.join(root, "sys/bus/pci/devices", bdf, "driver")))
+
+
+def test_vfio_manage_binds_gpus_with_their_iommu_group_companions(tmp_path):
+    import subprocess
+    root = str(fakesys.make_node(tmp_path / "r", n_gpus=2, companion_audio=True))
+    script = tmp_path / "vfio-manage.sh"
+    script.write_text(_vfio_script())
+    core = _FakePciCore(root)
+    env = dict(os.environ, SYSFS_ROOT=os.path.join(root, "sys"))
+    try:
+        p = subprocess.run(["bash", str(script), "bind", "--all"], env=env, capture_output=True, text=True, timeout=60)
+        assert p.returncode == 0, p.stdout + p.stderr
+        for bus in ("05", "15"):
+            assert _driver(root, f"0000:{bus}:00.0") == "vfio-pci"
+            assert _driver(root, f"0000:{bus}:00.1") == "vfio-pci"      # the audio companion followed
+        assert p.stdout.count("bound") == 4
+        p = subprocess.run(["bash", str(script), "bind", "--all"], env=env, capture_output=True, text=True, timeout=60)
+        assert p.returncode == 0 and "already bound" in p.stdout
+        p = subprocess.run(["bash", str(script), "unbind", "--all"], env=env, capture_output=True, text=True,
+                           timeout=60)
+        assert p.returncode == 0, p.stdout + p.stderr
+        assert _driver(root, "0000:05:00.0") == "amdgpu" and _driver(root, "0000:05:00.1") == "snd_hda_intel"
+    finally:
+        core.close()
