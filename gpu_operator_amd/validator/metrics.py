@@ -82,6 +82,9 @@ class NodeMetrics:
         rc = sd.read(S.RCCL_READY) or {}
         if rc.get("peak_busbw_gbps") is not None:
             self.busbw.labels(n, str(rc.get("ranks"))).set(rc["peak_busbw_gbps"])
+        for ranks, bw in (rc.get("busbw_by_ranks") or {}).items():     # the 2/4/8-rank sweep
+            if bw is not None:
+                self.busbw.labels(n, str(ranks)).set(bw)
 
     def refresh_driver(self) -> None:
         n = self.ctx.node_name

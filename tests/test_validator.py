@@ -218,7 +218,8 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
     sd.create(S.TOOLKIT_READY, {"ts": t + 3.0})
     sd.create(S.HIP_READY, {"ts": t + 9.0, "gemm_tflops_total": 10900.0, "gemm_tflops_per_gpu": 1362.5})
     sd.create(S.PLUGIN_READY, {"ts": t + 9.5})
-    sd.create(S.RCCL_READY, {"ts": t + 14.0, "peak_busbw_gbps": 310.0, "ranks": 8})
+    sd.create(S.RCCL_READY, {"ts": t + 14.0, "peak_busbw_gbps": 310.0, "ranks": 8,
+                             "busbw_by_ranks": {"2": 141.0, "4": 230.5, "8": 310.0}})
     assert S.time_to_ready(sd) == pytest.approx(14.0)
     ctx = ctx_for(tmp_path, node_root, client=FakeClient([node_obj()]))
     ctx.status = sd
@@ -232,6 +233,7 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
     assert 'amd_gpu_operator_node_driver_validation{node="n1"} 1.0' in text
     assert 'amd_gpu_operator_amd_pci_devices_total{node="n1"} 8.0' in text
     assert 'amd_gpu_operator_validator_allreduce_busbw_gbps{node="n1",ranks="8"} 310.0' in text
+    assert 'amd_gpu_operator_validator_allreduce_busbw_gbps{node="n1",ranks="2"} 141.0' in text
 
 
 def test_cli_driver_component(tmp_path, node_root, capsys):
