@@ -66,3 +66,12 @@ def test_driver_container_scenario_gates_on_the_startup_probe(node):
     b, m = r["barriers_s"], r["marks_s"]
     assert "driver:startup-probe:ok" in m                     # amdgpu-driver probe && touch .driver-ctr-ready
     assert b[".driver-ctr-ready"] < b["driver-ready"] < b["toolkit-ready"]
+
+
+def test_a_node_without_a_driver_never_becomes_ready(tmp_path):
+    empty = tmp_path / "nodriver"
+    empty.mkdir()
+    h = ttr.Harness(sys_root=str(empty), dev_root=str(empty), hip_mode="skip", timeout=8)
+    r = h.run("ours")
+    assert r["time_to_ready_s"] is None and r["errors"]
+    assert "host-driver-ready" not in r["barriers_s"] and "toolkit:driver-validation:done" not in r["marks_s"]
