@@ -1,3 +1,6 @@
+# K-scaling probe of the production GEMM vs hipBLASLt (8192x8192xK, K=2k..32k) plus a
+# kernel trace of the 8192^3 comparison.  Run on the GPU box: gpurun -- bash tools/kscale_probe.sh
+# Output: gpurun_out/kp/sweep.jsonl (per-shape TFLOPS), gpurun_out/kp/tr (rocprofv3 CSV).
 set -e
 mkdir -p gpurun_out/kp
 timeout -k 10 300 python3 tools/gemm_sweep.py --shapes 8192x8192x2048,8192x8192x4096,8192x8192x8192,8192x8192x16384,8192x8192x32768 --variants p0,25 --iters 30 --rounds 3 > gpurun_out/kp/sweep.jsonl 2>gpurun_out/kp/sweep.err
