@@ -240,6 +240,317 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
   }
 }
+// w4t: the w4s kernel with the whole K-tile schedule taken from a schedule class SC, so the
+// read/DMA/barrier placement can differ per operand panel. SC provides, in MFMA slots 0..127
+// (an op "at slot i" issues right after MFMA i):
+//   r1(j)   read of R1 <- tile t kk1, j < 8: A fragment j, j >= 8: B fragment j-8
+//   wa, ba  lgkmcnt(0) and barrier after which tile t's A panel is free (A DMA pieces may start)
+//   wb, bb  the same for the B panel (wa == wb and ba == bb: one barrier for both)
+//   dma(p)  DMA piece p of tile t+2 (p < 8: A panel, p >= 8: B panel)
+//   w2, b2  vmcnt(pieces issued so far) + lgkmcnt(0), then a barrier: tile t+1 landed
+//   r0(j)   read of R0 <- tile t+1 kk0, j in w4_isb order
+// With split panels, A's kk1 fragments are read first and A's DMA overlaps B's kk1 reads, so
+// the fragment reads run at one per two MFMAs instead of the v18 burst of one per MFMA (a
+// 64 KiB burst per CU that the LDS serves at 128 B/clk while the burst itself spans only 17
+// MFMAs).
+template <class SC>
+__host__ __device__ constexpr int w4t_issued_by_w2() {
+  int n = 0;
+  for (int p = 0; p < 16; ++p) n += SC::dma(p) <= SC::w2 ? 1 : 0;
+  return n;
+}
+// inverse lookups (the op of a kind issued at slot i, or -1): constexpr loops instead of a
+// 16-way static_for per slot keep the compile time of a schedule at a few seconds
+template <class SC>
+__host__ __device__ constexpr int w4t_r1_at(int i) {
+  for (int j = 0; j < 16; ++j)
+    if (SC::r1(j) == i) return j;
+  return -1;
+}
+template <class SC>
+__host__ __device__ constexpr int w4t_dma_at(int i) {
+  for (int j = 0; j < 16; ++j)
+    if (SC::dma(j) == i) return j;
+  return -1;
+}
+template <class SC>
+__host__ __device__ constexpr int w4t_r0_at(int i) {
+  for (int j = 0; j < 16; ++j)
+    if (SC::r0(j) == i) return j;
+  return -1;
+}
+template <class SC>
+__host__ __device__ constexpr bool w4t_valid() {
+  for (int j = 0; j < 16; ++j) {
+    for (int q = 0; q < j; ++q)                          // at most one op of a kind per slot
+      if (SC::r1(q) == SC::r1(j) || SC::dma(q) == SC::dma(j) || SC::r0(q) == SC::r0(j)) return false;
+    if (SC::r1(j) < 0 || SC::r1(j) >= (j < 8 ? SC::wa : SC::wb)) return false;
+    if (SC::r0(j) <= SC::b2 || SC::r0(j) > 127) return false;
+    if (SC::dma(j) <= (j < 8 ? SC::ba : SC::bb) || SC::dma(j) > 127) return false;
+    for (int q = 0; q < j; ++q)
+      if (SC::r0(q) > SC::r0(j)) return false;          // R0 reads in consumption order
+  }
+  const bool one = SC::wa == SC::wb && SC::ba == SC::bb;
+  return SC::wa < SC::ba && SC::wb < SC::bb && (one || SC::wb > SC::ba) && SC::w2 > SC::bb && SC::b2 == SC::w2 + 1 &&
+         SC::ba >= 1;
+}
+
+// v18's schedule (B1=17, D0=19, DS=5, B2=80, RS=40) in w4t form: the parity reference.
+struct W4SchedV18 {
+  static constexpr int r1(int j) { return j; }
+  static constexpr int wa = 16, ba = 17, wb = 16, bb = 17, w2 = 79, b2 = 80;
+  static constexpr int dma(int p) { return 19 + 5 * p; }
+  static constexpr int r0(int j) { return 81 + (j * 40) / 16; }
+};
+// hipBLASLt's gfx950 MT256x256x64 custom kernel places its loop this way (disassembled from the
+// shipped code object, docs/validator-gemm.md): A kk1 reads every other MFMA, A-panel barrier,
+// A DMA interleaved with B kk1 reads, B-panel barrier, the rest of the DMA, landing barrier,
+// kk0 reads every other MFMA.
+struct W4SchedSplit {
+  static constexpr int r1(int j) {
+    constexpr int b[8] = {23, 26, 29, 32, 35, 38, 40, 42};
+    return j < 8 ? 2 * j : b[j - 8];
+  }
+  static constexpr int wa = 20, ba = 21, wb = 50, bb = 51, w2 = 91, b2 = 92;
+  static constexpr int dma(int p) {
+    constexpr int s[16] = {22, 25, 28, 31, 34, 52, 55, 58, 61, 64, 85, 87, 89, 96, 100, 124};
+    return s[p];
+  }
+  static constexpr int r0(int j) { return 93 + 2 * j; }
+};
+// One barrier, but the 16 kk1 reads spread over 32 MFMAs and the DMA behind them.
+struct W4SchedSpread {
+  static constexpr int r1(int j) { return 2 * j; }
+  static constexpr int wa = 33, ba = 34, wb = 33, bb = 34, w2 = 91, b2 = 92;
+  static constexpr int dma(int p) { return 35 + (p * 7) / 2; }
+  static constexpr int r0(int j) { return 93 + 2 * j; }
+};
+// Split panels with every DMA piece issued early and evenly (long landing time).
+struct W4SchedSplitEarly {
+  static constexpr int r1(int j) { return j < 8 ? 2 * j : 23 + 3 * (j - 8); }
+  static constexpr int wa = 16, ba = 17, wb = 46, bb = 47, w2 = 91, b2 = 92;
+  static constexpr int dma(int p) { return p < 8 ? 18 + 3 * p + 1 : 48 + 4 * (p - 8); }
+  static constexpr int r0(int j) { return 93 + 2 * j; }
+};
+// Split panels, tighter: B reads right behind the A barrier, landing barrier at v18's slot 80.
+struct W4SchedSplitTight {
+  static constexpr int r1(int j) { return j < 8 ? 2 * j : 18 + 2 * (j - 8); }
+  static constexpr int wa = 16, ba = 17, wb = 34, bb = 35, w2 = 79, b2 = 80;
+  static constexpr int dma(int p) { return p < 8 ? 19 + 2 * p : 36 + 3 * (p - 8); }
+  static constexpr int r0(int j) { return 81 + (j * 40) / 16; }
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ADMA: an LDS-DMA piece and the MFMA of its slot in ONE asm statement, M0 written first: the
+// MFMA is the wait state the M0 -> LDS-DMA hazard needs, where hipcc (blind to what an asm MFMA
+// is) pads every piece with an s_nop of its own. hipcc does not count asm loads: every vmcnt
+// the kernel relies on is explicit (prologue, w2).
+template <int I>
+__device__ __forceinline__ void w4_mfma_dma(const bf16x8& b, const bf16x8& a, uint32_t m0v, uint32_t voff,
+                                            u32x4 rs, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %4\n\tv_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]\n\t"
+               "buffer_load_dwordx4 %5, %6, %7 offen lds"
+               :: "i"(4 * I), "i"(4 * I + 3), "v"(b), "v"(a), "s"(m0v), "v"(voff), "s"(rs), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void w4_dma(uint32_t m0v, uint32_t voff, u32x4 rs, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(m0v), "v"(voff), "s"(rs), "s"(soff) : "memory");
+}
+
+template <class SC, int SERP = 0, bool ROT = false, bool SQ = false, bool ADMA = false>
+__global__ void __launch_bounds__(W4_THREADS, 1)
+gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                      __bf16* __restrict__ C, int M, int N, int K) {
+  static_assert(w4t_valid<SC>(), "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tiles_m = M / BM;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  if constexpr (SQ) tile_coords_sq(blockIdx.x, tiles_n, tm, tn);
+  else tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const __bf16* gA = A + (size_t)tm * BM * K;
+  const __bf16* gB = Bt + (size_t)tn * BN * K;
+  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto mk_rs = [&](const __bf16* base) {
+    const uint64_t p = (uint64_t)(uintptr_t)base;
+    u32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    r[2] = panel_bytes;
+    r[3] = 0x00020000u;
+    return r;
+  };
+  const u32x4 sA = mk_rs(gA), sB = mk_rs(gB);
+  auto dma_m0 = [&](int i, char* buf) -> uint32_t {
+    const int rblk = ((i & 7) << 2) + wid;
+    // the low 32 bits of a generic LDS address are the LDS offset (the shared aperture is the
+    // high half): no addrspacecast, whose null check would cost a compare and select per piece
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)buf) + (uint32_t)((i >= 8 ? PANEL_BYTES : 0) + rblk * 1024);
+  };
+  auto dma_soff = [&](int i, int k0) -> uint32_t {
+    const int rblk = ((i & 7) << 2) + wid;
+    return (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u;
+  };
+  auto dma_piece = [&](int i, int k0, char* buf) {
+    if constexpr (ADMA) {
+      w4_dma(dma_m0(i, buf), voff, i >= 8 ? sB : sA, dma_soff(i, k0));
+    } else {
+      const int rblk = ((i & 7) << 2) + wid;
+      char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
+                                               (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+    }
+  };
+
+  int lane_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15;
+    const int c = kk * 4 + (lane >> 4);
+    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * ROW_BYTES;
+  const int b_off = PANEL_BYTES + wc * 128 * ROW_BYTES;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  W4Frags R0, R1;
+  char* const buf0 = smem;
+  char* const buf1 = smem + BUF_BYTES;
+  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {      // w4_isb order
+    constexpr int j = decltype(J)::value;
+    constexpr int x = w4_idx(j);
+    if constexpr (w4_isb(j))
+      F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
+    else
+      F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
+  };
+  auto read_r1 = [&](const char* buf, auto J) {                             // A first, then B
+    constexpr int j = decltype(J)::value;
+    if constexpr (j >= 8)
+      R1.b[j - 8] = *reinterpret_cast<const bf16x8*>(buf + b_off + (j - 8) * 16 * ROW_BYTES + lane_off[1]);
+    else
+      R1.a[j] = *reinterpret_cast<const bf16x8*>(buf + a_off + j * 16 * ROW_BYTES + lane_off[1]);
+  };
+  constexpr int issued = w4t_issued_by_w2<SC>();
+  constexpr bool split = SC::ba != SC::bb;
+  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX, auto LO, auto HI) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value;
+    static_for<decltype(LO)::value, decltype(HI)::value>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int jr1 = w4t_r1_at<SC>(i), jdma = w4t_dma_at<SC>(i), jr0 = w4t_r0_at<SC>(i);
+      constexpr bool fused = ADMA && dm && jdma >= 0;
+      if constexpr (fused) {
+        if constexpr (i < 64)
+          w4_mfma_dma<i>(R0.b[i & 7], R0.a[i >> 3], dma_m0(jdma, cur), voff, jdma >= 8 ? sB : sA, dma_soff(jdma, dk));
+        else
+          w4_mfma_dma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3], dma_m0(jdma, cur), voff, jdma >= 8 ? sB : sA,
+                              dma_soff(jdma, dk));
+      } else if constexpr (i < 64) {
+        w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
+      } else {
+        w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
+      }
+      if constexpr (jr1 >= 0) read_r1(cur, std::integral_constant<int, jr1>{});
+      if constexpr (i == SC::wa || (split && i == SC::wb)) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && (i == SC::ba || (split && i == SC::bb))) __builtin_amdgcn_s_barrier();
+      if constexpr (!fused && dm && jdma >= 0) dma_piece(jdma, dk, cur);
+      if constexpr (nx && i == SC::w2) {
+        constexpr int n = dm ? issued : 0;
+        __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | 0x70);
+      }
+      if constexpr (nx && i == SC::b2) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && jr0 >= 0) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  const int ktiles = K / BK;        // >= 2 (host guarantees)
+  const bool rev = SERP > 0 && (((int)blockIdx.x / NXCD) / (SERP > 0 ? SERP : 1)) & 1;
+  auto kof = [&](int kt) { return (rev ? ktiles - 1 - kt : kt) * BK; };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(0), buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(1), buf1);
+  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
+  bar();
+  static_for<0, 16>([&](auto J) { read_frag(R0, buf0, 0, J); });
+
+  using S0 = std::integral_constant<int, 0>;
+  using SB = std::integral_constant<int, SC::ba>;
+  using SE = std::integral_constant<int, 128>;
+  char* cur = buf0;
+  char* nxt = buf1;
+  if constexpr (ROT) {
+    iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, SB{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+      iter(cur, nxt, 0, T_{}, T_{}, S0{}, SB{});
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, SB{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
+  } else {
+    for (int t = 0; t < ktiles - 2; ++t) {
+      iter(cur, nxt, kof(t + 2), T_{}, T_{}, S0{}, SE{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    iter(cur, nxt, 0, F_{}, T_{}, S0{}, SE{});
+    iter(nxt, nullptr, 0, F_{}, F_{}, S0{}, SE{});
+  }
+
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  bar();
+  constexpr int CROW = BN * 2;
+  static_for<0, 64>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int m = i >> 3, n = i & 7;
+    float x0, x1, x2, x3;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+    const int r = wr * 128 + m * 16 + (lane & 15);
+    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
+    bf16x4 v;
+    v[0] = (__bf16)x0;
+    v[1] = (__bf16)x1;
+    v[2] = (__bf16)x2;
+    v[3] = (__bf16)x3;
+    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
+  });
+  bar();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < (BM * BN * 2) / (W4_THREADS * 16); ++i) {
+    const int r = i * (W4_THREADS / 32) + (tid >> 5);
+    const int ch = tid & 31;
+    const int sw = r & 15;
+    const int pg = (2 * ch) ^ sw;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
+    uint4 v = raw;
+    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+  }
+}
+
 // v25/v26: v18 made persistent. gridDim = one workgroup per CU; XCD x (= blockIdx % 8) owns a
 // contiguous run of output tiles (the bijective split of xcd_remap) that its gridDim/8
 // workgroups walk in strides. The K-tile stream runs on across tile boundaries: the last two

@@ -1129,6 +1129,17 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
   } else if (v == 45 && kk && (M / BM) % 16 == 0 && (N / BN) % 16 == 0) {
     hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
                        0, s, a, b, c, M, N, K);
+  } else if ((v == 65 || v == 66) && kk) {            // w4t + fused MFMA/LDS-DMA asm (no s_nop per piece)
+    auto kern = v == 65 ? gemm_bf16_256x256_w4t<W4SchedV18, 32, true, false, true>
+                        : gemm_bf16_256x256_w4t<W4SchedSplit, 32, true, false, true>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+  } else if (v >= 60 && v <= 64 && kk) {            // w4t schedules, all with v44's serpentine K + rotation
+    auto kern = v == 60 ? gemm_bf16_256x256_w4t<W4SchedV18, 32, true>
+              : v == 61 ? gemm_bf16_256x256_w4t<W4SchedSplit, 32, true>
+              : v == 62 ? gemm_bf16_256x256_w4t<W4SchedSpread, 32, true>
+              : v == 63 ? gemm_bf16_256x256_w4t<W4SchedSplitEarly, 32, true>
+                        : gemm_bf16_256x256_w4t<W4SchedSplitTight, 32, true>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
   } else {
     return (int)hipErrorInvalidValue;
   }
