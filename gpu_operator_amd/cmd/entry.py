@@ -33,6 +33,29 @@ SCRIPTS = {
 }
 
 
+NATIVE_TOOLS = ("amd-barrier-wait", "amd-hip-smoke", "amd-gemm-validate", "amd-rccl-validate", "amd-node-probe",
+                "amd-container-runtime")
+
+
+def install_wrappers(bin_dir: str) -> str:
+    """Put every console script of this package (a one-line ``exec python -m ...entry <name>``
+    wrapper) and the native tools on a directory, as a container image's PATH would have them."""
+    import os
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    native = os.path.join(here, "_native", "bin")
+    os.makedirs(bin_dir, exist_ok=True)
+    for name in SCRIPTS:
+        p = os.path.join(bin_dir, name)
+        with open(p, "w") as f:
+            f.write(f'#!/bin/sh\nexec "{sys.executable}" -m gpu_operator_amd.cmd.entry {name} "$@"\n')
+        os.chmod(p, 0o755)
+    for name in NATIVE_TOOLS:
+        src, dst = os.path.join(native, name), os.path.join(bin_dir, name)
+        if os.path.exists(src) and not os.path.lexists(dst):
+            os.symlink(src, dst)
+    return bin_dir
+
+
 def run(name: str, argv=None) -> int:
     target = SCRIPTS.get(name)
     if target is None:

@@ -1,0 +1,502 @@
+"""The reference's end-to-end test, executed on one node of real processes.
+
+Reference: ``tests/scripts/end-to-end.sh`` with ``checks.sh`` (install the operator, every
+operand pod Ready, no operand restarts, a GPU workload pod, ClusterPolicy updates reaching the
+DaemonSets, operator restart, disabling and re-enabling operands, uninstall). There it needs an
+AWS GPU instance and a kind/kubeadm cluster; here the cluster is:
+
+  * the API server: k8s/apiserver.py over HTTP, serving this repo's CRDs with their schemas
+    (prune/default/validate on admission);
+  * the operator: ``amd-gpu-operator`` as its own OS process, talking to that API server
+    through a kubeconfig (informer cache, watches, leader-election-free);
+  * the DaemonSet controller: k8s/sim.py (pods per matching node, revisions, DaemonSet
+    status from the pods' real Ready conditions);
+  * the node: e2e/kubelet.py, which runs every pod bound to it as OS processes, including
+    the validator's HIP workload pod and the test's GPU workload pod, with device-plugin
+    gRPC Allocate for ``amd.com/gpu``.
+
+On an MI355X box (``sys_root="/"``, ``dev_root="/"``) the operands read the real GPU: the
+device plugin advertises it, the validator's HIP workload pod runs the MFMA GEMM probe on it,
+and the test workload pod runs ``amd-hip-smoke`` through a device-plugin allocation. On CPU
+(fake sysfs, ``hip_mode="skip"``) the same flow runs without GPU work.
+
+Timings reported: ``time_to_ready_s`` (ClusterPolicy created -> ClusterPolicy ``ready`` with
+every operand pod Ready: the node's whole bring-up including the operator's reconcile),
+per-operand ready times, the re-enable time after ``deploy.operands=false``, and the operator
+restart recovery time (checks.sh:97-113 bounds it at 100 s).
+"""
+
+from __future__ import annotations
+
+import glob
+import json
+import logging
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+import urllib.request
+from typing import Any, Callable, Dict, List, Optional
+
+import yaml
+
+from ..k8s import errors
+from ..k8s import objects as o
+
+log = logging.getLogger("amd-e2e")
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+NS = "amd-gpu-operator"
+CP_NAME = "cluster-policy"
+GPU = "amd.com/gpu"
+OPERANDS_LABEL = "amd.com/gpu.deploy.operands"
+RESTART_BOUND_S = 100.0               # checks.sh:97-113: 10 x 10 s
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class StepFailed(AssertionError):
+    pass
+
+
+class E2E:
+    def __init__(self, workdir: Optional[str] = None, sys_root: str = "/", dev_root: str = "/",
+                 hip_mode: str = "pod", timeout: float = 240.0, node: str = "e2e-node",
+                 workload_cmd: Optional[List[str]] = None, keep: bool = False):
+        # unix socket paths (kubelet.sock, plugin endpoints) must stay under 108 bytes: short base
+        self.wd = workdir or tempfile.mkdtemp(prefix="amd-e2e-", dir="/tmp" if os.path.isdir("/tmp") else None)
+        self.sys_root, self.dev_root = sys_root, dev_root
+        self.hip_mode, self.timeout, self.node, self.keep = hip_mode, timeout, node, keep
+        # the GPU workload: a HIP kernel on the allocated GPU; on CPU, proof of the allocation
+        self.workload_cmd = workload_cmd or (
+            ["amd-hip-smoke"] if hip_mode != "skip" else
+            ["sh", "-c", 'test -n "$AMD_VISIBLE_DEVICES" && echo "allocated: $AMD_VISIBLE_DEVICES"'])
+        self.marks: Dict[str, float] = {}
+        self.steps: List[Dict[str, Any]] = []
+        self.result: Dict[str, Any] = {}
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self.operator: Optional[subprocess.Popen] = None
+        self.t0 = time.monotonic()
+
+    # -- bookkeeping ---------------------------------------------------------------------------
+    def mark(self, name: str, **_kw) -> None:
+        with self._lock:
+            self.marks.setdefault(name, round(time.monotonic() - self.t0, 3))
+
+    def _wait(self, what: str, fn: Callable[[], Any], timeout: Optional[float] = None, period: float = 0.1):
+        deadline = time.monotonic() + (timeout or self.timeout)
+        last = None
+        while time.monotonic() < deadline:
+            try:
+                last = fn()
+                if last:
+                    return last
+            except errors.ApiError as e:
+                last = e
+            time.sleep(period)
+        raise StepFailed(f"timed out after {timeout or self.timeout:.0f}s waiting for {what} (last: {last!r})")
+
+    def step(self, name: str, fn: Callable[[], Any]) -> Any:
+        t = time.monotonic()
+        rec: Dict[str, Any] = {"name": name}
+        try:
+            out = fn()
+            rec.update(ok=True, detail=out)
+            return out
+        except Exception as e:
+            rec.update(ok=False, error=f"{type(e).__name__}: {e}")
+            raise
+        finally:
+            rec["seconds"] = round(time.monotonic() - t, 3)
+            self.steps.append(rec)
+            log.info("step %s: %s (%.2fs)", name, "ok" if rec.get("ok") else rec.get("error"), rec["seconds"])
+
+    # -- cluster -------------------------------------------------------------------------------
+    def _node_obj(self) -> Dict:
+        labels = {"feature.node.kubernetes.io/pci-1002.present": "true",
+                  "feature.node.kubernetes.io/kernel-version.full": os.uname().release,
+                  "feature.node.kubernetes.io/system-os_release.ID": "ubuntu",
+                  "feature.node.kubernetes.io/system-os_release.VERSION_ID": "22.04",
+                  "kubernetes.io/hostname": self.node}
+        return {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node, "labels": labels},
+                "status": {"capacity": {}, "allocatable": {},
+                           "nodeInfo": {"containerRuntimeVersion": "containerd://1.7.13",
+                                        "kernelVersion": os.uname().release}}}
+
+    def _crds(self) -> List[Dict]:
+        out = []
+        for p in sorted(glob.glob(os.path.join(REPO, "config", "crd", "bases", "*.yaml"))):
+            with open(p) as f:
+                out += [d for d in yaml.safe_load_all(f) if d]
+        return out
+
+    def cluster_policy(self) -> Dict:
+        with open(os.path.join(REPO, "config", "samples", "amd_v1_clusterpolicy.yaml")) as f:
+            cp = yaml.safe_load(f)
+        spec = cp["spec"]
+        spec.setdefault("driver", {})["enabled"] = False          # the host's preinstalled amdgpu
+        v = spec.setdefault("validator", {})
+        env = [{"name": "HIP_VALIDATION_MODE", "value": self.hip_mode}]
+        v.setdefault("hip", {})["env"] = list(env)
+        v.setdefault("rccl", {})["env"] = list(env)
+        # a job box exposes its own GPUs' KFD agents only, while PCI sysfs lists every GPU of the
+        # host: the driver check counts what it can open (what an unprivileged validator sees)
+        v.setdefault("driver", {})["env"] = [{"name": "DRIVER_VALIDATION_STRICT", "value": "false"}]
+        me = spec.setdefault("metricsExporter", {})
+        me["env"] = [e for e in me.get("env") or [] if e.get("name") != "METRICS_EXPORTER_LISTEN"] + \
+            [{"name": "METRICS_EXPORTER_LISTEN", "value": f"127.0.0.1:{self.exporter_port}"}]
+        return cp
+
+    def setup(self) -> None:
+        from ..cmd.entry import install_wrappers
+        from ..k8s.apiserver import FakeAPIServer
+        from ..k8s.fake import FakeClient
+        from ..k8s.sim import ClusterSim
+        from .kubelet import ProcessKubelet
+
+        self.base = os.path.join(self.wd, "e2e")
+        shutil.rmtree(self.base, ignore_errors=True)
+        os.makedirs(self.base)
+        self.bin = install_wrappers(os.path.join(self.base, "bin"))
+        ns = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NS}}
+        self.backing = FakeClient([ns, self._node_obj()] + self._crds(),
+                                  unserved_kinds={"ServiceMonitor", "PrometheusRule"})
+        self.api = FakeAPIServer(self.backing).start()
+        self.kubeconfig = os.path.join(self.base, "kubeconfig")
+        with open(self.kubeconfig, "w") as f:
+            yaml.safe_dump({"apiVersion": "v1", "kind": "Config", "current-context": "e2e",
+                            "clusters": [{"name": "e2e", "cluster": {"server": self.api.url}}],
+                            "contexts": [{"name": "e2e", "context": {"cluster": "e2e", "user": "e2e"}}],
+                            "users": [{"name": "e2e", "user": {}}]}, f)
+        self.exporter_port = _free_port()
+        self.env = {k: v for k, v in os.environ.items() if not k.startswith(("AMD_MOUNTS", "KUBECONFIG"))}
+        self.env.update({
+            "PATH": f"{self.bin}:{os.environ.get('PATH', '/usr/bin:/bin')}",
+            "PYTHONPATH": REPO + (os.pathsep + os.environ["PYTHONPATH"] if os.environ.get("PYTHONPATH") else ""),
+            "KUBECONFIG": self.kubeconfig, "PYTHONUNBUFFERED": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+            "AMD_SYSFS_ROOT": self.sys_root, "AMD_DEV_ROOT": self.dev_root,
+            # no containerd runs on this node: the toolkit edits its config (which the kubelet's
+            # runtime-handler gate reads) but has no daemon to restart
+            "RESTART_MODE": "none",
+        })
+        self.kubelet = ProcessKubelet(self.backing, self.node, self.base, self.env, self.sys_root, self.dev_root,
+                                      events=self.mark).start()
+        self.dsc = ClusterSim(self.backing, kubelet=False)
+
+        def ds_controller():
+            while not self._stop.is_set():
+                try:
+                    self.dsc.sync()
+                except Exception as e:  # noqa: BLE001 - objects racing with deletion
+                    log.debug("ds controller: %s", e)
+                self._stop.wait(0.1)
+        self._dsc_thread = threading.Thread(target=ds_controller, name="ds-controller", daemon=True)
+        self._dsc_thread.start()
+        self.metrics_port, self.health_port = _free_port(), _free_port()
+
+    def start_operator(self) -> subprocess.Popen:
+        env = dict(self.env, OPERATOR_NAMESPACE=NS)
+        logf = open(os.path.join(self.base, f"operator.{len(glob.glob(os.path.join(self.base, 'operator.*')))}.log"),
+                    "ab")
+        self.operator = subprocess.Popen(
+            [os.path.join(self.bin, "amd-gpu-operator"), "--kubeconfig", self.kubeconfig,
+             "--metrics-bind-address", f"127.0.0.1:{self.metrics_port}",
+             "--health-probe-bind-address", f"127.0.0.1:{self.health_port}"],
+            env=env, stdout=logf, stderr=subprocess.STDOUT, start_new_session=True)
+        logf.close()
+        return self.operator
+
+    def stop_operator(self, sig=signal.SIGTERM) -> None:
+        p, self.operator = self.operator, None
+        if p is None or p.poll() is not None:
+            return
+        os.killpg(p.pid, sig)
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+
+    def teardown(self) -> None:
+        self._stop.set()
+        self.stop_operator()
+        self.kubelet.stop()
+        self.api.stop()
+        if not self.keep:
+            shutil.rmtree(self.base, ignore_errors=True)
+
+    # -- observations --------------------------------------------------------------------------
+    def cp_state(self) -> Optional[str]:
+        try:
+            return (self.backing.get("amd.com/v1", "ClusterPolicy", CP_NAME).get("status") or {}).get("state")
+        except errors.NotFound:
+            return None
+
+    def operand_daemonsets(self) -> List[Dict]:
+        return [d for d in self.backing.list("apps/v1", "DaemonSet", NS)
+                if ((d.get("status") or {}).get("desiredNumberScheduled") or 0) > 0]
+
+    def operand_pods(self) -> List[Dict]:
+        return [p for p in self.backing.list("v1", "Pod", NS)
+                if any(r.get("kind") == "DaemonSet" for r in p["metadata"].get("ownerReferences") or [])]
+
+    def all_ready(self) -> Optional[Dict[str, int]]:
+        if self.cp_state() != "ready":
+            return None
+        dss = self.operand_daemonsets()
+        if not dss:
+            return None
+        out = {}
+        for d in dss:
+            st = d.get("status") or {}
+            if st.get("numberReady") != st.get("desiredNumberScheduled") or st.get("numberUnavailable"):
+                return None
+            # rolled out: the controller has seen this generation and every pod runs its template
+            if st.get("observedGeneration", 0) < d["metadata"].get("generation", 1) or \
+                    st.get("updatedNumberScheduled") != st.get("desiredNumberScheduled"):
+                return None
+            out[o.name(d)] = st["numberReady"]
+        return out
+
+    def validations(self) -> List[str]:
+        d = self.kubelet.host_path("/run/amd/validations")
+        return sorted(os.listdir(d)) if os.path.isdir(d) else []
+
+    # -- the reference's steps -----------------------------------------------------------------
+    def install_operator(self) -> Dict:
+        self.t0 = time.monotonic()
+        self.backing.create(self.cluster_policy())
+        self.mark("clusterpolicy:created")
+        self.start_operator()
+        return {"operator_pid": self.operator.pid}
+
+    def verify_operator(self, tag: str) -> Dict:
+        t = time.monotonic()
+        ready = self._wait("ClusterPolicy ready and every operand pod Ready", self.all_ready)
+        dt = time.monotonic() - t
+        self.mark(f"{tag}:ready")
+        files = self.validations()
+        for f in ("toolkit-ready", "hip-ready", "plugin-ready"):
+            if f not in files:
+                raise StepFailed(f"validation barrier {f} missing: {files}")
+        cap = (self.backing.get("v1", "Node", self.node).get("status") or {}).get("allocatable") or {}
+        if int(cap.get(GPU, 0) or 0) < 1:
+            raise StepFailed(f"node advertises no {GPU}: {cap}")
+        out = {"daemonsets": ready, "seconds": round(dt, 3), "validations": files, GPU: cap.get(GPU)}
+        for f in ("hip-ready", "host-driver-ready", "rccl-ready"):
+            try:
+                with open(os.path.join(self.kubelet.host_path("/run/amd/validations"), f)) as fh:
+                    out[f] = json.load(fh)
+            except (OSError, ValueError):
+                pass
+        labels = o.get_labels(self.backing.get("v1", "Node", self.node))
+        out["gpu_labels"] = {k: v for k, v in labels.items()
+                             if k.startswith("amd.com/gpu.") and not k.startswith("amd.com/gpu.deploy.")}
+        return out
+
+    def verify_operand_restarts(self) -> Dict:
+        out = {}
+        for p in self.operand_pods():
+            n = sum(cs.get("restartCount", 0) for cs in (p.get("status") or {}).get("containerStatuses") or [])
+            out[o.name(p)] = n
+        bad = {k: v for k, v in out.items() if v}
+        if bad:
+            raise StepFailed(f"operand containers restarted: {bad}")
+        return out
+
+    def workload_pod(self) -> Dict:
+        return {"apiVersion": "v1", "kind": "Pod",
+                "metadata": {"name": "gpu-operator-test", "namespace": "default", "labels": {"app": "gpu-operator-test"}},
+                "spec": {"restartPolicy": "OnFailure",
+                         "containers": [{"name": "hip-smoke", "image": "amd-gpu-operator-node",
+                                         "command": list(self.workload_cmd),
+                                         "resources": {"limits": {GPU: 1}}}]}}
+
+    def install_and_verify_workload(self) -> Dict:
+        if not any(o.name(n) == "default" for n in self.backing.list("v1", "Namespace")):
+            self.backing.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "default"}})
+        self.backing.create(self.workload_pod())
+
+        def done():
+            p = self.backing.get("v1", "Pod", "gpu-operator-test", "default")
+            ph = (p.get("status") or {}).get("phase")
+            if ph == "Failed":
+                raise StepFailed(f"workload pod failed: {p.get('status')}")
+            return p if ph == "Succeeded" else None
+        p = self._wait("the GPU workload pod to succeed", done)
+        run_dir = [d for d in glob.glob(os.path.join(self.base, "pods", "default_gpu-operator-test_*"))]
+        log_text = ""
+        for d in run_dir:
+            lp = os.path.join(d, "logs", "hip-smoke.log")
+            if os.path.exists(lp):
+                with open(lp, errors="replace") as f:
+                    log_text = f.read()[-2000:]
+        return {"phase": p["status"]["phase"], "node": p["spec"].get("nodeName"), "log_tail": log_text.strip()[-400:]}
+
+    def _ds(self, name: str) -> Dict:
+        return self.backing.get("apps/v1", "DaemonSet", name, NS)
+
+    def _plugin_ds_name(self) -> str:
+        return next(o.name(d) for d in self.backing.list("apps/v1", "DaemonSet", NS) if "device-plugin" in o.name(d)
+                    and "sandbox" not in o.name(d))
+
+    def update_clusterpolicy(self) -> Dict:
+        """update-clusterpolicy.sh: an env and an image-version change reach the DaemonSet and the
+        restarted pod."""
+        name = self._plugin_ds_name()
+        cp = self.backing.get("amd.com/v1", "ClusterPolicy", CP_NAME)
+        dp = cp["spec"].setdefault("devicePlugin", {})
+        dp["env"] = list(dp.get("env") or []) + [{"name": "MY_TEST_ENV_NAME", "value": "test"}]
+        self.backing.update(cp)
+
+        def env_in_ds():
+            c = self._ds(name)["spec"]["template"]["spec"]["containers"][0]
+            return any(e.get("name") == "MY_TEST_ENV_NAME" and e.get("value") == "test" for e in c.get("env") or [])
+        self._wait("the device-plugin DaemonSet to carry the new env", env_in_ds)
+
+        def env_in_process():
+            runs = [r for r in self.kubelet.running().values() if r.name.startswith(name)]
+            for r in runs:
+                c0 = r.pod["spec"]["containers"][0]["name"]
+                p = r.procs.get(c0)
+                if p is None or p.poll() is not None or not r.ready:
+                    continue
+                with open(f"/proc/{p.pid}/environ", "rb") as f:
+                    if b"MY_TEST_ENV_NAME=test\0" in f.read():
+                        return p.pid
+            return None
+        pid = self._wait("a device-plugin process started with the new env", env_in_process)
+        cp = self.backing.get("amd.com/v1", "ClusterPolicy", CP_NAME)
+        cp["spec"]["devicePlugin"]["version"] = "v0.1.1"
+        self.backing.update(cp)
+        self._wait("the device-plugin image update",
+                   lambda: self._ds(name)["spec"]["template"]["spec"]["containers"][0]["image"].endswith(":v0.1.1"))
+        self._wait("the updated device plugin Ready", self.all_ready)
+        return {"daemonset": name, "env_pid": pid}
+
+    def restart_operator(self) -> Dict:
+        """checks.sh test_restart_operator: the operator pod is killed; its replacement must get
+        the ClusterPolicy back to ready without churning the operands."""
+        before = {o.name(p): p["metadata"]["uid"] for p in self.operand_pods()}
+        self.stop_operator(signal.SIGKILL)
+        t = time.monotonic()
+        self.start_operator()
+
+        def healthy():
+            try:
+                with urllib.request.urlopen(f"http://127.0.0.1:{self.health_port}/readyz", timeout=1) as r:
+                    return r.status == 200 and self.all_ready()
+            except OSError:
+                return None
+        self._wait("the restarted operator healthy and the ClusterPolicy ready", healthy, timeout=RESTART_BOUND_S)
+        dt = time.monotonic() - t
+        time.sleep(1.0)                                  # a reconcile pass after the restart
+        after = {o.name(p): p["metadata"]["uid"] for p in self.operand_pods()}
+        churned = sorted(k for k in before if after.get(k) != before[k])
+        if churned:
+            raise StepFailed(f"operand pods recreated by the restarted operator: {churned}")
+        return {"recovery_s": round(dt, 3), "bound_s": RESTART_BOUND_S}
+
+    def disable_operands(self) -> Dict:
+        pids = self.kubelet.all_pids()
+        self.backing.patch("v1", "Node", self.node, {"metadata": {"labels": {OPERANDS_LABEL: "false"}}})
+        self._wait("every operand pod deleted", lambda: not self.operand_pods())
+
+        def gone():
+            alive = []
+            for pid in pids:
+                try:
+                    os.kill(pid, 0)
+                    alive.append(pid)
+                except ProcessLookupError:
+                    pass
+                except PermissionError:
+                    alive.append(pid)
+            return not alive or None
+        self._wait("operand processes to exit", gone, timeout=30)
+        return {"terminated_processes": len(pids)}
+
+    def enable_operands(self) -> Dict:
+        t = time.monotonic()
+        self.backing.patch("v1", "Node", self.node, {"metadata": {"labels": {OPERANDS_LABEL: "true"}}})
+        out = self.verify_operator("reenable")
+        out["reenable_time_to_ready_s"] = round(time.monotonic() - t, 3)
+        return out
+
+    def uninstall(self) -> Dict:
+        try:
+            self.backing.delete("v1", "Pod", "gpu-operator-test", "default")
+        except errors.NotFound:
+            pass
+        self.backing.delete("amd.com/v1", "ClusterPolicy", CP_NAME)
+        self._wait("operand DaemonSets garbage-collected", lambda: not self.backing.list("apps/v1", "DaemonSet", NS))
+        self._wait("operand pods gone", lambda: not self.operand_pods())
+        self._wait("every node process gone", lambda: not self.kubelet.all_pids(), timeout=30)
+        self.stop_operator()
+        return {"ok": True}
+
+    # -- the flow -------------------------------------------------------------------------------
+    def run(self) -> Dict[str, Any]:
+        self.setup()
+        try:
+            self.step("install-operator", self.install_operator)
+            first = self.step("verify-operator", lambda: self.verify_operator("install"))
+            self.result["time_to_ready_s"] = self.marks.get("install:ready")
+            self.result["operands_ready"] = first["daemonsets"]
+            self.step("verify-operand-restarts", self.verify_operand_restarts)
+            self.step("install+verify-workload", self.install_and_verify_workload)
+            self.step("update-clusterpolicy", self.update_clusterpolicy)
+            rs = self.step("restart-operator", self.restart_operator)
+            self.result["operator_restart_recovery_s"] = rs["recovery_s"]
+            self.step("disable-operands", self.disable_operands)
+            en = self.step("enable-operands", self.enable_operands)
+            self.result["reenable_time_to_ready_s"] = en["reenable_time_to_ready_s"]
+            self.step("uninstall", self.uninstall)
+        except Exception as e:  # noqa: BLE001 - reported in the result
+            self.result["error"] = f"{type(e).__name__}: {e}"
+            self.result["pods"] = {o.name(p): (p.get("status") or {}).get("phase")
+                                   for p in self.backing.list("v1", "Pod")}
+            node = self.backing.get("v1", "Node", self.node)
+            self.result["node_labels"] = {k: v for k, v in o.get_labels(node).items() if k.startswith("amd.com/")}
+            self.result["clusterpolicy_state"] = self.cp_state()
+            self.result["logs_dir"] = self.base
+            self.keep = True
+        finally:
+            self.teardown()
+        self.result.update(ok=all(s.get("ok") for s in self.steps) and "error" not in self.result,
+                           steps=self.steps, marks_s=dict(sorted(self.marks.items(), key=lambda kv: kv[1])),
+                           hip_mode=self.hip_mode, sys_root=self.sys_root)
+        return self.result
+
+
+def main(argv=None) -> int:
+    import argparse
+    ap = argparse.ArgumentParser(prog="python -m gpu_operator_amd.e2e")
+    ap.add_argument("--sys-root", default="/")
+    ap.add_argument("--dev-root", default="/")
+    ap.add_argument("--hip-mode", default="pod", choices=["pod", "local", "skip"])
+    ap.add_argument("--fake-gpus", type=int, default=0, help="run on a fake sysfs with N GPUs (CPU rehearsal)")
+    ap.add_argument("--timeout", type=float, default=240.0)
+    ap.add_argument("--keep", action="store_true")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    sys_root, dev_root = a.sys_root, a.dev_root
+    if a.fake_gpus:
+        from ..devices import fakesys
+        sys_root = dev_root = str(fakesys.make_node(os.path.join(tempfile.mkdtemp(prefix="amd-e2e-sys-"), "root"),
+                                                    n_gpus=a.fake_gpus))
+    r = E2E(sys_root=sys_root, dev_root=dev_root, hip_mode=a.hip_mode, timeout=a.timeout, keep=a.keep).run()
+    print(json.dumps(r, default=str))
+    return 0 if r["ok"] else 1

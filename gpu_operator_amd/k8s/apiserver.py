@@ -49,6 +49,8 @@ class FakeAPIServer:
         self.version = version
         kinds = dict(o.CORE_KINDS)
         kinds.update(EXTRA_KINDS)
+        # kinds the backing store refuses (e.g. no prometheus-operator CRDs) are not discovered either
+        unserved = tuple(unserved) + tuple(getattr(self.client, "unserved_kinds", ()) or ())
         self.kinds = {k: v for k, v in kinds.items() if k not in unserved}
         # api_version -> plural -> kind
         self.by_plural: Dict[str, Dict[str, str]] = {}

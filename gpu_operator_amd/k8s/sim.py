@@ -26,10 +26,23 @@ def _node_matches(pod_spec: Dict, node: Dict) -> bool:
     return not any(labels.get(k) != v for k, v in sel.items())
 
 
+def pod_ready(pod: Dict) -> bool:
+    """The Ready condition a kubelet reports."""
+    for c in (pod.get("status") or {}).get("conditions") or []:
+        if c.get("type") == "Ready":
+            return c.get("status") == "True"
+    return False
+
+
 class ClusterSim:
-    def __init__(self, client: FakeClient, ready_fn: Optional[ReadyFn] = None):
+    """``kubelet=False``: only the DaemonSet controller runs here; pod status belongs to an
+    external kubelet (e2e/kubelet.py runs the pods as processes) and readiness is read from the
+    pods' Ready condition."""
+
+    def __init__(self, client: FakeClient, ready_fn: Optional[ReadyFn] = None, kubelet: bool = True):
         self.client = client
         self.ready_fn = ready_fn or (lambda pod, node: True)
+        self.kubelet = kubelet
 
     def _revision(self, ds: Dict) -> str:
         return o.stable_hash(ds["spec"].get("template"))[:10]
@@ -80,6 +93,9 @@ class ClusterSim:
             by_node[node_name] = self.client.create(pod)
         available = 0
         for node_name, pod in by_node.items():
+            if not self.kubelet:
+                available += 1 if pod_ready(pod) else 0
+                continue
             ready = self.ready_fn(pod, nodes[node_name])
             cstat = [{"name": c["name"], "ready": ready} for c in (pod["spec"].get("containers") or [])]
             st = {"phase": "Running" if ready else "Pending", "containerStatuses": cstat}

@@ -36,6 +36,7 @@ from typing import Dict, Iterable, List, Optional
 import yaml
 
 from .. import devices
+from ..utils import mounts
 from . import kubeletapi as K
 
 log = logging.getLogger("amd-device-plugin")
@@ -340,7 +341,7 @@ def main(argv=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
     ap = argparse.ArgumentParser(prog="amd-device-plugin")
     ap.add_argument("--config-file", default=os.environ.get("CONFIG_FILE"))
-    ap.add_argument("--plugin-dir", default=K.DEVICE_PLUGIN_PATH)
+    ap.add_argument("--plugin-dir", default=mounts.path(K.DEVICE_PLUGIN_PATH))
     a = ap.parse_args(argv)
     stop = threading.Event()
     reload_ = threading.Event()

@@ -27,6 +27,7 @@ from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
 from prometheus_client.registry import Collector, CollectorRegistry
 
 from .. import devices
+from ..utils import mounts
 from . import kubeletapi as K
 
 log = logging.getLogger("amd-metrics-exporter")
@@ -219,7 +220,7 @@ def main(argv=None) -> int:
 
     from ..runtime.manager import _Server
     reg = build_registry(load_fields(a.fields), kubernetes=a.kubernetes == "true",
-                         hostname=os.environ.get("NODE_NAME", ""))
+                         pod_socket=mounts.path(K.POD_RESOURCES_SOCKET), hostname=os.environ.get("NODE_NAME", ""))
     host, _, port = a.listen.rpartition(":")
     srv = _Server((host or "0.0.0.0", int(port)), {"/metrics": lambda: (200, CONTENT_TYPE_LATEST,
                                                                         generate_latest(reg))})

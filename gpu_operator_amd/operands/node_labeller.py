@@ -24,6 +24,7 @@ import threading
 from typing import Dict, List, Optional
 
 from .. import devices, models
+from ..utils import mounts
 from ..k8s import objects as o
 
 log = logging.getLogger("amd-node-labeller")
@@ -135,8 +136,8 @@ def main(argv=None, client=None) -> int:
     ap.add_argument("--output", default=os.environ.get("LABELLER_OUTPUT", "node"))
     ap.add_argument("--sleep-interval", default=os.environ.get("LABELLER_SLEEP_INTERVAL", "60s"))
     ap.add_argument("--node-name", default=os.environ.get("NODE_NAME", ""))
-    ap.add_argument("--nfd-file", default=NFD_FEATURE_FILE)
-    ap.add_argument("--barrier-dir", default="/run/amd/validations")
+    ap.add_argument("--nfd-file", default=mounts.path(NFD_FEATURE_FILE))
+    ap.add_argument("--barrier-dir", default=mounts.path("/run/amd/validations"))
     a = ap.parse_args(argv)
     if a.output == "node" and client is None:
         from ..k8s.rest import RestClient

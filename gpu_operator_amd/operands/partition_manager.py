@@ -41,6 +41,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import yaml
 
 from .. import devices
+from ..utils import mounts
 from ..k8s import errors
 from ..k8s import objects as o
 
@@ -303,8 +304,8 @@ def main(argv=None, client=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
     ap = argparse.ArgumentParser(prog="amd-partition-manager")
     ap.add_argument("--node-name", default=os.environ.get("NODE_NAME", ""))
-    ap.add_argument("--config-file", default=os.environ.get("CONFIG_FILE", "/partition-config/config.yaml"))
-    ap.add_argument("--gpu-clients-file", default=os.environ.get("GPU_CLIENTS_FILE", "/gpu-clients/clients.yaml"))
+    ap.add_argument("--config-file", default=os.environ.get("CONFIG_FILE", mounts.path("/partition-config/config.yaml")))
+    ap.add_argument("--gpu-clients-file", default=os.environ.get("GPU_CLIENTS_FILE", mounts.path("/gpu-clients/clients.yaml")))
     ap.add_argument("--default", default=os.environ.get("DEFAULT_PARTITION_CONFIG", ""))
     ap.add_argument("--namespace", default=os.environ.get("OPERATOR_NAMESPACE", ""))
     ap.add_argument("--resync", type=float, default=300.0)
@@ -315,6 +316,7 @@ def main(argv=None, client=None) -> int:
         from ..k8s.rest import RestClient
         client = RestClient()
     pm = PartitionManager(client, a.node_name, a.config_file, default_config=a.default, namespace=a.namespace,
+                          barrier_dir=mounts.path("/run/amd/validations"),
                           host_services=load_clients(a.gpu_clients_file), reload_cmd=a.reload_cmd)
     kick = threading.Event()
 

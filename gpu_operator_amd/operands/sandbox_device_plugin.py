@@ -25,6 +25,7 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 from .. import devices, models
+from ..utils import mounts
 from . import kubeletapi as K
 
 log = logging.getLogger("amd-sandbox-device-plugin")
@@ -205,7 +206,7 @@ class SandboxDevicePlugin:
 def main(argv=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
     ap = argparse.ArgumentParser(prog="amd-sandbox-device-plugin")
-    ap.add_argument("--plugin-dir", default=K.DEVICE_PLUGIN_PATH)
+    ap.add_argument("--plugin-dir", default=mounts.path(K.DEVICE_PLUGIN_PATH))
     a = ap.parse_args(argv)
     p = SandboxDevicePlugin(os.environ.get("AMD_SYSFS_ROOT"), plugin_dir=a.plugin_dir)
     p.start()

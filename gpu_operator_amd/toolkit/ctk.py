@@ -29,6 +29,7 @@ import threading
 import time
 from typing import Callable, Dict, List, Optional
 
+from ..utils import mounts
 from . import cdi, runtime_config
 
 log = logging.getLogger("amd-ctk")
@@ -80,15 +81,15 @@ class Installer:
     @classmethod
     def from_env(cls, **kw) -> "Installer":
         runtime = os.environ.get("RUNTIME", "containerd")
-        return cls(root=os.environ.get("ROOT", "/usr/local/amd"), runtime=runtime,
-                   runtime_config=os.environ.get("RUNTIME_CONFIG", DEFAULT_CONFIGS[runtime]),
-                   runtime_socket=os.environ.get("RUNTIME_SOCKET", DEFAULT_SOCKETS[runtime]),
+        return cls(root=os.environ.get("ROOT", mounts.path("/usr/local/amd")), runtime=runtime,
+                   runtime_config=os.environ.get("RUNTIME_CONFIG", mounts.path(DEFAULT_CONFIGS[runtime])),
+                   runtime_socket=os.environ.get("RUNTIME_SOCKET", mounts.path(DEFAULT_SOCKETS[runtime])),
                    handler=os.environ.get("RUNTIME_CLASS", "amd"),
                    set_default=_env_bool("CONTAINERD_SET_AS_DEFAULT") or _env_bool("SET_AS_DEFAULT"),
                    cdi_enabled=_env_bool("CDI_ENABLED"), mode=os.environ.get("AMD_RUNTIME_MODE", "auto"),
-                   cdi_dir=os.environ.get("CDI_SPEC_DIR", "/var/run/cdi"),
+                   cdi_dir=os.environ.get("CDI_SPEC_DIR", mounts.path("/var/run/cdi")),
                    sys_root=os.environ.get("AMD_SYSFS_ROOT", "/"),
-                   dev_root=os.environ.get("AMD_DEV_ROOT", "/host"),   # devtmpfs is the host's
+                   dev_root=os.environ.get("AMD_DEV_ROOT", mounts.path("/host")),   # devtmpfs is the host's
                    annotation_prefixes=os.environ.get("AMD_CONTAINER_RUNTIME_MODES_CDI_ANNOTATION_PREFIXES",
                                                       "amd.cdi.k8s.io/"),
                    restart_mode=os.environ.get("RESTART_MODE", ""), **kw)
@@ -246,7 +247,7 @@ def main(argv=None, stop: Optional[threading.Event] = None) -> int:
             print(n)
         return 0
     if a.cmd == "runtime":
-        cfg = a.config or DEFAULT_CONFIGS[a.runtime]
+        cfg = a.config or mounts.path(DEFAULT_CONFIGS[a.runtime])
         if a.action == "configure":
             runtime_config.configure(a.runtime, cfg, runtime_config.handler_binaries(a.root, a.handler, a.cdi),
                                      default=a.handler if a.set_as_default else None, cdi=a.cdi)

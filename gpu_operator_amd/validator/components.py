@@ -24,6 +24,7 @@ from typing import Any, Callable, Dict, List, Optional
 from .. import devices
 from ..k8s import errors
 from ..k8s import objects as o
+from ..utils import mounts
 from . import status as S
 from . import workload as W
 
@@ -387,7 +388,7 @@ def validate_rdma(ctx: Context) -> Dict[str, Any]:
         if ctx.env.get("USE_HOST_MOFED") == "true":
             if not os.path.isdir(os.path.join(ctx.sys_root, "sys/module/mlx5_core")):
                 raise ValidationError("mlx5_core not loaded on host")
-        elif not os.path.exists("/run/mellanox/drivers/.driver-ready"):
+        elif not os.path.exists(mounts.path("/run/mellanox/drivers/.driver-ready")):
             raise ValidationError("MOFED driver container not ready")
         return {"rdma": True}
     info = retry(ctx, "rdma", check)

@@ -25,6 +25,7 @@ import time
 
 from . import components as comp
 from . import status as S
+from ..utils import mounts
 
 
 def _bool(v: str) -> bool:
@@ -38,7 +39,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("-w", "--with-wait", default=e("WITH_WAIT", "false"))
     ap.add_argument("-l", "--with-workload", default=e("WITH_WORKLOAD", "true"))
     ap.add_argument("-r", "--cleanup-all", default=e("CLEANUP_ALL", "false"))
-    ap.add_argument("-o", "--output-dir", default=e("OUTPUT_DIR", S.DEFAULT_DIR))
+    ap.add_argument("-o", "--output-dir", default=e("OUTPUT_DIR", mounts.path(S.DEFAULT_DIR)))
     ap.add_argument("-s", "--sleep-interval-seconds", type=float, default=float(e("SLEEP_INTERVAL_SECONDS", "5")))
     ap.add_argument("--wait-timeout-seconds", type=float, default=float(e("WAIT_TIMEOUT_SECONDS", "3600")))
     ap.add_argument("-m", "--partition-strategy",
@@ -47,7 +48,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("-n", "--node-name", default=e("NODE_NAME", ""))
     ap.add_argument("--namespace", default=e("OPERATOR_NAMESPACE", ""))
     ap.add_argument("-g", "--default-gpu-workload-config", default=e("DEFAULT_GPU_WORKLOAD_CONFIG", "vm-passthrough"))
-    ap.add_argument("--host-root", default=e("HOST_ROOT", "/host"))
+    ap.add_argument("--host-root", default=e("HOST_ROOT", mounts.path("/host")))
     ap.add_argument("--sys-root", default=e("AMD_SYSFS_ROOT", "/"))
     ap.add_argument("--dev-root", default=e("AMD_DEV_ROOT", "/"))
     ap.add_argument("--kubeconfig", default=e("KUBECONFIG", None))
@@ -57,7 +58,8 @@ def build_parser() -> argparse.ArgumentParser:
 def make_context(a, client=None) -> comp.Context:
     return comp.Context(
         status=S.StatusDir(a.output_dir), node_name=a.node_name, namespace=a.namespace, client=client,
-        host_root=a.host_root, sys_root=a.sys_root, dev_root=a.dev_root, with_wait=_bool(a.with_wait),
+        host_root=a.host_root, driver_root=mounts.path("/run/amd/driver"), sys_root=a.sys_root, dev_root=a.dev_root,
+        with_wait=_bool(a.with_wait),
         with_workload=_bool(a.with_workload), sleep_interval=a.sleep_interval_seconds,
         wait_timeout=a.wait_timeout_seconds, partition_strategy=a.partition_strategy,
         default_workload=a.default_gpu_workload_config)

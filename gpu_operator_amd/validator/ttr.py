@@ -198,15 +198,8 @@ class Harness:
         for d in (self.vdir, self.pdir, self.amd_root, os.path.dirname(self.cfg), self.bin, self.logs,
                   os.path.join(base, "cdi")):
             os.makedirs(d, exist_ok=True)
-        from ..cmd.entry import SCRIPTS
-        for name in SCRIPTS:
-            p = os.path.join(self.bin, name)
-            with open(p, "w") as f:
-                f.write(f'#!/bin/sh\nexec "{sys.executable}" -m gpu_operator_amd.cmd.entry {name} "$@"\n')
-            os.chmod(p, 0o755)
-        for name in ("amd-barrier-wait", "amd-hip-smoke", "amd-gemm-validate", "amd-rccl-validate"):
-            if os.path.exists(os.path.join(NATIVE_BIN, name)):
-                os.symlink(os.path.join(NATIVE_BIN, name), os.path.join(self.bin, name))
+        from ..cmd.entry import install_wrappers
+        install_wrappers(self.bin)
         # the API server (HTTP) with this node, and a kubeconfig for the agents
         from ..k8s.apiserver import FakeAPIServer
         from ..k8s.fake import FakeClient

@@ -202,7 +202,10 @@ def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict
     return results
 
 
-def emit(results: List[Dict], termination_log: Optional[str] = "/dev/termination-log") -> None:
+def emit(results: List[Dict], termination_log: Optional[str] = None) -> None:
+    if termination_log is None:
+        from ..utils import mounts
+        termination_log = mounts.path("/dev/termination-log")
     text = "\n".join(json.dumps(r, separators=(",", ":")) for r in results)
     print(text, flush=True)
     if termination_log and os.path.isdir(os.path.dirname(termination_log)):

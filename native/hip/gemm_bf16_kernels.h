@@ -358,7 +358,10 @@ __device__ __forceinline__ void w4_dma(uint32_t m0v, uint32_t voff, u32x4 rs, ui
                :: "s"(m0v), "v"(voff), "s"(rs), "s"(soff) : "memory");
 }
 
-template <class SC, int SERP = 0, bool ROT = false, bool SQ = false, bool ADMA = false>
+// STAG > 0: K-start stagger (hipBLASLt's StaggerU idea): co-resident workgroup j of an XCD starts
+// its K walk at K-tile (j % STAG) * ktiles / STAG and wraps, so the chip's simultaneous DMA
+// requests spread over STAG K-columns instead of one.
+template <class SC, int SERP = 0, bool ROT = false, bool SQ = false, bool ADMA = false, int STAG = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -483,7 +486,12 @@ gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ B
 
   const int ktiles = K / BK;        // >= 2 (host guarantees)
   const bool rev = SERP > 0 && (((int)blockIdx.x / NXCD) / (SERP > 0 ? SERP : 1)) & 1;
-  auto kof = [&](int kt) { return (rev ? ktiles - 1 - kt : kt) * BK; };
+  const int kst = STAG > 0 ? ((((int)blockIdx.x / NXCD) % (STAG > 0 ? STAG : 1)) * ktiles) / (STAG > 0 ? STAG : 1) : 0;
+  auto kof = [&](int kt) {
+    int k = (rev ? ktiles - 1 - kt : kt) + kst;
+    if (STAG > 0 && k >= ktiles) k -= ktiles;
+    return k * BK;
+  };
 #pragma unroll
   for (int i = 0; i < 16; ++i) dma_piece(i, kof(0), buf0);
 #pragma unroll

@@ -1,0 +1,60 @@
+"""The reference's end-to-end flow (tests/scripts/end-to-end.sh + checks.sh) executed on real
+processes: in-process HTTP API server with this repo's CRDs, the operator as its own process,
+the DaemonSet controller, and a kubelet that runs every pod on the node as OS processes
+(gpu_operator_amd/e2e). CPU rehearsal: fake sysfs with 8 GPUs, no GPU work
+(HIP_VALIDATION_MODE=skip); the MI355X run is tests/test_e2e_gpu.py.
+
+Steps (reference script -> here): install-operator.sh, verify-operator.sh (check_pod_ready for
+every operand), verify-operand-restarts.sh (check_no_restarts), install-workload.sh +
+verify-workload.sh (a pod with an amd.com/gpu limit, allocated through the device plugin's
+gRPC Allocate), update-clusterpolicy.sh (env and image version reach the DaemonSet and the
+restarted pod), checks.sh test_restart_operator (recovery within 100 s, no operand churn),
+disable-operands.sh / verify-disable-operands.sh, enable-operands.sh, uninstall-operator.sh.
+"""
+
+import os
+
+import pytest
+
+from gpu_operator_amd.devices import fakesys
+from gpu_operator_amd.e2e.harness import E2E
+from gpu_operator_amd.utils import mounts
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BARRIER = os.path.join(ROOT, "gpu_operator_amd", "_native", "bin", "amd-barrier-wait")
+
+
+@pytest.mark.skipif(not os.path.exists(BARRIER), reason="native binaries not built")
+def test_reference_end_to_end_flow_on_real_processes(tmp_path):
+    node = str(fakesys.make_node(tmp_path / "root", n_gpus=8))
+    r = E2E(sys_root=node, dev_root=node, hip_mode="skip", timeout=90).run()
+    assert r["ok"], r
+    names = [s["name"] for s in r["steps"]]
+    assert names == ["install-operator", "verify-operator", "verify-operand-restarts", "install+verify-workload",
+                     "update-clusterpolicy", "restart-operator", "disable-operands", "enable-operands", "uninstall"]
+    assert set(r["operands_ready"]) >= {"amd-container-toolkit-daemonset", "amd-device-plugin-daemonset",
+                                        "amd-node-labeller", "amd-metrics-exporter", "amd-operator-validator"}
+    st = {s["name"]: s for s in r["steps"]}
+    v = st["verify-operator"]["detail"]
+    assert {"host-driver-ready", "toolkit-ready", "hip-ready", "plugin-ready"} <= set(v["validations"])
+    assert v["amd.com/gpu"] == "8"                   # device plugin -> kubelet ListAndWatch -> Node
+    assert st["install+verify-workload"]["detail"]["phase"] == "Succeeded"
+    assert "allocated:" in st["install+verify-workload"]["detail"]["log_tail"]
+    assert r["operator_restart_recovery_s"] < 100
+    assert st["disable-operands"]["detail"]["terminated_processes"] >= 6
+    m = r["marks_s"]
+    # the node-side order the operator's states and the barriers impose
+    assert m["clusterpolicy:created"] <= m["amd-container-toolkit-daemonset-e2e-node:sandbox"] \
+        < m["amd-operator-validator-e2e-node:sandbox"]
+    assert r["time_to_ready_s"] < 30
+
+
+def test_mount_table_rewrites_container_paths_once():
+    pairs = sorted([("/run/amd", "/n/run/amd"), ("/run/amd/validations", "/v"), ("/host", "/h"),
+                    ("/bin/entrypoint.sh", "/cm/entrypoint.sh")], key=lambda p: len(p[0]), reverse=True)
+    assert mounts.translate("/run/amd/validations/x", pairs) == "/v/x"
+    assert mounts.translate("/run/amd/driver", pairs) == "/n/run/amd/driver"
+    assert mounts.translate("/run/amdx", pairs) == "/run/amdx"
+    text = 'cd /run/amd/validations && exec /bin/entrypoint.sh --root=/host $ROOT/run/amd "/run/amd"'
+    assert mounts.rewrite_text(text, pairs) == \
+        'cd /v && exec /cm/entrypoint.sh --root=/h $ROOT/run/amd "/n/run/amd"'
