@@ -186,6 +186,7 @@ def main(argv=None) -> int:
             extras.update(_allreduce_extra(ctx))
         if world == 1 and not cpu:
             extras.update(_time_to_ready_extra())
+            extras.update(_e2e_extra())
 
     if rank == 0:
         shape = f"{m}^3" if m == n == k else f"{m}x{n}x{k}"
@@ -369,6 +370,25 @@ def _time_to_ready_extra():
     errs = ours["errors"] + ref["errors"]
     if errs:
         out["time_to_ready_errors"] = "; ".join(errs)[:300]
+    return out
+
+
+def _e2e_extra():
+    """The reference's end-to-end flow on this box (gpu_operator_amd/e2e): ClusterPolicy created
+    -> operator process reconciles -> every operand pod Ready on the node (validator's HIP
+    workload pod included), then workload, update, operator-restart, disable/enable, uninstall.
+    Outside the timed region; reported as extras only."""
+    try:
+        from gpu_operator_amd.e2e.harness import E2E
+        r = E2E(sys_root="/", dev_root="/", hip_mode="pod", timeout=120).run()
+    except Exception as e:  # noqa: BLE001 - an extra must never fail the bench
+        return {"e2e_error": str(e)[:300]}
+    out = {"e2e_ok": r["ok"], "e2e_time_to_ready_s": r.get("time_to_ready_s"),
+           "e2e_reenable_time_to_ready_s": r.get("reenable_time_to_ready_s"),
+           "e2e_operator_restart_recovery_s": r.get("operator_restart_recovery_s"),
+           "e2e_steps_s": {s["name"]: s["seconds"] for s in r["steps"]}}
+    if not r["ok"]:
+        out["e2e_error"] = str(r.get("error"))[:300]
     return out
 
 

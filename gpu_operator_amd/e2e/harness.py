@@ -89,6 +89,7 @@ class E2E:
         self._stop = threading.Event()
         self.operator: Optional[subprocess.Popen] = None
         self.t0 = time.monotonic()
+        self.installed_at = 0.0
 
     # -- bookkeeping ---------------------------------------------------------------------------
     def mark(self, name: str, **_kw) -> None:
@@ -142,10 +143,13 @@ class E2E:
                 out += [d for d in yaml.safe_load_all(f) if d]
         return out
 
-    def cluster_policy(self) -> Dict:
+    def cluster_policy(self, sandbox: bool = False) -> Dict:
         with open(os.path.join(REPO, "config", "samples", "amd_v1_clusterpolicy.yaml")) as f:
             cp = yaml.safe_load(f)
         spec = cp["spec"]
+        if sandbox:
+            # end-to-end.sh's second install: sandboxWorkloads.enabled=true, defaultWorkload=container
+            spec["sandboxWorkloads"] = {"enabled": True, "defaultWorkload": "container"}
         spec.setdefault("driver", {})["enabled"] = False          # the host's preinstalled amdgpu
         v = spec.setdefault("validator", {})
         env = [{"name": "HIP_VALIDATION_MODE", "value": self.hip_mode}]
@@ -275,10 +279,12 @@ class E2E:
         return sorted(os.listdir(d)) if os.path.isdir(d) else []
 
     # -- the reference's steps -----------------------------------------------------------------
-    def install_operator(self) -> Dict:
-        self.t0 = time.monotonic()
-        self.backing.create(self.cluster_policy())
-        self.mark("clusterpolicy:created")
+    def install_operator(self, sandbox: bool = False) -> Dict:
+        if not sandbox:
+            self.t0 = time.monotonic()
+        self.installed_at = time.time()
+        self.backing.create(self.cluster_policy(sandbox))
+        self.mark("clusterpolicy:created" + (":sandbox" if sandbox else ""))
         self.start_operator()
         return {"operator_pid": self.operator.pid}
 
@@ -301,6 +307,10 @@ class E2E:
                     out[f] = json.load(fh)
             except (OSError, ValueError):
                 pass
+        # barriers survive in /run across installs (as on a node): this install must have rewritten them
+        stale = [f for f in ("hip-ready", "host-driver-ready") if (out.get(f) or {}).get("ts", 0) < self.installed_at]
+        if stale:
+            raise StepFailed(f"validation barriers not rewritten by this install: {stale}")
         labels = o.get_labels(self.backing.get("v1", "Node", self.node))
         out["gpu_labels"] = {k: v for k, v in labels.items()
                              if k.startswith("amd.com/gpu.") and not k.startswith("amd.com/gpu.deploy.")}
@@ -464,6 +474,13 @@ class E2E:
             en = self.step("enable-operands", self.enable_operands)
             self.result["reenable_time_to_ready_s"] = en["reenable_time_to_ready_s"]
             self.step("uninstall", self.uninstall)
+            # end-to-end.sh, second half: the operator with sandbox workloads enabled still serves
+            # container workloads (defaultWorkload=container)
+            self.step("install-operator[sandbox]", lambda: self.install_operator(sandbox=True))
+            sb = self.step("verify-operator[sandbox]", lambda: self.verify_operator("sandbox"))
+            self.result["sandbox_operands_ready"] = sb["daemonsets"]
+            self.step("install+verify-workload[sandbox]", self.install_and_verify_workload)
+            self.step("uninstall[sandbox]", self.uninstall)
         except Exception as e:  # noqa: BLE001 - reported in the result
             self.result["error"] = f"{type(e).__name__}: {e}"
             self.result["pods"] = {o.name(p): (p.get("status") or {}).get("phase")

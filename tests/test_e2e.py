@@ -31,7 +31,9 @@ def test_reference_end_to_end_flow_on_real_processes(tmp_path):
     assert r["ok"], r
     names = [s["name"] for s in r["steps"]]
     assert names == ["install-operator", "verify-operator", "verify-operand-restarts", "install+verify-workload",
-                     "update-clusterpolicy", "restart-operator", "disable-operands", "enable-operands", "uninstall"]
+                     "update-clusterpolicy", "restart-operator", "disable-operands", "enable-operands", "uninstall",
+                     "install-operator[sandbox]", "verify-operator[sandbox]", "install+verify-workload[sandbox]",
+                     "uninstall[sandbox]"]
     assert set(r["operands_ready"]) >= {"amd-container-toolkit-daemonset", "amd-device-plugin-daemonset",
                                         "amd-node-labeller", "amd-metrics-exporter", "amd-operator-validator"}
     st = {s["name"]: s for s in r["steps"]}
