@@ -362,7 +362,7 @@ def transform_toolkit(obj: Obj, spec: cp.ClusterPolicySpec, n) -> None:
 # device plugin (reference: TransformDevicePlugin :1187-1256, handleDevicePluginConfig)
 # ---------------------------------------------------------------------------------------------
 def _config_manager(obj: Obj, main: Obj, image: str, cm_name: str, default: str, label: str,
-                    mount_target: str, config_env: str) -> None:
+                    mount_target: str, config_env: str, process: str) -> None:
     """config-manager init + sidecar: pick the named config from a ConfigMap according to a
     node label, write it to a shared dir and signal the main process on change."""
     common_env = [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
@@ -373,7 +373,8 @@ def _config_manager(obj: Obj, main: Obj, image: str, cm_name: str, default: str,
                   {"name": "FALLBACK_STRATEGIES", "value": "named,single"},
                   {"name": "SEND_SIGNAL", "value": "true"},
                   {"name": "SIGNAL", "value": "1"},
-                  {"name": "PROCESS_TO_SIGNAL", "value": main.get("command", ["amd-device-plugin"])[0]}]
+                  # the program the entrypoint execs: the main container's command is `sh -c`
+                  {"name": "PROCESS_TO_SIGNAL", "value": process}]
     mounts = [{"name": "available-configs", "mountPath": "/available-configs"},
               {"name": "config", "mountPath": "/config"}]
     init = {"name": "config-manager-init", "image": image, "command": ["amd-config-manager"],
@@ -406,7 +407,7 @@ def transform_device_plugin(obj: Obj, spec: cp.ClusterPolicySpec, n) -> None:
     cfg = spec.devicePlugin.config
     if cfg is not None and cfg.name:
         _config_manager(obj, c, c["image"], cfg.name, cfg.default or "", C.DEVICE_PLUGIN_CONFIG_LABEL,
-                        "config.yaml", "CONFIG_FILE")
+                        "config.yaml", "CONFIG_FILE", "amd-device-plugin")
     set_runtime_class(obj, n.runtime, spec.operator.runtime_class())
 
 

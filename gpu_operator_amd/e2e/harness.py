@@ -90,6 +90,7 @@ class E2E:
         self.operator: Optional[subprocess.Popen] = None
         self.t0 = time.monotonic()
         self.installed_at = 0.0
+        self.expected_operands: List[str] = []
 
     # -- bookkeeping ---------------------------------------------------------------------------
     def mark(self, name: str, **_kw) -> None:
@@ -176,7 +177,7 @@ class E2E:
         self.bin = install_wrappers(os.path.join(self.base, "bin"))
         ns = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NS}}
         self.backing = FakeClient([ns, self._node_obj()] + self._crds(),
-                                  unserved_kinds={"ServiceMonitor", "PrometheusRule"})
+                                  unserved_kinds={"ServiceMonitor", "PrometheusRule"}, collect_orphans=True)
         self.api = FakeAPIServer(self.backing).start()
         self.kubeconfig = os.path.join(self.base, "kubeconfig")
         with open(self.kubeconfig, "w") as f:
@@ -257,6 +258,10 @@ class E2E:
                 if any(r.get("kind") == "DaemonSet" for r in p["metadata"].get("ownerReferences") or [])]
 
     def all_ready(self) -> Optional[Dict[str, int]]:
+        """ClusterPolicy ready and every scheduled operand DaemonSet rolled out and Ready; once the
+        first install has established the operand set, every one of those must be scheduled too
+        (a DaemonSet whose node label is not set yet has 0 desired pods and counts as ready for
+        the operator)."""
         if self.cp_state() != "ready":
             return None
         dss = self.operand_daemonsets()
@@ -272,6 +277,8 @@ class E2E:
                     st.get("updatedNumberScheduled") != st.get("desiredNumberScheduled"):
                 return None
             out[o.name(d)] = st["numberReady"]
+        if self.expected_operands and not set(self.expected_operands) <= set(out):
+            return None
         return out
 
     def validations(self) -> List[str]:
@@ -310,7 +317,13 @@ class E2E:
         # barriers survive in /run across installs (as on a node): this install must have rewritten them
         stale = [f for f in ("hip-ready", "host-driver-ready") if (out.get(f) or {}).get("ts", 0) < self.installed_at]
         if stale:
-            raise StepFailed(f"validation barriers not rewritten by this install: {stale}")
+            pods = {o.name(p): [p["metadata"].get("uid", "")[:8], (p.get("status") or {}).get("phase"),
+                                [c.get("type") + "=" + c.get("status") for c in (p.get("status") or {}).get("conditions") or []]]
+                    for p in self.operand_pods() if "validator" in o.name(p)}
+            dss = {o.name(d): d.get("status") for d in self.backing.list("apps/v1", "DaemonSet", NS)
+                   if "validator" in o.name(d)}
+            raise StepFailed(f"validation barriers not rewritten by this install: {stale}; pods {pods}; ds {dss}; "
+                             f"installed_at {self.installed_at:.3f} ts {[(f, (out.get(f) or {}).get('ts')) for f in stale]}")
         labels = o.get_labels(self.backing.get("v1", "Node", self.node))
         out["gpu_labels"] = {k: v for k, v in labels.items()
                              if k.startswith("amd.com/gpu.") and not k.startswith("amd.com/gpu.deploy.")}
@@ -396,6 +409,58 @@ class E2E:
         self._wait("the updated device plugin Ready", self.all_ready)
         return {"daemonset": name, "env_pid": pid}
 
+    def _alloc(self) -> int:
+        st = self.backing.get("v1", "Node", self.node).get("status") or {}
+        return int((st.get("allocatable") or {}).get(GPU, 0) or 0)
+
+    def _cp_update(self, fn) -> None:
+        cp = self.backing.get("amd.com/v1", "ClusterPolicy", CP_NAME)
+        fn(cp["spec"])
+        self.backing.update(cp)
+
+    def time_slicing(self, replicas: int = 10, pods: int = 5) -> Dict:
+        """update-clusterpolicy.sh's time-slicing test: a sharing config in a ConfigMap, named by
+        devicePlugin.config, multiplies the advertised amd.com/gpu; the labeller reports the
+        replicas and a -SHARED product; more GPU pods than physical GPUs all run; removing the config
+        restores the physical count."""
+        phys = self._alloc()
+        cfg = {"version": "v1", "sharing": {"timeSlicing": {"resources": [{"name": GPU, "replicas": replicas}]}}}
+        self.backing.create({"apiVersion": "v1", "kind": "ConfigMap",
+                             "metadata": {"name": "time-slicing-config", "namespace": NS},
+                             "data": {"any": yaml.safe_dump(cfg)}})
+        self._cp_update(lambda sp: sp.setdefault("devicePlugin", {}).update(
+            config={"name": "time-slicing-config", "default": "any"}))
+        self._wait(f"{GPU} x{replicas} advertised", lambda: self._alloc() == phys * replicas)
+
+        def shared_labels():
+            lb = o.get_labels(self.backing.get("v1", "Node", self.node))
+            return lb if lb.get("amd.com/gpu.replicas") == str(replicas) and \
+                lb.get("amd.com/gpu.product", "").endswith("-SHARED") else None
+        lb = self._wait("the labeller's replicas / -SHARED labels", shared_labels)
+        self._wait("the device plugin rollout", self.all_ready)
+        names = [f"time-slicing-{i}" for i in range(pods)]
+        for n in names:
+            pod = self.workload_pod()
+            pod["metadata"]["name"] = n
+            self.backing.create(pod)
+
+        def all_done():
+            ph = [(self.backing.get("v1", "Pod", n, "default").get("status") or {}).get("phase") for n in names]
+            if "Failed" in ph:
+                raise StepFailed(f"time-sliced pod failed: {ph}")
+            return ph if all(p == "Succeeded" for p in ph) else None
+        self._wait(f"{pods} time-sliced GPU pods to succeed", all_done)
+        for n in names:
+            self.backing.delete("v1", "Pod", n, "default")
+        self._cp_update(lambda sp: sp.get("devicePlugin", {}).pop("config", None))
+        self._wait(f"{GPU} back to the physical count", lambda: self._alloc() == phys)
+        self._wait("replicas label back to 1", lambda: o.get_labels(self.backing.get("v1", "Node", self.node))
+                   .get("amd.com/gpu.replicas") == "1")
+        self._wait("the device plugin rollout", self.all_ready)
+        return {"physical": phys, "advertised": phys * replicas, "pods": pods,
+                "labels": {k: lb[k] for k in ("amd.com/gpu.replicas", "amd.com/gpu.sharing-strategy",
+                                              "amd.com/gpu.product")}}
+
     def restart_operator(self) -> Dict:
         """checks.sh test_restart_operator: the operator pod is killed; its replacement must get
         the ClusterPolicy back to ready without churning the operands."""
@@ -465,9 +530,11 @@ class E2E:
             first = self.step("verify-operator", lambda: self.verify_operator("install"))
             self.result["time_to_ready_s"] = self.marks.get("install:ready")
             self.result["operands_ready"] = first["daemonsets"]
+            self.expected_operands = sorted(first["daemonsets"])
             self.step("verify-operand-restarts", self.verify_operand_restarts)
             self.step("install+verify-workload", self.install_and_verify_workload)
             self.step("update-clusterpolicy", self.update_clusterpolicy)
+            self.step("time-slicing", self.time_slicing)
             rs = self.step("restart-operator", self.restart_operator)
             self.result["operator_restart_recovery_s"] = rs["recovery_s"]
             self.step("disable-operands", self.disable_operands)

@@ -27,8 +27,13 @@ Interceptor = Callable[[str, str, str, Any], None]   # (verb, apiVersion, kind, 
 
 class FakeClient:
     def __init__(self, objs: Optional[List[Obj]] = None, server_version: str = "v1.29.2",
-                 unserved_kinds: Optional[Set[str]] = None):
+                 unserved_kinds: Optional[Set[str]] = None, collect_orphans: bool = False):
         self._lock = threading.RLock()
+        # collect_orphans: the garbage collector's other half -- an object created with owner
+        # references none of which exists (its owner was deleted while a controller was still
+        # writing it) is removed right after its creation. Off by default: unit tests build
+        # objects with synthetic owner uids.
+        self.collect_orphans = collect_orphans
         self._store: Dict[Tuple[str, str, str, str], Obj] = {}
         self._rv = itertools.count(1)
         self._watchers: List[Tuple[str, str, str, WatchCallback]] = []
@@ -108,7 +113,15 @@ class FakeClient:
             self._bump(obj)
             self._store[k] = obj
             out = copy.deepcopy(obj)
+            refs = [r.get("uid") for r in md.get("ownerReferences") or []]
+            orphan = self.collect_orphans and bool(refs) and not any(
+                (x.get("metadata") or {}).get("uid") in refs for x in self._store.values())
         self._notify(ADDED, out)
+        if orphan:
+            try:
+                self.delete(out["apiVersion"], out["kind"], md["name"], o.namespace(out))
+            except errors.NotFound:
+                pass
         return out
 
     def update(self, obj: Obj, _status: bool = False) -> Obj:

@@ -50,8 +50,21 @@ class ClusterSim:
     def sync(self) -> None:
         """One pass of DaemonSet controller + kubelet over every DaemonSet."""
         nodes = {o.name(n): n for n in self.client.list("v1", "Node")}
-        for ds in self.client.list("apps/v1", "DaemonSet"):
+        dss = self.client.list("apps/v1", "DaemonSet")
+        self._collect_orphans({d["metadata"]["uid"] for d in dss})
+        for ds in dss:
             self._sync_ds(ds, nodes)
+
+    def _collect_orphans(self, live_uids) -> None:
+        """The garbage collector's half: a pod whose controlling DaemonSet is gone is deleted
+        (a pass that raced the DaemonSet's deletion may have created it after the cascade)."""
+        for p in self.client.list("v1", "Pod"):
+            ref = o.controller_of(p)
+            if ref and ref.get("kind") == "DaemonSet" and ref.get("uid") not in live_uids:
+                try:
+                    self.client.delete("v1", "Pod", o.name(p), o.namespace(p))
+                except errors.NotFound:
+                    pass
 
     def _sync_ds(self, ds: Dict, nodes: Dict[str, Dict]) -> None:
         ns, name = o.namespace(ds), o.name(ds)
@@ -80,6 +93,13 @@ class ClusterSim:
                 except errors.NotFound:
                     pass
                 by_node.pop(node_name)
+        if want.difference(by_node):
+            try:                                   # never create pods for a DaemonSet being deleted
+                cur = self.client.get("apps/v1", "DaemonSet", name, ns)
+            except errors.NotFound:
+                return
+            if cur["metadata"].get("uid") != ds["metadata"]["uid"] or cur["metadata"].get("deletionTimestamp"):
+                return
         for node_name in sorted(want):
             if node_name in by_node:
                 continue

@@ -94,10 +94,13 @@ def find_pids(name: str, proc: str = "/proc") -> List[int]:
             continue
         if not argv or not argv[0]:
             continue
-        exe = os.path.basename(argv[0].decode(errors="replace"))
+        args = [a.decode(errors="replace") for a in argv if a]
+        exe = os.path.basename(args[0])
         # python console scripts: "python /usr/local/bin/<name> ..."
-        second = os.path.basename(argv[1].decode(errors="replace")) if len(argv) > 1 and argv[1] else ""
-        if exe == name or second == name:
+        second = os.path.basename(args[1]) if len(args) > 1 else ""
+        # the package's own runner: "python -m gpu_operator_amd.cmd.entry <name> ..."
+        runner = len(args) > 3 and args[1] == "-m" and args[2] == "gpu_operator_amd.cmd.entry" and args[3] == name
+        if exe == name or second == name or runner:
             out.append(int(d))
     return out
 

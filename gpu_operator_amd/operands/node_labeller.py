@@ -32,7 +32,8 @@ log = logging.getLogger("amd-node-labeller")
 PREFIX = "amd.com/gpu."
 OWNED = re.compile(r"^amd\.com/gpu\.(product|family|gfx|device-id|count|cu-count|simd-count|lds-kib|vram|"
                    r"compute-partition|memory-partition|partition\.capable|partition\.count|numa-nodes|"
-                   r"xgmi\.hive-id|xgmi\.links|xgmi\.fully-connected|driver-version)$")
+                   r"xgmi\.hive-id|xgmi\.links|xgmi\.fully-connected|driver-version|replicas|"
+                   r"sharing-strategy)$")
 NFD_FEATURE_FILE = "/etc/kubernetes/node-feature-discovery/features.d/amd-gpu"
 
 FAMILIES = models.GFX_FAMILY
@@ -96,6 +97,26 @@ def compute_labels(root: Optional[str] = None) -> Dict[str, str]:
     return labels
 
 
+def sharing_labels(node: Dict, want: Dict[str, str]) -> Dict[str, str]:
+    """Time-slicing as GFD reports it (``gpu.replicas``, ``gpu.sharing-strategy``, product
+    ``-SHARED``): read from what the device plugin actually advertises -- the Node's allocatable
+    ``amd.com/gpu`` over the GPU (partition) count -- rather than from a second copy of its config.
+    Nothing until the plugin has registered (allocatable absent or 0)."""
+    alloc = ((node.get("status") or {}).get("allocatable") or {}).get("amd.com/gpu")
+    try:
+        n, parts = int(alloc or 0), int(want.get(PREFIX + "partition.count", "0"))
+    except ValueError:
+        return {}
+    if n <= 0 or parts <= 0:
+        return {}
+    if n > parts and n % parts == 0:
+        out = {PREFIX + "replicas": str(n // parts), PREFIX + "sharing-strategy": "time-slicing"}
+        if want.get(PREFIX + "product"):
+            out[PREFIX + "product"] = sanitize(want[PREFIX + "product"][:56] + "-SHARED")
+        return out
+    return {PREFIX + "replicas": "1", PREFIX + "sharing-strategy": "none"}
+
+
 def label_patch(current: Dict[str, str], want: Dict[str, str]) -> Dict[str, Optional[str]]:
     patch: Dict[str, Optional[str]] = {k: v for k, v in want.items() if current.get(k) != v}
     for k in current:
@@ -105,7 +126,9 @@ def label_patch(current: Dict[str, str], want: Dict[str, str]) -> Dict[str, Opti
 
 
 def apply_node(client, node: str, want: Dict[str, str]) -> Dict[str, Optional[str]]:
-    cur = o.get_labels(client.get("v1", "Node", node))
+    obj = client.get("v1", "Node", node)
+    cur = o.get_labels(obj)
+    want = dict(want, **sharing_labels(obj, want))
     patch = label_patch(cur, want)
     if patch:
         client.patch("v1", "Node", node, {"metadata": {"labels": patch}})
@@ -144,6 +167,19 @@ def main(argv=None, client=None) -> int:
         client = RestClient()
     period = parse_duration(a.sleep_interval)
     stop = threading.Event()
+    kick = threading.Event()
+    if a.output == "node":
+        # re-label as soon as the advertised amd.com/gpu count changes (time-slicing replicas)
+        seen: Dict[str, Optional[str]] = {}
+
+        def on_node(ev):
+            if o.name(ev.obj) != a.node_name:
+                return
+            v = ((ev.obj.get("status") or {}).get("allocatable") or {}).get("amd.com/gpu")
+            if seen.get("v", "unset") != v:
+                seen["v"] = v
+                kick.set()
+        client.watch("v1", "Node", on_node)
     while not stop.is_set():
         try:
             want = compute_labels()
@@ -156,12 +192,14 @@ def main(argv=None, client=None) -> int:
         if a.oneshot:
             return 0
         # wake early when the partition manager (re)writes its barrier, else resync periodically
-        wait_for_change(os.path.join(a.barrier_dir, "partition-applied"), period, stop)
+        wait_for_change(os.path.join(a.barrier_dir, "partition-applied"), period, stop, kick)
     return 0
 
 
-def wait_for_change(path: str, period: float, stop: threading.Event) -> bool:
-    """Return True as soon as ``path`` is created or rewritten, False after ``period``."""
+def wait_for_change(path: str, period: float, stop: threading.Event,
+                    kick: Optional[threading.Event] = None) -> bool:
+    """Return True as soon as ``path`` is created or rewritten or ``kick`` is set, False after
+    ``period``."""
     def mtime():
         try:
             return os.stat(path).st_mtime_ns
@@ -172,13 +210,17 @@ def wait_for_change(path: str, period: float, stop: threading.Event) -> bool:
     step = 1.0
     waited = 0.0
     while waited < deadline and not stop.is_set():
+        if kick is not None and kick.is_set():
+            kick.clear()
+            return True
+        slice_ = min(step, deadline - waited)
         if start is None and os.path.isdir(os.path.dirname(path)):
-            # absent: block on inotify for its creation (bounded by the remaining period)
-            got = devices.wait_files(os.path.dirname(path), [os.path.basename(path)],
-                                     timeout=deadline - waited)
-            return bool(got)
-        stop.wait(step)
-        waited += step
+            # absent: block on inotify for its creation, a slice at a time so a kick is seen
+            if devices.wait_files(os.path.dirname(path), [os.path.basename(path)], timeout=slice_):
+                return True
+        else:
+            (kick or stop).wait(slice_)
+        waited += slice_
         if mtime() != start:
             return True
     return False

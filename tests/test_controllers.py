@@ -143,6 +143,9 @@ def test_device_plugin_custom_config_adds_config_manager():
     assert container(ds, "config-manager-init", init=True) is not None
     side = container(ds, "config-manager")
     assert env(side)["NODE_LABEL"] == C.DEVICE_PLUGIN_CONFIG_LABEL and env(side)["DEFAULT_CONFIG"] == "default"
+    # the plugin container runs `sh -c entrypoint.sh`, which execs amd-device-plugin: that is the
+    # process a config change must signal, not the shell
+    assert env(side)["PROCESS_TO_SIGNAL"] == "amd-device-plugin"
     assert env(container(ds, "amd-device-plugin"))["CONFIG_FILE"] == "/config/config.yaml"
     assert ds["spec"]["template"]["spec"]["shareProcessNamespace"] is True
 

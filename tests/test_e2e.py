@@ -31,7 +31,7 @@ def test_reference_end_to_end_flow_on_real_processes(tmp_path):
     assert r["ok"], r
     names = [s["name"] for s in r["steps"]]
     assert names == ["install-operator", "verify-operator", "verify-operand-restarts", "install+verify-workload",
-                     "update-clusterpolicy", "restart-operator", "disable-operands", "enable-operands", "uninstall",
+                     "update-clusterpolicy", "time-slicing", "restart-operator", "disable-operands", "enable-operands", "uninstall",
                      "install-operator[sandbox]", "verify-operator[sandbox]", "install+verify-workload[sandbox]",
                      "uninstall[sandbox]"]
     assert set(r["operands_ready"]) >= {"amd-container-toolkit-daemonset", "amd-device-plugin-daemonset",
@@ -42,6 +42,9 @@ def test_reference_end_to_end_flow_on_real_processes(tmp_path):
     assert v["amd.com/gpu"] == "8"                   # device plugin -> kubelet ListAndWatch -> Node
     assert st["install+verify-workload"]["detail"]["phase"] == "Succeeded"
     assert "allocated:" in st["install+verify-workload"]["detail"]["log_tail"]
+    ts = st["time-slicing"]["detail"]
+    assert ts["advertised"] == 80 and ts["labels"]["amd.com/gpu.replicas"] == "10"
+    assert ts["labels"]["amd.com/gpu.product"].endswith("-SHARED")
     assert r["operator_restart_recovery_s"] < 100
     assert st["disable-operands"]["detail"]["terminated_processes"] >= 6
     m = r["marks_s"]

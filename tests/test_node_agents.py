@@ -374,3 +374,32 @@ def test_metrics_pod_attribution(spx, tmp_path):
         assert s["2"]["pod"] == "train-0" and s["2"]["namespace"] == "ml" and s["0"]["pod"] == ""
     finally:
         srv.stop(0)
+
+
+def test_labeller_sharing_labels_follow_advertised_replicas(spx):
+    """GFD's gpu.replicas / sharing-strategy / product -SHARED, read from what the device plugin
+    advertises (allocatable amd.com/gpu over the partition count)."""
+    want = nl.compute_labels(spx)
+    parts = int(want["amd.com/gpu.partition.count"])
+    node = lambda n: {"status": {"allocatable": {"amd.com/gpu": str(n)}}}  # noqa: E731
+    assert nl.sharing_labels({"status": {}}, want) == {}                    # plugin not registered yet
+    assert nl.sharing_labels(node(parts), want) == {"amd.com/gpu.replicas": "1",
+                                                     "amd.com/gpu.sharing-strategy": "none"}
+    s = nl.sharing_labels(node(parts * 10), want)
+    assert s["amd.com/gpu.replicas"] == "10" and s["amd.com/gpu.sharing-strategy"] == "time-slicing"
+    assert s["amd.com/gpu.product"].endswith("-SHARED")
+    # both labels are owned: dropping sharing removes/reverts them
+    assert nl.OWNED.match("amd.com/gpu.replicas") and nl.OWNED.match("amd.com/gpu.sharing-strategy")
+
+
+def test_config_manager_finds_the_plugin_under_any_launcher(tmp_path):
+    from gpu_operator_amd.operands import config_manager as cm
+    proc = tmp_path / "proc"
+    for pid, argv in {"11": ["/usr/bin/python3", "/usr/local/bin/amd-device-plugin", "--x"],
+                      "12": ["amd-device-plugin"],
+                      "13": ["/usr/bin/python3", "-m", "gpu_operator_amd.cmd.entry", "amd-device-plugin"],
+                      "14": ["/bin/sh", "-c", "/bin/entrypoint.sh"],
+                      "15": ["/usr/bin/python3", "-m", "gpu_operator_amd.cmd.entry", "amd-node-labeller"]}.items():
+        (proc / pid).mkdir(parents=True)
+        (proc / pid / "cmdline").write_bytes(b"\0".join(a.encode() for a in argv) + b"\0")
+    assert sorted(cm.find_pids("amd-device-plugin", str(proc))) == [11, 12, 13]
