@@ -65,7 +65,12 @@ def main(argv=None) -> int:
     # leader election keeps reading Leases from the API server itself
     client = api if a.no_cache else CachedClient(api)
     metrics = OperatorMetrics()
-    mgr = Manager(api, namespace, registry=metrics.registry, metrics_addr=a.metrics_bind_address,
+    # controllers watch through the same informers the reconcilers read from (controller-runtime's
+    # event handlers sit on the cache's informers): with a separate watch stream an event could
+    # trigger a reconcile that still reads the pre-event object from the cache, and the cache's
+    # own copy of that event would then trigger nothing -- a lost update (found by the e2e flow:
+    # a node's deploy.operands=true after a disable was never acted on)
+    mgr = Manager(client, namespace, registry=metrics.registry, metrics_addr=a.metrics_bind_address,
                   probe_addr=a.health_probe_bind_address, leader_elect=a.leader_elect,
                   lease_duration=parse_duration(a.leader_lease_duration),
                   renew_deadline=parse_duration(a.leader_lease_renew_deadline),

@@ -218,7 +218,8 @@ class E2E:
         self.operator = subprocess.Popen(
             [os.path.join(self.bin, "amd-gpu-operator"), "--kubeconfig", self.kubeconfig,
              "--metrics-bind-address", f"127.0.0.1:{self.metrics_port}",
-             "--health-probe-bind-address", f"127.0.0.1:{self.health_port}"],
+             "--health-probe-bind-address", f"127.0.0.1:{self.health_port}",
+             "--zap-log-level", os.environ.get("AMD_E2E_OPERATOR_LOG_LEVEL", "info")],
             env=env, stdout=logf, stderr=subprocess.STDOUT, start_new_session=True)
         logf.close()
         return self.operator
@@ -423,7 +424,8 @@ class E2E:
         devicePlugin.config, multiplies the advertised amd.com/gpu; the labeller reports the
         replicas and a -SHARED product; more GPU pods than physical GPUs all run; removing the config
         restores the physical count."""
-        phys = self._alloc()
+        # the plugin re-registers after each rollout: its count is 0 until the kubelet has it again
+        phys = self._wait(f"{GPU} advertised", lambda: self._alloc() or None)
         cfg = {"version": "v1", "sharing": {"timeSlicing": {"resources": [{"name": GPU, "replicas": replicas}]}}}
         self.backing.create({"apiVersion": "v1", "kind": "ConfigMap",
                              "metadata": {"name": "time-slicing-config", "namespace": NS},

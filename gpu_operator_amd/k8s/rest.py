@@ -250,6 +250,7 @@ class RestClient:
                     if not rv:
                         body = self._request("GET", self._path(api_version, kind, namespace)).json()
                         rv = body["metadata"]["resourceVersion"]
+                        log.debug("watch %s: list at rv=%s (%d items)", kind, rv, len(body.get("items", [])))
                         fresh = {}
                         for it in body.get("items", []):
                             it.setdefault("apiVersion", api_version)
@@ -280,6 +281,7 @@ class RestClient:
                         if t == "BOOKMARK":
                             continue
                         k = (o.namespace(obj), o.name(obj))
+                        log.debug("watch %s: %s %s rv=%s", kind, t, o.name(obj), rv)
                         old = known.get(k)
                         if t == DELETED:
                             known.pop(k, None)

@@ -62,7 +62,10 @@ class Controller:
         def on_event(ev: WatchEvent) -> None:
             try:
                 if w.predicate is not None and not w.predicate(ev):
+                    log.debug("%s: %s %s %s filtered", self.name, ev.type, w.kind, (ev.obj.get("metadata") or {}).get("name"))
                     return
+                log.debug("%s: %s %s %s rv=%s", self.name, ev.type, w.kind, (ev.obj.get("metadata") or {}).get("name"),
+                          (ev.obj.get("metadata") or {}).get("resourceVersion"))
                 for req in w.mapper(ev):
                     self.queue.add(req)
             except Exception:  # noqa: BLE001 - a bad event must not kill the watch
