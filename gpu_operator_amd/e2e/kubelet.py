@@ -216,7 +216,9 @@ class PodRun:
             if "hostPath" in v:
                 hp = self.kl.host_path(v["hostPath"]["path"])
                 t = v["hostPath"].get("type", "")
-                if t in ("DirectoryOrCreate", "Directory", "") and not os.path.splitext(hp)[1]:
+                # directories are created in the node tree only; /sys and /dev are the machine's
+                if t in ("DirectoryOrCreate", "Directory", "") and not os.path.splitext(hp)[1] and \
+                        hp.startswith(self.kl.host):
                     os.makedirs(hp, exist_ok=True)
                 out[name] = (hp, v)
             elif "configMap" in v:
