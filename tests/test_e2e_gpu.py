@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+@pytest.mark.timeout(400)
 def test_reference_end_to_end_flow_on_mi355x():
     r = E2E(sys_root="/", dev_root="/", hip_mode="pod", timeout=150).run()
     assert r["ok"], {k: v for k, v in r.items() if k != "marks_s"}
