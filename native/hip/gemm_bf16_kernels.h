@@ -361,7 +361,10 @@ __device__ __forceinline__ void w4_dma(uint32_t m0v, uint32_t voff, u32x4 rs, ui
 // STAG > 0: K-start stagger (hipBLASLt's StaggerU idea): co-resident workgroup j of an XCD starts
 // its K walk at K-tile (j % STAG) * ktiles / STAG and wraps, so the chip's simultaneous DMA
 // requests spread over STAG K-columns instead of one.
-template <class SC, int SERP = 0, bool ROT = false, bool SQ = false, bool ADMA = false, int STAG = 0>
+// BOUT: B-outer MFMA order -- the B fragment (srcA) stays for 8 consecutive MFMAs while the A
+// fragment (srcB) changes, hipBLASLt's operand order; the kk0 reads follow (b0, a0..a7, b1..b7).
+template <class SC, int SERP = 0, bool ROT = false, bool SQ = false, bool ADMA = false, int STAG = 0,
+          bool BOUT = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -434,10 +437,12 @@ gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   W4Frags R0, R1;
   char* const buf0 = smem;
   char* const buf1 = smem + BUF_BYTES;
-  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {      // w4_isb order
+  auto read_frag = [&](W4Frags& F, const char* buf, int kk, auto J) {      // consumption order
     constexpr int j = decltype(J)::value;
-    constexpr int x = w4_idx(j);
-    if constexpr (w4_isb(j))
+    // A-outer (w4_isb): a0, b0..b7, a1..a7; B-outer: b0, a0..a7, b1..b7
+    constexpr bool isb = BOUT ? (j == 0 || j >= 9) : w4_isb(j);
+    constexpr int x = BOUT ? (j == 0 ? 0 : (j <= 8 ? j - 1 : j - 8)) : w4_idx(j);
+    if constexpr (isb)
       F.b[x] = *reinterpret_cast<const bf16x8*>(buf + b_off + x * 16 * ROW_BYTES + lane_off[kk]);
     else
       F.a[x] = *reinterpret_cast<const bf16x8*>(buf + a_off + x * 16 * ROW_BYTES + lane_off[kk]);
@@ -457,17 +462,14 @@ gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ B
       constexpr int i = decltype(I)::value;
       constexpr int jr1 = w4t_r1_at<SC>(i), jdma = w4t_dma_at<SC>(i), jr0 = w4t_r0_at<SC>(i);
       constexpr bool fused = ADMA && dm && jdma >= 0;
-      if constexpr (fused) {
-        if constexpr (i < 64)
-          w4_mfma_dma<i>(R0.b[i & 7], R0.a[i >> 3], dma_m0(jdma, cur), voff, jdma >= 8 ? sB : sA, dma_soff(jdma, dk));
-        else
-          w4_mfma_dma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3], dma_m0(jdma, cur), voff, jdma >= 8 ? sB : sA,
-                              dma_soff(jdma, dk));
-      } else if constexpr (i < 64) {
-        w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
-      } else {
-        w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
-      }
+      constexpr int s64 = i & 63;
+      constexpr int ai = BOUT ? (s64 & 7) : (s64 >> 3), bi = BOUT ? (s64 >> 3) : (s64 & 7);
+      constexpr int acc = ai * 8 + bi;                     // accumulator m*8+n (the epilogue's order)
+      W4Frags& F = i < 64 ? R0 : R1;
+      if constexpr (fused)
+        w4_mfma_dma<acc>(F.b[bi], F.a[ai], dma_m0(jdma, cur), voff, jdma >= 8 ? sB : sA, dma_soff(jdma, dk));
+      else
+        w4_mfma<acc>(F.b[bi], F.a[ai]);
       if constexpr (jr1 >= 0) read_r1(cur, std::integral_constant<int, jr1>{});
       if constexpr (i == SC::wa || (split && i == SC::wb)) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
       if constexpr (dm && (i == SC::ba || (split && i == SC::bb))) __builtin_amdgcn_s_barrier();

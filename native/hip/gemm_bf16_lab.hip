@@ -1129,6 +1129,10 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
   } else if (v == 45 && kk && (M / BM) % 16 == 0 && (N / BN) % 16 == 0) {
     hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
                        0, s, a, b, c, M, N, K);
+  } else if ((v == 70 || v == 71) && kk) {            // w4t, B-outer MFMA operand order
+    auto kern = v == 70 ? gemm_bf16_256x256_w4t<W4SchedV18, 32, true, false, false, 0, true>
+                        : gemm_bf16_256x256_w4t<W4SchedSplit, 32, true, false, false, 0, true>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
   } else if (v >= 67 && v <= 69 && kk) {            // w4t v18 schedule + K-start stagger
     auto kern = v == 67 ? gemm_bf16_256x256_w4t<W4SchedV18, 0, true, false, false, 8>
               : v == 68 ? gemm_bf16_256x256_w4t<W4SchedV18, 32, true, false, false, 4>
