@@ -41,7 +41,7 @@ import tempfile
 import threading
 import time
 import urllib.request
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import yaml
 
@@ -129,13 +129,17 @@ class E2E:
             log.info("step %s: %s (%.2fs)", name, "ok" if rec.get("ok") else rec.get("error"), rec["seconds"])
 
     # -- cluster -------------------------------------------------------------------------------
-    def _node_obj(self) -> Dict:
+    def node_specs(self) -> List[Tuple[str, str, str]]:
+        """(node name, sysfs root, dev root) of every node this harness runs a kubelet for."""
+        return [(self.node, self.sys_root, self.dev_root)]
+
+    def _node_obj(self, name: str) -> Dict:
         labels = {"feature.node.kubernetes.io/pci-1002.present": "true",
                   "feature.node.kubernetes.io/kernel-version.full": os.uname().release,
                   "feature.node.kubernetes.io/system-os_release.ID": "ubuntu",
                   "feature.node.kubernetes.io/system-os_release.VERSION_ID": "22.04",
-                  "kubernetes.io/hostname": self.node}
-        return {"apiVersion": "v1", "kind": "Node", "metadata": {"name": self.node, "labels": labels},
+                  "kubernetes.io/hostname": name}
+        return {"apiVersion": "v1", "kind": "Node", "metadata": {"name": name, "labels": labels},
                 "status": {"capacity": {}, "allocatable": {},
                            "nodeInfo": {"containerRuntimeVersion": "containerd://1.7.13",
                                         "kernelVersion": os.uname().release}}}
@@ -179,7 +183,8 @@ class E2E:
         os.makedirs(self.base)
         self.bin = install_wrappers(os.path.join(self.base, "bin"))
         ns = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NS}}
-        self.backing = FakeClient([ns, self._node_obj()] + self._crds(),
+        nodes = [self._node_obj(n) for n, _, _ in self.node_specs()]
+        self.backing = FakeClient([ns] + nodes + self._crds(),
                                   unserved_kinds={"ServiceMonitor", "PrometheusRule"}, collect_orphans=True)
         self.api = FakeAPIServer(self.backing).start()
         self.kubeconfig = os.path.join(self.base, "kubeconfig")
@@ -203,8 +208,14 @@ class E2E:
             # what it can open, as an unprivileged container on such a node would
             "DRIVER_VALIDATION_STRICT": "false",
         })
-        self.kubelet = ProcessKubelet(self.backing, self.node, self.base, self.env, self.sys_root, self.dev_root,
-                                      events=self.mark).start()
+        specs = self.node_specs()
+        self.kubelets = []
+        for name, sys_root, dev_root in specs:
+            env = dict(self.env, AMD_SYSFS_ROOT=sys_root, AMD_DEV_ROOT=dev_root)
+            base = self.base if len(specs) == 1 else os.path.join(self.base, name)
+            self.kubelets.append(ProcessKubelet(self.backing, name, base, env, sys_root, dev_root,
+                                                events=self.mark).start())
+        self.kubelet = self.kubelets[0]
         self.dsc = ClusterSim(self.backing, kubelet=False)
 
         def ds_controller():
@@ -245,7 +256,8 @@ class E2E:
     def teardown(self) -> None:
         self._stop.set()
         self.stop_operator()
-        self.kubelet.stop()
+        for k in self.kubelets:
+            k.stop()
         self.api.stop()
         if not self.keep:
             shutil.rmtree(self.base, ignore_errors=True)
@@ -576,6 +588,126 @@ class E2E:
         return self.result
 
 
+class MultiNodeE2E(E2E):
+    """The same stack over N nodes on one machine (CPU rehearsal): one process kubelet per node,
+    each on its own fake sysfs with ``gpus`` GPUs. What the single-node flow cannot show: the
+    operator fanning its DaemonSets out over nodes, per-node scheduling of GPU pods, and a
+    per-node operands switch (``deploy.operands=false`` on one node) leaving the other nodes'
+    pods untouched. The reference has no multi-node test at all."""
+
+    def __init__(self, nodes: int = 3, gpus: int = 8, **kw):
+        kw.setdefault("hip_mode", "skip")
+        super().__init__(**kw)
+        self.n_nodes, self.gpus = nodes, gpus
+        self.names = [f"{self.node}-{i}" for i in range(nodes)]
+
+    def node_specs(self) -> List[Tuple[str, str, str]]:
+        from ..devices import fakesys
+        out = []
+        for n in self.names:
+            root = str(fakesys.make_node(os.path.join(self.wd, "sys", n), n_gpus=self.gpus))
+            out.append((n, root, root))
+        return out
+
+    def cluster_policy(self, sandbox: bool = False) -> Dict:
+        cp = super().cluster_policy(sandbox)
+        # one host, many nodes: every exporter binds an ephemeral port (no pod network namespaces)
+        for e in cp["spec"]["metricsExporter"]["env"]:
+            if e["name"] == "METRICS_EXPORTER_LISTEN":
+                e["value"] = "127.0.0.1:0"
+        return cp
+
+    def _pods_by_node(self) -> Dict[str, Dict[str, str]]:
+        out: Dict[str, Dict[str, str]] = {n: {} for n in self.names}
+        for p in self.operand_pods():
+            out.setdefault(p["spec"].get("nodeName", ""), {})[o.name(p)] = p["metadata"]["uid"]
+        return out
+
+    def verify_nodes(self) -> Dict:
+        ready = self._wait("every operand pod Ready on every node", self.all_ready)
+        per = {}
+        for k in self.kubelets:
+            files = os.listdir(k.host_path("/run/amd/validations"))
+            alloc = ((self.backing.get("v1", "Node", k.node).get("status") or {}).get("allocatable") or {}).get(GPU)
+            if not {"toolkit-ready", "hip-ready", "plugin-ready"} <= set(files) or alloc != str(self.gpus):
+                raise StepFailed(f"node {k.node}: validations {sorted(files)}, {GPU}={alloc}")
+            per[k.node] = {GPU: alloc, "validations": len(files)}
+        if any(v != self.n_nodes for v in ready.values()):
+            raise StepFailed(f"operand DaemonSets not on every node: {ready}")
+        return {"daemonsets": ready, "nodes": per}
+
+    def workload_per_node(self) -> Dict:
+        names = []
+        for n in self.names:
+            pod = self.workload_pod()
+            pod["metadata"]["name"] = f"gpu-test-{n}"
+            pod["spec"]["nodeSelector"] = {"kubernetes.io/hostname": n}
+            self.backing.create(pod)
+            names.append(pod["metadata"]["name"])
+
+        def done():
+            ps = [self.backing.get("v1", "Pod", x, "default") for x in names]
+            if any((p.get("status") or {}).get("phase") == "Failed" for p in ps):
+                raise StepFailed("a workload pod failed")
+            return ps if all((p.get("status") or {}).get("phase") == "Succeeded" for p in ps) else None
+        ps = self._wait("one GPU pod per node to succeed", done)
+        placed = {o.name(p): p["spec"]["nodeName"] for p in ps}
+        if sorted(placed.values()) != sorted(self.names):
+            raise StepFailed(f"pods not spread one per node: {placed}")
+        for x in names:
+            self.backing.delete("v1", "Pod", x, "default")
+        return placed
+
+    def disable_one_node(self) -> Dict:
+        target, others = self.names[0], self.names[1:]
+        before = self._pods_by_node()
+        self.backing.patch("v1", "Node", target, {"metadata": {"labels": {OPERANDS_LABEL: "false"}}})
+        self._wait(f"operand pods gone from {target}", lambda: not self._pods_by_node().get(target))
+        time.sleep(1.0)
+        after = self._pods_by_node()
+        touched = [n for n in others if after.get(n) != before.get(n)]
+        if touched:
+            raise StepFailed(f"disabling {target} touched the pods of {touched}")
+        self.backing.patch("v1", "Node", target, {"metadata": {"labels": {OPERANDS_LABEL: "true"}}})
+        t = time.monotonic()
+        self._wait(f"{target} back", lambda: self.all_ready() and len(self._pods_by_node().get(target, {})) ==
+                   len(before[target]))
+        return {"node": target, "untouched": others, "reenable_s": round(time.monotonic() - t, 3)}
+
+    def uninstall_all(self) -> Dict:
+        self.backing.delete("amd.com/v1", "ClusterPolicy", CP_NAME)
+        self._wait("operand pods gone", lambda: not self.operand_pods())
+        self._wait("every node process gone", lambda: not any(k.all_pids() for k in self.kubelets), timeout=30)
+        self.stop_operator()
+        return {"ok": True}
+
+    def run(self) -> Dict[str, Any]:
+        self.setup()
+        try:
+            self.step("install-operator", self.install_operator)
+            first = self.step("verify-operator", self.verify_nodes)
+            self.mark("install:ready")
+            self.result["time_to_ready_s"] = self.marks.get("install:ready")
+            self.result["operands_ready"] = first["daemonsets"]
+            self.expected_operands = sorted(first["daemonsets"])
+            self.step("verify-operand-restarts", self.verify_operand_restarts)
+            self.step("workload-per-node", self.workload_per_node)
+            rs = self.step("restart-operator", self.restart_operator)
+            self.result["operator_restart_recovery_s"] = rs["recovery_s"]
+            self.step("disable-one-node", self.disable_one_node)
+            self.step("uninstall", self.uninstall_all)
+        except Exception as e:  # noqa: BLE001 - reported in the result
+            self.result["error"] = f"{type(e).__name__}: {e}"
+            self.result["logs_dir"] = self.base
+            self.keep = True
+        finally:
+            self.teardown()
+        self.result.update(ok=all(s.get("ok") for s in self.steps) and "error" not in self.result,
+                           steps=self.steps, nodes=self.n_nodes, gpus_per_node=self.gpus,
+                           marks_s=dict(sorted(self.marks.items(), key=lambda kv: kv[1])))
+        return self.result
+
+
 def main(argv=None) -> int:
     import argparse
     ap = argparse.ArgumentParser(prog="python -m gpu_operator_amd.e2e")
@@ -585,8 +717,13 @@ def main(argv=None) -> int:
     ap.add_argument("--fake-gpus", type=int, default=0, help="run on a fake sysfs with N GPUs (CPU rehearsal)")
     ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--nodes", type=int, default=1, help="N > 1: that many nodes on fake sysfs (CPU rehearsal)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    if a.nodes > 1:
+        r = MultiNodeE2E(nodes=a.nodes, gpus=a.fake_gpus or 8, timeout=a.timeout, keep=a.keep).run()
+        print(json.dumps(r, default=str))
+        return 0 if r["ok"] else 1
     sys_root, dev_root = a.sys_root, a.dev_root
     if a.fake_gpus:
         from ..devices import fakesys

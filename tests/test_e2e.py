@@ -63,3 +63,18 @@ def test_mount_table_rewrites_container_paths_once():
     text = 'cd /run/amd/validations && exec /bin/entrypoint.sh --root=/host $ROOT/run/amd "/run/amd"'
     assert mounts.rewrite_text(text, pairs) == \
         'cd /v && exec /cm/entrypoint.sh --root=/h $ROOT/run/amd "/n/run/amd"'
+
+
+@pytest.mark.skipif(not os.path.exists(BARRIER), reason="native binaries not built")
+def test_three_node_cluster_on_real_processes():
+    """One operator, three nodes (a process kubelet each, fake sysfs with 8 GPUs each): every
+    operand DaemonSet fans out to all nodes, one GPU pod per node lands on its node, and
+    deploy.operands=false on one node leaves the other nodes' operand pods untouched."""
+    from gpu_operator_amd.e2e.harness import MultiNodeE2E
+    r = MultiNodeE2E(nodes=3, gpus=8, timeout=90).run()
+    assert r["ok"], r
+    assert all(v == 3 for v in r["operands_ready"].values()), r["operands_ready"]
+    st = {s["name"]: s for s in r["steps"]}
+    assert sorted(st["workload-per-node"]["detail"].values()) == ["e2e-node-0", "e2e-node-1", "e2e-node-2"]
+    d = st["disable-one-node"]["detail"]
+    assert d["node"] == "e2e-node-0" and d["untouched"] == ["e2e-node-1", "e2e-node-2"]
