@@ -73,7 +73,14 @@ class StepFailed(AssertionError):
 class E2E:
     def __init__(self, workdir: Optional[str] = None, sys_root: str = "/", dev_root: str = "/",
                  hip_mode: str = "pod", timeout: float = 240.0, node: str = "e2e-node",
-                 workload_cmd: Optional[List[str]] = None, keep: bool = False):
+                 workload_cmd: Optional[List[str]] = None, keep: bool = False, driver: str = "host"):
+        """``driver="container"``: the driver DaemonSet installs amdgpu (CPU rehearsal only: a fake
+        sysfs without the module and the simulated kernel of devices/fakekernel.py on PATH)."""
+        if driver not in ("host", "container"):
+            raise ValueError(driver)
+        if driver == "container" and os.path.realpath(sys_root) == "/":
+            raise ValueError("the driver-container flow needs a fake sysfs (it loads a simulated amdgpu)")
+        self.driver = driver
         # unix socket paths (kubelet.sock, plugin endpoints) must stay under 108 bytes: short base
         self.wd = workdir or tempfile.mkdtemp(prefix="amd-e2e-", dir="/tmp" if os.path.isdir("/tmp") else None)
         self.sys_root, self.dev_root = sys_root, dev_root
@@ -155,10 +162,13 @@ class E2E:
         with open(os.path.join(REPO, "config", "samples", "amd_v1_clusterpolicy.yaml")) as f:
             cp = yaml.safe_load(f)
         spec = cp["spec"]
+        if self.driver == "container":
+            spec.setdefault("driver", {})["enabled"] = True
         if sandbox:
             # end-to-end.sh's second install: sandboxWorkloads.enabled=true, defaultWorkload=container
             spec["sandboxWorkloads"] = {"enabled": True, "defaultWorkload": "container"}
-        spec.setdefault("driver", {})["enabled"] = False          # the host's preinstalled amdgpu
+        if self.driver == "host":
+            spec.setdefault("driver", {})["enabled"] = False      # the host's preinstalled amdgpu
         v = spec.setdefault("validator", {})
         env = [{"name": "HIP_VALIDATION_MODE", "value": self.hip_mode}]
         v.setdefault("hip", {})["env"] = list(env)
@@ -182,6 +192,9 @@ class E2E:
         shutil.rmtree(self.base, ignore_errors=True)
         os.makedirs(self.base)
         self.bin = install_wrappers(os.path.join(self.base, "bin"))
+        if self.driver == "container":
+            from ..devices import fakekernel
+            fakekernel.install_tools(self.bin)
         ns = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NS}}
         nodes = [self._node_obj(n) for n, _, _ in self.node_specs()]
         self.backing = FakeClient([ns] + nodes + self._crds(),
@@ -214,7 +227,8 @@ class E2E:
             env = dict(self.env, AMD_SYSFS_ROOT=sys_root, AMD_DEV_ROOT=dev_root)
             base = self.base if len(specs) == 1 else os.path.join(self.base, name)
             self.kubelets.append(ProcessKubelet(self.backing, name, base, env, sys_root, dev_root,
-                                                events=self.mark).start())
+                                                events=self.mark, image_env=self.image_env,
+                                                host_links={} if self.driver == "container" else None).start())
         self.kubelet = self.kubelets[0]
         self.dsc = ClusterSim(self.backing, kubelet=False)
 
@@ -228,6 +242,14 @@ class E2E:
         self._dsc_thread = threading.Thread(target=ds_controller, name="ds-controller", daemon=True)
         self._dsc_thread.start()
         self.metrics_port, self.health_port = _free_port(), _free_port()
+
+    @staticmethod
+    def image_env(image: str) -> Dict[str, str]:
+        """The ENV an image's config carries (docker/Dockerfile.driver: DRIVER_VERSION)."""
+        repo, _, tag = image.rpartition(":")
+        if repo.endswith("amdgpu-driver") and tag:
+            return {"DRIVER_VERSION": tag.split("-")[0]}
+        return {}
 
     def start_operator(self) -> subprocess.Popen:
         env = dict(self.env, OPERATOR_NAMESPACE=NS)
@@ -335,7 +357,16 @@ class E2E:
             except (OSError, ValueError):
                 pass
         # barriers survive in /run across installs (as on a node): this install must have rewritten them
-        stale = [f for f in ("hip-ready", "host-driver-ready") if (out.get(f) or {}).get("ts", 0) < self.installed_at]
+        for f in ("driver-ready",):
+            try:
+                with open(os.path.join(self.kubelet.host_path("/run/amd/validations"), f)) as fh:
+                    out[f] = json.load(fh)
+            except (OSError, ValueError):
+                pass
+        drv = "driver-ready" if self.driver == "container" else "host-driver-ready"
+        if drv not in out:
+            raise StepFailed(f"{drv} missing: {files}")
+        stale = [f for f in ("hip-ready", drv) if (out.get(f) or {}).get("ts", 0) < self.installed_at]
         if stale:
             pods = {o.name(p): [p["metadata"].get("uid", "")[:8], (p.get("status") or {}).get("phase"),
                                 [c.get("type") + "=" + c.get("status") for c in (p.get("status") or {}).get("conditions") or []]]
@@ -482,6 +513,55 @@ class E2E:
                 "labels": {k: lb[k] for k in ("amd.com/gpu.replicas", "amd.com/gpu.sharing-strategy",
                                               "amd.com/gpu.product")}}
 
+    def _module_version(self) -> Optional[str]:
+        try:
+            with open(os.path.join(self.sys_root, "sys/module/amdgpu/version")) as f:
+                return f.read().strip()
+        except OSError:
+            return None
+
+    def driver_upgrade(self, new_version: str = "6.12.13") -> Dict:
+        """driver.version bump with autoUpgrade: the upgrade controller's state machine drives the
+        node (cordon, evict the GPU pod, delete the driver pod, the new driver container unloads
+        and loads amdgpu, validation, uncordon) -- the reference's test_image_updates, where the
+        driver pod is deleted by hand, done by the operator itself."""
+        from ..controllers.upgrade import DONE, UPGRADE_STATE_LABEL
+        # a controller-managed GPU pod (kubectl-drain semantics: bare pods need podDeletion.force)
+        job = self.backing.create({"apiVersion": "batch/v1", "kind": "Job",
+                                   "metadata": {"name": "gpu-long-running", "namespace": "default"},
+                                   "spec": {"template": {"spec": {"containers": []}}}})
+        pod = self.workload_pod()
+        pod["metadata"]["name"] = "gpu-long-running"
+        pod["metadata"]["ownerReferences"] = [{"apiVersion": "batch/v1", "kind": "Job", "name": "gpu-long-running",
+                                               "uid": job["metadata"]["uid"], "controller": True}]
+        pod["spec"]["restartPolicy"] = "Never"
+        pod["spec"]["containers"][0]["command"] = ["sleep", "600"]
+        self.backing.create(pod)
+        self._wait("the long-running GPU pod to run", lambda: (self.backing.get(
+            "v1", "Pod", "gpu-long-running", "default").get("status") or {}).get("phase") == "Running")
+        before = self._module_version()
+        self._cp_update(lambda sp: sp.setdefault("driver", {}).update(version=new_version))
+        t = time.monotonic()
+        states: List[str] = []
+
+        def done():
+            node = self.backing.get("v1", "Node", self.node)
+            st = o.get_labels(node).get(UPGRADE_STATE_LABEL, "")
+            if st and (not states or states[-1] != st):
+                states.append(st)
+            if st == "upgrade-failed":
+                raise StepFailed(f"upgrade failed: {states}")
+            return st == DONE and self._module_version() == new_version and \
+                not (node.get("spec") or {}).get("unschedulable") and self.all_ready()
+        self._wait("the driver upgrade to complete", done, period=0.05)
+        try:
+            self.backing.get("v1", "Pod", "gpu-long-running", "default")
+            raise StepFailed("the GPU pod was not evicted before the driver pod restarted")
+        except errors.NotFound:
+            pass
+        return {"from": before, "to": self._module_version(), "states": states,
+                "seconds": round(time.monotonic() - t, 3)}
+
     def restart_operator(self) -> Dict:
         """checks.sh test_restart_operator: the operator pod is killed; its replacement must get
         the ClusterPolicy back to ready without churning the operands."""
@@ -545,6 +625,8 @@ class E2E:
 
     # -- the flow -------------------------------------------------------------------------------
     def run(self) -> Dict[str, Any]:
+        if self.driver == "container":
+            return self.run_driver_container()
         self.setup()
         try:
             self.step("install-operator", self.install_operator)
@@ -585,6 +667,32 @@ class E2E:
         self.result.update(ok=all(s.get("ok") for s in self.steps) and "error" not in self.result,
                            steps=self.steps, marks_s=dict(sorted(self.marks.items(), key=lambda kv: kv[1])),
                            hip_mode=self.hip_mode, sys_root=self.sys_root)
+        return self.result
+
+
+    def run_driver_container(self) -> Dict[str, Any]:
+        """The flow with the driver DaemonSet installing amdgpu (driver.enabled=true)."""
+        self.setup()
+        try:
+            self.step("install-operator", self.install_operator)
+            first = self.step("verify-operator", lambda: self.verify_operator("install"))
+            self.result["time_to_ready_s"] = self.marks.get("install:ready")
+            self.result["operands_ready"] = first["daemonsets"]
+            self.expected_operands = sorted(first["daemonsets"])
+            self.step("verify-operand-restarts", self.verify_operand_restarts)
+            self.step("install+verify-workload", self.install_and_verify_workload)
+            up = self.step("driver-upgrade", self.driver_upgrade)
+            self.result["driver_upgrade_s"] = up["seconds"]
+            self.step("uninstall", self.uninstall)
+        except Exception as e:  # noqa: BLE001 - reported in the result
+            self.result["error"] = f"{type(e).__name__}: {e}"
+            self.result["logs_dir"] = self.base
+            self.keep = True
+        finally:
+            self.teardown()
+        self.result.update(ok=all(s.get("ok") for s in self.steps) and "error" not in self.result,
+                           steps=self.steps, driver="container",
+                           marks_s=dict(sorted(self.marks.items(), key=lambda kv: kv[1])))
         return self.result
 
 
@@ -682,6 +790,8 @@ class MultiNodeE2E(E2E):
         return {"ok": True}
 
     def run(self) -> Dict[str, Any]:
+        if self.driver == "container":
+            return self.run_driver_container()
         self.setup()
         try:
             self.step("install-operator", self.install_operator)
@@ -718,6 +828,8 @@ def main(argv=None) -> int:
     ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--nodes", type=int, default=1, help="N > 1: that many nodes on fake sysfs (CPU rehearsal)")
+    ap.add_argument("--driver-container", action="store_true",
+                    help="the driver DaemonSet installs a simulated amdgpu on a fake sysfs (CPU rehearsal)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
     if a.nodes > 1:
@@ -725,6 +837,14 @@ def main(argv=None) -> int:
         print(json.dumps(r, default=str))
         return 0 if r["ok"] else 1
     sys_root, dev_root = a.sys_root, a.dev_root
+    if a.driver_container:
+        from ..devices import fakesys
+        root = str(fakesys.make_node(os.path.join(tempfile.mkdtemp(prefix="amd-e2e-sys-"), "root"),
+                                     n_gpus=a.fake_gpus or 8, live=False, kfd=False))
+        r = E2E(sys_root=root, dev_root=root, hip_mode="skip", timeout=a.timeout, keep=a.keep,
+                driver="container").run()
+        print(json.dumps(r, default=str))
+        return 0 if r["ok"] else 1
     if a.fake_gpus:
         from ..devices import fakesys
         sys_root = dev_root = str(fakesys.make_node(os.path.join(tempfile.mkdtemp(prefix="amd-e2e-sys-"), "root"),

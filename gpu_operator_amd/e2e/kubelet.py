@@ -263,6 +263,7 @@ class PodRun:
 
     def _env(self, c: Dict, pairs: List[Tuple[str, str]]) -> Dict[str, str]:
         env = dict(self.kl.base_env)
+        env.update(self.kl.image_env(c.get("image", "")))          # the image's own ENV
         env["AMD_MOUNTS"] = json.dumps(pairs)
         env["HOSTNAME"] = self.name
         md, spec = self.pod["metadata"], self.pod.get("spec") or {}
@@ -476,8 +477,25 @@ class PodRun:
     def start(self) -> None:
         self.thread.start()
 
+    def _pre_stop(self) -> None:
+        """lifecycle.preStop exec hooks of the running main containers, before the SIGTERM."""
+        vols = None
+        for c in (self.pod.get("spec") or {}).get("containers") or []:
+            cmd = (((c.get("lifecycle") or {}).get("preStop") or {}).get("exec") or {}).get("command")
+            p = self.procs.get(c["name"])
+            if not cmd or p is None or p.poll() is not None:
+                continue
+            try:
+                vols = vols or self._volumes()
+                pairs = self._mount_pairs(c, vols)
+                subprocess.run([mounts.rewrite_text(a, pairs) for a in cmd], env=self._env(c, pairs),
+                               capture_output=True, timeout=GRACE_S)
+            except (OSError, subprocess.TimeoutExpired) as e:
+                log.info("preStop of %s/%s: %s", self.name, c["name"], e)
+
     def kill(self, grace: float = GRACE_S) -> None:
         self.stop_evt.set()
+        self._pre_stop()
         for p in self.procs.values():
             if p.poll() is None:
                 try:
@@ -503,7 +521,8 @@ class PodRun:
 
 class ProcessKubelet:
     def __init__(self, client, node: str, base: str, base_env: Dict[str, str], sys_root: str = "/",
-                 dev_root: str = "/", events=None, host_links: Optional[Dict[str, str]] = None):
+                 dev_root: str = "/", events=None, host_links: Optional[Dict[str, str]] = None,
+                 image_env=None):
         self.client, self.node, self.base = client, node, base
         self.host = os.path.join(base, "host")
         # the node tree is synthetic (every hostPath a pod writes lands in it); what the host has
@@ -521,6 +540,8 @@ class ProcessKubelet:
         self.base_env.setdefault("AMD_SYSFS_ROOT", sys_root)
         self.base_env.setdefault("AMD_DEV_ROOT", dev_root)
         self._events = events or (lambda name, **kw: None)
+        # an image's ENV (images are not pulled: the harness says what a tag's config carries)
+        self.image_env = image_env or (lambda image: {})
         self.pods: Dict[str, PodRun] = {}
         self._lock = threading.Lock()
         self._stop = threading.Event()

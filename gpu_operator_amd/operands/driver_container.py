@@ -37,6 +37,7 @@ import time
 from typing import Callable, Dict, List, Optional, Tuple
 
 from .. import devices
+from ..utils import mounts
 
 log = logging.getLogger("amdgpu-driver")
 
@@ -113,7 +114,7 @@ class DriverContainer:
 
     # -- sources -------------------------------------------------------------------------------
     def precompiled_modules(self) -> List[str]:
-        d = os.path.join(self.image_root, "opt/amdgpu/precompiled", self.kernel)
+        d = mounts.path(os.path.join(self.image_root, "opt/amdgpu/precompiled", self.kernel))
         mods = {_mod_name(p): p for p in glob.glob(os.path.join(d, "*.ko*"))}
         if "amdgpu" not in mods:
             return []
@@ -121,7 +122,7 @@ class DriverContainer:
         return sorted(mods.values()) + ordered       # unknown helpers first, amdgpu last
 
     def install_firmware(self) -> int:
-        src = os.path.join(self.image_root, "opt/amdgpu/firmware")
+        src = mounts.path(os.path.join(self.image_root, "opt/amdgpu/firmware"))
         if not os.path.isdir(src):
             return 0
         dst = os.path.join(self.firmware_dir, "updates", "amdgpu")
@@ -228,7 +229,10 @@ def main(argv=None, stop: Optional[threading.Event] = None, dc: Optional[DriverC
     ap.add_argument("command", choices=["init", "probe", "load-only"])
     a = ap.parse_args(argv)
     dc = dc or DriverContainer(sys_root=os.environ.get("AMD_SYSFS_ROOT", "/"),
-                               dev_root=os.environ.get("AMD_DEV_ROOT", "/"))
+                               dev_root=os.environ.get("AMD_DEV_ROOT", "/"),
+                               host_etc=mounts.path("/host-etc"), run_dir=mounts.path("/run/amd"),
+                               firmware_dir=mounts.path("/lib/firmware"),
+                               params_file=mounts.path(os.environ.get("KERNEL_MODULE_PARAMS", "/drivers/amdgpu.conf")))
     if a.command == "probe":
         ok, why = dc.ready()
         print(why)

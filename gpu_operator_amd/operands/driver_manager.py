@@ -27,6 +27,7 @@ import time
 from typing import Callable, Dict, List, Optional
 
 from .. import devices
+from ..utils import mounts
 from ..controllers.upgrade import gpu_pod_filter
 from ..k8s import errors
 from ..k8s import objects as o
@@ -88,7 +89,8 @@ class DriverManager:
         e = os.environ
         t = lambda k, d: e.get(k, d).lower() == "true"  # noqa: E731
         return cls(client, e.get("NODE_NAME", ""), e.get("OPERATOR_NAMESPACE", ""),
-                   sys_root=e.get("AMD_SYSFS_ROOT", "/"),
+                   sys_root=e.get("AMD_SYSFS_ROOT", "/"), run_dir=mounts.path("/run/amd"),
+                   host_root=mounts.path("/host"),
                    evict_gpu_pods=t("ENABLE_GPU_POD_EVICTION", "true"), auto_drain=t("ENABLE_AUTO_DRAIN", "false"),
                    drain_force=t("DRAIN_USE_FORCE", "false"), drain_selector=e.get("DRAIN_POD_SELECTOR_LABEL", ""),
                    drain_timeout=_dur(e.get("DRAIN_TIMEOUT_SECONDS", "0s")),

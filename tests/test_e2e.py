@@ -78,3 +78,23 @@ def test_three_node_cluster_on_real_processes():
     assert sorted(st["workload-per-node"]["detail"].values()) == ["e2e-node-0", "e2e-node-1", "e2e-node-2"]
     d = st["disable-one-node"]["detail"]
     assert d["node"] == "e2e-node-0" and d["untouched"] == ["e2e-node-1", "e2e-node-2"]
+
+
+@pytest.mark.skipif(not os.path.exists(BARRIER), reason="native binaries not built")
+def test_driver_container_install_and_auto_upgrade_on_real_processes(tmp_path):
+    """driver.enabled=true on a node without amdgpu (fake sysfs, the simulated kernel of
+    devices/fakekernel.py on PATH): the driver DaemonSet's driver-manager and driver container
+    install amdgpu, its startup probe releases the validator (container-driver mode), and a
+    driver.version bump runs the upgrade controller's whole state machine -- the Job-managed GPU
+    pod is evicted and gone before the driver pod restarts, the new container unloads and loads
+    the new version, the node is uncordoned."""
+    node = str(fakesys.make_node(tmp_path / "root", n_gpus=8, live=False, kfd=False))
+    r = E2E(sys_root=node, dev_root=node, hip_mode="skip", timeout=90, driver="container").run()
+    assert r["ok"], r
+    st = {s["name"]: s for s in r["steps"]}
+    assert "amdgpu-driver-daemonset" in r["operands_ready"]
+    assert st["verify-operator"]["detail"]["driver-ready"]["mode"] == "container"
+    up = st["driver-upgrade"]["detail"]
+    assert (up["from"], up["to"]) == ("6.12.12", "6.12.13")
+    assert up["states"][-7:] == ["cordon-required", "wait-for-jobs-required", "pod-deletion-required",
+                                 "pod-restart-required", "validation-required", "uncordon-required", "upgrade-done"]
