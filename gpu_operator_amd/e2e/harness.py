@@ -419,6 +419,34 @@ class E2E:
                     log_text = f.read()[-2000:]
         return {"phase": p["status"]["phase"], "node": p["spec"].get("nodeName"), "log_tail": log_text.strip()[-400:]}
 
+    def exporter_attribution(self) -> Dict:
+        """The metrics exporter's per-pod GPU attribution (the dcgm-exporter role): a running pod
+        holding an ``amd.com/gpu`` shows up as the ``pod`` label of that GPU's series, through
+        the kubelet's pod-resources API."""
+        pod = self.workload_pod()
+        pod["metadata"]["name"] = "gpu-attribution"
+        pod["spec"]["restartPolicy"] = "Never"
+        pod["spec"]["containers"][0]["command"] = ["sleep", "600"]
+        self.backing.create(pod)
+        self._wait("the attributed pod to run", lambda: (self.backing.get(
+            "v1", "Pod", "gpu-attribution", "default").get("status") or {}).get("phase") == "Running")
+
+        def scrape():
+            try:
+                with urllib.request.urlopen(f"http://127.0.0.1:{self.exporter_port}/metrics", timeout=2) as r:
+                    text = r.read().decode()
+            except OSError:
+                return None
+            hits = [ln for ln in text.splitlines() if ln.startswith("amd_gpu_") and 'pod="gpu-attribution"' in ln]
+            return (text, hits) if hits else None
+        text, hits = self._wait("a GPU series labelled with the pod", scrape)
+        series = [ln for ln in text.splitlines() if ln.startswith("amd_gpu_")]
+        self.backing.delete("v1", "Pod", "gpu-attribution", "default")
+        self._wait("the attributed pod gone", lambda: not any(
+            r.name == "gpu-attribution" for k in self.kubelets for r in k.running().values()))
+        names = sorted({h.split("{", 1)[0] for h in hits})
+        return {"series": len(series), "attributed_metrics": names[:12], "sample": hits[0][:300]}
+
     def _ds(self, name: str) -> Dict:
         return self.backing.get("apps/v1", "DaemonSet", name, NS)
 
@@ -636,6 +664,7 @@ class E2E:
             self.expected_operands = sorted(first["daemonsets"])
             self.step("verify-operand-restarts", self.verify_operand_restarts)
             self.step("install+verify-workload", self.install_and_verify_workload)
+            self.step("exporter-attribution", self.exporter_attribution)
             self.step("update-clusterpolicy", self.update_clusterpolicy)
             self.step("time-slicing", self.time_slicing)
             rs = self.step("restart-operator", self.restart_operator)

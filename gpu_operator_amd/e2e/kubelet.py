@@ -198,6 +198,8 @@ class PodRun:
         return st
 
     def publish(self) -> None:
+        if self.phase in ("Succeeded", "Failed"):
+            self.kl.plugins.release(self.uid)      # a terminated pod's devices are free again
         spec = self.pod.get("spec") or {}
         status = {"phase": self.phase, "hostIP": "127.0.0.1", "podIP": "127.0.0.1",
                   "conditions": [{"type": "Ready", "status": "True" if self.ready else "False"},

@@ -31,7 +31,7 @@ def test_reference_end_to_end_flow_on_real_processes(tmp_path):
     assert r["ok"], r
     names = [s["name"] for s in r["steps"]]
     assert names == ["install-operator", "verify-operator", "verify-operand-restarts", "install+verify-workload",
-                     "update-clusterpolicy", "time-slicing", "restart-operator", "disable-operands", "enable-operands", "uninstall",
+                     "exporter-attribution", "update-clusterpolicy", "time-slicing", "restart-operator", "disable-operands", "enable-operands", "uninstall",
                      "install-operator[sandbox]", "verify-operator[sandbox]", "install+verify-workload[sandbox]",
                      "uninstall[sandbox]"]
     assert set(r["operands_ready"]) >= {"amd-container-toolkit-daemonset", "amd-device-plugin-daemonset",
@@ -42,6 +42,8 @@ def test_reference_end_to_end_flow_on_real_processes(tmp_path):
     assert v["amd.com/gpu"] == "8"                   # device plugin -> kubelet ListAndWatch -> Node
     assert st["install+verify-workload"]["detail"]["phase"] == "Succeeded"
     assert "allocated:" in st["install+verify-workload"]["detail"]["log_tail"]
+    ex = st["exporter-attribution"]["detail"]
+    assert ex["series"] > 0 and ex["attributed_metrics"], ex
     ts = st["time-slicing"]["detail"]
     assert ts["advertised"] == 80 and ts["labels"]["amd.com/gpu.replicas"] == "10"
     assert ts["labels"]["amd.com/gpu.product"].endswith("-SHARED")
