@@ -58,6 +58,14 @@ __device__ __forceinline__ void w4_mfma(const bf16x8& b, const bf16x8& a) {
 __device__ __forceinline__ constexpr int w4_isb(int j) { return j >= 1 && j <= 8; }
 __device__ __forceinline__ constexpr int w4_idx(int j) { return j == 0 ? 0 : (j <= 8 ? j - 1 : j - 8); }
 
+// the R0 read (j in w4_isb order) issued at slot i of a w4s iteration, or -1: read j sits at
+// slot B2 + 1 + j*RS/16 (a constexpr lookup keeps the compile time of a variant at seconds)
+__host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
+  for (int j = 0; j < 16; ++j)
+    if (b2 + 1 + (j * rs) / 16 == i) return j;
+  return -1;
+}
+
 // RSPAN / DSPAN: the 16 fragment reads / DMA pieces of a block are spread over its first
 // RSPAN / DSPAN groups of 4 MFMAs (16 = evenly; smaller = earlier, more latency slack).
 // KO (profiling only, wrong results): bit0 drops the per-tile wait+barrier, bit1 the DMA, bit2
@@ -153,12 +161,8 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
         __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
       }
       if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
-      if constexpr (nx && i > B2) {
-        static_for<0, 16>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
-        });
-      }
+      constexpr int jr0 = w4s_r0_at(B2, RS, i);
+      if constexpr (nx && jr0 >= 0) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -660,12 +664,8 @@ gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ 
         else __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
       }
       if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
-      if constexpr (nx && i > B2) {
-        static_for<0, 16>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          if constexpr (B2 + 1 + (j * RS) / 16 == i) read_frag(R0, nxt, 0, J);
-        });
-      }
+      constexpr int jr0 = w4s_r0_at(B2, RS, i);
+      if constexpr (nx && jr0 >= 0) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
       __builtin_amdgcn_sched_barrier(0);
     });
   };

@@ -18,6 +18,14 @@
 
 namespace {
 
+// smallest j in [0, n] with j*span/n >= q: items j of a span placed at group j*span/n, so the
+// items of group q are [lab_span_lo(q), lab_span_lo(q+1))
+constexpr int lab_span_lo(int q, int span, int n) {
+  for (int j = 0; j < n; ++j)
+    if (j * span / n >= q) return j;
+  return n;
+}
+
 // Stage one 256-row x 64-k panel (32 KiB) of a K-major operand into LDS.
 // 32 wave-instructions of 1 KiB (8 rows each); wave w issues rows blocks {w, w+8, w+16, w+24}.
 __device__ __forceinline__ void stage_panel(const __bf16* __restrict__ g, int ld, int k0,
@@ -821,14 +829,13 @@ gemm_bf16_256x256_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt
         constexpr int i = q * 4 + decltype(U)::value;
         w4_mfma<i>(Fc.b[i & 7], Fc.a[i >> 3]);
       });
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(RD)::value && !(KO & 4) && j * RSPAN / 16 == q) read_frag(Fn, nbuf, nkk, J);
-      });
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(DM)::value && !(KO & 2) && j * DSPAN / 16 == q) dma_piece(j, dk, dbuf);
-      });
+      // the reads / pieces j with j*SPAN/16 == q: a contiguous range, instantiated alone
+      if constexpr (decltype(RD)::value && !(KO & 4))
+        static_for<lab_span_lo(q, RSPAN, 16), lab_span_lo(q + 1, RSPAN, 16)>([&](auto J) { read_frag(Fn, nbuf, nkk, J); });
+      if constexpr (decltype(DM)::value && !(KO & 2))
+        static_for<lab_span_lo(q, DSPAN, 16), lab_span_lo(q + 1, DSPAN, 16)>([&](auto J) {
+          dma_piece(decltype(J)::value, dk, dbuf);
+        });
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -977,14 +984,12 @@ gemm_bf16_256x256_w4r(const __bf16* __restrict__ A, const __bf16* __restrict__ B
         constexpr int i = q * 4 + decltype(U)::value;
         w4_mfma<i>(Fc.b[i & 7], Fc.a[i >> 3]);
       });
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(RD)::value && j * RSPAN / 16 == q) read_frag(Fn, rs, J);
-      });
-      static_for<0, 8>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if constexpr (decltype(DM)::value && j * DSPAN / 8 == q) dma_piece(j, dh, ds);
-      });
+      if constexpr (decltype(RD)::value)
+        static_for<lab_span_lo(q, RSPAN, 16), lab_span_lo(q + 1, RSPAN, 16)>([&](auto J) { read_frag(Fn, rs, J); });
+      if constexpr (decltype(DM)::value)
+        static_for<lab_span_lo(q, DSPAN, 8), lab_span_lo(q + 1, DSPAN, 8)>([&](auto J) {
+          dma_piece(decltype(J)::value, dh, ds);
+        });
       __builtin_amdgcn_sched_barrier(0);
     });
   };
