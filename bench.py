@@ -346,8 +346,20 @@ def _fp8_extra(ctx):
     res = ctx.timed(step, steps, ctx.args.warmup)
     chk = G.verify(a, bt, c, nrows=16, seed=ctx.rank)
     per_gpu = G.tflops(m, n, k, res["elapsed_s"] / steps)
-    return {"fp8_per_gpu_tflops": _r(per_gpu), "fp8_total_tflops": _r(per_gpu * ctx.world),
-            "fp8_check_ok": chk.ok, "fp8_steps": steps, "fp8_step_ms_median": res["median_ms"]}
+    out = {"fp8_per_gpu_tflops": _r(per_gpu), "fp8_total_tflops": _r(per_gpu * ctx.world),
+           "fp8_check_ok": chk.ok, "fp8_steps": steps, "fp8_step_ms_median": res["median_ms"]}
+    # hipBLASLt's fp8 on the same operands (per-tensor unit scales; ours is block-scaled, 1 E8M0
+    # scale per 32 elements, also unit here), same protocol
+    try:
+        one = torch.ones((), dtype=torch.float32, device=ctx.dev)
+        btt = bt.t()
+        blas = ctx.timed(lambda: torch._scaled_mm(a, btt, scale_a=one, scale_b=one, out_dtype=torch.bfloat16),
+                         steps, ctx.args.warmup)
+        bt_tf = G.tflops(m, n, k, blas["elapsed_s"] / steps)
+        out.update(fp8_hipblaslt_tflops=_r(bt_tf), fp8_ratio_vs_hipblaslt=round(per_gpu / bt_tf, 4))
+    except (RuntimeError, NotImplementedError, AttributeError) as e:   # no hipBLASLt fp8 path
+        out["fp8_hipblaslt_error"] = str(e)[:200]
+    return out
 
 
 def _time_to_ready_extra():
