@@ -260,6 +260,180 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
   }
 }
 
+// q16: fp8 on the UNSCALED double-rate `v_mfma_f32_16x16x128_f8f6f4` (gfx950's f8f6f4 family runs
+// fp8 at twice the bf16 rate with or without the block scales; the older `*_fp8_fp8` forms are
+// the bf16-rate ones). hipBLASLt's gfx950 fp8 kernel (MT256x256x128, MI 16x16x128) is built on
+// it. The 16x16 output shape is also the one that holds clocks better under the power limit
+// (MI355X_MICROARCH.md, DVFS give-back item 7).
+// A wave's 128x128 sub-tile is 8x8 MFMAs of 16x16 (the bf16 w4s accumulator layout, so the bf16
+// epilogue applies as is). A fragment is 16 rows x 128 k = 32 B per lane (8 VGPRs, two
+// ds_read_b128: chunks 2g and 2g+1 of the 128-B row for lane group g = lane >> 4). A K-tile needs
+// 8 A + 8 B fragments = 128 VGPRs -- exactly one set, no double buffer -- because the 64 MFMAs run
+// in quarter blocks that free half of the fragments early:
+//   slots  0..15  B0 x A0      B0 = b0..3, B1 = b4..7, A0 = a0..3, A1 = a4..7
+//   slots 16..31  B0 x A1      B0 is dead after slot 31
+//   slots 32..47  B1 x A0      A0 is dead after slot 47
+//   slots 48..63  B1 x A1
+// and the reads: A1, B1 of tile t at slots 0..15 (their registers died at the previous tile's
+// slot 63); B0, A0 of tile t+1 after their last use (slots RB0.., RA0..). Barriers: after the A1/B1
+// reads every wave is done with tile t (DMA of tile t+2 may overwrite it); before B0' the
+// landing wait for tile t+1.
+template <int I>
+__device__ __forceinline__ void f8q_mfma(const i32x8& b, const i32x8& a) {
+  asm volatile("v_mfma_f32_16x16x128_f8f6f4 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+               :: "i"(4 * I), "i"(4 * I + 3), "v"(b), "v"(a));
+}
+
+template <int W1 = 16, int D0 = 18, int DS = 1, int W2 = 34, int RB0 = 36, int RA0 = 48, int SERP = 0,
+          bool SQ = false>
+__global__ void __launch_bounds__(F8_THREADS, 1)
+gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
+                     __bf16* __restrict__ C, int M, int N, int K) {
+  constexpr int SLOTS = 64;
+  static_assert(W1 >= 16 && D0 > W1 && D0 + 15 * DS < SLOTS && W2 > W1 && RB0 > W2 && RB0 >= 32 &&
+                RB0 + 8 <= SLOTS && RA0 >= 48 && RA0 + 8 <= SLOTS, "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[F8_LDS];
+
+  const int tiles_m = M / F8_BM;
+  const int tiles_n = N / F8_BN;
+  const int nwg = tiles_m * tiles_n;
+  int tm, tn;
+  if constexpr (SQ) tile_coords_sq(blockIdx.x, tiles_n, tm, tn);
+  else tile_coords(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const uint8_t* gA = A + (size_t)tm * F8_BM * K;
+  const uint8_t* gB = Bt + (size_t)tn * F8_BN * K;
+  const uint32_t panel_bytes = (uint32_t)F8_BM * (uint32_t)K;
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)gA, 0, panel_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, int k0, char* buf) {
+    const int rblk = ((i & 7) << 2) + wid;
+    char* lds = buf + (i >= 8 ? F8_PANEL : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K + (uint32_t)k0, 0, 0);
+  };
+
+  // the lane's two 16-byte chunks (2g, 2g+1) of row (lane & 15) of a 16-row fragment, swizzled
+  // as the DMA wrote them (chunk c of row R at c ^ ((R >> 1) & 7))
+  int lane_off[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = lane & 15;
+    const int c = 2 * (lane >> 4) + h;
+    lane_off[h] = r * F8_ROW + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * F8_ROW;
+  const int b_off = F8_PANEL + wc * 128 * F8_ROW;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  i32x8 FA[8], FB[8];
+  char* const buf0 = smem;
+  char* const buf1 = smem + F8_BUF;
+  // read j of a set: j = 0..3 -> fragment base + j, one ds_read_b128 per half h
+  auto read = [&](bool isb, int x, int h, const char* buf) {
+    const char* base = buf + (isb ? b_off : a_off) + x * 16 * F8_ROW + lane_off[h];
+    return *reinterpret_cast<const i32x4*>(base);
+  };
+  auto read_frag = [&](i32x8& F, bool isb, int x, const char* buf) {
+    const i32x4 lo = read(isb, x, 0, buf);
+    const i32x4 hi = read(isb, x, 1, buf);
+    F = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto iter = [&](char* cur, char* nxt, int dk, auto DM, auto NX) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value;
+    static_for<0, SLOTS>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int blk = i >> 4, w = i & 15;
+      constexpr int bi = (blk >> 1) * 4 + (w >> 2), ai = (blk & 1) * 4 + (w & 3);
+      f8q_mfma<ai * 8 + bi>(FB[bi], FA[ai]);                      // accumulator m*8+n
+      // A1 (a4..7) at slots 0..7, B1 (b4..7) at 8..15: one fragment per two slots
+      if constexpr (i < 16 && (i & 1) == 0) read_frag(i < 8 ? FA[4 + i / 2] : FB[4 + (i - 8) / 2], i >= 8, 4 + (i & 7) / 2, cur);
+      if constexpr (i == W1) __builtin_amdgcn_s_waitcnt(0xC07F);                 // lgkmcnt(0)
+      if constexpr (dm && i == W1 + 1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
+      if constexpr (nx && i == W2) {
+        constexpr int issued = !dm ? 0 : ((W2 - D0) / DS + 1 > 16 ? 16 : (W2 - D0) / DS + 1);
+        __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);   // vmcnt(n) lgkmcnt(0)
+      }
+      if constexpr (nx && i == W2 + 1) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i >= RB0 && i < RB0 + 8 && ((i - RB0) & 1) == 0) read_frag(FB[(i - RB0) / 2], true, (i - RB0) / 2, nxt);
+      if constexpr (nx && i >= RA0 && i < RA0 + 8 && ((i - RA0) & 1) == 0) read_frag(FA[(i - RA0) / 2], false, (i - RA0) / 2, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  const int ktiles = K / F8_BK;     // >= 2 (host guarantees)
+  const bool rev = SERP > 0 && (((int)blockIdx.x / NXCD) / (SERP > 0 ? SERP : 1)) & 1;
+  auto kof = [&](int kt) { return (rev ? ktiles - 1 - kt : kt) * F8_BK; };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(0), buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, kof(1), buf1);
+  __builtin_amdgcn_s_waitcnt(0x4F70);               // vmcnt(16): tile 0 landed, tile 1 in flight
+  bar();
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    read_frag(FB[x], true, x, buf0);
+    read_frag(FA[x], false, x, buf0);
+  }
+
+  char* cur = buf0;
+  char* nxt = buf1;
+  for (int t = 0; t < ktiles - 2; ++t) {
+    iter(cur, nxt, kof(t + 2), T_{}, T_{});
+    char* tmp = cur; cur = nxt; nxt = tmp;
+  }
+  iter(cur, nxt, 0, F_{}, T_{});
+  iter(nxt, nullptr, 0, F_{}, F_{});
+
+  // epilogue: the bf16 w4s one (same 16x16 accumulator layout)
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  bar();
+  constexpr int CROW = F8_BN * 2;
+  static_for<0, 64>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int m = i >> 3, n = i & 7;
+    float x0, x1, x2, x3;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+    const int r = wr * 128 + m * 16 + (lane & 15);
+    const int g = (wc * 128 + n * 16 + 4 * (lane >> 4)) >> 2;
+    bf16x4 v;
+    v[0] = (__bf16)x0;
+    v[1] = (__bf16)x1;
+    v[2] = (__bf16)x2;
+    v[3] = (__bf16)x3;
+    *reinterpret_cast<bf16x4*>(smem + r * CROW + ((g ^ (r & 15)) << 3)) = v;
+  });
+  bar();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < (F8_BM * F8_BN * 2) / (F8_THREADS * 16); ++i) {
+    const int r = i * (F8_THREADS / 32) + (tid >> 5);
+    const int ch = tid & 31;
+    const int sw = r & 15;
+    const int pg = (2 * ch) ^ sw;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
+    uint4 v = raw;
+    if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+    *reinterpret_cast<uint4*>(C + (size_t)(tm * F8_BM + r) * N + tn * F8_BN + ch * 8) = v;
+  }
+}
+
 // Persistent fp8 kernel (variants 10/11): the bf16 v25 structure (gemm_bf16.hip) on the fp8 body.
 // gridDim = one workgroup per CU (a multiple of 8); XCD x (= blockIdx % 8) owns the contiguous run
 // of tiles xcd_remap gives it and its gridDim/8 workgroups walk it in strides. The K-tile stream

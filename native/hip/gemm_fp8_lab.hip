@@ -25,6 +25,12 @@ int amdgo_lab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, int
   } else if (v == 13 && (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0) {
     hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true, true>), dim3(nwg), dim3(F8_THREADS), 0, s,
                        a, b, c, M, N, K);
+  } else if (v >= 20 && v <= 22) {                   // q16: unscaled 16x16x128 f8f6f4 MFMA
+    auto kern = v == 20 ? gemm_fp8_256x256_q16<>
+              : v == 21 ? gemm_fp8_256x256_q16<16, 18, 1, 34, 36, 48, 32>
+                        : gemm_fp8_256x256_q16<16, 18, 1, 34, 36, 48, 32, true>;
+    if (v == 22 && ((M / F8_BM) % 16 || (N / F8_BN) % 16)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
   } else if (v >= 1 && v <= 9) {
     auto kern = v == 1 ? gemm_fp8_256x256_w4s<5, 5, 16, 20, 10>
               : v == 2 ? gemm_fp8_256x256_w4s<5, 6, 12, 18, 12>

@@ -183,3 +183,28 @@ def test_shipped_library_exports_no_lab_entry_points():
             G.set_fp8_variant(bad)
     G.set_variant(0)
     G.set_fp8_variant(0)
+
+
+@pytest.fixture(scope="module")
+def asm_fp8_lab(tmp_path_factory):
+    return _compile(tmp_path_factory, "gemm_fp8_lab.hip")
+
+
+def test_fp8_q16_kernel_audit(asm_fp8_lab):
+    """q16 (unscaled v_mfma_f32_16x16x128_f8f6f4): 256 pinned AGPRs, one 128-VGPR fragment set
+    (no spills into AGPRs), 64 MFMAs / 32 ds_read_b128 / 16 LDS-DMA pieces per K-tile, two
+    barriers per K-tile (buffer free, next tile landed)."""
+    kernels = _kernels(asm_fp8_lab, "gemm_fp8_256x256_q16")
+    assert len(kernels) == 3
+    for body, st in kernels:
+        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+        assert st["NumVgprs"] <= 160, st
+        _no_compiler_agpr_access(body)
+        assert "v_mfma_scale" not in body
+        loop = re.search(r"; =>\s*This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
+        assert loop, "main loop not found"
+        text = loop.group(1)
+        assert text.count("v_mfma_f32_16x16x128_f8f6f4") == 64
+        assert text.count("ds_read_b128") == 32
+        assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
+        assert text.count("s_barrier") == 2
