@@ -545,6 +545,7 @@ class ProcessKubelet:
         # an image's ENV (images are not pulled: the harness says what a tag's config carries)
         self.image_env = image_env or (lambda image: {})
         self.pods: Dict[str, PodRun] = {}
+        self._terminating: set = set()                 # deleted pods whose processes are being killed
         self._lock = threading.Lock()
         self._stop = threading.Event()
         os.makedirs(self.host, exist_ok=True)
@@ -633,6 +634,7 @@ class ProcessKubelet:
             gone = [uid for uid in self.pods if uid not in live]
             for uid in gone:
                 run = self.pods.pop(uid)
+                self._terminating.add(run)          # still holds processes until the reap finishes
                 threading.Thread(target=self._reap, args=(run,), daemon=True).start()
             for uid, p in live.items():
                 if uid not in self.pods and (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed"):
@@ -641,7 +643,11 @@ class ProcessKubelet:
                     run.start()
 
     def _reap(self, run: PodRun) -> None:
-        run.kill()
+        try:
+            run.kill()
+        finally:
+            with self._lock:
+                self._terminating.discard(run)
         self.event(f"{run.name}:killed")
 
     def _loop(self) -> None:
@@ -692,7 +698,8 @@ class ProcessKubelet:
 
     def all_pids(self) -> List[int]:
         with self._lock:
-            return [pid for r in self.pods.values() for pid in r.pids()]
+            runs = list(self.pods.values()) + list(self._terminating)
+        return [pid for r in runs for pid in r.pids()]
 
     def cleanup(self) -> None:
         shutil.rmtree(self.base, ignore_errors=True)
