@@ -116,8 +116,11 @@ TARGETS: List[Target] = [
 # Tools-only: superseded GEMM generations, placement sweeps and knock-out timings for A/B profiling
 # (tools/gemm_lab.py). Never loaded by the validator; built on request (`--lab`).
 LAB_TARGETS: List[Target] = [
-    Target("libamdgo_gemm_lab.so", ["hip/gemm_bf16_lab.hip", "hip/gemm_fp8_lab.hip"], "hip-shared",
-           headers=GEMM_HEADERS),
+    # one library per dtype: an fp8 schedule edit rebuilds only the fp8 lab
+    Target("libamdgo_gemm_lab_bf16.so", ["hip/gemm_bf16_lab.hip"], "hip-shared",
+           headers=["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h"]),
+    Target("libamdgo_gemm_lab_fp8.so", ["hip/gemm_fp8_lab.hip"], "hip-shared",
+           headers=["include/gemm_tile_common.h", "hip/gemm_fp8_kernels.h"]),
 ]
 
 

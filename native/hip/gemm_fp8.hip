@@ -2,20 +2,26 @@
 //
 //   C[M,N] (bf16) = A[M,K] (fp8 e4m3fn, K-major) * Bt[N,K]^T (fp8 e4m3fn, K-major), fp32 accumulation.
 //
-// Kernels and design: gemm_fp8_kernels.h (block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 with unit
-// scales = the matrix cores' fp8 rate). Only the measured production kernels are reachable; the
+// Kernels and design: gemm_fp8_kernels.h. Only the measured production kernels are reachable; the
 // variant is an API argument, never read from the environment (placement sweeps live in the
 // tools-only gemm_fp8_lab.hip).
-//   0 = automatic (default): v9 (v4 schedule + serpentine K + loop rotation); v10 (persistent) for
-//       K <= 2048 with >= 2 tiles per CU; v13 (v9 + square cross-XCD raster) for >= 16 dispatch waves
-//       with K >= 16384 on 16x16-tile multiples; v7 / v4 on devices without 256 CUs.
-//   4 / 7 / 9 / 10 / 13 = that kernel pinned (no automatic switch; falls back when the shape or the
+//   0 = automatic (default): v15 (q16: unscaled double-rate v_mfma_f32_16x16x128_f8f6f4, DMA pieces
+//       every third MFMA slot, serpentine K); v16 (v15 + square cross-XCD raster) on 16x16-tile
+//       multiples; v10 (persistent, block-scaled 32x32x64) for K <= 2048 with >= 2 tiles per CU;
+//       v17 (q16 without serpentine K) on devices without 256 CUs.
+//   10 / 15 / 16 / 17 = that kernel pinned (no automatic switch; falls back when the shape or the
 //       device cannot run it).
+// q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
+// (profiles/r2_fp8_q16/): 8192^3 +5.3 %, 16384^3 +3.1 %, 4096^3 +4.1 %, 16384x8192x8192 +2.2 %.
 // Fast path: M % 256 == 0, N % 256 == 0, K % 128 == 0, K >= 256; otherwise the generic kernel.
 
 #include "gemm_fp8_kernels.h"
 
 static int g_fp8_variant = 0;
+
+// q16 schedule (lab v28 / v32): free barrier after slot 17, DMA pieces at slots 18, 21, .., 63,
+// landing wait at 34, B0' reads from slot 35, A0' reads from 43 (block 2 walks A0 slowly).
+#define Q16(SERP, SQ) (gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, SERP, SQ, 2, 2, true>)
 
 static int resolve_fp8_variant(int M, int N, int K) {
   if (M % F8_BM || N % F8_BN || K % F8_BK || K < 2 * F8_BK) return 0;
@@ -25,18 +31,14 @@ static int resolve_fp8_variant(int M, int N, int K) {
   const bool sq = (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0;
   int v = g_fp8_variant;
   if (v == 0) {
-    v = 9;
+    v = sq ? 16 : 15;
     // Short K (<= 16 K-tiles) with several tiles per CU: the persistent kernel hides each tile's
     // prologue and epilogue under the neighbouring K-loops.
     if (K <= 16 * F8_BK && nwg >= 2 * cus) v = 10;
-    // The square cross-XCD raster (as bf16 v45) only pays for fp8 on the biggest grids: at
-    // 16384^3 +4.3 %, but 12288^3, 16384x8192x8192 and 16384^2x8192 ran 1-3 % behind v9
-    // (profiles/r1_s6_sq). fp8 panels are half the bytes, so the panel traffic it saves matters less.
-    else if (sq && nwg >= 16 * cus && K >= 128 * F8_BK) v = 13;
   }
-  if (v == 13 && !sq) v = 9;
-  if (v == 10 && pgrid < NXCD) v = 9;
-  if ((v == 9 || v == 13) && cus != 256) v = 7;
+  if (v == 16 && !sq) v = 15;
+  if (v == 10 && pgrid < NXCD) v = 15;
+  if ((v == 15 || v == 16) && cus != 256) v = 17;   // serpentine K assumes 32 co-resident tiles per XCD
   return v;
 }
 
@@ -44,7 +46,7 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
-  if (v != 0 && v != 4 && v != 7 && v != 9 && v != 10 && v != 13) return (int)hipErrorInvalidValue;
+  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17) return (int)hipErrorInvalidValue;
   g_fp8_variant = v;
   return 0;
 }
@@ -62,24 +64,18 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
   const int cus = device_cu_count();
   const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;
   switch (resolve_fp8_variant(M, N, K)) {
-    case 4:
-      hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6>), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
-      break;
-    case 7:
-      hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 0, true>), dim3(nwg), dim3(F8_THREADS), 0, s,
-                         a, b, c, M, N, K);
-      break;
-    case 9:
-      hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true>), dim3(nwg), dim3(F8_THREADS), 0, s,
-                         a, b, c, M, N, K);
-      break;
     case 10:
       hipLaunchKernelGGL((gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>), dim3(pgrid), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
-    case 13:
-      hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true, true>), dim3(nwg), dim3(F8_THREADS), 0, s,
-                         a, b, c, M, N, K);
+    case 15:
+      hipLaunchKernelGGL(Q16(32, false), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 16:
+      hipLaunchKernelGGL(Q16(32, true), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 17:
+      hipLaunchKernelGGL(Q16(0, false), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {
       dim3 grid((N + G8 - 1) / G8, (M + G8 - 1) / G8);

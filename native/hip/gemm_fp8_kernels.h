@@ -284,14 +284,27 @@ __device__ __forceinline__ void f8q_mfma(const i32x8& b, const i32x8& a) {
                :: "i"(4 * I), "i"(4 * I + 3), "v"(b), "v"(a));
 }
 
+// Schedule parameters: W1 = lgkmcnt(0) slot (barrier at W1 + 1: tile t's buffer is free); DMA piece
+// j of tile t+2 at slot D0 + j DS; W2 = landing wait for tile t+1 (barrier at W2 + 1); B0' fragment j
+// read at RB0 + j RBS, A0' fragment j at RA0 + j RAS. ASLOW: block 2 (B1 x A0) walks A0 slowly, so
+// a0 dies at slot 35, a1 at 39, ... (else every A0 fragment lives to slot 47). Block 1 always walks
+// B0 slowly (b0 dies at slot 19, b1 at 23, ...).
 template <int W1 = 16, int D0 = 18, int DS = 1, int W2 = 34, int RB0 = 36, int RA0 = 48, int SERP = 0,
-          bool SQ = false>
+          bool SQ = false, int RBS = 2, int RAS = 2, bool ASLOW = false>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
   constexpr int SLOTS = 64;
-  static_assert(W1 >= 16 && D0 > W1 && D0 + 15 * DS < SLOTS && W2 > W1 && RB0 > W2 && RB0 >= 32 &&
-                RB0 + 8 <= SLOTS && RA0 >= 48 && RA0 + 8 <= SLOTS, "schedule");
+  constexpr auto rb_ok = [] {
+    for (int j = 0; j < 4; ++j) {
+      if (RB0 + j * RBS <= 19 + 4 * j || RB0 + j * RBS >= SLOTS) return false;     // b_j dead, in range
+      const int ra = RA0 + j * RAS;
+      if (ra <= (ASLOW ? 35 + 4 * j : 47) || ra >= SLOTS) return false;             // a_j dead, in range
+    }
+    return true;
+  }();
+  static_assert(W1 >= 15 && D0 > W1 && D0 + 15 * DS < SLOTS && W2 > W1 && RB0 > W2 && RA0 > W2 && rb_ok,
+                "schedule");
   __shared__ __attribute__((aligned(16))) char smem[F8_LDS];
 
   const int tiles_m = M / F8_BM;
@@ -353,7 +366,9 @@ gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
     static_for<0, SLOTS>([&](auto I) {
       constexpr int i = decltype(I)::value;
       constexpr int blk = i >> 4, w = i & 15;
-      constexpr int bi = (blk >> 1) * 4 + (w >> 2), ai = (blk & 1) * 4 + (w & 3);
+      constexpr bool aslow = ASLOW && blk == 2;
+      constexpr int bi = (blk >> 1) * 4 + (aslow ? (w & 3) : (w >> 2));
+      constexpr int ai = (blk & 1) * 4 + (aslow ? (w >> 2) : (w & 3));
       f8q_mfma<ai * 8 + bi>(FB[bi], FA[ai]);                      // accumulator m*8+n
       // A1 (a4..7) at slots 0..7, B1 (b4..7) at 8..15: one fragment per two slots
       if constexpr (i < 16 && (i & 1) == 0) read_frag(i < 8 ? FA[4 + i / 2] : FB[4 + (i - 8) / 2], i >= 8, 4 + (i & 7) / 2, cur);
@@ -361,12 +376,14 @@ gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
       if constexpr (dm && i == W1 + 1) __builtin_amdgcn_s_barrier();
       if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
       if constexpr (nx && i == W2) {
-        constexpr int issued = !dm ? 0 : ((W2 - D0) / DS + 1 > 16 ? 16 : (W2 - D0) / DS + 1);
+        constexpr int issued = !dm || W2 < D0 ? 0 : ((W2 - D0) / DS + 1 > 16 ? 16 : (W2 - D0) / DS + 1);
         __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);   // vmcnt(n) lgkmcnt(0)
       }
       if constexpr (nx && i == W2 + 1) __builtin_amdgcn_s_barrier();
-      if constexpr (nx && i >= RB0 && i < RB0 + 8 && ((i - RB0) & 1) == 0) read_frag(FB[(i - RB0) / 2], true, (i - RB0) / 2, nxt);
-      if constexpr (nx && i >= RA0 && i < RA0 + 8 && ((i - RA0) & 1) == 0) read_frag(FA[(i - RA0) / 2], false, (i - RA0) / 2, nxt);
+      if constexpr (nx && i >= RB0 && i <= RB0 + 3 * RBS && (i - RB0) % RBS == 0)
+        read_frag(FB[(i - RB0) / RBS], true, (i - RB0) / RBS, nxt);
+      if constexpr (nx && i >= RA0 && i <= RA0 + 3 * RAS && (i - RA0) % RAS == 0)
+        read_frag(FA[(i - RA0) / RAS], false, (i - RA0) / RAS, nxt);
       __builtin_amdgcn_sched_barrier(0);
     });
   };

@@ -91,14 +91,41 @@ def _no_compiler_agpr_access(body: str):
     assert not outside, outside[:5]
 
 
+def _audit_q16(kernels):
+    for body, st in kernels:
+        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+        assert st["NumVgprs"] <= 160, st
+        _no_compiler_agpr_access(body)
+        assert "v_mfma_scale" not in body
+        loop = re.search(r"; =>\s*This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
+        assert loop, "main loop not found"
+        text = loop.group(1)
+        assert text.count("v_mfma_f32_16x16x128_f8f6f4") == 64
+        assert text.count("ds_read_b128") == 32
+        assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
+        assert text.count("s_barrier") == 2
+        # fragments are loaded straight into the 8-VGPR operand tuples: no VALU copies before MFMAs
+        assert "v_mov_b32" not in text
+
+
 def test_fp8_kernel_audit(asm_fp8):
-    """fp8 w4s: 256 pinned AGPRs, no scratch, 32 scaled MFMAs per K-tile, 2 barriers, 16 DMA pieces."""
-    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_w4sI")
-    assert len(kernels) == 4    # production: v4, v7, v9, v13 (square raster)
+    """fp8 production q16 (unscaled v_mfma_f32_16x16x128_f8f6f4): 256 pinned AGPRs, one 128-VGPR
+    fragment set (no spills into AGPRs), 64 MFMAs / 32 ds_read_b128 / 16 LDS-DMA pieces per
+    K-tile, two barriers per K-tile (buffer free, next tile landed)."""
+    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_q16")
+    assert len(kernels) == 3    # production: v15, v16 (square raster), v17 (no serpentine K)
+    _audit_q16(kernels)
+    assert "gemm_fp8_256x256_w4sI" not in asm_fp8     # superseded: lab only
+
+
+def test_fp8_w4s_lab_kernel_audit(asm_fp8_lab):
+    """fp8 w4s (block-scaled 32x32x64, the round-1 default, now lab v1-v9/v13): 256 pinned AGPRs,
+    no scratch, 32 scaled MFMAs per K-tile, 2 barriers, 16 DMA pieces."""
+    kernels = _kernels(asm_fp8_lab, "gemm_fp8_256x256_w4sI")
+    assert len(kernels) == 10
     for body, st in kernels:
         assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
         _no_compiler_agpr_access(body)
-        assert len(re.findall(r"v_mfma_scale_f32_32x32x64_f8f6f4", body)) == 3 * 32
         assert "v_mfma_f32" not in body.replace("v_mfma_scale_f32", "")
         loop = re.search(r"; =>\s*This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
         assert loop, "main loop not found"
@@ -107,7 +134,6 @@ def test_fp8_kernel_audit(asm_fp8):
         assert text.count("ds_read_b128") == 32
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
         assert text.count("s_barrier") == 2
-        # fragments are loaded straight into the 8-VGPR operand tuples: no VALU copies before MFMAs
         assert "v_mov_b32" not in text
 
 
@@ -191,20 +217,7 @@ def asm_fp8_lab(tmp_path_factory):
 
 
 def test_fp8_q16_kernel_audit(asm_fp8_lab):
-    """q16 (unscaled v_mfma_f32_16x16x128_f8f6f4): 256 pinned AGPRs, one 128-VGPR fragment set
-    (no spills into AGPRs), 64 MFMAs / 32 ds_read_b128 / 16 LDS-DMA pieces per K-tile, two
-    barriers per K-tile (buffer free, next tile landed)."""
+    """q16 lab placements (v20-v35): the same invariants as the production q16 kernels."""
     kernels = _kernels(asm_fp8_lab, "gemm_fp8_256x256_q16")
-    assert len(kernels) == 3
-    for body, st in kernels:
-        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
-        assert st["NumVgprs"] <= 160, st
-        _no_compiler_agpr_access(body)
-        assert "v_mfma_scale" not in body
-        loop = re.search(r"; =>\s*This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
-        assert loop, "main loop not found"
-        text = loop.group(1)
-        assert text.count("v_mfma_f32_16x16x128_f8f6f4") == 64
-        assert text.count("ds_read_b128") == 32
-        assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
-        assert text.count("s_barrier") == 2
+    assert len(kernels) == 16
+    _audit_q16(kernels)

@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[0, 4, 7, 9, 10, 13])   # the production set (gemm.FP8_VARIANTS)
+@pytest.fixture(params=[0, 10, 15, 16, 17])   # the production set (gemm.FP8_VARIANTS)
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
@@ -33,7 +33,7 @@ def fp8_variant(request):
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 512), (1024, 1024, 1024),
                                    (2048, 512, 4096), (768, 2304, 640), (256, 512, 384),
                                    (4608, 4608, 512),     # > 256 tiles: serpentine waves reverse K
-                                   (4096, 8192, 256), (8192, 4096, 384)])   # 16x16-tile super-tiles (v13)
+                                   (4096, 8192, 256), (8192, 4096, 384)])   # 16x16-tile super-tiles (v16)
 def test_fp8_fast_path_matches_fp32_reference(cuda_device, fp8_variant, m, n, k):
     import torch
     from gpu_operator_amd.ops import gemm as G
@@ -117,13 +117,13 @@ def test_fill_uniform_fp8_range_and_determinism(cuda_device):
 
 
 def test_fp8_square_raster_covers_every_tile(cuda_device):
-    """The square cross-XCD raster (v13) over 12288x12288x8192 (48x48 tiles, 9 dispatch waves,
+    """The square cross-XCD raster (q16 v16) over 12288x12288x8192 (48x48 tiles, 9 dispatch waves,
     snaking super-rows); one checked row per tile row covers every output tile."""
     import torch
     from gpu_operator_amd.ops import gemm as G
 
     old = G.get_fp8_variant()
-    G.set_fp8_variant(13)
+    G.set_fp8_variant(16)
     try:
         _check_square_raster_fp8(cuda_device, G, torch)
     finally:
@@ -145,10 +145,11 @@ def _check_square_raster_fp8(cuda_device, G, torch):
 def test_fp8_production_variant_set_is_closed(cuda_device):
     from gpu_operator_amd.ops import gemm as G
 
-    for bad in (1, 2, 3, 5, 6, 8, 11, 12, 14, 99):
+    for bad in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 20, 28, 99):
         with pytest.raises(ValueError):
             G.set_fp8_variant(bad)
     assert G.get_fp8_variant() == 0
-    assert G.resolve_fp8_variant(8192, 8192, 8192) in (9, 7)
+    assert G.resolve_fp8_variant(8192, 8192, 8192) in (16, 17)
+    assert G.resolve_fp8_variant(8192 + 256, 8192, 8192) in (15, 17)
     assert G.resolve_fp8_variant(16384, 16384, 1024) == 10
     assert G.resolve_fp8_variant(300, 256, 256) == 0

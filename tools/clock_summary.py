@@ -35,8 +35,10 @@ def main(root: str) -> None:
         t = sum(durs[i] for i in ids) / len(ids)
         gui = sum(ctr[i].get("GRBM_GUI_ACTIVE", 0) for i in ids) / len(ids)
         cnt = sum(ctr[i].get("GRBM_COUNT", 0) for i in ids) / len(ids)
+        extra = sorted({c for i in ids for c in ctr[i]} - {"GRBM_GUI_ACTIVE", "GRBM_COUNT"})
+        more = "  ".join(f"{c}={sum(ctr[i].get(c, 0) for i in ids) / len(ids):.4g}" for c in extra)
         print(f"{os.path.basename(d.rstrip('/')):12s} {len(ids):10d} {t * 1e6:9.1f} {gui:12.4g} {cnt:12.4g} "
-              f"{gui / t / 1e9:10.3f}")
+              f"{gui / t / 1e9:10.3f}  {more}")
 
 
 if __name__ == "__main__":

@@ -1,4 +1,4 @@
-"""Loader for the tools-only GEMM experiment library (``_native/libamdgo_gemm_lab.so``).
+"""Loader for the tools-only GEMM experiment libraries (``_native/libamdgo_gemm_lab_{bf16,fp8}.so``).
 
 Build it with ``python -m gpu_operator_amd._build --lab``. It holds every superseded bf16/fp8 GEMM
 generation, placement sweep and knock-out timing (native/hip/gemm_bf16_lab.hip, gemm_fp8_lab.hip)
@@ -16,23 +16,23 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-LAB_PATH = os.path.join(ROOT, "gpu_operator_amd", "_native", "libamdgo_gemm_lab.so")
+LAB_DIR = os.path.join(ROOT, "gpu_operator_amd", "_native")
 KNOCKOUT_BF16 = range(20, 25)       # timings with deliberately wrong results
-_LIB = None
+_LIBS = {}
 
 
-def load() -> ctypes.CDLL:
-    global _LIB
-    if _LIB is None:
-        if not os.path.exists(LAB_PATH):
-            raise FileNotFoundError(f"{LAB_PATH}: build it with `python -m gpu_operator_amd._build --lab`")
-        lib = ctypes.CDLL(LAB_PATH)
+def load(dtype: str = "bf16") -> ctypes.CDLL:
+    if dtype not in _LIBS:
+        path = os.path.join(LAB_DIR, f"libamdgo_gemm_lab_{dtype}.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path}: build it with `python -m gpu_operator_amd._build --lab`")
+        lib = ctypes.CDLL(path)
         vp, i = ctypes.c_void_p, ctypes.c_int
-        for f in ("amdgo_lab_gemm_bf16", "amdgo_lab_gemm_fp8"):
-            getattr(lib, f).argtypes = [i, vp, vp, vp, i, i, i, vp]
-            getattr(lib, f).restype = i
-        _LIB = lib
-    return _LIB
+        fn = getattr(lib, f"amdgo_lab_gemm_{dtype}")
+        fn.argtypes = [i, vp, vp, vp, i, i, i, vp]
+        fn.restype = i
+        _LIBS[dtype] = lib
+    return _LIBS[dtype]
 
 
 def _run(fn, v, a, bt, c):
@@ -48,8 +48,8 @@ def _run(fn, v, a, bt, c):
 
 
 def gemm_bf16(v: int, a, bt, c):
-    return _run(load().amdgo_lab_gemm_bf16, v, a, bt, c)
+    return _run(load("bf16").amdgo_lab_gemm_bf16, v, a, bt, c)
 
 
 def gemm_fp8(v: int, a, bt, c):
-    return _run(load().amdgo_lab_gemm_fp8, v, a, bt, c)
+    return _run(load("fp8").amdgo_lab_gemm_fp8, v, a, bt, c)
