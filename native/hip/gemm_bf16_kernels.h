@@ -83,8 +83,10 @@ __host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
 //                    iteration's pieces) landed, this iteration's stay in flight -- then a barrier
 //   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
 // Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
+// KO (lab knock-out timings only, wrong results): bit0 drops the lgkmcnt(0) before the free barrier,
+// bit1 the landing vmcnt (keeps lgkmcnt(0)), bit2 the free barrier, bit3 the landing barrier.
 template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
-          bool SQ = false>
+          bool SQ = false, int KO = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -152,15 +154,15 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
       if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
       else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
       if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
-      if constexpr (i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
+      if constexpr (i == B1 - 1 && !(KO & 1)) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && i == B1 && !(KO & 4)) __builtin_amdgcn_s_barrier();
       if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
       if constexpr (nx && i == B2 - 1) {
-        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
+        constexpr int issued = (KO & 2) ? 63 : !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
         // vmcnt(issued) lgkmcnt(0): vmcnt low 4 bits [3:0], high 2 bits [15:14]; expcnt 7
         __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
       }
-      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i == B2 && !(KO & 8)) __builtin_amdgcn_s_barrier();
       constexpr int jr0 = w4s_r0_at(B2, RS, i);
       if constexpr (nx && jr0 >= 0) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
       __builtin_amdgcn_sched_barrier(0);
