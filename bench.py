@@ -329,7 +329,7 @@ def _hipblaslt_extra(ctx, a, bt, ours_tflops):
 
 
 def _fp8_extra(ctx):
-    """Same shape on the fp8 (OCP e4m3fn) block-scaled MFMA kernel, after and outside the timed
+    """Same shape on the fp8 (OCP e4m3fn) MFMA kernel (q16: double-rate 16x16x128), after and outside the timed
     bf16 region: the matrix cores at their fp8 rate, reported as extra fields only."""
     torch = ctx.torch
     from gpu_operator_amd.ops import gemm as G
@@ -348,8 +348,7 @@ def _fp8_extra(ctx):
     per_gpu = G.tflops(m, n, k, res["elapsed_s"] / steps)
     out = {"fp8_per_gpu_tflops": _r(per_gpu), "fp8_total_tflops": _r(per_gpu * ctx.world),
            "fp8_check_ok": chk.ok, "fp8_steps": steps, "fp8_step_ms_median": res["median_ms"]}
-    # hipBLASLt's fp8 on the same operands (per-tensor unit scales; ours is block-scaled, 1 E8M0
-    # scale per 32 elements, also unit here), same protocol
+    # hipBLASLt's fp8 on the same operands (per-tensor unit scales; ours is unscaled), same protocol
     try:
         one = torch.ones((), dtype=torch.float32, device=ctx.dev)
         btt = bt.t()

@@ -86,8 +86,8 @@ def collect_counters(shape: str, run: Callable = subprocess.run) -> List[Dict]:
 
 def run_hip(shapes: List[str], counters: bool = False, iters: int = 20,
             run: Callable = subprocess.run, dtype: str = "bf16") -> List[Dict]:
-    """hip-smoke, then the MFMA GEMM probe in ``dtype`` (bf16, fp8 e4m3fn on the block-scaled
-    matrix-core path, or both), then optionally one counter-collection pass."""
+    """hip-smoke, then the MFMA GEMM probe in ``dtype`` (bf16, fp8 e4m3fn on the double-rate
+    16x16x128 matrix-core path, or both), then optionally one counter-collection pass."""
     results: List[Dict] = []
     rc, r = run_json([binary("amd-hip-smoke")], run)
     results += r or [{"event": "hip-smoke", "ok": False, "rc": rc}]

@@ -84,7 +84,9 @@ __host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
 //   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
 // Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
 // KO (lab knock-out timings only, wrong results): bit0 drops the lgkmcnt(0) before the free barrier,
-// bit1 the landing vmcnt (keeps lgkmcnt(0)), bit2 the free barrier, bit3 the landing barrier.
+// bit1 the landing vmcnt (keeps lgkmcnt(0)), bit2 the free barrier, bit3 the landing barrier, bit4
+// the steady-state DMA pieces, bit5 the fragment reads of the loop, bit6 the XOR chunk permutation
+// of the DMA's global addresses (lanes read their row's chunks in order; the LDS image is then wrong).
 template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
           bool SQ = false, int KO = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
@@ -111,7 +113,7 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
   const int par = wid & 1;
   const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
-                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+                        (uint32_t)(((lane & 7) ^ ((KO & 64) ? 0 : ((par * 4 + (lane >> 4)) & 7))) * 16);
   auto dma_piece = [&](int i, int k0, char* buf) {
     // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
     const int rblk = ((i & 7) << 2) + wid;
@@ -153,10 +155,10 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
       constexpr int i = decltype(I)::value;
       if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
       else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
-      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
+      if constexpr (i < 16 && !(KO & 32)) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
       if constexpr (i == B1 - 1 && !(KO & 1)) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
       if constexpr (dm && i == B1 && !(KO & 4)) __builtin_amdgcn_s_barrier();
-      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
+      if constexpr (dm && !(KO & 16) && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
       if constexpr (nx && i == B2 - 1) {
         constexpr int issued = (KO & 2) ? 63 : !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
         // vmcnt(issued) lgkmcnt(0): vmcnt low 4 bits [3:0], high 2 bits [15:14]; expcnt 7
@@ -164,7 +166,7 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
       }
       if constexpr (nx && i == B2 && !(KO & 8)) __builtin_amdgcn_s_barrier();
       constexpr int jr0 = w4s_r0_at(B2, RS, i);
-      if constexpr (nx && jr0 >= 0) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
+      if constexpr (nx && jr0 >= 0 && !(KO & 32)) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
       __builtin_amdgcn_sched_barrier(0);
     });
   };

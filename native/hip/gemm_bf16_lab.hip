@@ -10,7 +10,8 @@
 // LDS-staged, fully coalesced epilogue, 6-9 = v5 phase/knob variants; 10-14 = one wave per SIMD with
 // a 128x128 wave tile; 15-17 = half-tile ring; 18/19 = the K-tile schedule; 20-24 = knock-outs;
 // 80-85 = v44 knock-outs (KO bits of w4s: 1 lgkmcnt, 2 landing vmcnt, 4 free barrier, 8 landing
-// barrier; 84 = 1|4, 85 = all);
+// barrier, 16 DMA, 32 fragment reads, 64 DMA chunk order; 84 = 1|4, 85 = 15, 86 = 16, 87 = 32,
+// 88 = 63, 89 = 64);
 // 25-27 = persistent; 30-35 = barrier-placement sweep; 40/41 = serpentine K, 42/43 = loop rotation,
 // 44 = both (production default), 45 = 44 + square raster. Measured: profiles/r1_gemm_v4/,
 // profiles/r1_s2_gemm/, profiles/r1_s6_sq/.
@@ -1136,8 +1137,12 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
   } else if (v == 45 && kk && (M / BM) % 16 == 0 && (N / BN) % 16 == 0) {
     hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
                        0, s, a, b, c, M, N, K);
-  } else if (v >= 80 && v <= 85 && kk) {            // v44 knock-outs (WRONG results by design)
-    auto kern = v == 80 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 1>
+  } else if (v >= 80 && v <= 89 && kk) {            // v44 knock-outs (WRONG results by design)
+    auto kern = v == 89 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 64>
+              : v == 86 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 16>
+              : v == 87 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 32>
+              : v == 88 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 63>
+              : v == 80 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 1>
               : v == 81 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 2>
               : v == 82 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 4>
               : v == 83 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 8>
@@ -1171,6 +1176,6 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
 }
 
 // 1 if variant v produces correct results (everything except the knock-out timings 20-24, 80-85).
-int amdgo_lab_variant_is_exact(int v) { return !(v >= 20 && v <= 24) && !(v >= 80 && v <= 85); }
+int amdgo_lab_variant_is_exact(int v) { return !(v >= 20 && v <= 24) && !(v >= 80 && v <= 89); }
 
 }  // extern "C"

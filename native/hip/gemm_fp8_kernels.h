@@ -2,12 +2,15 @@
 //
 //   C[M,N] (bf16) = A[M,K] (fp8 e4m3fn, K-major) * Bt[N,K]^T (fp8 e4m3fn, K-major), fp32 accumulation.
 //
-// gfx950 runs fp8 at twice the bf16 rate only through the block-scaled MFMA
-// (`v_mfma_scale_f32_32x32x64_f8f6f4`, MI355X_MICROARCH.md "Matrix cores"; the unscaled
-// `*_fp8_fp8` forms run at the bf16 rate). This kernel issues it with unit E8M0 scales (127 = 2^0),
-// i.e. a plain fp8 GEMM, OCP e4m3fn encoding (not MI300's fnuz).
+// gfx950 runs fp8 at twice the bf16 rate through the f8f6f4 MFMA family, scaled
+// (`v_mfma_scale_f32_32x32x64_f8f6f4`) or not (`v_mfma_f32_16x16x128_f8f6f4`); the older
+// `*_fp8_fp8` forms run at the bf16 rate. OCP e4m3fn encoding (not MI300's fnuz).
+//   * gemm_fp8_256x256_q16  -- the production kernel (gemm_fp8.hip v15/v16/v17): unscaled
+//                              16x16x128, described at its definition below;
+//   * gemm_fp8_256x256_w4sp -- persistent, block-scaled with unit E8M0 scales (v10, short K);
+//   * gemm_fp8_256x256_w4s  -- the round-1 block-scaled kernel (lab only), described next.
 //
-// Design: the bf16 v18 kernel's schedule (gemm_bf16.hip, docs/validator-gemm.md) carried over in
+// w4s design: the bf16 v18 kernel's schedule (gemm_bf16.hip, docs/validator-gemm.md) carried over in
 // bytes. A K-tile is 128 fp8 = the same 128-byte LDS row as 64 bf16, so the LDS image, the
 // buffer_load...lds DMA pieces, the XOR swizzle and the 2x2 wave grid (4 wave64s, one per SIMD,
 // each owning a 128x128 sub-tile of the 256x256 workgroup tile) are unchanged. What changes:

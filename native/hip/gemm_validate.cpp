@@ -2,7 +2,7 @@
 // validator/cuda-workload-validation.yaml:20).
 //
 // Runs the hand-written CDNA4 MFMA GEMMs -- bf16 (gemm_bf16.hip) and/or fp8 e4m3fn on the
-// block-scaled matrix-core path (gemm_fp8.hip) -- concurrently on every selected GPU, one host
+// double-rate matrix-core path (gemm_fp8.hip) -- concurrently on every selected GPU, one host
 // thread per GPU, on uniform [-1,1) operands; checks sampled output rows against an independent
 // fp32 reference kernel; prints one JSON line per (dtype, GPU, shape) and an aggregate line.
 // Exit status 0 only if every check passed.
