@@ -23,6 +23,9 @@
 //        waves with K >= 8192 on 16x16-tile multiples; v42 / v18 on devices without 256 CUs.
 //   18 / 25 / 42 / 44 / 45 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
+// Every w4s kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
+// add per K-tile, loop-invariant soffsets; 17 fewer SALU per K-tile, +0.6-0.8 % at 8192^3 and
+// 16384^3, profiles/r2_sched/sweep_vk.jsonl).
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
 
 #include "gemm_bf16_kernels.h"
@@ -81,7 +84,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   const int nwg = (M / BM) * (N / BN);
   switch (resolve_variant(M, N, K)) {
     case 18:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40>), dim3(nwg), dim3(W4_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 25:
@@ -89,15 +92,15 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 42:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true, false, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 44:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 45:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true>), dim3(nwg), dim3(W4_THREADS),
                          0, s, a, b, c, M, N, K);
       break;
     default: {

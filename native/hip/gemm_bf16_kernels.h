@@ -88,7 +88,7 @@ __host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
 // the steady-state DMA pieces, bit5 the fragment reads of the loop, bit6 the XOR chunk permutation
 // of the DMA's global addresses (lanes read their row's chunks in order; the LDS image is then wrong).
 template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
-          bool SQ = false, int KO = 0>
+          bool SQ = false, int KO = 0, bool VK = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -118,8 +118,12 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
     const int rblk = ((i & 7) << 2) + wid;
     char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
-                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+    if constexpr (VK)   // K offset in the lane offset (one VALU add per K-tile), loop-invariant soffset
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff + (uint32_t)k0 * 2u,
+                                               (uint32_t)rblk * 8u * (uint32_t)K * 2u, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
+                                               (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
   };
 
   int lane_off[2];

@@ -293,7 +293,7 @@ __device__ __forceinline__ void f8q_mfma(const i32x8& b, const i32x8& a) {
 // a0 dies at slot 35, a1 at 39, ... (else every A0 fragment lives to slot 47). Block 1 always walks
 // B0 slowly (b0 dies at slot 19, b1 at 23, ...).
 template <int W1 = 16, int D0 = 18, int DS = 1, int W2 = 34, int RB0 = 36, int RA0 = 48, int SERP = 0,
-          bool SQ = false, int RBS = 2, int RAS = 2, bool ASLOW = false>
+          bool SQ = false, int RBS = 2, int RAS = 2, bool ASLOW = false, bool VK = false>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
@@ -332,8 +332,12 @@ gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
   auto dma_piece = [&](int i, int k0, char* buf) {
     const int rblk = ((i & 7) << 2) + wid;
     char* lds = buf + (i >= 8 ? F8_PANEL : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
-                                             (uint32_t)rblk * 8u * (uint32_t)K + (uint32_t)k0, 0, 0);
+    if constexpr (VK)   // K offset in the lane offset: loop-invariant soffsets (as bf16 w4s VK)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff + (uint32_t)k0,
+                                               (uint32_t)rblk * 8u * (uint32_t)K, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff,
+                                               (uint32_t)rblk * 8u * (uint32_t)K + (uint32_t)k0, 0, 0);
   };
 
   // the lane's two 16-byte chunks (2g, 2g+1) of row (lane & 15) of a 16-row fragment, swizzled

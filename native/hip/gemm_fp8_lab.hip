@@ -25,12 +25,13 @@ int amdgo_lab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, int
   } else if (v == 13 && (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0) {
     hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true, true>), dim3(nwg), dim3(F8_THREADS), 0, s,
                        a, b, c, M, N, K);
-  } else if (v >= 20 && v <= 35) {                   // q16: unscaled 16x16x128 f8f6f4 MFMA
+  } else if (v >= 20 && v <= 37) {                   // q16: unscaled 16x16x128 f8f6f4 MFMA
     // 20-22: one DMA piece per slot; 23: pieces every other slot; 24: landing wait right after the
     // free barrier, reads as soon as each fragment dies; 25: mid landing wait; 26/27 = 24/25 with the
     // serpentine K and the square raster; 28-30: pieces every third slot, landing wait at 34 / 42 /
     // 26; 31 / 32 = 27 / 28 without the square raster; 33 = 28 with the free barrier one slot
-    // earlier; 34 = 28 with reads every third slot between the DMA pieces, 35 = 34 unsquared
+    // earlier; 34 = 28 with reads every third slot between the DMA pieces, 35 = 34 unsquared;
+    // 36 / 37 = 28 / 32 with the K offset in the lane offset (VK)
     auto kern = v == 20 ? gemm_fp8_256x256_q16<>
               : v == 21 ? gemm_fp8_256x256_q16<16, 18, 1, 34, 36, 48, 32>
               : v == 22 ? gemm_fp8_256x256_q16<16, 18, 1, 34, 36, 48, 32, true>
@@ -46,8 +47,10 @@ int amdgo_lab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, int
               : v == 32 ? gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, 32, false, 2, 2, true>
               : v == 33 ? gemm_fp8_256x256_q16<15, 17, 3, 34, 35, 43, 32, true, 2, 2, true>
               : v == 34 ? gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 46, 32, true, 3, 3, true>
-                        : gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 46, 32, false, 3, 3, true>;
-    if ((v == 22 || v == 23 || (v >= 26 && v <= 30) || v == 33 || v == 34) && ((M / F8_BM) % 16 || (N / F8_BN) % 16))
+              : v == 35 ? gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 46, 32, false, 3, 3, true>
+              : v == 36 ? gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, 32, true, 2, 2, true, true>
+                        : gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, 32, false, 2, 2, true, true>;
+    if ((v == 22 || v == 23 || (v >= 26 && v <= 30) || v == 33 || v == 34 || v == 36) && ((M / F8_BM) % 16 || (N / F8_BN) % 16))
       return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
   } else if (v >= 1 && v <= 9) {
