@@ -322,7 +322,9 @@ def _hipblaslt_extra(ctx, a, bt, ours_tflops):
     out = {"hipblaslt_tflops": _r(blas), "ratio_vs_hipblaslt": round(ours_tflops / blas, 4),
            "hipblaslt_step_ms_median": res["median_ms"]}
     try:
-        out["blas_library"] = str(torch.backends.cuda.preferred_blas_library()).split(".")[-1]
+        # torch names its backends after CUDA: on ROCm "Cublaslt" is hipBLASLt, "Cublas" rocBLAS
+        lib = str(torch.backends.cuda.preferred_blas_library()).split(".")[-1]
+        out["blas_library"] = {"Cublaslt": "hipBLASLt", "Cublas": "rocBLAS"}.get(lib, lib)
     except Exception:  # noqa: BLE001 - informational only
         pass
     return out
