@@ -8,9 +8,11 @@
 //   0 = automatic (default): v15 (q16: unscaled double-rate v_mfma_f32_16x16x128_f8f6f4, DMA pieces
 //       every third MFMA slot, serpentine K); v16 (v15 + square cross-XCD raster) on 16x16-tile
 //       multiples; v10 (persistent, block-scaled 32x32x64) for K <= 2048 with >= 2 tiles per CU;
-//       v17 (q16 without serpentine K) on devices without 256 CUs.
-//   10 / 15 / 16 / 17 = that kernel pinned (no automatic switch; falls back when the shape or the
-//       device cannot run it).
+//       v17 (q16 without serpentine K) on devices without 256 CUs; v18 (persistent q16: the next
+//       tile's prologue DMA under the current tile's last K-tiles) for 2048 <= K <= 8192 with >= 4
+//       tiles per CU (8192^3 +0.7-1.2 %, 16384^2x4096 +2.9 %; profiles/r2_fp8_q16/sweep_q16p*.jsonl).
+//   10 / 15 / 16 / 17 / 18 = that kernel pinned (no automatic switch; falls back when the shape or
+//       the device cannot run it).
 // q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
 // (profiles/r2_fp8_q16/): 8192^3 +5.3 %, 16384^3 +3.1 %, 4096^3 +4.1 %, 16384x8192x8192 +2.2 %.
 // Fast path: M % 256 == 0, N % 256 == 0, K % 128 == 0, K >= 256; otherwise the generic kernel.
@@ -32,12 +34,15 @@ static int resolve_fp8_variant(int M, int N, int K) {
   int v = g_fp8_variant;
   if (v == 0) {
     v = sq ? 16 : 15;
-    // Short K (<= 16 K-tiles) with several tiles per CU: the persistent kernel hides each tile's
-    // prologue and epilogue under the neighbouring K-loops.
-    if (K <= 16 * F8_BK && nwg >= 2 * cus) v = 10;
+    // Short K (<= 12 K-tiles) with several tiles per CU: the persistent block-scaled kernel hides
+    // each tile's prologue and epilogue under the neighbouring K-loops; up to 64 K-tiles with >= 4
+    // tiles per CU the persistent q16 does (it loses to v10 at K = 1024-1536 and to the square
+    // raster at K = 16384).
+    if (K <= 12 * F8_BK && nwg >= 2 * cus) v = 10;
+    else if (K <= 64 * F8_BK && nwg >= 4 * cus) v = 18;
   }
   if (v == 16 && !sq) v = 15;
-  if (v == 10 && pgrid < NXCD) v = 15;
+  if ((v == 10 || v == 18) && pgrid < NXCD) v = 15;
   if ((v == 15 || v == 16) && cus != 256) v = 17;   // serpentine K assumes 32 co-resident tiles per XCD
   return v;
 }
@@ -46,7 +51,7 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
-  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17) return (int)hipErrorInvalidValue;
+  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18) return (int)hipErrorInvalidValue;
   g_fp8_variant = v;
   return 0;
 }
@@ -67,6 +72,9 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
     case 10:
       hipLaunchKernelGGL((gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>), dim3(pgrid), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
+      break;
+    case 18:
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16p<>), dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 15:
       hipLaunchKernelGGL(Q16(32, false), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);

@@ -688,6 +688,210 @@ gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__
   }
 }
 
+// Persistent q16 (fp8 v18): the w4sp frame (one workgroup per CU, K-stream across tiles, the next
+// tile's K-tiles 0 and 1 DMA'd by the current tile's last two iterations, wave-private epilogue
+// that zeroes the accumulators as it reads them) around the q16 iteration (unscaled 16x16x128,
+// quarter-block slot order, the production placement). For short K with several tiles per CU.
+template <int W1 = 16, int D0 = 18, int DS = 3, int W2 = 34, int RB0 = 35, int RA0 = 43, bool SERP = false,
+          int RBS = 2, int RAS = 2, bool ASLOW = true>
+__global__ void __launch_bounds__(F8_THREADS, 1)
+gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
+                      __bf16* __restrict__ C, int M, int N, int K) {
+  constexpr int SLOTS = 64;
+  static_assert(W1 >= 15 && D0 > W1 && D0 + 15 * DS < SLOTS && W2 > W1 && RB0 > W2 && RA0 > W2, "schedule");
+  __shared__ __attribute__((aligned(16))) char smem[F8P_LDS];
+
+  const int tiles_m = M / F8_BM;
+  const int tiles_n = N / F8_BN;
+  const int nwg = tiles_m * tiles_n;
+  const int xcd = blockIdx.x % NXCD;
+  const int per = gridDim.x / NXCD;                       // workgroups per XCD (host: gridDim % 8 == 0)
+  const int q = nwg / NXCD, rem = nwg % NXCD;
+  const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+  const int t_end = t_begin + q + (xcd < rem ? 1 : 0);
+  int tile = t_begin + (int)(blockIdx.x / NXCD);
+  if (tile >= t_end) return;                              // uniform over the workgroup
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const uint32_t panel_bytes = (uint32_t)F8_BM * (uint32_t)K;
+  auto rsrc = [&](const uint8_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, panel_bytes, 0x00020000);
+  };
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, tm, tn);
+  __amdgpu_buffer_rsrc_t rA = rsrc(A + (size_t)tm * F8_BM * K);
+  __amdgpu_buffer_rsrc_t rB = rsrc(Bt + (size_t)tn * F8_BN * K);
+  const int par = wid & 1;
+  const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K +
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+  auto dma_piece = [&](int i, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int k0, char* buf) {
+    const int rblk = ((i & 7) << 2) + wid;
+    char* lds = buf + (i >= 8 ? F8_PANEL : 0) + rblk * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff,
+                                             (uint32_t)rblk * 8u * (uint32_t)K + (uint32_t)k0, 0, 0);
+  };
+  int lane_off[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = lane & 15;
+    const int c = 2 * (lane >> 4) + h;
+    lane_off[h] = r * F8_ROW + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+  const int a_off = wr * 128 * F8_ROW;
+  const int b_off = F8_PANEL + wc * 128 * F8_ROW;
+
+  asm volatile("" ::: W4_AGPR_CLOBBERS);
+  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+
+  i32x8 FA[8], FB[8];
+  char* const buf0 = smem;
+  char* const buf1 = smem + F8_BUF;
+  auto read_frag = [&](i32x8& F, bool isb, int x, const char* buf) {
+    const char* base = buf + (isb ? b_off : a_off) + x * 16 * F8_ROW;
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(base + lane_off[0]);
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(base + lane_off[1]);
+    F = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  // FRESH = a tile's first iteration: the epilogue's vmcnt(0) already retired its K-tile 1, and a
+  // counted vmcnt would also wait for the epilogue's C stores.
+  auto iter = [&](char* cur, char* nxt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int dk, auto FR,
+                  auto DM, auto NX) {
+    constexpr bool dm = decltype(DM)::value, nx = decltype(NX)::value, fresh = decltype(FR)::value;
+    static_for<0, SLOTS>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int blk = i >> 4, w = i & 15;
+      constexpr bool aslow = ASLOW && blk == 2;
+      constexpr int bi = (blk >> 1) * 4 + (aslow ? (w & 3) : (w >> 2));
+      constexpr int ai = (blk & 1) * 4 + (aslow ? (w >> 2) : (w & 3));
+      f8q_mfma<ai * 8 + bi>(FB[bi], FA[ai]);
+      if constexpr (i < 16 && (i & 1) == 0) read_frag(i < 8 ? FA[4 + i / 2] : FB[4 + (i - 8) / 2], i >= 8, 4 + (i & 7) / 2, cur);
+      if constexpr (i == W1) __builtin_amdgcn_s_waitcnt(0xC07F);                 // lgkmcnt(0)
+      if constexpr (dm && i == W1 + 1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, ra, rb, dk, cur);
+      if constexpr (nx && i == W2) {
+        constexpr int issued = !dm || W2 < D0 ? 0 : ((W2 - D0) / DS + 1 > 16 ? 16 : (W2 - D0) / DS + 1);
+        if constexpr (fresh) __builtin_amdgcn_s_waitcnt(0xC07F);             // lgkmcnt(0) only
+        else __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
+      }
+      if constexpr (nx && i == W2 + 1) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i >= RB0 && i <= RB0 + 3 * RBS && (i - RB0) % RBS == 0)
+        read_frag(FB[(i - RB0) / RBS], true, (i - RB0) / RBS, nxt);
+      if constexpr (nx && i >= RA0 && i <= RA0 + 3 * RAS && (i - RA0) % RAS == 0)
+        read_frag(FA[(i - RA0) / RAS], false, (i - RA0) / RAS, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  // Wave-private epilogue: 4 passes of 32 C rows (accumulator rows m = 2p, 2p+1) x 128 cols.
+  char* const stg = smem + F8_LDS + wid * F8P_EPI_WAVE;
+  auto epilogue = [&](int tm_, int tn_) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // MFMA D -> reads
+    static_for<0, 4>([&](auto P) {
+      constexpr int p = decltype(P)::value;
+      static_for<0, 16>([&](auto I) {
+        constexpr int u = decltype(I)::value;
+        constexpr int m = 2 * p + (u >> 3), n = u & 7;
+        constexpr int a0 = 4 * (m * 8 + n);
+        float x0, x1, x2, x3;
+        asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                     "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
+                     "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
+                     "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
+                     : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                     : "i"(a0), "i"(a0 + 1), "i"(a0 + 2), "i"(a0 + 3));
+        const int r = (u >> 3) * 16 + (lane & 15);                 // C row inside the pass
+        const int gi = 4 * n + (lane >> 4);                        // 8-byte column group 0..31
+        bf16x4 v;
+        v[0] = (__bf16)x0;
+        v[1] = (__bf16)x1;
+        v[2] = (__bf16)x2;
+        v[3] = (__bf16)x3;
+        *reinterpret_cast<bf16x4*>(stg + r * 256 + ((gi ^ (r & 15)) << 3)) = v;
+      });
+      asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
+      if constexpr (p == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // see FRESH
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = k * 4 + (lane >> 4);
+        const int ch = lane & 15;
+        const int sw = r & 15;
+        const int pg = (2 * ch) ^ sw;
+        const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
+        uint4 v = raw;
+        if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * F8_BM + wr * 128 + p * 32 + r) * N + tn_ * F8_BN +
+                                  wc * 128 + ch * 8) = v;
+      }
+      asm volatile("" ::: "memory");
+    });
+  };
+
+  const int ktiles = K / F8_BK;     // >= 2 (host guarantees)
+  bool rev = false;
+  auto kof = [&](int kt, bool r) { return (r ? ktiles - 1 - kt : kt) * F8_BK; };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(0, rev), buf0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma_piece(i, rA, rB, kof(1, rev), buf1);
+  __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0): K-tiles 0 and 1 landed (FRESH iteration)
+  bar();
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    read_frag(FB[x], true, x, buf0);
+    read_frag(FA[x], false, x, buf0);
+  }
+
+  char* cur = buf0;
+  char* nxt = buf1;
+  for (;;) {
+    const int next = tile + per;
+    const bool has_next = next < t_end;
+    int ntm = tm, ntn = tn;
+    __amdgpu_buffer_rsrc_t nA = rA, nB = rB;
+    if (has_next) {
+      tile_coords(next, tiles_m, tiles_n, ntm, ntn);
+      nA = rsrc(A + (size_t)ntm * F8_BM * K);
+      nB = rsrc(Bt + (size_t)ntn * F8_BN * K);
+    }
+    const int nsteady = has_next ? ktiles : ktiles - 2;
+    auto dma_of = [&](int t, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rb) {
+      const bool nt = t + 2 >= ktiles;               // DMA the next tile's K-tile t+2-ktiles
+      ra = nt ? nA : rA;
+      rb = nt ? nB : rB;
+      return nt ? kof(t + 2 - ktiles, SERP && !rev) : kof(t + 2, rev);
+    };
+    __amdgpu_buffer_rsrc_t ra, rb;
+    if (nsteady > 0) {
+      const int dk = dma_of(0, ra, rb);
+      iter(cur, nxt, ra, rb, dk, T_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    for (int t = 1; t < nsteady; ++t) {
+      const int dk = dma_of(t, ra, rb);
+      iter(cur, nxt, ra, rb, dk, F_{}, T_{}, T_{});
+      char* tmp = cur; cur = nxt; nxt = tmp;
+    }
+    if (!has_next) {
+      iter(cur, nxt, rA, rB, 0, F_{}, F_{}, T_{});
+      iter(nxt, nullptr, rA, rB, 0, F_{}, F_{}, F_{});
+    }
+    epilogue(tm, tn);
+    if (!has_next) break;
+    tile = next;
+    rev = SERP && !rev;
+    tm = ntm;
+    tn = ntn;
+    rA = nA;
+    rB = nB;
+  }
+}
+
 // OCP e4m3fn -> f32 in software (independent of the matrix cores): bias 7, no infinities,
 // S.1111.111 = NaN, exponent 0 = subnormal m/8 * 2^-6.
 __device__ __forceinline__ float e4m3_to_f32(uint8_t v) {

@@ -2,7 +2,8 @@
 // placement of the fp8 kernels under its variant number, without automatic switches.
 //   1 .. 4 = schedule placements, 5 / 6 = 4 / 3 with serpentine K, 7 / 8 = 4 / 3 with the loop
 //   rotated at slot B1, 9 = 4 with both, 10 / 11 = persistent with the schedules of 4 / 3,
-//   12 = 10 with serpentine K, 13 = 9 with the square cross-XCD raster.
+//   12 = 10 with serpentine K, 13 = 9 with the square cross-XCD raster; 20-37 = q16 placements;
+//   40 / 41 = persistent q16 (41: serpentine K).
 #include "gemm_fp8_kernels.h"
 
 extern "C" {
@@ -21,6 +22,9 @@ int amdgo_lab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, int
     auto kern = v == 10 ? gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>
               : v == 11 ? gemm_fp8_256x256_w4sp<4, 5, 20, 22, 8>
                         : gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6, true>;
+    hipLaunchKernelGGL(kern, dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+  } else if ((v == 40 || v == 41) && pgrid >= NXCD) {   // persistent q16 (41: serpentine K)
+    auto kern = v == 40 ? gemm_fp8_256x256_q16p<> : gemm_fp8_256x256_q16p<16, 18, 3, 34, 35, 43, true>;
     hipLaunchKernelGGL(kern, dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
   } else if (v == 13 && (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0) {
     hipLaunchKernelGGL((gemm_fp8_256x256_w4s<6, 7, 16, 24, 6, 32, true, true>), dim3(nwg), dim3(F8_THREADS), 0, s,

@@ -112,7 +112,7 @@ def test_fp8_kernel_audit(asm_fp8):
     """fp8 production q16 (unscaled v_mfma_f32_16x16x128_f8f6f4): 256 pinned AGPRs, one 128-VGPR
     fragment set (no spills into AGPRs), 64 MFMAs / 32 ds_read_b128 / 16 LDS-DMA pieces per
     K-tile, two barriers per K-tile (buffer free, next tile landed)."""
-    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_q16")
+    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_q16I")
     assert len(kernels) == 3    # production: v15, v16 (square raster), v17 (no serpentine K)
     _audit_q16(kernels)
     assert "gemm_fp8_256x256_w4sI" not in asm_fp8     # superseded: lab only
@@ -135,6 +135,19 @@ def test_fp8_w4s_lab_kernel_audit(asm_fp8_lab):
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", text)) == 16
         assert text.count("s_barrier") == 2
         assert "v_mov_b32" not in text
+
+
+def test_fp8_persistent_q16_kernel_audit(asm_fp8):
+    """Persistent q16 (v18): pinned AGPRs, one fragment set, unscaled 16x16x128 only; the fresh,
+    steady, last-with-read and last iterations are each one 64-MFMA body."""
+    kernels = _kernels(asm_fp8, "gemm_fp8_256x256_q16pI")
+    assert len(kernels) == 1
+    for body, st in kernels:
+        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+        assert st["NumVgprs"] <= 192, st
+        _no_compiler_agpr_access(body)
+        assert "v_mfma_scale" not in body
+        assert len(re.findall(r"v_mfma_f32_16x16x128_f8f6f4", body)) == 4 * 64
 
 
 def test_fp8_persistent_kernel_audit(asm_fp8):
@@ -222,6 +235,6 @@ def asm_fp8_lab(tmp_path_factory):
 
 def test_fp8_q16_kernel_audit(asm_fp8_lab):
     """q16 lab placements (v20-v37): the same invariants as the production q16 kernels."""
-    kernels = _kernels(asm_fp8_lab, "gemm_fp8_256x256_q16")
+    kernels = _kernels(asm_fp8_lab, "gemm_fp8_256x256_q16I")
     assert len(kernels) == 18
     _audit_q16(kernels)

@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[0, 10, 15, 16, 17])   # the production set (gemm.FP8_VARIANTS)
+@pytest.fixture(params=[0, 10, 15, 16, 17, 18])   # the production set (gemm.FP8_VARIANTS)
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
@@ -145,11 +145,13 @@ def _check_square_raster_fp8(cuda_device, G, torch):
 def test_fp8_production_variant_set_is_closed(cuda_device):
     from gpu_operator_amd.ops import gemm as G
 
-    for bad in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 20, 28, 99):
+    for bad in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 19, 20, 28, 40, 99):
         with pytest.raises(ValueError):
             G.set_fp8_variant(bad)
     assert G.get_fp8_variant() == 0
-    assert G.resolve_fp8_variant(8192, 8192, 8192) in (16, 17)
-    assert G.resolve_fp8_variant(8192 + 256, 8192, 8192) in (15, 17)
+    assert G.resolve_fp8_variant(8192, 8192, 8192) == 18
+    assert G.resolve_fp8_variant(16384, 16384, 16384) in (16, 17)
+    assert G.resolve_fp8_variant(4096, 4096, 4096) in (16, 17)
+    assert G.resolve_fp8_variant(4096 + 256, 4096, 4096) in (15, 17)
     assert G.resolve_fp8_variant(16384, 16384, 1024) == 10
     assert G.resolve_fp8_variant(300, 256, 256) == 0
