@@ -1137,9 +1137,13 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
   } else if (v == 45 && kk && (M / BM) % 16 == 0 && (N / BN) % 16 == 0) {
     hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
                        0, s, a, b, c, M, N, K);
-  } else if (v == 90 && kk) {                       // v44 with the K offset in voffset
-    hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true>), dim3(nwg),
-                       dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+  } else if (v >= 90 && v <= 94 && kk) {            // v44 + VK (90); DMA spacing 6 / 7 slots (91-94)
+    auto kern = v == 90 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true>
+              : v == 91 ? gemm_bf16_256x256_w4s<17, 19, 6, 80, 40, 32, true, false, 0, true>
+              : v == 92 ? gemm_bf16_256x256_w4s<17, 19, 7, 80, 40, 32, true, false, 0, true>
+              : v == 93 ? gemm_bf16_256x256_w4s<17, 19, 6, 96, 24, 32, true, false, 0, true>
+                        : gemm_bf16_256x256_w4s<17, 18, 6, 64, 48, 32, true, false, 0, true>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
   } else if (v >= 80 && v <= 89 && kk) {            // v44 knock-outs (WRONG results by design)
     auto kern = v == 89 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 64>
               : v == 86 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 16>
