@@ -4,8 +4,9 @@
 (the layout the MFMA fragments read without a transpose):
 
 * bf16 operands: ``native/hip/gemm_bf16.hip`` (``gemm_bf16``);
-* fp8 OCP e4m3fn operands: ``native/hip/gemm_fp8.hip`` (``gemm_fp8``), the block-scaled
-  ``v_mfma_scale_f32_32x32x64_f8f6f4`` with unit scales, i.e. the matrix cores' fp8 rate.
+* fp8 OCP e4m3fn operands: ``native/hip/gemm_fp8.hip`` (``gemm_fp8``), the unscaled double-rate
+  ``v_mfma_f32_16x16x128_f8f6f4`` (the block-scaled 32x32x64 form for short K), i.e. the matrix
+  cores' fp8 rate.
 
 Replaces the reference validator's ``vectorAdd`` pass/fail probe
 (reference: validator/cuda-workload-validation.yaml:20) with a matrix-core
