@@ -19,11 +19,11 @@
 // Only numerically exact, measured production kernels are reachable from here. The variant is an
 // API argument (amdgo_gemm_set_variant), never read from the environment; superseded generations
 // and knock-out timings live in the tools-only gemm_bf16_lab.hip.
-//   0  = automatic (default): v44; v25 for short K with >= 2 tiles per CU; v45 for >= 8 dispatch
+//   0  = automatic (default): v44; v25 for K <= 4096 with >= 2 tiles per CU; v45 for >= 8 dispatch
 //        waves with K >= 8192 on 16x16-tile multiples; v42 / v18 on devices without 256 CUs.
 //   18 / 25 / 42 / 44 / 45 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
-// Every w4s kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
+// Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
 // add per K-tile, loop-invariant soffsets; 17 fewer SALU per K-tile, +0.6-0.8 % at 8192^3 and
 // 16384^3, profiles/r2_sched/sweep_vk.jsonl).
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
@@ -49,9 +49,10 @@ static int resolve_variant(int M, int N, int K) {
   int v = g_variant;
   if (v == 0) {
     v = 44;
-    // Short K (K-loop of <= 32 K-tiles) with several tiles per CU: the persistent v25 hides each
-    // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %).
-    if (K <= 32 * BK && nwg >= 2 * cus) v = 25;
+    // Short K (K-loop of <= 64 K-tiles) with several tiles per CU: the persistent v25 hides each
+    // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %;
+    // K = 3072 +1.2 %, K = 4096 +0.3-0.7 %: profiles/r2_sched/sweep_persistent_midk.jsonl).
+    if (K <= 64 * BK && nwg >= 2 * cus) v = 25;
     // Big grids (>= 8 dispatch waves) with long K: the square cross-XCD raster (v45) streams fewer
     // distinct panels per wave (profiles/r1_s6_sq: 12288^3 +5.5 %, 16384x8192x8192 +2.9 %,
     // 16384^3 +3.4 %; at 4 waves or K = 4096 it measured 1 % behind v44, so those stay on v44).
@@ -88,7 +89,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          a, b, c, M, N, K);
       break;
     case 25:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, false, true>), dim3(persistent_grid(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 42:

@@ -585,7 +585,7 @@ gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ B
 constexpr int W4P_EPI_WAVE = 8192;                       // 32 rows x 128 cols x bf16
 constexpr int W4P_LDS = LDS_BYTES + 4 * W4P_EPI_WAVE;     // 160 KiB
 
-template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, bool SERP = false>
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, bool SERP = false, bool VK = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
@@ -622,8 +622,12 @@ gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ 
     // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
     const int rblk = ((i & 7) << 2) + wid;
     char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff,
-                                             (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
+    if constexpr (VK)   // K offset in the lane offset, loop-invariant soffsets (as w4s VK)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff + (uint32_t)k0 * 2u,
+                                               (uint32_t)rblk * 8u * (uint32_t)K * 2u, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rb : ra, (lds_void*)lds, 16, voff,
+                                               (uint32_t)rblk * 8u * (uint32_t)K * 2u + (uint32_t)k0 * 2u, 0, 0);
   };
 
   int lane_off[2];

@@ -123,7 +123,7 @@ def test_production_variant_set_is_closed(cuda_device):
     assert G.get_variant() == 0
 
 
-@pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 44), (16384, 16384, 1024, 25),
+@pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 44), (16384, 16384, 1024, 25), (8192, 8192, 4096, 25),
                                         (12288, 12288, 8192, 45), (4096, 4096, 4096, 44),
                                         (256, 256, 64, 0), (300, 256, 256, 0)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
