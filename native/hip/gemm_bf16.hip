@@ -21,7 +21,8 @@
 // and knock-out timings live in the tools-only gemm_bf16_lab.hip.
 //   0  = automatic (default): v44; v25 for K <= 4096 with >= 2 tiles per CU; v45 for >= 8 dispatch
 //        waves with K >= 8192 on 16x16-tile multiples; v42 / v18 on devices without 256 CUs.
-//   18 / 25 / 42 / 44 / 45 = that kernel pinned (no automatic switch; still falls back to a kernel
+//   47 / 48 = v44 / v45 with permuted A-panel DMA rows (PA), the default when K is not a power of two.
+//   18 / 25 / 42 / 44 / 45 / 47 / 48 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
 // Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
 // add per K-tile, loop-invariant soffsets; 17 fewer SALU per K-tile, +0.6-0.8 % at 8192^3 and
@@ -59,8 +60,18 @@ static int resolve_variant(int M, int N, int K) {
     else if (sq && nwg >= 8 * cus && K >= 128 * BK) v = 45;
   }
   if (v == 45 && !sq) v = 44;                           // square raster needs 16x16 super-tiles
+  if (v == 48 && !sq) v = 47;
+  if ((v == 47 || v == 48) && cus != 256) v = 42;
   if (v == 25 && persistent_grid(nwg) < NXCD) v = 44;
   if ((v == 44 || v == 45) && cus != 256) v = 42;       // serpentine K assumes 32 co-resident WGs / XCD
+  // K not a power of two: A-panel DMA instructions read rows 32 apart (PA, v47 / v48). At a 24 KiB
+  // row stride adjacent rows cost 8-11 % (12288^3 1405 -> 1557 TF, 8192^2x12288 1457 -> 1579,
+  // 12288^2x10240 +5 %); at power-of-two K it is neutral (8192) or worse (16384: -8 %).
+  // profiles/r2_sched/sweep_pa.jsonl
+  if (g_variant == 0 && (K & (K - 1)) != 0) {
+    if (v == 44) v = 47;
+    else if (v == 45) v = 48;
+  }
   return v;
 }
 
@@ -68,7 +79,8 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
-  if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45) return (int)hipErrorInvalidValue;
+  if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48)
+    return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
 }
@@ -99,6 +111,14 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
     case 44:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
+      break;
+    case 47:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true, true>), dim3(nwg),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 48:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true, true>), dim3(nwg),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 45:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true>), dim3(nwg), dim3(W4_THREADS),

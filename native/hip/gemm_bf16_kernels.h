@@ -86,9 +86,11 @@ __host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
 // KO (lab knock-out timings only, wrong results): bit0 drops the lgkmcnt(0) before the free barrier,
 // bit1 the landing vmcnt (keeps lgkmcnt(0)), bit2 the free barrier, bit3 the landing barrier, bit4
 // the steady-state DMA pieces, bit5 the fragment reads of the loop, bit6 the XOR chunk permutation
-// of the DMA's global addresses (lanes read their row's chunks in order; the LDS image is then wrong).
+// of the DMA's global addresses (lanes read their row's chunks in order; the LDS image is then wrong),
+// bit7 (A) / bit8 (B) DMA instructions that read rows rblk + 32 g instead of 8 rblk + g (timing of
+// the row grouping; the LDS image is then a row permutation of the right one).
 template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
-          bool SQ = false, int KO = 0, bool VK = false>
+          bool SQ = false, int KO = 0, bool VK = false, bool PA = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -114,10 +116,21 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   const int par = wid & 1;
   const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
                         (uint32_t)(((lane & 7) ^ ((KO & 64) ? 0 : ((par * 4 + (lane >> 4)) & 7))) * 16);
+  const uint32_t voff_p = (uint32_t)(lane >> 3) * 32u * (uint32_t)K * 2u +
+                          (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
   auto dma_piece = [&](int i, int k0, char* buf) {
     // piece p = 4i + wid; p >= 32 (the B panel) <=> i >= 8, a compile-time fact once unrolled
     const int rblk = ((i & 7) << 2) + wid;
     char* lds = buf + (i >= 8 ? PANEL_BYTES : 0) + rblk * 1024;
+    // PA: an A-panel DMA instruction reads panel rows rblk + 32 g (g = lane >> 3) into LDS slots
+    // 8 rblk + g, so its 8 rows are 32 rows apart instead of adjacent (at a 24 KiB row stride,
+    // K = 12288, adjacent rows cost 10 %); LDS slot s then holds panel row 32 (s & 7) + (s >> 3),
+    // which the epilogue's row mapping undoes. B keeps adjacent rows: its slots are C columns.
+    if ((((KO & 128) || PA) && i < 8) || ((KO & 256) && i >= 8)) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff_p + (uint32_t)k0 * 2u,
+                                               (uint32_t)rblk * (uint32_t)K * 2u, 0, 0);
+      return;
+    }
     if constexpr (VK)   // K offset in the lane offset (one VALU add per K-tile), loop-invariant soffset
       __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff + (uint32_t)k0 * 2u,
                                                (uint32_t)rblk * 8u * (uint32_t)K * 2u, 0, 0);
@@ -249,7 +262,8 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+    const int gr = PA ? 32 * (r & 7) + (r >> 3) : r;           // LDS slot -> panel row (PA)
+    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + gr) * N + tn * BN + ch * 8) = v;
   }
 }
 // w4t: the w4s kernel with the whole K-tile schedule taken from a schedule class SC, so the

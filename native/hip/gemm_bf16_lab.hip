@@ -1144,6 +1144,16 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
               : v == 93 ? gemm_bf16_256x256_w4s<17, 19, 6, 96, 24, 32, true, false, 0, true>
                         : gemm_bf16_256x256_w4s<17, 18, 6, 64, 48, 32, true, false, 0, true>;
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+  } else if ((v == 98 && kk && (M / BM) % 16 == 0 && (N / BN) % 16 == 0) || (v == 99 && kk)) {   // + PA
+    auto kern = v == 98 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true, true>
+                        : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true, true>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+  } else if (v >= 95 && v <= 97 && kk) {            // v45+VK with permuted DMA row grouping (WRONG results)
+    if ((M / BM) % 16 || (N / BN) % 16) return (int)hipErrorInvalidValue;
+    auto kern = v == 95 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 128, true>
+              : v == 96 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 256, true>
+                        : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 384, true>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
   } else if (v >= 80 && v <= 89 && kk) {            // v44 knock-outs (WRONG results by design)
     auto kern = v == 89 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 64>
               : v == 86 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 16>
@@ -1183,6 +1193,6 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
 }
 
 // 1 if variant v produces correct results (everything except the knock-out timings 20-24, 80-85).
-int amdgo_lab_variant_is_exact(int v) { return !(v >= 20 && v <= 24) && !(v >= 80 && v <= 89); }
+int amdgo_lab_variant_is_exact(int v) { return !(v >= 20 && v <= 24) && !(v >= 80 && v <= 89) && !(v >= 95 && v <= 97); }
 
 }  // extern "C"

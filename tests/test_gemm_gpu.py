@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -116,7 +116,7 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
@@ -124,6 +124,7 @@ def test_production_variant_set_is_closed(cuda_device):
 
 
 @pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 44), (16384, 16384, 1024, 25), (8192, 8192, 4096, 25),
+                                        (12288, 12288, 12288, 48), (8192, 8192, 12288, 47),
                                         (12288, 12288, 8192, 45), (4096, 4096, 4096, 44),
                                         (256, 256, 64, 0), (300, 256, 256, 0)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
@@ -132,6 +133,6 @@ def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     from gpu_operator_amd.ops import gemm as G
 
     if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
-        want = {44: 42, 45: 42}.get(want, want)
+        want = {44: 42, 45: 42, 47: 42, 48: 42}.get(want, want)
     assert G.get_variant() == 0
     assert G.resolve_variant(m, n, k) == want
