@@ -484,13 +484,13 @@ def transform_partition_manager(obj: Obj, spec: cp.ClusterPolicySpec, n) -> None
     if spec.cdi.is_enabled():
         o.set_env(c, "CDI_ENABLED", "true")
     o.set_env(c, "PARTITION_STRATEGY", spec.partition.get_strategy())
-    # An NPS change needs amdgpu reloaded. When the driver container owns the module, reload it
-    # with that container's modprobe and module tree (its root is bind-mounted at /run/amd/driver);
-    # with a host driver the agent's default (modprobe via /host) applies. A user-set
-    # DRIVER_RELOAD_CMD in spec.partitionManager.env wins.
+    # An NPS change needs amdgpu reloaded. When the driver container owns the module, only it has
+    # the module tree that loaded it (precompiled .ko under /opt/amdgpu or its DKMS build): the
+    # partition manager asks it through a request file in the shared /run/amd/driver and waits for
+    # its answer (operands/driver_container.py, serve_reloads). With a host driver the agent's
+    # default (modprobe via /host) applies. A user-set DRIVER_RELOAD_CMD wins.
     if spec.driver.is_enabled() and not any(e.get("name") == "DRIVER_RELOAD_CMD" for e in c.get("env", [])):
-        o.set_env(c, "DRIVER_RELOAD_CMD",
-                  "chroot /run/amd/driver modprobe -r amdgpu; chroot /run/amd/driver modprobe amdgpu")
+        o.set_env(c, "DRIVER_RELOAD_VIA", "driver-container")
 
 
 # ---------------------------------------------------------------------------------------------

@@ -295,6 +295,18 @@ class UpgradeStateManager:
         return [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node}")
                 if self.pod_filter(p) and (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
 
+    @staticmethod
+    def _daemon_or_mirror(p: Dict) -> Optional[str]:
+        """Why eviction cannot clear ``p`` from the node, or None: a DaemonSet pod comes straight
+        back (it tolerates the cordon) and a mirror (static) pod is not the API server's to delete
+        -- kubectl drain's IgnoreAllDaemonSets / mirror filters (reference pod_manager.go:147,186-197)."""
+        owner = o.controller_of(p)
+        if owner and owner.get("kind") == "DaemonSet":
+            return "DaemonSet-managed"
+        if "kubernetes.io/config.mirror" in o.get_annotations(p):
+            return "mirror pod"
+        return None
+
     def _drain_or_failed(self, ns: NodeState, drain_enabled: bool, why: str) -> None:
         """reference: pod_manager.go:369-377 (updateNodeToDrainOrFailed)."""
         self.client.create_event(ns.node, EVENT_REASON,
@@ -318,7 +330,10 @@ class UpgradeStateManager:
         blocked = []
         for p in pods:
             uses_emptydir = any("emptyDir" in v for v in (p.get("spec") or {}).get("volumes") or [])
-            if uses_emptydir and not (pd and pd.deleteEmptyDir):
+            why = self._daemon_or_mirror(p)
+            if why:
+                blocked.append(f"{o.name(p)} ({why})")
+            elif uses_emptydir and not (pd and pd.deleteEmptyDir):
                 blocked.append(f"{o.name(p)} (emptyDir)")
             elif o.controller_of(p) is None and not (pd and pd.force):
                 blocked.append(f"{o.name(p)} (unmanaged)")
@@ -436,9 +451,12 @@ class UpgradeStateManager:
     def _pod_restart(self, state: ClusterUpgradeState) -> None:
         for ns in list(state.node_states.get(POD_RESTART_REQUIRED, [])):
             if self.pod_revision_hash(ns.driver_pod) != self.ds_revision_hash(ns.driver_ds):
-                if self.pod_filter is not None and self._gpu_pods_on(o.name(ns.node)):
+                if self.pod_filter is not None and [p for p in self._gpu_pods_on(o.name(ns.node))
+                                                    if not self._daemon_or_mirror(p)]:
                     # never unload amdgpu under a pod that still holds /dev/kfd (one that started
-                    # after the eviction, e.g. with a toleration for the cordon): evict again
+                    # after the eviction, e.g. with a toleration for the cordon): evict again.
+                    # DaemonSet / mirror GPU pods are not evictable: pod deletion routed them to
+                    # drain (which skips them) or upgrade-failed, so they cannot loop the node here
                     log.info("node %s: GPU pods present again; back to pod deletion", o.name(ns.node))
                     self.set_state(ns.node, POD_DELETION_REQUIRED)
                     self._move(state, ns, POD_RESTART_REQUIRED, POD_DELETION_REQUIRED)

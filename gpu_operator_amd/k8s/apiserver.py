@@ -250,7 +250,7 @@ class FakeAPIServer:
                     if ev.type in (ADDED, MODIFIED) and rv <= since:
                         return
                     events.put(ev)
-                stop = srv.client.watch(av, kind, cb, ns)
+                stop = srv.client.watch(av, kind, cb, ns, field_selector=q.get("fieldSelector"))
                 registering[0] = False
                 self.send_response(200)
                 self.send_header("Content-Type", "application/json")

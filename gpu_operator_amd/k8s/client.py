@@ -50,7 +50,7 @@ class Client(Protocol):
     def server_version(self) -> str: ...
 
     def watch(self, api_version: str, kind: str, callback: WatchCallback,
-              namespace: str = "") -> Callable[[], None]: ...
+              namespace: str = "", field_selector: Optional[str] = None) -> Callable[[], None]: ...
 
     def create_event(self, involved: Obj, reason: str, message: str, type_: str = "Normal") -> None: ...
 

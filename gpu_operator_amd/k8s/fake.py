@@ -36,7 +36,7 @@ class FakeClient:
         self.collect_orphans = collect_orphans
         self._store: Dict[Tuple[str, str, str, str], Obj] = {}
         self._rv = itertools.count(1)
-        self._watchers: List[Tuple[str, str, str, WatchCallback]] = []
+        self._watchers: List[Tuple[str, str, str, WatchCallback, Optional[str]]] = []
         self.interceptors: List[Interceptor] = []
         self.unserved_kinds: Set[str] = set(unserved_kinds or ())
         self.version = server_version
@@ -58,8 +58,9 @@ class FakeClient:
             raise errors.NoKindMatch(f"no matches for kind {kind} in version {api_version}")
 
     def _notify(self, etype: str, obj: Obj, old: Optional[Obj] = None) -> None:
-        for av, kind, ns, cb in list(self._watchers):
-            if av == obj.get("apiVersion") and kind == obj.get("kind") and (not ns or ns == o.namespace(obj)):
+        for av, kind, ns, cb, fs in list(self._watchers):
+            if av == obj.get("apiVersion") and kind == obj.get("kind") and (not ns or ns == o.namespace(obj)) \
+                    and o.field_selector_matches(fs, obj):
                 cb(WatchEvent(etype, copy.deepcopy(obj), copy.deepcopy(old) if old else None))
 
     def _bump(self, obj: Obj) -> None:
@@ -250,12 +251,13 @@ class FakeClient:
         return self.version
 
     def watch(self, api_version: str, kind: str, callback: WatchCallback,
-              namespace: str = "") -> Callable[[], None]:
-        entry = (api_version, kind, namespace, callback)
+              namespace: str = "", field_selector: Optional[str] = None) -> Callable[[], None]:
+        entry = (api_version, kind, namespace, callback, field_selector)
         with self._lock:
             self._watchers.append(entry)
             existing = [copy.deepcopy(v) for (av, k, ns, _), v in sorted(self._store.items())
-                        if av == api_version and k == kind and (not namespace or ns == namespace)]
+                        if av == api_version and k == kind and (not namespace or ns == namespace)
+                        and o.field_selector_matches(field_selector, v)]
         for obj in existing:
             callback(WatchEvent(ADDED, obj))
 

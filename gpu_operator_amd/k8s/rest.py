@@ -239,8 +239,12 @@ class RestClient:
             log.debug("event creation failed: %s", e)
 
     def watch(self, api_version: str, kind: str, callback: WatchCallback,
-              namespace: str = "") -> Callable[[], None]:
+              namespace: str = "", field_selector: Optional[str] = None) -> Callable[[], None]:
+        """List+watch ``kind``; ``field_selector`` (e.g. ``metadata.name=<node>``) is sent to the
+        API server on both, so a node agent receives its own Node's events only instead of every
+        Node update in the cluster."""
         stop = threading.Event()
+        sel = {"fieldSelector": field_selector} if field_selector else {}
 
         def run():
             rv = ""
@@ -248,7 +252,7 @@ class RestClient:
             while not stop.is_set():
                 try:
                     if not rv:
-                        body = self._request("GET", self._path(api_version, kind, namespace)).json()
+                        body = self._request("GET", self._path(api_version, kind, namespace), params=sel or None).json()
                         rv = body["metadata"]["resourceVersion"]
                         log.debug("watch %s: list at rv=%s (%d items)", kind, rv, len(body.get("items", [])))
                         fresh = {}
@@ -263,7 +267,7 @@ class RestClient:
                         known = fresh
                     r = self._request("GET", self._path(api_version, kind, namespace),
                                       params={"watch": "1", "resourceVersion": rv,
-                                              "allowWatchBookmarks": "true", "timeoutSeconds": "300"},
+                                              "allowWatchBookmarks": "true", "timeoutSeconds": "300", **sel},
                                       stream=True, timeout=(10, 330))
                     # chunk_size=None: yield each chunk as it arrives (the API server sends one
                     # event per chunk); a fixed size would hold small events back

@@ -160,7 +160,7 @@ class ConfigManager:
             old = o.get_labels(ev.old).get(self.label) if ev.old else None
             if ev.old is None or old != o.get_labels(ev.obj).get(self.label):
                 wake.set()
-        cancel = self.client.watch("v1", "Node", on_node)
+        cancel = self.client.watch("v1", "Node", on_node, field_selector=f"metadata.name={self.node}")
         try:
             while not stop.is_set():
                 try:

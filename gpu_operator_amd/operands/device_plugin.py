@@ -67,6 +67,7 @@ class Device:
     hive: int
     healthy: bool = True
     replica_of: Optional[str] = None
+    vram_bytes: int = 0          # this device's HBM share from sysfs (a partition's under CPX/NPSx)
 
 
 @dataclass
@@ -114,7 +115,7 @@ def discover(cfg: Config, root: Optional[str] = None) -> List[Device]:
         did = f"amdgpu-{g['unique_id']:016x}" if cfg.device_id_strategy == "uuid" and g["unique_id"] \
             else str(g["index"])
         out.append(Device(did, res, g["drm_render_minor"], g["drm_card"], g["numa_node"], g["pci_bdf"],
-                          g["unique_id"], part, g["xgmi_hive_id"]))
+                          g["unique_id"], part, g["xgmi_hive_id"], vram_bytes=int(g.get("vram_total") or 0)))
     if cfg.partition_strategy == "single":
         modes = {d.partition for d in out}
         if len(modes) > 1:

@@ -19,6 +19,13 @@ kernel modules + firmware (no user-space driver libraries to expose), so:
 
 ``probe``  exit 0 iff the driver is live with all GPUs enumerated (the startupProbe; it
            touches ``.driver-ctr-ready`` on success, which the validator waits on).
+
+Reload on request: a memory-partition (NPS) change only takes effect once amdgpu reloads, and
+only this container has the module tree that loaded it (precompiled ``.ko`` files under
+``/opt/amdgpu`` or its DKMS build). While ``init`` blocks it serves a node-local request file,
+``/run/amd/driver/reload-request`` (JSON ``{"id": ...}``, written by the partition manager):
+it unloads the modules, loads them again through the same precompiled / DKMS path, waits for
+readiness, rewrites the ``.driver-ctr`` marker and answers in ``reload-result`` with the same id.
 """
 
 from __future__ import annotations
@@ -42,6 +49,8 @@ from ..utils import mounts
 log = logging.getLogger("amdgpu-driver")
 
 LOAD_ORDER = ["amdkcl", "amdttm", "amddrm_ttm_helper", "amddrm_buddy", "amdxcp", "amdgpu"]
+RELOAD_REQUEST = "reload-request"
+RELOAD_RESULT = "reload-result"
 
 
 class DriverError(Exception):
@@ -112,6 +121,10 @@ class DriverContainer:
     def marker(self) -> str:
         return os.path.join(self.run_dir, "driver", ".driver-ctr")
 
+    @property
+    def driver_dir(self) -> str:
+        return os.path.join(self.run_dir, "driver")
+
     # -- sources -------------------------------------------------------------------------------
     def precompiled_modules(self) -> List[str]:
         d = mounts.path(os.path.join(self.image_root, "opt/amdgpu/precompiled", self.kernel))
@@ -156,6 +169,68 @@ class DriverContainer:
         self._run(["modprobe", "amdgpu"] + params, "modprobe amdgpu")
         return "dkms", ["amdgpu"]
 
+    def unload(self) -> List[str]:
+        """Remove what ``load`` inserted: precompiled modules in reverse load order (amdgpu
+        first), else ``modprobe -r amdgpu`` (DKMS). The GPU clients are gone by now (the partition
+        manager paused them); a module still in use fails the unload."""
+        mods = [_mod_name(m) for m in self.precompiled_modules()]
+        if mods:
+            loaded = [m for m in reversed(mods) if os.path.isdir(os.path.join(self.sys_root, "sys/module", m))]
+            for m in loaded:
+                self._run(["rmmod", m], f"rmmod {m}")
+            return loaded
+        self._run(["modprobe", "-r", "amdgpu"], "modprobe -r amdgpu")
+        return ["amdgpu"]
+
+    def _write_marker(self, info: Dict) -> None:
+        os.makedirs(os.path.dirname(self.marker), exist_ok=True)
+        with open(self.marker + ".tmp", "w") as f:
+            json.dump(info, f)
+        os.replace(self.marker + ".tmp", self.marker)
+
+    def reload(self) -> Dict:
+        t0 = time.monotonic()
+        removed = self.unload()
+        mode, mods = self.load()
+        why = self.wait_ready()
+        info = {"kernel": self.kernel, "mode": mode, "modules": mods, "unloaded": removed,
+                "version": self.driver_version, "reload_s": round(time.monotonic() - t0, 3), "ts": time.time(),
+                "state": why}
+        self._write_marker(info)
+        log.info("amdgpu reloaded: %s", info)
+        return info
+
+    def serve_reloads(self, stop: threading.Event, period: float = 1.0) -> None:
+        """Answer reload requests until ``stop`` (event-driven: inotify on the driver dir)."""
+        os.makedirs(self.driver_dir, exist_ok=True)
+        req = os.path.join(self.driver_dir, RELOAD_REQUEST)
+        while not stop.is_set():
+            if not os.path.exists(req):
+                try:
+                    devices.wait_files(self.driver_dir, [RELOAD_REQUEST], timeout=period)
+                except Exception:  # noqa: BLE001 - no inotify (no native library): poll
+                    stop.wait(period)
+                continue
+            try:
+                with open(req) as f:
+                    rid = (json.load(f) or {}).get("id", "")
+            except (OSError, ValueError):
+                rid = ""
+            try:
+                os.unlink(req)
+            except FileNotFoundError:
+                pass
+            try:
+                res = {"id": rid, "ok": True, "info": self.reload()}
+            except DriverError as e:
+                log.error("reload failed: %s", e)
+                res = {"id": rid, "ok": False, "error": str(e)}
+            res["ts"] = time.time()
+            out = os.path.join(self.driver_dir, RELOAD_RESULT)
+            with open(out + ".tmp", "w") as f:
+                json.dump(res, f)
+            os.replace(out + ".tmp", out)
+
     # -- readiness -----------------------------------------------------------------------------
     def ready(self) -> Tuple[bool, str]:
         st = devices.driver_state(self.sys_root, self.dev_root)
@@ -198,10 +273,7 @@ class DriverContainer:
         info = {"kernel": self.kernel, "os": f"{osr.get('ID', '')}{osr.get('VERSION_ID', '')}",
                 "mode": mode, "modules": mods, "firmware_files": fw, "version": self.driver_version,
                 "load_s": round(time.monotonic() - t0, 3), "ts": time.time(), "state": why}
-        os.makedirs(os.path.dirname(self.marker), exist_ok=True)
-        with open(self.marker + ".tmp", "w") as f:
-            json.dump(info, f)
-        os.replace(self.marker + ".tmp", self.marker)
+        self._write_marker(info)
         log.info("amdgpu ready: %s", info)
         return info
 
@@ -247,7 +319,7 @@ def main(argv=None, stop: Optional[threading.Event] = None, dc: Optional[DriverC
     stop = stop or threading.Event()
     if threading.current_thread() is threading.main_thread():
         signal.signal(signal.SIGTERM, lambda *_: stop.set())
-    stop.wait()
+    dc.serve_reloads(stop)
     dc.shutdown()
     return 0
 

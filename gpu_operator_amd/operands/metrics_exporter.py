@@ -68,6 +68,11 @@ LINK_FIELDS = {
     "gpu_xgmi_link_up": ("gauge", "xGMI link status (1 up, 0 down)"),
 }
 ALL_FIELDS = list(FIELDS) + list(GM_FIELDS) + list(LINK_FIELDS)
+# hwmon / RAS / PCIe readings of the physical device (one PCI function): under CPX/DPX every
+# partition agent would report the same value again
+DEVICE_LEVEL_FIELDS = frozenset({"gpu_power_watts", "gpu_temperature_edge_celsius", "gpu_temperature_junction_celsius",
+                                 "gpu_temperature_memory_celsius", "gpu_ecc_correctable_total",
+                                 "gpu_ecc_uncorrectable_total", "gpu_pcie_bandwidth_bytes"})
 
 
 def load_fields(path: Optional[str]) -> List[str]:
@@ -145,15 +150,22 @@ class GPUCollector(Collector):
                 lbl = labels
             cls = CounterMetricFamily if kind == "counter" else GaugeMetricFamily
             fams[f] = cls("amd_" + f.replace("_total", "") if kind == "counter" else "amd_" + f, help_, labels=lbl)
+        # the PMFW gpu_metrics table (energy, socket power, per-link xGMI bytes) belongs to the
+        # physical device, which CPX/DPX enumerate once per partition: its series come from the
+        # lowest-index agent of each PCI function only, so sums over `gpu` do not multiply them
+        owner = {}
+        for g in sorted(gpus, key=lambda g: g["index"]):
+            owner.setdefault(g["pci_bdf"], g["index"])
         for g in gpus:
             t = tele.get(g["index"], {})
             did = f"amdgpu-{g['unique_id']:016x}"
             ns, pod, ctr = pods.get(did, ("", "", ""))
             lv = [str(g["index"]), did, g["pci_bdf"], g["compute_partition"] or "SPX", g["product_name"],
                   self.hostname, ns, pod, ctr]
-            m = gm.get(g["index"])
+            first = owner.get(g["pci_bdf"]) == g["index"]
+            m = gm.get(g["index"]) if first else None
             for f in self.fields:
-                if f in LINK_FIELDS:
+                if f in LINK_FIELDS or (f in DEVICE_LEVEL_FIELDS and not first):
                     continue
                 if f in GM_FIELDS:
                     if m is None:

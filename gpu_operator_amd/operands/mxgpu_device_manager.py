@@ -183,7 +183,7 @@ def main(argv=None, client=None) -> int:
         if o.name(ev.obj) == node and (ev.old is None or o.get_labels(ev.old).get(CONFIG_LABEL) !=
                                        o.get_labels(ev.obj).get(CONFIG_LABEL)):
             kick.set()
-    client.watch("v1", "Node", on_node)
+    client.watch("v1", "Node", on_node, field_selector=f"metadata.name={node}")
     while True:
         log.info("reconcile: %s", m.reconcile())
         kick.wait(a.resync)

@@ -179,7 +179,7 @@ def main(argv=None, client=None) -> int:
             if seen.get("v", "unset") != v:
                 seen["v"] = v
                 kick.set()
-        client.watch("v1", "Node", on_node)
+        client.watch("v1", "Node", on_node, field_selector=f"metadata.name={a.node_name}")
     while not stop.is_set():
         try:
             want = compute_labels()

@@ -14,7 +14,8 @@ agents and render nodes. This agent:
    for those pods to be gone; stops listed host services;
 3. applies the memory (NPS) modes; an NPS change only takes effect once amdgpu reloads, so the
    node goes ``reload-required`` -> ``reloading``: ``modprobe -r amdgpu && modprobe amdgpu`` on
-   the host (or DRIVER_RELOAD_CMD, e.g. through the driver container), then a bounded wait for
+   the host, a request to the driver container when it owns the module (DRIVER_RELOAD_VIA=
+   driver-container), or DRIVER_RELOAD_CMD; then a bounded wait for
    ``initstate=live``; then the compute modes (validated against ``available_*_partition``);
 4. waits (bounded) until the KFD agent count matches the new layout — the re-enumeration;
 5. restores the deploy labels (the device plugin comes back and re-registers the new
@@ -29,6 +30,7 @@ All state lives on the Node, so a restarted agent resumes or re-verifies (SURVEY
 from __future__ import annotations
 
 import argparse
+import json
 import logging
 import os
 import shlex
@@ -100,7 +102,7 @@ class PartitionManager:
                  pods_timeout: float = 300.0, host_services: Optional[List[str]] = None,
                  run: Callable = subprocess.run, namespace: str = "",
                  reload_driver: Optional[Callable[[], None]] = None, reload_cmd: str = "",
-                 reload_timeout: float = 600.0):
+                 reload_timeout: float = 600.0, reload_via: str = "", driver_dir: str = "/run/amd/driver"):
         self.client = client
         self.node = node
         self.config_file = config_file
@@ -116,6 +118,8 @@ class PartitionManager:
         self.reload_driver = reload_driver or self._reload_driver   # tests inject the driver's reload
         self.reload_cmd = reload_cmd
         self.reload_timeout = reload_timeout
+        self.reload_via = reload_via          # "driver-container": ask the driver pod (request file)
+        self.driver_dir = driver_dir
 
     # -- node state -----------------------------------------------------------------------------
     def _node(self) -> Dict:
@@ -190,7 +194,14 @@ class PartitionManager:
     # -- driver reload (memory partition) ----------------------------------------------------------
     def _reload_driver(self) -> None:
         """Unload and reload amdgpu so a new NPS mode takes effect. The GPU clients
-        are paused and the host services stopped by now; a failing step is a PartitionError."""
+        are paused and the host services stopped by now; a failing step is a PartitionError.
+
+        With the driver container owning the module (``reload_via="driver-container"``) the
+        reload is its job -- only it has the module tree that loaded amdgpu: a request file in the
+        shared driver dir, answered by ``amdgpu-driver`` with a result carrying the same id."""
+        if self.reload_via == "driver-container":
+            self._reload_via_driver_container()
+            return
         cmds = [shlex.split(c) for c in self.reload_cmd.split(";") if c.strip()] if self.reload_cmd else \
             [["chroot", "/host", "modprobe", "-r", "amdgpu"], ["chroot", "/host", "modprobe", "amdgpu"]]
         for cmd in cmds:
@@ -201,6 +212,40 @@ class PartitionManager:
             if getattr(p, "returncode", 0) != 0:
                 err = (getattr(p, "stderr", "") or "").strip()[-300:]
                 raise PartitionError(f"driver reload: {' '.join(cmd)} exited {p.returncode}: {err}")
+
+    def _reload_via_driver_container(self) -> None:
+        import uuid
+        from .driver_container import RELOAD_REQUEST, RELOAD_RESULT
+        rid = uuid.uuid4().hex
+        os.makedirs(self.driver_dir, exist_ok=True)
+        req = os.path.join(self.driver_dir, RELOAD_REQUEST)
+        with open(req + ".tmp", "w") as f:
+            json.dump({"id": rid, "node": self.node, "ts": time.time()}, f)
+        os.replace(req + ".tmp", req)
+        res_path = os.path.join(self.driver_dir, RELOAD_RESULT)
+        deadline = time.monotonic() + self.reload_timeout
+        while True:
+            try:
+                with open(res_path) as f:
+                    res = json.load(f)
+                if res.get("id") == rid:
+                    break
+            except (OSError, ValueError):
+                pass
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise PartitionError(f"driver container did not answer reload request {rid} within "
+                                     f"{self.reload_timeout:.0f}s (is the driver pod running?)")
+            if os.path.exists(res_path):            # an older request's answer: poll for ours
+                time.sleep(min(0.1, left))
+                continue
+            try:
+                devices.wait_files(self.driver_dir, [RELOAD_RESULT], timeout=min(1.0, left))
+            except Exception:  # noqa: BLE001 - no inotify: poll
+                time.sleep(min(0.2, left))
+        if not res.get("ok"):
+            raise PartitionError(f"driver container reload failed: {res.get('error')}")
+        log.info("driver container reloaded amdgpu: %s", res.get("info"))
 
     def wait_driver_live(self) -> None:
         deadline = time.monotonic() + self.reload_timeout
@@ -311,13 +356,16 @@ def main(argv=None, client=None) -> int:
     ap.add_argument("--resync", type=float, default=300.0)
     ap.add_argument("--reload-cmd", default=os.environ.get("DRIVER_RELOAD_CMD", ""),
                     help="';'-separated commands that reload amdgpu (default: modprobe -r/modprobe via /host)")
+    ap.add_argument("--reload-via", default=os.environ.get("DRIVER_RELOAD_VIA", ""), choices=["", "driver-container"],
+                    help="driver-container: ask the amdgpu driver pod to reload (it owns the module tree)")
     a = ap.parse_args(argv)
     if client is None:
         from ..k8s.rest import RestClient
         client = RestClient()
     pm = PartitionManager(client, a.node_name, a.config_file, default_config=a.default, namespace=a.namespace,
                           barrier_dir=mounts.path("/run/amd/validations"),
-                          host_services=load_clients(a.gpu_clients_file), reload_cmd=a.reload_cmd)
+                          host_services=load_clients(a.gpu_clients_file), reload_cmd=a.reload_cmd,
+                          reload_via=a.reload_via, driver_dir=mounts.path("/run/amd/driver"))
     kick = threading.Event()
 
     def on_node(ev):
@@ -326,7 +374,7 @@ def main(argv=None, client=None) -> int:
         old = o.get_labels(ev.old) if ev.old else {}
         if old.get(CONFIG_LABEL) != o.get_labels(ev.obj).get(CONFIG_LABEL):
             kick.set()
-    client.watch("v1", "Node", on_node)
+    client.watch("v1", "Node", on_node, field_selector=f"metadata.name={a.node_name}")
     while True:
         try:
             log.info("reconcile: %s", pm.reconcile())

@@ -204,16 +204,17 @@ class CachedClient:
     def server_version(self) -> str:
         return self.client.server_version()
 
-    def watch(self, api_version: str, kind: str, callback: WatchCallback, namespace: str = "") -> Callable[[], None]:
+    def watch(self, api_version: str, kind: str, callback: WatchCallback, namespace: str = "",
+              field_selector: Optional[str] = None) -> Callable[[], None]:
         """Controllers' event sources share the informer's stream (one WATCH per kind)."""
         inf = self._informer(api_version, kind)
         if inf is None:
-            return self.client.watch(api_version, kind, callback, namespace)
+            return self.client.watch(api_version, kind, callback, namespace, field_selector=field_selector)
 
         def filtered(ev: WatchEvent) -> None:
-            if not namespace or o.namespace(ev.obj) == namespace:
+            if (not namespace or o.namespace(ev.obj) == namespace) and o.field_selector_matches(field_selector, ev.obj):
                 callback(ev)
-        for obj in inf.list(namespace, None, None):
+        for obj in inf.list(namespace, None, field_selector):
             callback(WatchEvent("ADDED", obj))
         inf.handlers.append(filtered)
 

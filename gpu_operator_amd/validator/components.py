@@ -180,10 +180,134 @@ def validate_toolkit(ctx: Context) -> Dict[str, Any]:
 
 
 # ---------------------------------------------------------------------------------------------
-# HIP (matrix-core GEMM + smoke) -- replaces the CUDA vectorAdd validation
+# node shape: GPU model, physical GPUs, GPU pods holding devices
 # ---------------------------------------------------------------------------------------------
+GEMM_FLOOR_FRACTION = 0.40     # of the model's dense peak: healthy MI355X runs 0.59-0.65 on random data
+BUSBW_FLOOR_FRACTION = 0.25    # of one xGMI link: a healthy 8-GPU mesh runs well above one link
+FABRIC_ANNOTATION = "amd.com/gpu.fabric-validation"
+
+
 def _validator_env(ctx: Context) -> Dict[str, str]:
     return {k: v for k, v in ctx.env.items() if k.startswith("VALIDATOR_")}
+
+
+def _gpus(ctx: Context) -> List[Dict[str, Any]]:
+    try:
+        return devices.enumerate_gpus(ctx.sys_root)
+    except Exception as e:  # noqa: BLE001 - no sysfs access / no native library: callers fall back
+        log.info("GPU enumeration failed: %s", e)
+        return []
+
+
+def node_model(ctx: Context, gpus: Optional[List[Dict[str, Any]]] = None):
+    """The catalog entry (models/) of this node's GPUs, or None."""
+    from .. import models
+    for g in (gpus if gpus is not None else _gpus(ctx)):
+        hit = models.by_device_id(g.get("device_id", 0))
+        if hit:
+            return hit[0]
+    return None
+
+
+def physical_gpus(ctx: Context, node: Optional[Dict[str, Any]] = None) -> List[Dict[str, Any]]:
+    """One KFD agent per physical GPU (a CPX GPU shows one agent per partition, all on one PCI
+    function): the lowest-index agent of each BDF. The HIP device index of that agent is its
+    position in KFD order."""
+    first: Dict[str, Dict[str, Any]] = {}
+    for g in sorted(_gpus(ctx), key=lambda g: g["index"]):
+        first.setdefault(g["pci_bdf"], g)
+    return list(first.values())
+
+
+def physical_gpu_count(ctx: Context, node: Optional[Dict[str, Any]] = None) -> int:
+    """Physical GPUs of the node: KFD agents grouped by PCI function; without sysfs, the
+    labeller's ``amd.com/gpu.count`` label (also physical GPUs); never ``allocatable``, which
+    counts time-slicing replicas or partitions."""
+    n = len(physical_gpus(ctx, node))
+    if n == 0 and node is not None:
+        try:
+            n = int(o.get_labels(node).get("amd.com/gpu.count", "0") or 0)
+        except ValueError:
+            n = 0
+    return n
+
+
+def _requests_gpu(pod: Dict[str, Any]) -> bool:
+    for c in ((pod.get("spec") or {}).get("containers") or []) + ((pod.get("spec") or {}).get("initContainers") or []):
+        res = c.get("resources") or {}
+        for k in list((res.get("limits") or {})) + list((res.get("requests") or {})):
+            if k == GPU_RESOURCE or k.startswith(PARTITION_RESOURCE_PREFIX):
+                return True
+    return False
+
+
+def gpu_pods_on_node(ctx: Context) -> List[str]:
+    """Running pods on this node that hold GPU resources (``amd.com/gpu`` or a partition
+    resource), excluding the validator's own validation pods. A throughput number taken beside
+    them measures the sharing, not the hardware."""
+    if ctx.client is None or not ctx.node_name:
+        return []
+    try:
+        pods = ctx.client.list("v1", "Pod", field_selector=f"spec.nodeName={ctx.node_name}")
+    except Exception as e:  # noqa: BLE001 - treat as unknown: do not block validation on it
+        log.info("listing pods on %s failed: %s", ctx.node_name, e)
+        return []
+    own = {"amd-hip-validator", "amd-rccl-validator", "amd-device-plugin-validator"}
+    out = []
+    for p in pods:
+        if (p.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+            continue
+        if o.get_labels(p).get("app") in own or not _requests_gpu(p):
+            continue
+        out.append(f"{o.namespace(p)}/{o.name(p)}")
+    return sorted(out)
+
+
+def _env_float(ctx: Context, key: str) -> Optional[float]:
+    v = ctx.env.get(key, "")
+    if v == "":
+        return None
+    try:
+        return float(v)
+    except ValueError:
+        raise ValidationError(f"{key}={v!r} is not a number")
+
+
+def gemm_floors(ctx: Context, gpus: Optional[List[Dict[str, Any]]] = None) -> Dict[str, float]:
+    """Per-GPU TFLOP/s floors of the GEMM probe, by dtype. ``GEMM_MIN_TFLOPS_BF16`` /
+    ``GEMM_MIN_TFLOPS_FP8`` (spec.validator.hip.env) win when set (0 = no floor); otherwise
+    ``GEMM_FLOOR_FRACTION`` (default 0.40) of the node model's dense peak, scaled to the CUs of
+    one HIP device (a CPX partition has 1/8 of the GPU). Unknown model: no floor."""
+    gpus = gpus if gpus is not None else _gpus(ctx)
+    model = node_model(ctx, gpus)
+    frac = _env_float(ctx, "GEMM_FLOOR_FRACTION")
+    frac = GEMM_FLOOR_FRACTION if frac is None else frac
+    share = 1.0
+    if model is not None and model.cus and gpus:
+        share = min(1.0, min(g["cu_count"] for g in gpus) / model.cus)
+    out = {}
+    for dtype, key, peak in (("bf16", "GEMM_MIN_TFLOPS_BF16", model.bf16_dense_tflops if model else 0.0),
+                             ("fp8", "GEMM_MIN_TFLOPS_FP8", model.fp8_dense_tflops if model else 0.0)):
+        v = _env_float(ctx, key)
+        out[dtype] = round(v if v is not None else peak * frac * share, 1)
+    return out
+
+
+def busbw_floor(ctx: Context) -> float:
+    """All-reduce bus-bandwidth floor (GB/s) for the largest rank count: ``RCCL_MIN_BUSBW_GBPS``
+    when set, else ``BUSBW_FLOOR_FRACTION`` of the model's per-link xGMI bandwidth."""
+    v = _env_float(ctx, "RCCL_MIN_BUSBW_GBPS")
+    if v is not None:
+        return v
+    model = node_model(ctx)
+    return round(model.xgmi_link_gbps * BUSBW_FLOOR_FRACTION, 1) if model else 0.0
+
+
+# ---------------------------------------------------------------------------------------------
+# HIP (matrix-core GEMM + smoke) -- replaces the CUDA vectorAdd validation
+# ---------------------------------------------------------------------------------------------
+def _dtype_key(name: str) -> str:
+    return "fp8" if name.startswith("fp8") else "bf16"
 
 
 def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
@@ -192,22 +316,76 @@ def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
     smoke = [r for r in results if r.get("event") == "hip-smoke"]
     out: Dict[str, Any] = {"gemm": per, "aggregate": agg}
     if agg:
-        head = max(agg, key=lambda r: r["m"] * r["n"] * r["k"])
+        # headline: bf16 before fp8, the largest shape, then the most GPUs
+        head = max(agg, key=lambda r: (_dtype_key(r.get("dtype", "bf16")) == "bf16", r["m"] * r["n"] * r["k"],
+                                       r.get("gpus", 1)))
         out["gemm_tflops_total"] = head["total_tflops"]
         out["gemm_tflops_per_gpu"] = head["per_gpu_tflops"]
-        out["gpus"] = head["gpus"]
+        out["gpus"] = head.get("gpus")
+        by: Dict[str, Dict[str, Any]] = {}
+        for r in agg:
+            big = max(x["m"] * x["n"] * x["k"] for x in agg if x.get("dtype") == r.get("dtype"))
+            if r["m"] * r["n"] * r["k"] != big:
+                continue
+            by.setdefault(_dtype_key(r.get("dtype", "bf16")), {})[str(r.get("gpus", 1))] = {
+                "total_tflops": r["total_tflops"], "per_gpu_tflops": r["per_gpu_tflops"],
+                **({"efficiency": r["efficiency"]} if "efficiency" in r else {})}
+        out["tflops_by_dtype_gpus"] = by
+    sc = [r for r in results if r.get("event") == "scaling"]
+    if sc:
+        out["scaling_skipped"] = sorted({r["gpus"] for r in sc if r.get("skipped")})
     if smoke:
         out["smoke_ok"] = all(s.get("ok") for s in smoke)
     out["counters"] = [r for r in results if r.get("event") == "counters"]
     return out
 
 
-def _run_local_hip(ctx: Context) -> List[Dict[str, Any]]:
+def gate_gemm(info: Dict[str, Any], floors: Dict[str, float], busy: List[str]) -> List[str]:
+    """Why a GEMM result must not open hip-ready: failed checks, and (on a node no GPU pod is
+    sharing) any GPU below its dtype's floor. Also checked in the pod (``--min-tflops``); done
+    here again so an older workload image cannot pass a slow GPU."""
+    bad = [f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('error', 'check failed')}"
+           for r in info["gemm"] if not r.get("ok")]
+    bad += [f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: not ok" for r in info["aggregate"]
+            if r.get("ok") is False and not bad]
+    if info.get("smoke_ok") is False:
+        bad.append("hip-smoke failed")
+    if not busy:
+        for r in info["gemm"]:
+            floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0)
+            if r.get("ok") and floor and r.get("tflops", 0.0) < floor:
+                bad.append(f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('tflops')} TFLOP/s "
+                           f"below the {floor} floor")
+        for r in info["aggregate"]:          # the slowest GPU of each set (per-GPU lines may be cut)
+            floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0)
+            slow = r.get("min_gpu_tflops", r.get("per_gpu_tflops", 0.0))
+            if floor and slow < floor and not bad:
+                bad.append(f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: slowest GPU {slow} TFLOP/s "
+                           f"below the {floor} floor")
+    return bad
+
+
+def _hip_env(ctx: Context, floors: Dict[str, float], busy: List[str]) -> Dict[str, str]:
+    env = _validator_env(ctx)
+    for k, v in ctx.env.items():
+        if k.startswith(("GEMM_", "HIP_", "HSA_")) and k != "HIP_VALIDATION_MODE":
+            env[k] = v
+    env.setdefault("GEMM_SCALING", "1,2,4,8")
+    # beside running GPU pods the numbers measure the sharing: check correctness, gate nothing
+    env["GEMM_MIN_TFLOPS_BF16"] = "0" if busy else f"{floors['bf16']:g}"
+    env["GEMM_MIN_TFLOPS_FP8"] = "0" if busy else f"{floors['fp8']:g}"
+    return env
+
+
+def _run_local_hip(ctx: Context, floors: Optional[Dict[str, float]] = None) -> List[Dict[str, Any]]:
     """The HIP workload in this process's container (HIP_VALIDATION_MODE=local)."""
     from .workload_main import run_hip
+    floors = floors or {}
     t0 = ctx.clock()
     results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run,
-                      dtype=ctx.env.get("GEMM_DTYPE", "bf16"))
+                      dtype=ctx.env.get("GEMM_DTYPE", "bf16"), scaling=ctx.env.get("GEMM_SCALING") or None,
+                      iters=int(ctx.env.get("GEMM_ITERS", "50")),
+                      min_tflops=floors.get("bf16", 0.0), min_tflops_fp8=floors.get("fp8", 0.0))
     if ctx.poll_mode:
         # the reference spawns the workload pod and polls its phase every sleep_interval, first
         # right after creating it (validator/main.go:1042-1059): it sees the result at the
@@ -227,21 +405,29 @@ def _local_workload(ctx: Context, mode: str) -> Dict[str, Any]:
 
 
 def validate_hip(ctx: Context) -> Dict[str, Any]:
+    """hip-smoke + the MFMA GEMM probe (bf16 and fp8, 1/2/4/8-GPU sweep), gated on correctness
+    and on per-GPU throughput floors (models/ defaults, spec.validator.hip.env overrides). The
+    reference gates on vectorAdd's exit code alone (validator/main.go:1176-1211)."""
     mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
     if mode == "skip":                  # no GPU work (CPU rehearsals of the node bring-up)
         info = {"skipped": True}
         ctx.status.create(S.HIP_READY, info)
         return info
+    floors = gemm_floors(ctx)
+    busy = gpu_pods_on_node(ctx)
     if mode == "local":
-        results = _run_local_hip(ctx)
+        results = _run_local_hip(ctx, {} if busy else floors)
     else:
         res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                                 _validator_env(ctx), timeout=ctx.pod_timeout)
+                                 _hip_env(ctx, floors, busy), timeout=ctx.pod_timeout)
         results = res["results"]
     info = summarize_gemm(results)
-    bad = [r for r in info["gemm"] if not r.get("ok")]
-    if bad or info.get("smoke_ok") is False:
-        raise ValidationError(f"HIP validation failed: {bad or 'hip-smoke'}")
+    info["floors_tflops"] = floors
+    if busy:
+        info["floor_skipped"] = f"{len(busy)} GPU pod(s) running on the node: {busy[:8]}"
+    bad = gate_gemm(info, floors, busy)
+    if bad:
+        raise ValidationError(f"HIP validation failed: {bad[:8]}")
     ctx.status.create(S.HIP_READY, info)
     return info
 
@@ -284,7 +470,7 @@ def wait_gpu_resources(ctx: Context) -> Dict[str, int]:
         if r:
             found.update(r)
             done.set()
-    stop = ctx.client.watch("v1", "Node", on_event)
+    stop = ctx.client.watch("v1", "Node", on_event, field_selector=f"metadata.name={ctx.node_name}")
     try:
         deadline = ctx.clock() + ctx.resource_timeout
         while not done.is_set():
@@ -335,40 +521,150 @@ def summarize_rccl(results: List[Dict[str, Any]]) -> Dict[str, Any]:
             and fabric.get("ok", True) is not False}
 
 
-def _run_rccl_local(ctx: Context, ngpu: int) -> List[Dict[str, Any]]:
+def _run_rccl_local(ctx: Context, ngpu: int, floor: float) -> List[Dict[str, Any]]:
     from .workload_main import run_rccl
     ranks = ctx.env.get("RCCL_RANKS") or ",".join(str(n) for n in (2, 4, 8) if n <= ngpu) or str(ngpu)
-    mb = float(ctx.env.get("RCCL_MIN_BUSBW_GBPS", "0") or 0)
     return run_rccl(int(ctx.env.get("RCCL_MAX_BYTES", 1 << 26)), ctx.env.get("RCCL_DTYPE", "bf16"), ranks=ranks,
-                    min_busbw=mb or None)
+                    min_busbw=floor or None)
+
+
+def run_topology_check(ctx: Context) -> Dict[str, Any]:
+    """xGMI topology + hive check with no GPU work (``amd-rccl-validate --topology-only``), in
+    this container: KFD io_links from sysfs, every GPU in one hive, 7 links per GPU on a full
+    MI355X node."""
+    from .workload_main import binary, _json_lines
+    try:
+        p = ctx.run([binary("amd-rccl-validate"), "--topology-only", "--sys-root", ctx.sys_root],
+                    capture_output=True, text=True, timeout=60)
+    except (OSError, FileNotFoundError, subprocess.TimeoutExpired) as e:
+        raise ValidationError(f"topology check could not run: {e}")
+    lines = _json_lines(p.stdout)
+    fabric = next((x for x in lines if x.get("event") == "fabric"), None)
+    if fabric is None:
+        raise ValidationError(f"topology check printed no fabric line (exit {p.returncode})")
+    return fabric
+
+
+def _last_full_fabric(node: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    raw = ((node.get("metadata") or {}).get("annotations") or {}).get(FABRIC_ANNOTATION)
+    try:
+        return json.loads(raw) if raw else None
+    except ValueError:
+        return None
+
+
+def _record_full_fabric(ctx: Context, info: Dict[str, Any]) -> None:
+    """Keep the last full collective result on the Node (survives validator restarts), so a
+    topology-only pass on a busy node can report when the fabric was last measured."""
+    rec = {"ts": round(time.time(), 3), "ranks": info.get("ranks"), "peak_busbw_gbps": info.get("peak_busbw_gbps"),
+           "busbw_by_ranks": {str(k): v for k, v in (info.get("busbw_by_ranks") or {}).items()},
+           "ok": bool(info.get("ok"))}
+    try:
+        ctx.client.patch("v1", "Node", ctx.node_name,
+                         {"metadata": {"annotations": {FABRIC_ANNOTATION: json.dumps(rec, separators=(",", ":"))}}})
+    except Exception as e:  # noqa: BLE001 - bookkeeping only; the barrier carries the result too
+        log.info("recording the fabric result on node %s failed: %s", ctx.node_name, e)
+
+
+def plan_rccl_pod(ctx: Context, node: Dict[str, Any], phys: List[Dict[str, Any]]) -> Dict[str, Any]:
+    """How the fabric pod gets every physical GPU of the node.
+
+    * whole GPUs advertised one-to-one (no time-slicing, no partitions): request them through
+      the scheduler, ``amd.com/gpu: N`` -- the pod cannot start beside a GPU pod;
+    * anything else (time-slicing replicas, CPX partitions, the mixed strategy): the advertised
+      resource does not map to physical GPUs (8 replicas may all be GPU 0), so the pod requests
+      none, runs privileged with every device visible (the hip pod's shape) and pins RCCL to the
+      first agent of each physical GPU with HIP_VISIBLE_DEVICES. The caller runs it only when no
+      GPU pod holds a device."""
+    n = len(phys)
+    alloc = ((node.get("status") or {}).get("allocatable") or {})
+    try:
+        whole = int(alloc.get(GPU_RESOURCE, 0) or 0)
+    except (TypeError, ValueError):
+        whole = 0
+    partitions = any(k.startswith(PARTITION_RESOURCE_PREFIX) for k in alloc)
+    agents_per_gpu = 1
+    gpus = _gpus(ctx)
+    if gpus and n:
+        agents_per_gpu = max(1, len(gpus) // n)
+    if whole == n and not partitions and agents_per_gpu == 1:
+        return {"shape": "scheduled", "gpu_limit": {GPU_RESOURCE: n}, "env": {}, "privileged": False}
+    visible = ",".join(str(g["index"]) for g in phys) if phys else ""
+    env = {"AMD_VISIBLE_DEVICES": "all"}
+    if visible and agents_per_gpu > 1:
+        env["HIP_VISIBLE_DEVICES"] = visible
+    return {"shape": "privileged-all", "gpu_limit": None, "env": env, "privileged": True,
+            "reason": f"allocatable {GPU_RESOURCE}={whole} over {n} physical GPU(s)"
+                      + (f", {agents_per_gpu} agents per GPU" if agents_per_gpu > 1 else "")
+                      + (", partition resources" if partitions else "")}
 
 
 def validate_rccl(ctx: Context) -> Dict[str, Any]:
+    """The xGMI fabric proof over every PHYSICAL GPU of the node (KFD agents by PCI function;
+    allocatable counts replicas or partitions). On a node where GPU pods already hold devices the
+    collective cannot run (it would fight them, or never schedule): the topology/hive check runs
+    instead and the last full result (Node annotation) is reported with its timestamp."""
     node = ctx.client.get("v1", "Node", ctx.node_name)
-    ngpu = int(((node.get("status") or {}).get("allocatable") or {}).get(GPU_RESOURCE, 0) or 0)
+    phys = physical_gpus(ctx, node)
+    ngpu = len(phys) or physical_gpu_count(ctx, node)
     if ngpu < 2:
-        info = {"skipped": f"{ngpu} GPU(s) allocatable: no fabric to validate", "ok": True}
+        info = {"skipped": f"{ngpu} physical GPU(s): no fabric to validate", "ok": True}
         ctx.status.create(S.RCCL_READY, info)
         return info
-    if ctx.env.get("HIP_VALIDATION_MODE", "pod") in ("local", "skip"):
-        info = {"skipped": f"{ngpu} GPU(s); local mode"} if ctx.env.get("HIP_VALIDATION_MODE") == "skip" else \
-            summarize_rccl(_run_rccl_local(ctx, ngpu))
+    floor = busbw_floor(ctx)
+    mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
+    if mode == "local":
+        info = summarize_rccl(_run_rccl_local(ctx, ngpu, floor))
+        info["min_busbw_gbps"] = floor
         if not info.get("skipped") and not info["ok"]:
             raise ValidationError(f"RCCL all-reduce validation failed: {info}")
         ctx.status.create(S.RCCL_READY, info)
         return info
+    busy = gpu_pods_on_node(ctx)
+    # RCCL_VALIDATION_MODE=dry-run (CPU rehearsals with a kubelet): the pod is planned, scheduled
+    # and run, the collective is not; HIP_VALIDATION_MODE=skip without it: nothing is spawned
+    dry = ctx.env.get("RCCL_VALIDATION_MODE", "") == "dry-run"
+    if mode == "skip" and not dry:
+        info = {"skipped": "HIP_VALIDATION_MODE=skip", "ok": True, "physical_gpus": ngpu,
+                "planned": "topology-only" if busy else plan_rccl_pod(ctx, node, phys)["shape"]}
+        ctx.status.create(S.RCCL_READY, info)
+        return info
+    if busy:
+        fabric = run_topology_check(ctx)
+        if fabric.get("ok") is False:
+            raise ValidationError(f"xGMI topology check failed: {fabric.get('reason', fabric)}")
+        info = {"mode": "topology-only", "physical_gpus": ngpu, "fabric": fabric, "ok": True,
+                "busy_pods": busy[:16], "last_full": _last_full_fabric(node),
+                "reason": f"{len(busy)} GPU pod(s) hold devices: the collective runs when the node is free"}
+        ctx.status.create(S.RCCL_READY, info)
+        return info
+    plan = plan_rccl_pod(ctx, node, phys)
     env = _validator_env(ctx)
     env.update({k: v for k, v in ctx.env.items() if k.startswith(("RCCL_", "NCCL_"))})
-    # the rank sweep stops at the node's GPU count; the busBW floor comes from
-    # spec.validator.rccl.env (RCCL_MIN_BUSBW_GBPS), so a slow fabric fails validation
+    env.update(plan["env"])
+    # the rank sweep stops at the node's physical GPU count; the busBW floor (models/ default or
+    # spec.validator.rccl.env RCCL_MIN_BUSBW_GBPS) gates the largest rank count
     env.setdefault("RCCL_RANKS", ",".join(str(n) for n in (2, 4, 8) if n <= ngpu) or str(ngpu))
     if ngpu not in [int(x) for x in env["RCCL_RANKS"].split(",") if x]:
         env["RCCL_RANKS"] += f",{ngpu}"
+    env["RCCL_MIN_BUSBW_GBPS"] = f"{floor:g}"
+    if dry:
+        env["RCCL_DRY_RUN"] = "1"
     out = W.run_workload_pod(ctx.client, "rccl-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                             env, timeout=ctx.pod_timeout, gpu_limit={GPU_RESOURCE: ngpu})
+                             env, timeout=ctx.pod_timeout, gpu_limit=plan["gpu_limit"],
+                             privileged=plan["privileged"])
     info = summarize_rccl(out["results"])
+    info.update(mode="full", physical_gpus=ngpu, pod_shape=plan["shape"], min_busbw_gbps=floor)
+    if plan.get("reason"):
+        info["pod_shape_reason"] = plan["reason"]
+    peak = info.get("peak_busbw_gbps")
+    if info["ok"] and not info["skipped"] and floor and peak is not None and peak < floor:
+        info["ok"] = False
+        info["error"] = f"peak busBW {peak} GB/s below the {floor} GB/s floor"
     if not info["ok"]:
         raise ValidationError(f"RCCL all-reduce validation failed: {info}")
+    if not info["skipped"]:
+        _record_full_fabric(ctx, info)
     ctx.status.create(S.RCCL_READY, info)
     return info
 

@@ -55,8 +55,12 @@ class NodeMetrics:
                                           "last time GPU resources were found", node, registry=r)
         self.pci_total = Gauge(p + "amd_pci_devices_total", "AMD GPU PCI functions (-1 if unknown)", node,
                                registry=r)
-        self.gemm_tflops = Gauge(p + "validator_gemm_tflops", "validator MFMA GEMM throughput",
-                                 node + ["scope"], registry=r)
+        self.gemm_tflops = Gauge(p + "validator_gemm_tflops",
+                                 "validator MFMA GEMM throughput on `gpus` GPUs at once (scope node = aggregate, "
+                                 "per_gpu = mean per GPU)", node + ["scope", "dtype", "gpus"], registry=r)
+        self.gemm_eff = Gauge(p + "validator_gemm_scaling_efficiency",
+                              "aggregate GEMM TFLOP/s on `gpus` GPUs / (gpus x the 1-GPU figure)",
+                              node + ["dtype", "gpus"], registry=r)
         self.busbw = Gauge(p + "validator_allreduce_busbw_gbps", "validator RCCL all-reduce peak bus bandwidth",
                            node + ["ranks"], registry=r)
         self._stop = threading.Event()
@@ -76,9 +80,18 @@ class NodeMetrics:
         if ttr is not None:
             self.ttr.labels(n).set(ttr)
         hip = sd.read(S.HIP_READY) or {}
-        if "gemm_tflops_total" in hip:
-            self.gemm_tflops.labels(n, "node").set(hip["gemm_tflops_total"])
-            self.gemm_tflops.labels(n, "per_gpu").set(hip.get("gemm_tflops_per_gpu", 0))
+        by = hip.get("tflops_by_dtype_gpus") or {}
+        if by:                                        # the 1/2/4/8-GPU sweep, per dtype
+            for dtype, per in by.items():
+                for gpus, v in per.items():
+                    self.gemm_tflops.labels(n, "node", dtype, str(gpus)).set(v["total_tflops"])
+                    self.gemm_tflops.labels(n, "per_gpu", dtype, str(gpus)).set(v["per_gpu_tflops"])
+                    if "efficiency" in v:
+                        self.gemm_eff.labels(n, dtype, str(gpus)).set(v["efficiency"])
+        elif "gemm_tflops_total" in hip:
+            g = str(hip.get("gpus") or "")
+            self.gemm_tflops.labels(n, "node", "bf16", g).set(hip["gemm_tflops_total"])
+            self.gemm_tflops.labels(n, "per_gpu", "bf16", g).set(hip.get("gemm_tflops_per_gpu", 0))
         rc = sd.read(S.RCCL_READY) or {}
         if rc.get("peak_busbw_gbps") is not None:
             self.busbw.labels(n, str(rc.get("ranks"))).set(rc["peak_busbw_gbps"])

@@ -158,12 +158,17 @@ def parse_results(msg: str) -> List[Dict[str, Any]]:
 
 
 def run_workload_pod(client, manifest: str, namespace: str, node: str, env: Dict[str, str],
-                     timeout: float = 300.0, gpu_limit: Optional[Dict[str, int]] = None) -> Dict[str, Any]:
+                     timeout: float = 300.0, gpu_limit: Optional[Dict[str, int]] = None,
+                     privileged: bool = False) -> Dict[str, Any]:
+    """``gpu_limit``: GPU resources the workload container requests through the scheduler;
+    ``privileged``: the container sees every device instead (AMD_VISIBLE_DEVICES=all in ``env``)."""
     template = load_pod_spec(manifest)
     pod = prepare_pod(client, template, namespace, node, env)
-    if gpu_limit:
-        for c in pod["spec"].get("initContainers", []):
+    for c in pod["spec"].get("initContainers", []):
+        if gpu_limit:
             c.setdefault("resources", {})["limits"] = dict(gpu_limit)
+        if privileged:
+            c.setdefault("securityContext", {})["privileged"] = True
     app = o.get_labels(pod).get("app", "")
     delete_stale(client, namespace, app, node)
     client.create(pod)

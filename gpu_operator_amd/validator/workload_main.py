@@ -1,12 +1,14 @@
 """``amd-validator-workload``: what runs inside the spawned validation pods.
 
     amd-validator-workload hip  [--gemm-shapes 8192,...] [--gemm-dtype bf16|fp8|both] [--counters]
+                                [--scaling 1,2,4,8] [--min-tflops X] [--min-tflops-fp8 Y]
     amd-validator-workload rccl [--ranks 2,4,8] [--processes N] [--max-bytes N] [--dtype float|bf16]
                                 [--min-busbw GBPS]
 
 Runs the native workload binaries (``amd-hip-smoke``, ``amd-gemm-validate``,
 ``amd-rccl-validate``), optionally collects rocprofv3 counters for one GEMM dispatch
-(MFMA ops, busy cycles, LDS bank conflicts, L2 hit/miss) and prints JSON result lines. The
+per GEMM dtype (MFMA ops against 2·M·N·K/512, busy cycles, LDS bank conflicts, L2 hit/miss) and
+prints JSON result lines. The
 same lines go to ``/dev/termination-log`` so the validator reads them back from the pod
 status. Exit status is non-zero if any check failed.
 """
@@ -26,8 +28,21 @@ import tempfile
 from typing import Callable, Dict, List, Optional
 
 BIN_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native", "bin")
-PMC_COUNTERS = ["SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
-                "TCC_HIT_sum", "TCC_MISS_sum"]
+# One rocprofv3 pass per GEMM dtype (8 SQ + 4 TCC slots per pass on gfx950): the MFMA op counter(s)
+# of that dtype, busy cycles, LDS bank conflicts / activity and L2 hits / misses. The f8f6f4
+# instruction the fp8 kernel issues is counted under F8 or F6F4 depending on the firmware, so the
+# fp8 pass collects both and sums them.
+PMC_PASSES = {
+    "bf16": {"kernel": "gemm_bf16_256x256", "mops": ["SQ_INSTS_VALU_MFMA_MOPS_BF16"]},
+    "fp8": {"kernel": "gemm_fp8_256x256", "mops": ["SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_INSTS_VALU_MFMA_MOPS_F6F4"]},
+}
+PMC_COMMON = ["SQ_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "TCC_HIT_sum", "TCC_MISS_sum"]
+PMC_COUNTERS = PMC_PASSES["bf16"]["mops"] + PMC_COMMON      # the bf16 pass (kept for callers)
+
+
+def rocprofv3_path() -> Optional[str]:
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    return prof if os.path.exists(prof) else None
 
 
 def binary(name: str) -> str:
@@ -59,47 +74,76 @@ def run_json(cmd: List[str], run: Callable = subprocess.run, timeout: float = 60
     return p.returncode, _json_lines(p.stdout)
 
 
-def collect_counters(shape: str, run: Callable = subprocess.run) -> List[Dict]:
-    """One profiled GEMM dispatch under rocprofv3 (counters only: no sys/runtime traces)."""
-    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
-    if not os.path.exists(prof):
-        return [{"event": "counters", "skipped": "rocprofv3 not available"}]
+def _shape_mnk(shape: str):
+    parts = [int(x) for x in shape.lower().split("x")]
+    return (parts[0],) * 3 if len(parts) == 1 else tuple(parts[:3])
+
+
+def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "bf16") -> List[Dict]:
+    """One profiled GEMM dispatch of ``dtype`` under rocprofv3 (counters only: no sys/runtime
+    traces, which this pool refuses beside --pmc). Adds the expected MFMA op count
+    (2·M·N·K / 512) and whether the measured one matches it."""
+    spec = PMC_PASSES[dtype]
+    prof = rocprofv3_path()
+    if prof is None:
+        return [{"event": "counters", "dtype": dtype, "skipped": "rocprofv3 not available"}]
     out = tempfile.mkdtemp(prefix="amdgo-pmc-")
     try:
-        cmd = [prof, "--pmc", *PMC_COUNTERS, "--output-format", "csv", "-d", out, "--",
+        cmd = [prof, "--pmc", *spec["mops"], *PMC_COMMON, "--output-format", "csv", "-d", out, "--",
                binary("amd-gemm-validate"), "--shapes", shape, "--iters", "1", "--warmup", "0",
-               "--devices", "0", "--check-rows", "1"]
+               "--no-stabilise", "--devices", "0", "--check-rows", "1", "--dtype", dtype]
         p = run(cmd, capture_output=True, text=True, timeout=300)
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if p.returncode != 0 or not files:
-            return [{"event": "counters", "skipped": f"rocprofv3 exit {p.returncode}"}]
+            return [{"event": "counters", "dtype": dtype, "ok": False,
+                     "error": f"rocprofv3 exit {p.returncode}: {(p.stderr or '')[-300:]}"}]
         agg: Dict[str, float] = {}
         with open(files[0]) as f:
             for row in csv.DictReader(f):
-                if "gemm_bf16_256x256" not in row.get("Kernel_Name", ""):
+                if spec["kernel"] not in row.get("Kernel_Name", ""):
                     continue
                 agg[row["Counter_Name"]] = agg.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
-        return [{"event": "counters", "kernel": "gemm_bf16_256x256", "shape": shape, **agg}]
+        if not agg:
+            return [{"event": "counters", "dtype": dtype, "ok": False,
+                     "error": f"no {spec['kernel']} dispatch in the counter records"}]
+        m, n, k = _shape_mnk(shape)
+        mops = sum(agg.get(c, 0.0) for c in spec["mops"])
+        want = 2.0 * m * n * k / 512
+        res = {"event": "counters", "dtype": dtype, "kernel": spec["kernel"], "shape": shape, **agg,
+               "mfma_mops": mops, "mfma_mops_expected": want, "mfma_mops_match": abs(mops - want) <= 1e-6 * want,
+               "lds_conflict_free": agg.get("SQ_LDS_BANK_CONFLICT", 1.0) == 0.0}
+        res["ok"] = res["mfma_mops_match"]
+        return [res]
     finally:
         shutil.rmtree(out, ignore_errors=True)
 
 
-def run_hip(shapes: List[str], counters: bool = False, iters: int = 20,
-            run: Callable = subprocess.run, dtype: str = "bf16") -> List[Dict]:
+def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
+            run: Callable = subprocess.run, dtype: str = "bf16", scaling: Optional[str] = None,
+            min_tflops: float = 0.0, min_tflops_fp8: float = 0.0) -> List[Dict]:
     """hip-smoke, then the MFMA GEMM probe in ``dtype`` (bf16, fp8 e4m3fn on the double-rate
-    16x16x128 matrix-core path, or both), then optionally one counter-collection pass."""
+    16x16x128 matrix-core path, or both) -- clock-stabilised like bench.py, optionally swept over
+    ``scaling`` GPU counts ("1,2,4,8") and gated on per-GPU floors -- then optionally one
+    counter-collection pass per dtype."""
     results: List[Dict] = []
     rc, r = run_json([binary("amd-hip-smoke")], run)
     results += r or [{"event": "hip-smoke", "ok": False, "rc": rc}]
     cmd = [binary("amd-gemm-validate"), "--shapes", ",".join(shapes), "--iters", str(iters)]
     if dtype != "bf16":
         cmd += ["--dtype", dtype]
-    rc, r = run_json(cmd, run)
+    if scaling:
+        cmd += ["--scaling", scaling]
+    if min_tflops:
+        cmd += ["--min-tflops", f"{min_tflops:g}"]
+    if min_tflops_fp8:
+        cmd += ["--min-tflops-fp8", f"{min_tflops_fp8:g}"]
+    rc, r = run_json(cmd, run, timeout=1200)
     results += r
     if rc != 0 and not any(x.get("event") == "gemm" for x in r):
         results.append({"event": "gemm", "ok": False, "rc": rc})
     if counters:
-        results += collect_counters(shapes[0], run)
+        for d in (["bf16", "fp8"] if dtype == "both" else [dtype]):
+            results += collect_counters(shapes[0], run, dtype=d)
     return results
 
 
@@ -146,6 +190,8 @@ def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run, ranks: 
     """The xGMI fabric proof: topology + fabric check, then a rank-count sweep in one process
     (``ranks`` "2,4,8") or, with ``processes`` N, one process per GPU joined through
     ncclCommInitRank. RCCL's INFO log is captured and summarised (algorithm/protocol per size)."""
+    if os.environ.get("RCCL_DRY_RUN") == "1":
+        return _rccl_dry_run(ranks)
     base = ["--max-bytes", str(max_bytes), "--dtype", dtype, "--min-bytes", str(min_bytes)]
     if min_busbw:
         base += ["--min-busbw", str(min_busbw)]
@@ -169,6 +215,22 @@ def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run, ranks: 
         return results
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _rccl_dry_run(ranks: Optional[str]) -> List[Dict]:
+    """RCCL_DRY_RUN=1 (CPU rehearsals of node bring-up, HIP_VALIDATION_MODE=skip): the pod is
+    planned, scheduled and run, the topology/hive check reads the (fake) sysfs, and no collective
+    runs. What the pod was given (visible devices, rank list) is reported for the test to check."""
+    cmd = [binary("amd-rccl-validate"), "--topology-only", "--sys-root", os.environ.get("AMD_SYSFS_ROOT", "/")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=60)
+    results = [x for x in _json_lines(p.stdout) if x.get("event") in ("fabric", "topology")]
+    fabric = next((x for x in results if x.get("event") == "fabric"), {"ok": False, "reason": "no fabric line"})
+    rl = [int(x) for x in (ranks or "").split(",") if x.strip()]
+    results.append({"event": "summary", "ok": bool(fabric.get("ok")), "skipped": "dry-run",
+                    "ranks": max(rl) if rl else None, "ranks_planned": rl,
+                    "amd_visible_devices": os.environ.get("AMD_VISIBLE_DEVICES"),
+                    "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES")})
+    return results
 
 
 def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict]:
@@ -202,6 +264,32 @@ def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict
     return results
 
 
+TERMINATION_LOG_BYTES = 4000       # kubelet keeps at most 4 KiB of a termination message
+_SUMMARY_EVENTS = ("aggregate", "summary", "hip-smoke", "counters", "scaling", "fabric", "ranks_summary",
+                   "rccl-debug")
+
+
+def termination_message(results: List[Dict], limit: int = TERMINATION_LOG_BYTES) -> str:
+    """The lines the validator reads back from the pod status, whole lines only, most important
+    first: summaries (aggregates carry the slowest GPU), then failing per-GPU lines, then passing
+    ones -- so a truncated message never hides a failure."""
+    def line(r):
+        if r.get("event") == "rccl-debug":
+            r = {k: v for k, v in r.items() if k != "lines"}
+        return json.dumps(r, separators=(",", ":"))
+    ordered = [r for r in results if r.get("event") in _SUMMARY_EVENTS]
+    ordered += [r for r in results if r.get("event") not in _SUMMARY_EVENTS and r.get("ok") is False]
+    ordered += [r for r in results if r.get("event") not in _SUMMARY_EVENTS and r.get("ok") is not False]
+    out, size = [], 0
+    for r in ordered:
+        ln = line(r)
+        if size + len(ln) + 1 > limit:
+            continue
+        out.append(ln)
+        size += len(ln) + 1
+    return "\n".join(out)
+
+
 def emit(results: List[Dict], termination_log: Optional[str] = None) -> None:
     if termination_log is None:
         from ..utils import mounts
@@ -210,13 +298,8 @@ def emit(results: List[Dict], termination_log: Optional[str] = None) -> None:
     print(text, flush=True)
     if termination_log and os.path.isdir(os.path.dirname(termination_log)):
         try:
-            # kubelet keeps at most 4 KiB: put the summary lines last-in-first-kept
-            keep = [json.dumps(r, separators=(",", ":")) for r in results
-                    if r.get("event") in ("aggregate", "summary", "hip-smoke", "counters")]
-            keep += [json.dumps(r, separators=(",", ":")) for r in results if r.get("event") == "gemm"]
-            msg = "\n".join(keep)
             with open(termination_log, "w") as f:
-                f.write(msg[:4000])
+                f.write(termination_message(results))
         except OSError:
             pass
 
@@ -226,9 +309,14 @@ def main(argv=None) -> int:
     sub = ap.add_subparsers(dest="what", required=True)
     h = sub.add_parser("hip")
     h.add_argument("--gemm-shapes", default=os.environ.get("GEMM_SHAPES", "8192"))
-    h.add_argument("--iters", type=int, default=20)
+    h.add_argument("--iters", type=int, default=int(os.environ.get("GEMM_ITERS", "50")))
     h.add_argument("--counters", action="store_true")
     h.add_argument("--gemm-dtype", choices=["bf16", "fp8", "both"], default=os.environ.get("GEMM_DTYPE", "bf16"))
+    h.add_argument("--scaling", default=os.environ.get("GEMM_SCALING", ""),
+                   help="GPU counts for the scaling sweep, e.g. 1,2,4,8 (counts above the visible GPUs are skipped)")
+    h.add_argument("--min-tflops", type=float, default=float(os.environ.get("GEMM_MIN_TFLOPS_BF16", "0") or 0),
+                   help="per-GPU bf16 floor (the validator passes its model default or spec.validator.hip.env)")
+    h.add_argument("--min-tflops-fp8", type=float, default=float(os.environ.get("GEMM_MIN_TFLOPS_FP8", "0") or 0))
     r = sub.add_parser("rccl")
     r.add_argument("--max-bytes", type=int, default=int(os.environ.get("RCCL_MAX_BYTES", 1 << 30)))
     r.add_argument("--dtype", default=os.environ.get("RCCL_DTYPE", "float"))
@@ -237,7 +325,8 @@ def main(argv=None) -> int:
     r.add_argument("--min-busbw", type=float, default=float(os.environ.get("RCCL_MIN_BUSBW_GBPS", "0") or 0))
     a = ap.parse_args(argv)
     if a.what == "hip":
-        results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters, dtype=a.gemm_dtype)
+        results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters, dtype=a.gemm_dtype,
+                          scaling=a.scaling or None, min_tflops=a.min_tflops, min_tflops_fp8=a.min_tflops_fp8)
         ok = all(x.get("ok", True) for x in results if x.get("event") in ("gemm", "hip-smoke"))
     else:
         results = run_rccl(a.max_bytes, a.dtype, ranks=a.ranks, min_busbw=a.min_busbw, processes=a.processes)

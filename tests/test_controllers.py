@@ -257,12 +257,13 @@ def test_partition_manager_config_and_node_default_label():
     ds = daemonset(c, C.DS_PARTITION_MANAGER)
     e = env(container(ds, "amd-partition-manager"))
     assert e["DEFAULT_PARTITION_CONFIG"] == "spx-nps1"
-    # NPS changes reload amdgpu through the driver container's module tree
-    assert e["DRIVER_RELOAD_CMD"].startswith("chroot /run/amd/driver modprobe -r amdgpu")
+    # NPS changes: the driver container reloads amdgpu from its own module tree, on request
+    assert e["DRIVER_RELOAD_VIA"] == "driver-container" and "DRIVER_RELOAD_CMD" not in e
     c2 = cluster([gpu_node("a", extra_labels={C.PARTITION_CAPABLE_LABEL: "true"})],
                  sample_cp(**{"driver.enabled": False}))
     reconcile_once(c2)
-    assert "DRIVER_RELOAD_CMD" not in env(container(daemonset(c2, C.DS_PARTITION_MANAGER), "amd-partition-manager"))
+    e2 = env(container(daemonset(c2, C.DS_PARTITION_MANAGER), "amd-partition-manager"))
+    assert "DRIVER_RELOAD_CMD" not in e2 and "DRIVER_RELOAD_VIA" not in e2
 
 
 def test_daemonsets_common_config_labels_annotations_tolerations():

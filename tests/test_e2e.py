@@ -100,3 +100,45 @@ def test_driver_container_install_and_auto_upgrade_on_real_processes(tmp_path):
     assert (up["from"], up["to"]) == ("6.12.12", "6.12.13")
     assert up["states"][-7:] == ["cordon-required", "wait-for-jobs-required", "pod-deletion-required",
                                  "pod-restart-required", "validation-required", "uncordon-required", "upgrade-done"]
+
+
+@pytest.mark.skipif(not os.path.exists(BARRIER), reason="native binaries not built")
+def test_fabric_validation_on_time_slicing_and_busy_nodes(tmp_path):
+    """Whole GPUs: the fabric pod asks for the 8 physical GPUs. Time-slicing x10 (allocatable 80):
+    no replica request, every GPU visible, ranks 2,4,8. A GPU pod running during a validator
+    restart: topology-only, validator Ready, no collective pod."""
+    node = str(fakesys.make_node(tmp_path / "root", n_gpus=8))
+    r = E2E(sys_root=node, dev_root=node, hip_mode="skip", timeout=90).run_fabric_shapes()
+    assert r["ok"], r
+    inst = r["install"]
+    assert inst["rccl_pod"]["limits"] == {"amd.com/gpu": 8} and inst["rccl-ready"]["pod_shape"] == "scheduled"
+    assert inst["rccl-ready"]["physical_gpus"] == 8 and inst["rccl-ready"]["fabric"]["ok"]
+    ts = r["time-slicing"]
+    assert ts["allocatable"] == 80
+    assert ts["rccl-ready"]["pod_shape"] == "privileged-all" and ts["rccl-ready"]["physical_gpus"] == 8
+    assert ts["rccl_pod"]["limits"] is None and ts["rccl_pod"]["privileged"]
+    assert ts["rccl_pod"]["env"]["RCCL_RANKS"] == "2,4,8" and ts["rccl_pod"]["env"]["AMD_VISIBLE_DEVICES"] == "all"
+    busy = r["busy"]["rccl-ready"]
+    assert busy["mode"] == "topology-only" and busy["busy_pods"] == ["default/gpu-busy"] and busy["fabric"]["ok"]
+
+
+@pytest.mark.skipif(not os.path.exists(BARRIER), reason="native binaries not built")
+def test_fabric_validation_on_a_cpx_node(tmp_path):
+    """CPX: 64 KFD agents, allocatable amd.com/gpu=64; the fabric pod pins one agent per physical
+    GPU (HIP_VISIBLE_DEVICES, 8 entries) and plans ranks 2,4,8."""
+    node = str(fakesys.make_node(tmp_path / "root", n_gpus=8, compute="CPX"))
+    e = E2E(sys_root=node, dev_root=node, hip_mode="skip", timeout=90)
+    e.setup()
+    # the node's layout is CPX on purpose: the partition manager keeps it (no re-partition to SPX)
+    e.backing.patch("v1", "Node", e.node, {"metadata": {"labels": {"amd.com/gpu.partition.config": "cpx-nps1"}}})
+    try:
+        e.step("install-operator", e.install_operator)
+        v = e.step("verify-operator", lambda: e.verify_operator("install"))
+        shape = e._rccl_pod_shape()
+    finally:
+        e.teardown()
+    assert v["amd.com/gpu"] == "64"
+    rr = v["rccl-ready"]
+    assert rr["physical_gpus"] == 8 and rr["pod_shape"] == "privileged-all"
+    vis = shape["env"]["HIP_VISIBLE_DEVICES"].split(",")
+    assert len(vis) == 8 and vis[:2] == ["0", "8"] and shape["env"]["RCCL_RANKS"] == "2,4,8"

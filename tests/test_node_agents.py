@@ -1,5 +1,6 @@
 """Node labeller, partition manager and metrics exporter against fake MI355X sysfs trees."""
 
+import json
 import os
 import threading
 import time
@@ -403,3 +404,90 @@ def test_config_manager_finds_the_plugin_under_any_launcher(tmp_path):
         (proc / pid).mkdir(parents=True)
         (proc / pid / "cmdline").write_bytes(b"\0".join(a.encode() for a in argv) + b"\0")
     assert sorted(cm.find_pids("amd-device-plugin", str(proc))) == [11, 12, 13]
+
+
+def test_partition_nps_change_reloads_through_the_driver_container(spx, cfg, tmp_path):
+    """with driver.enabled the partition manager asks the driver container (the
+    only holder of the module tree that loaded amdgpu) through /run/amd/driver/reload-request; the
+    container rmmods its precompiled modules, insmods them again, rewrites .driver-ctr and answers
+    reload-result. The NPS change then completes (state success)."""
+    import shutil
+    import threading
+    from pathlib import Path
+    from gpu_operator_amd.operands import driver_container as dcm
+    kernel = "6.8.0-45-generic"
+    img = tmp_path / "image"
+    d = img / "opt/amdgpu/precompiled" / kernel
+    d.mkdir(parents=True)
+    for m in ("amdgpu", "amdxcp", "amdttm", "amdkcl"):
+        (d / f"{m}.ko.xz").write_text("x")
+    root = Path(spx)
+    for m in ("amdxcp", "amdttm", "amdkcl"):
+        (root / "sys/module" / m).mkdir(parents=True, exist_ok=True)
+    calls = []
+
+    def run(argv, **kw):
+        import subprocess as sp
+        calls.append([argv[0], dcm._mod_name(argv[1])])
+        mod = root / "sys/module" / dcm._mod_name(argv[1])
+        if argv[0] == "rmmod":
+            shutil.rmtree(mod, ignore_errors=True)
+        elif argv[0] == "insmod":
+            mod.mkdir(parents=True, exist_ok=True)
+            if dcm._mod_name(argv[1]) == "amdgpu":       # the module comes back in the new NPS mode
+                (mod / "initstate").write_text("live\n")
+                fakesys.set_compute_partition(spx, "SPX", "NPS2")
+        return sp.CompletedProcess(argv, 0, "", "")
+    run_dir = tmp_path / "run"
+    dc = dcm.DriverContainer(sys_root=spx, dev_root=spx, image_root=str(img), host_etc=str(tmp_path / "etc"),
+                             run_dir=str(run_dir), firmware_dir=str(tmp_path / "fw"),
+                             params_file=str(tmp_path / "none.conf"), kernel=kernel, run=run, ready_timeout=3.0)
+    dc._write_marker({"mode": "precompiled"})
+    stop = threading.Event()
+    t = threading.Thread(target=dc.serve_reloads, args=(stop, 0.2), daemon=True)
+    t.start()
+    try:
+        c = _cluster("all-cpx")
+        m = pm.PartitionManager(c, "n1", cfg, root=spx, barrier_dir=str(tmp_path / "barriers"), enum_timeout=3.0,
+                                pods_timeout=3.0, reload_timeout=5.0, reload_via="driver-container",
+                                driver_dir=str(run_dir / "driver"),
+                                reenumerate=lambda: fakesys.set_compute_partition(spx, "CPX", "NPS2"))
+        assert m.reconcile() == "applied"
+    finally:
+        stop.set()
+        t.join(5)
+    assert calls[:4] == [["rmmod", "amdgpu"], ["rmmod", "amdxcp"], ["rmmod", "amdttm"], ["rmmod", "amdkcl"]]
+    assert [c[1] for c in calls[4:]] == ["amdkcl", "amdttm", "amdxcp", "amdgpu"]
+    res = json.loads((run_dir / "driver" / dcm.RELOAD_RESULT).read_text())
+    assert res["ok"] and res["info"]["unloaded"][0] == "amdgpu"
+    assert json.loads((run_dir / "driver/.driver-ctr").read_text())["reload_s"] >= 0
+    assert o.get_labels(c.get("v1", "Node", "n1"))[pm.STATE_LABEL] == "success"
+
+
+def test_partition_driver_container_reload_timeout_fails(spx, cfg, tmp_path):
+    c = _cluster("all-cpx")
+    m = pm.PartitionManager(c, "n1", cfg, root=spx, barrier_dir=str(tmp_path / "b"), enum_timeout=1.0,
+                            pods_timeout=1.0, reload_timeout=0.5, reload_via="driver-container",
+                            driver_dir=str(tmp_path / "driver"))
+    assert m.reconcile() == "failed"
+    msg = [e for e in c.events if e["reason"] == "PartitionFailed"][0]["message"]
+    assert "did not answer reload request" in msg
+
+
+def test_metrics_device_level_series_once_per_physical_gpu_under_cpx(tmp_path):
+    """CPX enumerates 8 agents per GPU that share the PMFW gpu_metrics table and
+    the hwmon sensors; energy, power, per-link xGMI bytes and temperatures are emitted once per
+    physical device (its lowest-index agent), per-partition series stay per agent."""
+    from prometheus_client import generate_latest
+    root = str(fakesys.make_node(tmp_path / "cpx", n_gpus=2, compute="CPX"))
+    text = generate_latest(me.build_registry(me.load_fields(None), root=root, hostname="n1")).decode()
+
+    def series(name):
+        return [ln for ln in text.splitlines() if ln.startswith(name + "{")]
+    assert len(series("amd_gpu_energy_joules_total")) == 2
+    assert len(series("amd_gpu_power_watts")) == 2
+    assert len(series("amd_gpu_temperature_junction_celsius")) == 2
+    assert {ln.split('gpu="')[1].split('"')[0] for ln in series("amd_gpu_power_watts")} == {"0", "8"}
+    links = series("amd_gpu_xgmi_read_bytes_total")
+    assert links and {ln.split('gpu="')[1].split('"')[0] for ln in links} == {"0", "8"}
+    assert len(series("amd_gpu_vram_total_bytes")) == 16 and len(series("amd_gpu_sclk_mhz")) == 16

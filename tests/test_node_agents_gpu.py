@@ -195,3 +195,65 @@ def test_node_probe_reports_the_hive(gpus):
     j = json.loads(p.stdout.splitlines()[0])
     g = [x for x in j["gpus"] if x["gfx"] == "gfx950"][0]
     assert g["xgmi_links"] == 7 and g["xgmi_hive_id"] != 0
+
+
+def _other_kfd_clients():
+    """PIDs other than this one holding /dev/kfd open (readable /proc entries only)."""
+    me, out = os.getpid(), []
+    for pid in os.listdir("/proc"):
+        if not pid.isdigit() or int(pid) == me:
+            continue
+        try:
+            for fd in os.listdir(f"/proc/{pid}/fd"):
+                if os.readlink(f"/proc/{pid}/fd/{fd}") == "/dev/kfd":
+                    out.append(int(pid))
+                    break
+        except OSError:
+            continue
+    return out
+
+
+def test_partition_round_trip_spx_cpx_spx(gpus, tmp_path):
+    """SPX -> CPX -> SPX on the leased GPU through the partition manager (BASELINE config 5,
+    reference assets/state-mig-manager/0600_daemonset.yaml:26-104). Runs only where the compute
+    partition is writable and no other process has the GPU open; NPS is never touched on a shared
+    box. Asserts KFD agents 1 -> 8 -> 1, the device plugin's 8 partition devices with their
+    sysfs VRAM, and the labeller's compute-partition label."""
+    from gpu_operator_amd.k8s.fake import FakeClient
+    from gpu_operator_amd.operands import device_plugin as DP
+    from gpu_operator_amd.operands import node_labeller as NL
+    from gpu_operator_amd.operands import partition_manager as PM
+
+    phys = PM.physical_gpus("/")
+    g0 = phys[0]
+    attr = f"/sys/bus/pci/devices/{g0['pci_bdf']}/current_compute_partition"
+    if not os.path.exists(attr) or not os.access(attr, os.W_OK):
+        pytest.skip(f"{attr} is not writable by this user (partition changes need root on the node)")
+    if g0["compute_partition"] != "SPX" or "CPX" not in g0["available_compute_partitions"]:
+        pytest.skip(f"GPU is in {g0['compute_partition']}, CPX available: {g0['available_compute_partitions']}")
+    others = _other_kfd_clients()
+    if others:
+        pytest.skip(f"other KFD clients hold the GPU: {others[:8]}")
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text("version: v1\npartition-configs:\n"
+                   "  spx: [{devices: all, compute: SPX, memory: " + g0["memory_partition"] + "}]\n"
+                   "  cpx: [{devices: all, compute: CPX, memory: " + g0["memory_partition"] + "}]\n")
+    node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": "n", "labels": {}}}
+    c = FakeClient([node])
+    pm = PM.PartitionManager(c, "n", str(cfg), root="/", barrier_dir=str(tmp_path / "v"), enum_timeout=120)
+    agents0 = len(D.enumerate_gpus("/"))
+    try:
+        c.patch("v1", "Node", "n", {"metadata": {"labels": {PM.CONFIG_LABEL: "cpx"}}})
+        assert pm.reconcile() == "applied"
+        cpx = D.enumerate_gpus("/")
+        assert len(cpx) == agents0 - 1 + 8
+        devs = [d for d in DP.discover(DP.Config(), "/") if d.bdf == g0["pci_bdf"]]
+        assert len(devs) == 8 and {d.partition for d in devs} == {"CPX"}
+        sysfs_vram = {g["index"]: g["vram_total"] for g in cpx if g["pci_bdf"] == g0["pci_bdf"]}
+        assert all(d.vram_bytes > 0 for d in devs) and sorted(d.vram_bytes for d in devs) == sorted(sysfs_vram.values())
+        assert NL.compute_labels("/")["amd.com/gpu.compute-partition"] == "CPX"
+    finally:
+        c.patch("v1", "Node", "n", {"metadata": {"labels": {PM.CONFIG_LABEL: "spx"}}})
+        assert pm.reconcile() in ("applied", "in-sync")
+    assert len(D.enumerate_gpus("/")) == agents0
+    assert NL.compute_labels("/")["amd.com/gpu.compute-partition"] == "SPX"

@@ -158,3 +158,27 @@ def test_operator_process_end_to_end(tmp_path):
         assert leases and o.name(leases[0]) == "53822513.amd.com"
         labels = o.get_labels(backing.get("v1", "Node", "n1"))
         assert labels.get("amd.com/gpu.present") == "true" and labels.get("amd.com/gpu.deploy.device-plugin") == "true"
+
+
+def test_watch_with_field_selector_sees_only_its_node(api):
+    """node agents watch their own Node (metadata.name=<node>) -- the selector
+    reaches the API server on the list and on the watch, so other nodes' updates never arrive."""
+    srv, c = api
+    for n in ("a", "b"):
+        c.create({"apiVersion": "v1", "kind": "Node", "metadata": {"name": n, "labels": {}}})
+    seen = []
+    got = threading.Event()
+
+    def cb(ev):
+        seen.append((ev.type, o.name(ev.obj)))
+        if o.get_labels(ev.obj).get("x") == "2":
+            got.set()
+    stop = c.watch("v1", "Node", cb, field_selector="metadata.name=b")
+    try:
+        time.sleep(0.5)
+        c.patch("v1", "Node", "a", {"metadata": {"labels": {"x": "1"}}})
+        c.patch("v1", "Node", "b", {"metadata": {"labels": {"x": "2"}}})
+        assert got.wait(10)
+    finally:
+        stop()
+    assert seen == [("ADDED", "b"), ("MODIFIED", "b")]

@@ -366,3 +366,66 @@ def test_vfio_manage_binds_gpus_with_their_iommu_group_companions(tmp_path):
         assert _driver(root, "0000:05:00.0") == "amdgpu" and _driver(root, "0000:05:00.1") == "snd_hda_intel"
     finally:
         core.close()
+
+
+def _foreign_nic(root, group=10, bdf="0000:06:00.0"):
+    """A host NIC (Mellanox, class 0x0200) in the IOMMU group of the first GPU: a platform
+    without ACS isolation."""
+    from pathlib import Path
+    r = Path(root)
+    dev = r / "sys/bus/pci/devices" / bdf
+    dev.mkdir(parents=True)
+    (dev / "vendor").write_text("0x15b3\n")
+    (dev / "class").write_text("0x020000\n")
+    (dev / "driver_override").write_text("\n")
+    drv = r / "sys/bus/pci/drivers/mlx5_core"
+    drv.mkdir(parents=True, exist_ok=True)
+    os.symlink(os.path.relpath(drv, dev), dev / "driver")
+    grp = r / "sys/kernel/iommu_groups" / str(group)
+    os.symlink(os.path.relpath(grp, dev), dev / "iommu_group")
+    os.symlink(os.path.relpath(dev, grp / "devices"), grp / "devices" / bdf)
+    return bdf
+
+
+def test_vfio_manage_refuses_a_group_with_a_foreign_device(tmp_path):
+    """an IOMMU group that also holds a host NIC is refused -- the NIC keeps its
+    driver and gets no driver_override, the GPU stays on amdgpu -- while other GPUs still bind."""
+    import subprocess
+    root = str(fakesys.make_node(tmp_path / "r", n_gpus=2, companion_audio=True))
+    nic = _foreign_nic(root)
+    script = tmp_path / "vfio-manage.sh"
+    script.write_text(_vfio_script())
+    core = _FakePciCore(root)
+    env = dict(os.environ, SYSFS_ROOT=os.path.join(root, "sys"))
+    try:
+        p = subprocess.run(["bash", str(script), "bind", "--all"], env=env, capture_output=True, text=True, timeout=60)
+        assert p.returncode == 1 and "refusing to bind 0000:05:00.0" in p.stderr and nic in p.stderr
+        assert _driver(root, nic) == "mlx5_core"
+        assert open(os.path.join(root, "sys/bus/pci/devices", nic, "driver_override")).read().strip() == ""
+        assert _driver(root, "0000:05:00.0") == "amdgpu" and _driver(root, "0000:05:00.1") == "snd_hda_intel"
+        assert _driver(root, "0000:15:00.0") == "vfio-pci" and _driver(root, "0000:15:00.1") == "vfio-pci"
+    finally:
+        core.close()
+
+
+def test_vfio_manage_rolls_back_a_failed_companion(tmp_path):
+    """A companion that cannot take the override: it is re-probed to its host driver, and the
+    GPU is left on amdgpu (never half a group on vfio-pci)."""
+    import shutil
+    import subprocess
+    root = str(fakesys.make_node(tmp_path / "r", n_gpus=1, companion_audio=True))
+    ov = os.path.join(root, "sys/bus/pci/devices/0000:05:00.1/driver_override")
+    if os.path.exists(ov):
+        os.remove(ov)
+    os.makedirs(ov)                                       # writes to it fail, even as root
+    script = tmp_path / "vfio-manage.sh"
+    script.write_text(_vfio_script())
+    core = _FakePciCore(root)
+    env = dict(os.environ, SYSFS_ROOT=os.path.join(root, "sys"))
+    try:
+        p = subprocess.run(["bash", str(script), "bind", "--all"], env=env, capture_output=True, text=True, timeout=60)
+        assert p.returncode == 1 and "left 0000:05:00.0 with its host driver" in p.stderr
+        assert _driver(root, "0000:05:00.1") == "snd_hda_intel" and _driver(root, "0000:05:00.0") == "amdgpu"
+    finally:
+        core.close()
+        shutil.rmtree(ov, ignore_errors=True)

@@ -406,3 +406,55 @@ def test_gpu_pod_reappearing_before_driver_restart_is_evicted_first():
             break
     assert states(c)["n0"] == U.DONE and seen[0] == U.POD_DELETION_REQUIRED, seen
     assert not [p for p in c.list("v1", "Pod", "default") if o.name(p) == "late"]
+
+
+def _ds_gpu_pod(node, name="gpu-monitor"):
+    pod = gpu_workload(node, name)
+    pod["metadata"]["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "DaemonSet", "name": "mon",
+                                           "uid": "ds-uid", "controller": True}]
+    return pod
+
+
+def test_daemonset_gpu_pod_without_drain_fails_the_node_instead_of_looping():
+    """a DaemonSet-owned GPU pod comes straight back after eviction (it
+    tolerates the cordon). Pod deletion must treat it as blocked -- upgrade-failed without drain
+    -- not evict it and loop pod-deletion <-> pod-restart forever."""
+    clock = [1000.0]
+    c, rec, sim, up = setup(n_nodes=1, podDeletion={"timeoutSeconds": 30})
+    sim._collect_orphans = lambda live: None          # the pod's DaemonSet lives outside this sim
+    up.mgr.clock = lambda: clock[0]
+    up.reconcile(("", "cluster-policy"))
+    c.create(_ds_gpu_pod("n0"))
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    seen = []
+    for _ in range(12):
+        step(c, rec, sim, up)
+        seen.append(states(c)["n0"])
+        clock[0] += 10
+    assert states(c)["n0"] == U.FAILED, seen
+    assert seen.count(U.POD_DELETION_REQUIRED) <= 2, seen
+    assert [p for p in c.list("v1", "Pod", "default") if o.name(p) == "gpu-monitor"]     # never evicted
+    assert any("DaemonSet-managed" in e["message"] for e in c.events if e["reason"] == U.EVENT_REASON)
+
+
+def test_daemonset_gpu_pod_with_drain_completes_the_upgrade():
+    """With drain enabled the node goes to drain, which skips DaemonSet pods (kubectl drain
+    --ignore-daemonsets), and the driver restart is not blocked by the DaemonSet pod again."""
+    c, rec, sim, up = setup(n_nodes=1, podDeletion={"timeoutSeconds": 30},
+                            drain={"enable": True, "force": True, "timeoutSeconds": 30})
+    sim._collect_orphans = lambda live: None
+    up.reconcile(("", "cluster-policy"))
+    c.create(_ds_gpu_pod("n0"))
+    bump_driver(c)
+    rec.reconcile(("", "cluster-policy"))
+    sim.sync()
+    seen = []
+    for _ in range(40):
+        step(c, rec, sim, up)
+        seen.append(states(c)["n0"])
+        if seen[-1] == U.DONE:
+            break
+    assert states(c)["n0"] == U.DONE, seen
+    assert U.DRAIN_REQUIRED in seen and seen.count(U.POD_DELETION_REQUIRED) <= 2, seen

@@ -192,8 +192,9 @@ def test_rccl_requests_all_gpus_and_records_busbw(tmp_path, node_root):
     assert info["peak_busbw_gbps"] == 310.0 and ctx.status.exists(S.RCCL_READY)
 
 
-def test_rccl_single_gpu_node_skips(tmp_path, node_root):
-    ctx = ctx_for(tmp_path, node_root, client=FakeClient([node_obj(gpus=1)]))
+def test_rccl_single_gpu_node_skips(tmp_path):
+    root = str(fakesys.make_node(tmp_path / "r1", n_gpus=1))
+    ctx = ctx_for(tmp_path, root, client=FakeClient([node_obj(gpus=1)]))
     assert "skipped" in comp.validate_rccl(ctx)
 
 
@@ -216,7 +217,11 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
     sd.create(S.DRIVER_CTR_READY, {"ts": t})
     sd.create(S.DRIVER_READY, {"ts": t + 0.5})
     sd.create(S.TOOLKIT_READY, {"ts": t + 3.0})
-    sd.create(S.HIP_READY, {"ts": t + 9.0, "gemm_tflops_total": 10900.0, "gemm_tflops_per_gpu": 1362.5})
+    sd.create(S.HIP_READY, {"ts": t + 9.0, "gemm_tflops_total": 10900.0, "gemm_tflops_per_gpu": 1362.5,
+                            "tflops_by_dtype_gpus": {
+                                "bf16": {"1": {"total_tflops": 1400.0, "per_gpu_tflops": 1400.0, "efficiency": 1.0},
+                                         "8": {"total_tflops": 10900.0, "per_gpu_tflops": 1362.5,
+                                               "efficiency": 0.9732}}}})
     sd.create(S.PLUGIN_READY, {"ts": t + 9.5})
     sd.create(S.RCCL_READY, {"ts": t + 14.0, "peak_busbw_gbps": 310.0, "ranks": 8,
                              "busbw_by_ranks": {"2": 141.0, "4": 230.5, "8": 310.0}})
@@ -228,7 +233,9 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
     from prometheus_client import generate_latest
     text = generate_latest(m.registry).decode()
     assert 'amd_gpu_operator_node_time_to_ready_seconds{node="n1"} 14.0' in text
-    assert 'amd_gpu_operator_validator_gemm_tflops{node="n1",scope="node"} 10900.0' in text
+    assert 'amd_gpu_operator_validator_gemm_tflops{dtype="bf16",gpus="8",node="n1",scope="node"} 10900.0' in text
+    assert 'amd_gpu_operator_validator_gemm_tflops{dtype="bf16",gpus="1",node="n1",scope="per_gpu"} 1400.0' in text
+    assert 'amd_gpu_operator_validator_gemm_scaling_efficiency{dtype="bf16",gpus="8",node="n1"} 0.9732' in text
     assert 'amd_gpu_operator_node_device_plugin_devices_total{node="n1"} 8.0' in text
     assert 'amd_gpu_operator_node_driver_validation{node="n1"} 1.0' in text
     assert 'amd_gpu_operator_amd_pci_devices_total{node="n1"} 8.0' in text
@@ -299,10 +306,11 @@ def test_rccl_fails_validation_on_a_split_hive(tmp_path, node_root):
     assert not ctx.status.exists(S.RCCL_READY)
 
 
-def test_rccl_ranks_follow_the_node_gpu_count(tmp_path, node_root):
+def test_rccl_ranks_follow_the_node_gpu_count(tmp_path):
+    root = str(fakesys.make_node(tmp_path / "r4", n_gpus=4))
     c = FakeClient([node_obj(gpus=4)])
     k = FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG})
-    comp.validate_rccl(ctx_for(tmp_path, node_root, client=c))
+    comp.validate_rccl(ctx_for(tmp_path, root, client=c))
     assert _pod_env(k.seen[0])["RCCL_RANKS"] == "2,4"
     assert k.seen[0]["spec"]["initContainers"][0]["resources"]["limits"] == {"amd.com/gpu": 4}
 
@@ -383,3 +391,128 @@ def test_rccl_workload_cli_reads_env(monkeypatch):
     monkeypatch.setenv("RCCL_RANKS", "2,8")
     assert WM.main(["rccl"]) == 0
     assert seen == {"max_bytes": 1 << 30, "dtype": "float", "ranks": "2,8", "min_busbw": 123.5, "processes": 0}
+
+
+# -- throughput floors, node shapes, busy nodes ------------------------------
+def _gemm_msg(per_gpu, dtype="bf16", gpus=8):
+    return "\n".join(json.dumps(x) for x in [
+        {"event": "hip-smoke", "devices": gpus, "ok": True},
+        {"event": "aggregate", "dtype": dtype, "m": 8192, "n": 8192, "k": 8192, "gpus": gpus,
+         "total_tflops": per_gpu * gpus, "per_gpu_tflops": per_gpu, "min_gpu_tflops": per_gpu, "ok": True},
+        {"event": "gemm", "dtype": dtype, "device": 0, "m": 8192, "n": 8192, "k": 8192, "tflops": per_gpu,
+         "ok": True}])
+
+
+def test_gemm_floors_come_from_the_model_and_env(tmp_path, node_root):
+    f = comp.gemm_floors(ctx_for(tmp_path, node_root))
+    assert f == {"bf16": round(2516.6 * 0.40, 1), "fp8": round(5033.2 * 0.40, 1)}   # MI355X dense peaks
+    f = comp.gemm_floors(ctx_for(tmp_path, node_root, env={"GEMM_MIN_TFLOPS_BF16": "1200",
+                                                           "GEMM_MIN_TFLOPS_FP8": "0"}))
+    assert f == {"bf16": 1200.0, "fp8": 0.0}
+    cpx = str(fakesys.make_node(tmp_path / "cpx", compute="CPX"))       # a partition has 1/8 of the CUs
+    assert comp.gemm_floors(ctx_for(tmp_path, cpx))["bf16"] == round(2516.6 * 0.40 / 8, 1)
+    with pytest.raises(comp.ValidationError, match="not a number"):
+        comp.gemm_floors(ctx_for(tmp_path, node_root, env={"GEMM_MIN_TFLOPS_BF16": "fast"}))
+    assert comp.busbw_floor(ctx_for(tmp_path, node_root)) == round(153.6 * 0.25, 1)
+
+
+def test_hip_below_floor_opens_no_barrier(tmp_path, node_root):
+    c = FakeClient([node_obj()])
+    k = FakeKubelet(c, {"amd-hip-validator": _gemm_msg(600.0)})          # a GPU at ~1/4 of its rate
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    with pytest.raises(comp.ValidationError, match="below the 1006.6 floor"):
+        comp.validate_hip(ctx)
+    assert not ctx.status.exists(S.HIP_READY)
+    env = _pod_env(k.seen[0])
+    assert env["GEMM_MIN_TFLOPS_BF16"] == "1006.6" and env["GEMM_SCALING"] == "1,2,4,8"
+
+
+def test_hip_records_the_scaling_sweep(tmp_path, node_root):
+    msg = "\n".join(json.dumps(x) for x in [
+        {"event": "hip-smoke", "devices": 8, "ok": True},
+        {"event": "aggregate", "dtype": "bf16", "m": 8192, "n": 8192, "k": 8192, "gpus": 1, "total_tflops": 1550.0,
+         "per_gpu_tflops": 1550.0, "min_gpu_tflops": 1550.0, "efficiency": 1.0, "ok": True},
+        {"event": "aggregate", "dtype": "bf16", "m": 8192, "n": 8192, "k": 8192, "gpus": 8, "total_tflops": 12168.0,
+         "per_gpu_tflops": 1521.0, "min_gpu_tflops": 1510.0, "efficiency": 0.9813, "ok": True},
+        {"event": "aggregate", "dtype": "fp8_e4m3fn", "m": 8192, "n": 8192, "k": 8192, "gpus": 1,
+         "total_tflops": 3100.0, "per_gpu_tflops": 3100.0, "min_gpu_tflops": 3100.0, "efficiency": 1.0, "ok": True}])
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-hip-validator": msg})
+    info = comp.validate_hip(ctx_for(tmp_path, node_root, client=c))
+    assert info["gemm_tflops_total"] == 12168.0 and info["gpus"] == 8
+    assert info["tflops_by_dtype_gpus"]["bf16"]["8"]["efficiency"] == 0.9813
+    assert info["tflops_by_dtype_gpus"]["fp8"]["1"]["per_gpu_tflops"] == 3100.0
+
+
+def test_rccl_below_floor_opens_no_barrier(tmp_path, node_root):
+    msg = "\n".join(json.dumps(x) for x in [
+        {"event": "fabric", "physical_gpus": 8, "single_hive": True, "ok": True},
+        {"event": "summary", "ranks": 8, "peak_busbw_gbps": 1.0, "ok": True}])   # a pod without the floor
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-rccl-validator": msg})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    with pytest.raises(comp.ValidationError, match="below the 38.4 GB/s floor"):
+        comp.validate_rccl(ctx)
+    assert not ctx.status.exists(S.RCCL_READY)
+
+
+def test_rccl_full_run_records_the_node_annotation(tmp_path, node_root):
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG})
+    comp.validate_rccl(ctx_for(tmp_path, node_root, client=c))
+    ann = json.loads(c.get("v1", "Node", "n1")["metadata"]["annotations"][comp.FABRIC_ANNOTATION])
+    assert ann["ok"] and ann["peak_busbw_gbps"] == 310.0 and ann["busbw_by_ranks"]["8"] == 310.0
+
+
+def test_rccl_time_slicing_node_asks_for_the_physical_gpus(tmp_path, node_root):
+    c = FakeClient([node_obj(gpus=80)])                                 # 8 GPUs x 10 time-slicing replicas
+    k = FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG})
+    info = comp.validate_rccl(ctx_for(tmp_path, node_root, client=c))
+    c0 = k.seen[0]["spec"]["initContainers"][0]
+    assert "limits" not in (c0.get("resources") or {}) and c0["securityContext"]["privileged"]
+    assert _pod_env(k.seen[0])["AMD_VISIBLE_DEVICES"] == "all" and _pod_env(k.seen[0])["RCCL_RANKS"] == "2,4,8"
+    assert info["pod_shape"] == "privileged-all" and info["physical_gpus"] == 8
+
+
+def test_rccl_cpx_node_pins_one_agent_per_physical_gpu(tmp_path):
+    root = str(fakesys.make_node(tmp_path / "cpx", compute="CPX"))
+    n = node_obj(gpus=64)
+    c = FakeClient([n])
+    k = FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG})
+    info = comp.validate_rccl(ctx_for(tmp_path, root, client=c))
+    env = _pod_env(k.seen[0])
+    assert env["RCCL_RANKS"] == "2,4,8" and len(env["HIP_VISIBLE_DEVICES"].split(",")) == 8
+    assert env["HIP_VISIBLE_DEVICES"].split(",")[:2] == ["0", "8"]       # first partition of GPU 0, GPU 1
+    assert info["physical_gpus"] == 8
+
+
+def test_busy_node_runs_topology_only_and_keeps_the_last_full_result(tmp_path, node_root):
+    n = node_obj()
+    n["metadata"]["annotations"] = {comp.FABRIC_ANNOTATION: json.dumps({"ts": 1.0, "peak_busbw_gbps": 305.0,
+                                                                         "ok": True})}
+    job = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "train-0", "namespace": "default"},
+           "spec": {"nodeName": "n1", "containers": [{"name": "t", "resources": {"limits": {"amd.com/gpu": "8"}}}]},
+           "status": {"phase": "Running"}}
+    c = FakeClient([n, job])
+    k = FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG, "amd-hip-validator": _gemm_msg(700.0)})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    info = comp.validate_rccl(ctx)
+    assert info["mode"] == "topology-only" and info["busy_pods"] == ["default/train-0"]
+    assert info["fabric"]["ok"] and info["last_full"]["peak_busbw_gbps"] == 305.0
+    assert not [p for p in k.seen if o.get_labels(p).get("app") == "amd-rccl-validator"]   # no collective pod
+    assert ctx.status.exists(S.RCCL_READY)
+    # the GEMM numbers beside a training job measure the sharing: correctness only, no floor
+    hip = comp.validate_hip(ctx)
+    assert "floor_skipped" in hip and _pod_env(k.seen[-1])["GEMM_MIN_TFLOPS_BF16"] == "0"
+
+
+def test_termination_message_keeps_summaries_and_failures_first():
+    from gpu_operator_amd.validator.workload_main import termination_message
+    res = [{"event": "gemm", "device": i, "tflops": 1500.0, "pad": "x" * 200, "ok": True} for i in range(30)]
+    res += [{"event": "gemm", "device": 99, "tflops": 10.0, "ok": False},
+            {"event": "aggregate", "gpus": 8, "total_tflops": 1.0, "ok": False},
+            {"event": "rccl-debug", "algo_proto": {}, "lines": ["y" * 300] * 40}]
+    msg = termination_message(res)
+    lines = [json.loads(x) for x in msg.splitlines()]
+    assert len(msg) <= 4000 and lines[0]["event"] == "aggregate" and "lines" not in lines[1]
+    assert lines[2]["device"] == 99 and len(lines) < 33

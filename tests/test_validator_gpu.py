@@ -30,8 +30,58 @@ def test_gemm_validate_binary_checks_and_reports_tflops():
     assert start["gcn_arch"].startswith("gfx950") and start["cus"] == 256
     gemms = [x for x in lines if x["event"] == "gemm"]
     assert gemms and all(g["ok"] for g in gemms)
+    # clock stabilisation ran before the timed dispatches (>= 50 dispatches, or the time cap)
+    assert all(g["stabilise_dispatches"] >= 50 for g in gemms)
     agg = [x for x in lines if x["event"] == "aggregate" and x["m"] == 8192][0]
-    assert agg["per_gpu_tflops"] > 900           # MI355X bf16 dense, random operands
+    assert agg["per_gpu_tflops"] > 1200           # MI355X bf16, random operands, steady clock
+
+
+def test_gemm_validate_scaling_sweep_on_one_gpu():
+    """--scaling 1,2,4,8 on a 1-GPU box: gpus=1 measured (efficiency 1), 2/4/8 clean skips, exit 0."""
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "8192", "--iters", "20", "--scaling", "1,2,4,8")
+    assert rc == 0, err
+    aggs = [x for x in lines if x["event"] == "aggregate"]
+    assert [a["gpus"] for a in aggs] == [1] and aggs[0]["efficiency"] == 1.0 and aggs[0]["ok"]
+    skipped = [x["gpus"] for x in lines if x["event"] == "scaling" and x.get("skipped")]
+    assert skipped == [2, 4, 8]
+
+
+def test_gemm_validate_gates_on_the_floor():
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "4096", "--iters", "5", "--min-tflops", "1000000")
+    assert rc == 1
+    g = [x for x in lines if x["event"] == "gemm"][0]
+    assert not g["ok"] and "below floor" in g["error"]
+
+
+def test_pod_path_tflops_match_the_bench_protocol():
+    """The validator pod's number (amd-gemm-validate, what feeds validator_gemm_tflops and the
+    floors) is within 3 % of bench.py's protocol on the same box, for bf16 and fp8."""
+    import sys
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from gpu_operator_amd.ops import gemm as G
+    args = bench.parse_args(["--steps", "50", "--warmup", "5", "--stabilise-max-s", "6"])
+    dev = torch.device("cuda", 0)
+    ctx = bench.Ctx(args, torch, None, dev, 0, 0, 1, False, False)
+    m = n = k = 8192
+    a = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 1000)
+    bt = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 2000)
+    c = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+    bf16 = G.tflops(m, n, k, ctx.timed(lambda: G.gemm_bf16(a, bt, c), 50, 5)["elapsed_s"] / 50)
+    f8 = torch.float8_e4m3fn
+    a8 = G.fill_uniform_fp8_(torch.empty((m, k), dtype=f8, device=dev), 3000)
+    b8 = G.fill_uniform_fp8_(torch.empty((n, k), dtype=f8, device=dev), 4000)
+    fp8 = G.tflops(m, n, k, ctx.timed(lambda: G.gemm_fp8(a8, b8, c), 50, 5)["elapsed_s"] / 50)
+    del a, bt, c, a8, b8
+    torch.cuda.synchronize()
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "8192", "--dtype", "both", "--iters", "50")
+    assert rc == 0, err
+    pod = {x["dtype"]: x["per_gpu_tflops"] for x in lines if x["event"] == "aggregate"}
+    print(f"bench protocol bf16 {bf16:.1f} fp8 {fp8:.1f}; pod path {pod}")
+    assert pod["bf16"] >= 0.97 * bf16, (pod, bf16)
+    assert pod["fp8_e4m3fn"] >= 0.97 * fp8, (pod, fp8)
 
 
 def test_gemm_validate_binary_fp8_and_both():
@@ -85,13 +135,20 @@ def test_node_probe_on_real_hardware():
 
 
 def test_validator_workload_hip_with_counters(tmp_path):
+    """Counters for both kernels when the pod runs --gemm-dtype both; rocprofv3 ships in this image,
+    so a skipped or failed collection fails the test (it cannot pass vacuously)."""
     from gpu_operator_amd.validator import workload_main as W
-    results = W.run_hip(["4096"], counters=True, iters=5)
+    results = W.run_hip(["4096"], counters=True, iters=5, dtype="both")
     assert any(r.get("event") == "gemm" and r["ok"] for r in results)
-    ctr = [r for r in results if r.get("event") == "counters"]
-    assert ctr
-    if "skipped" not in ctr[0]:
-        assert ctr[0]["SQ_INSTS_VALU_MFMA_MOPS_BF16"] > 0
+    ctr = {r["dtype"]: r for r in results if r.get("event") == "counters"}
+    assert set(ctr) == {"bf16", "fp8"}, ctr
+    if W.rocprofv3_path() is None:
+        pytest.skip("rocprofv3 not installed")
+    for dtype, c in ctr.items():
+        assert "skipped" not in c and "error" not in c, c
+        assert c["mfma_mops_expected"] == 2 * 4096 ** 3 / 512
+        assert c["mfma_mops_match"], (dtype, c)              # MOPS = 2·M·N·K / 512
+        assert c["SQ_LDS_BANK_CONFLICT"] == 0, (dtype, c)
 
 
 def test_validator_hip_component_local_mode(tmp_path):
