@@ -17,7 +17,7 @@ import json
 import queue
 import re
 import threading
-from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from http.server import BaseHTTPRequestHandler
 from typing import Dict, List, Optional, Tuple
 from urllib.parse import parse_qs, urlparse
 
@@ -56,7 +56,8 @@ class FakeAPIServer:
         self.by_plural: Dict[str, Dict[str, str]] = {}
         for k, av in self.kinds.items():
             self.by_plural.setdefault(av, {})[plural(k)] = k
-        self.httpd = ThreadingHTTPServer(("127.0.0.1", 0), self._handler())
+        from ..runtime.manager import QuietHTTPServer
+        self.httpd = QuietHTTPServer(("127.0.0.1", 0), self._handler())
         self.httpd.daemon_threads = True
         self.port = self.httpd.server_address[1]
         self.url = f"http://127.0.0.1:{self.port}"

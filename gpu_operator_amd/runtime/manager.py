@@ -27,6 +27,25 @@ def _parse_addr(addr: str, default_port: int) -> Tuple[str, int]:
     return host or "0.0.0.0", int(port or default_port)
 
 
+_CLIENT_GONE = (ConnectionResetError, BrokenPipeError, ConnectionAbortedError, TimeoutError)
+
+
+class QuietHTTPServer(ThreadingHTTPServer):
+    """A ThreadingHTTPServer whose per-request errors go to logging: a client that disconnects
+    mid-response (an aborted Prometheus scrape, a probe timing out) is routine and logged at
+    debug level, anything else once with its traceback at error level -- socketserver's default
+    prints every one as a traceback on stderr."""
+
+    daemon_threads = True
+
+    def handle_error(self, request, client_address):  # noqa: D401 - socketserver hook
+        exc = sys.exc_info()[1]
+        if isinstance(exc, _CLIENT_GONE):
+            log.debug("client %s went away: %s", client_address, exc)
+            return
+        log.error("error serving %s", client_address, exc_info=True)
+
+
 class _Server:
     def __init__(self, addr: Tuple[str, int], routes: Dict[str, Callable[[], Tuple[int, str, bytes]]]):
         class Handler(BaseHTTPRequestHandler):
@@ -46,7 +65,7 @@ class _Server:
             def log_message(self, *a):  # quiet
                 pass
 
-        self.httpd = ThreadingHTTPServer(addr, Handler)
+        self.httpd = QuietHTTPServer(addr, Handler)
         self.port = self.httpd.server_address[1]
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
 

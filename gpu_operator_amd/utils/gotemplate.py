@@ -16,6 +16,7 @@ or, not, eq, ne, lt, gt, len, required, fail, toString, b64enc, contains).
 from __future__ import annotations
 
 import base64
+import glob
 import re
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -531,14 +532,40 @@ def deep_merge(base: Dict, over: Dict) -> Dict:
     return out
 
 
-def render_chart(chart_dir: str, values: Optional[Dict] = None, release: str = "amd-gpu-operator",
-                 namespace: str = "amd-gpu-operator") -> Dict[str, str]:
-    """Render every template of a chart; returns {template path: rendered text}."""
+def _load_chart(chart_dir: str) -> Tuple[Dict, Dict]:
     import os
     with open(os.path.join(chart_dir, "Chart.yaml")) as f:
         chart = yaml.safe_load(f)
-    with open(os.path.join(chart_dir, "values.yaml")) as f:
-        vals = deep_merge(yaml.safe_load(f) or {}, values or {})
+    vals: Dict = {}
+    if os.path.exists(os.path.join(chart_dir, "values.yaml")):
+        with open(os.path.join(chart_dir, "values.yaml")) as f:
+            vals = yaml.safe_load(f) or {}
+    return chart, vals
+
+
+def _condition_true(values: Dict, condition: str) -> bool:
+    """Helm's dependency ``condition``: the first of its comma-separated value paths that
+    resolves decides; none resolving keeps the dependency enabled."""
+    for path in [c.strip() for c in (condition or "").split(",") if c.strip()]:
+        cur: Any = values
+        for part in path.split("."):
+            if not isinstance(cur, dict) or part not in cur:
+                cur = None
+                break
+            cur = cur[part]
+        if isinstance(cur, bool):
+            return cur
+    return True
+
+
+def render_chart(chart_dir: str, values: Optional[Dict] = None, release: str = "amd-gpu-operator",
+                 namespace: str = "amd-gpu-operator", prefix: str = "") -> Dict[str, str]:
+    """Render every template of a chart and of its enabled dependencies vendored under
+    ``charts/<name>/`` (the subchart sees its own values.yaml merged with the parent's
+    ``<name>:`` section, as Helm does); returns {template path: rendered text}."""
+    import os
+    chart, base = _load_chart(chart_dir)
+    vals = deep_merge(base, values or {})
     dot = {"Values": vals, "Release": {"Name": release, "Namespace": namespace, "Service": "Helm"},
            "Chart": {"Name": chart["name"], "Version": chart["version"], "AppVersion": chart.get("appVersion", "")},
            "Capabilities": {"KubeVersion": {"Version": "v1.29.0"}}}
@@ -548,11 +575,52 @@ def render_chart(chart_dir: str, values: Optional[Dict] = None, release: str = "
     for n in names:
         with open(os.path.join(tdir, n)) as f:
             t.add(n, f.read())
-    return {n: t.render(n, dot) for n in names if not n.startswith("_") and n.endswith((".yaml", ".txt"))}
+    out = {prefix + "templates/" + n if prefix else n: t.render(n, dot)
+           for n in names if not n.startswith("_") and n.endswith((".yaml", ".txt"))}
+    for dep in chart.get("dependencies") or []:
+        sub = os.path.join(chart_dir, "charts", dep["name"])
+        if not os.path.isdir(sub) or not _condition_true(vals, dep.get("condition", "")):
+            continue
+        out.update(render_chart(sub, vals.get(dep.get("alias") or dep["name"]) or {}, release, namespace,
+                                prefix=f"{prefix}charts/{dep['name']}/"))
+    return out
+
+
+def chart_lock_digest(requested: List[Dict], locked: List[Dict]) -> str:
+    """The ``digest`` Helm writes into Chart.lock: sha256 over the compact JSON of [the
+    Chart.yaml dependencies, the locked ones], each encoded like Helm's chart.Dependency (name,
+    version and condition omitted when empty, repository always)."""
+    import hashlib
+    import json
+
+    def enc(d: Dict) -> Dict:
+        out: Dict[str, Any] = {"name": d["name"]}
+        if d.get("version"):
+            out["version"] = d["version"]
+        out["repository"] = d.get("repository", "")
+        for k in ("condition", "tags", "enabled", "import-values", "alias"):
+            if d.get(k):
+                out[k] = d[k]
+        return out
+    data = json.dumps([[enc(d) for d in requested], [enc(d) for d in locked]], separators=(",", ":"))
+    return "sha256:" + hashlib.sha256(data.encode()).hexdigest()
 
 
 def render_objects(chart_dir: str, values: Optional[Dict] = None, **kw) -> List[Dict]:
+    """Objects of every rendered template (subcharts included), plus the CRDs under the chart's
+    and its enabled subcharts' ``crds/`` only with ``include_crds=True``."""
+    import os
+    include_crds = kw.pop("include_crds", False)
     out = []
+    if include_crds:
+        chart, base = _load_chart(chart_dir)
+        vals = deep_merge(base, values or {})
+        dirs = [chart_dir] + [os.path.join(chart_dir, "charts", d["name"]) for d in chart.get("dependencies") or []
+                              if _condition_true(vals, d.get("condition", ""))]
+        for d in dirs:
+            for p in sorted(glob.glob(os.path.join(d, "crds", "*.yaml"))):
+                with open(p) as f:
+                    out += [doc for doc in yaml.safe_load_all(f) if doc]
     for name, text in render_chart(chart_dir, values, **kw).items():
         if not name.endswith(".yaml"):
             continue

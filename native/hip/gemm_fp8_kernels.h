@@ -270,7 +270,7 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
 // (MI355X_MICROARCH.md, DVFS give-back item 7).
 // A wave's 128x128 sub-tile is 8x8 MFMAs of 16x16 (the bf16 w4s accumulator layout, so the bf16
 // epilogue applies as is). A fragment is 16 rows x 128 k = 32 B per lane (8 VGPRs, two
-// ds_read_b128: chunks 2g and 2g+1 of the 128-B row for lane group g = lane >> 4). A K-tile needs
+// ds_read_b128: chunks g and g+4 of the 128-B row for lane group g = lane >> 4). A K-tile needs
 // 8 A + 8 B fragments = 128 VGPRs -- exactly one set, no double buffer -- because the 64 MFMAs run
 // in quarter blocks that free half of the fragments early:
 //   slots  0..15  B0 x A0      B0 = b0..3, B1 = b4..7, A0 = a0..3, A1 = a4..7
@@ -281,6 +281,15 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
 // slot 63); B0, A0 of tile t+1 after their last use (slots RB0.., RA0..). Barriers: after the A1/B1
 // reads every wave is done with tile t (DMA of tile t+2 may overwrite it); before B0' the
 // landing wait for tile t+1.
+// Which two 16-byte chunks of a 128-byte K-row lane group g (= lane >> 4) holds, h = 0 / 1.
+// Any lane -> k map gives the same sums as long as A and B use the same one, so it is chosen
+// for the LDS banks: gfx950 serves a ds_read_b128 32 lanes at a time from 128 banks (512 B), so
+// the two lane groups of a pass (g = 0, 1 or 2, 3) must read chunks of opposite parity -- under the
+// (R >> 1) & 7 row swizzle, chunks 2g / 2g+1 (0 and 2 in one pass) put two lanes on every bank
+// (SQ_LDS_BANK_CONFLICT = half of SQ_LDS_IDX_ACTIVE, profiles/r3_pmc), chunks g / g+4 none (the
+// bf16 kernels' kk*4 + g pattern).
+#define F8Q_CHUNK(g, h) ((g) + 4 * (h))
+
 template <int I>
 __device__ __forceinline__ void f8q_mfma(const i32x8& b, const i32x8& a) {
   asm volatile("v_mfma_f32_16x16x128_f8f6f4 a[%c0:%c1], %2, %3, a[%c0:%c1]"
@@ -340,13 +349,13 @@ gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
                                                (uint32_t)rblk * 8u * (uint32_t)K + (uint32_t)k0, 0, 0);
   };
 
-  // the lane's two 16-byte chunks (2g, 2g+1) of row (lane & 15) of a 16-row fragment, swizzled
-  // as the DMA wrote them (chunk c of row R at c ^ ((R >> 1) & 7))
+  // the lane's two 16-byte chunks (g, g + 4) of row (lane & 15) of a 16-row fragment, swizzled as
+  // the DMA wrote them (chunk c of row R at c ^ ((R >> 1) & 7)); see F8Q_CHUNK
   int lane_off[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int r = lane & 15;
-    const int c = 2 * (lane >> 4) + h;
+    const int c = F8Q_CHUNK(lane >> 4, h);
     lane_off[h] = r * F8_ROW + ((c ^ ((r >> 1) & 7)) << 4);
   }
   const int a_off = wr * 128 * F8_ROW;
@@ -737,7 +746,7 @@ gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int r = lane & 15;
-    const int c = 2 * (lane >> 4) + h;
+    const int c = F8Q_CHUNK(lane >> 4, h);                 // (g, g + 4): conflict-free, see F8Q_CHUNK
     lane_off[h] = r * F8_ROW + ((c ^ ((r >> 1) & 7)) << 4);
   }
   const int a_off = wr * 128 * F8_ROW;

@@ -68,11 +68,14 @@ def _by_kind(objs):
 
 def test_chart_default_render():
     k = _by_kind(_objs())
-    assert set(k) == {"ServiceAccount", "ClusterRole", "ClusterRoleBinding", "Deployment", "ClusterPolicy", "Job"}
+    assert set(k) == {"ServiceAccount", "ClusterRole", "ClusterRoleBinding", "Deployment", "ClusterPolicy", "Job",
+                      # the vendored NFD subchart (nfd.enabled=true by default)
+                      "Role", "RoleBinding", "ConfigMap", "DaemonSet"}
+    assert "SecurityContextConstraints" not in k                    # OpenShift only
     pol = cp.ClusterPolicy(k["ClusterPolicy"][0], strict=True)
     assert pol.spec.driver.is_enabled() and pol.spec.operator.runtimeClass == "amd"
     assert pol.spec.metricsExporter.is_enabled() and not pol.spec.rdc.is_enabled()
-    dep = k["Deployment"][0]
+    dep = [d for d in k["Deployment"] if d["metadata"]["name"] == "amd-gpu-operator"][0]
     c = dep["spec"]["template"]["spec"]["containers"][0]
     env = {e["name"]: e.get("value") for e in c["env"]}
     assert env["DRIVER_IMAGE"] == "registry.example.com/amd/amdgpu-driver:6.12.12"
@@ -81,7 +84,7 @@ def test_chart_default_render():
     assert c["readinessProbe"]["httpGet"]["port"] == 8081
     hooks = [j["metadata"]["annotations"]["helm.sh/hook"] for j in k["Job"]]
     assert hooks == ["pre-upgrade"]
-    role = k["ClusterRole"][0]
+    role = [r for r in k["ClusterRole"] if r["metadata"]["name"] == "amd-gpu-operator"][0]
     assert any("clusterpolicies" in r["resources"] for r in role["rules"])
 
 
@@ -91,10 +94,11 @@ def test_chart_overrides():
                         "devicePlugin": {"config": {"create": True, "default": "ts",
                                                     "data": {"ts": "version: v1\n"}}},
                         "driver": {"usePrecompiled": True}}))
-    assert "--leader-elect" not in k["Deployment"][0]["spec"]["template"]["spec"]["containers"][0]["args"]
+    op = [d for d in k["Deployment"] if d["metadata"]["name"] == "amd-gpu-operator"][0]
+    assert "--leader-elect" not in op["spec"]["template"]["spec"]["containers"][0]["args"]
     assert sorted(j["metadata"]["annotations"]["helm.sh/hook"] for j in k["Job"]) == ["pre-delete", "pre-upgrade"]
     assert k["NodeFeatureRule"][0]["spec"]["rules"][0]["labels"]["amd.com/gpu.family.nfd"] == "cdna4"
-    cm = k["ConfigMap"][0]
+    cm = [m for m in k["ConfigMap"] if m["metadata"]["name"] == "amd-device-plugin-config"][0]
     assert cm["metadata"]["name"] == "amd-device-plugin-config" and cm["data"]["ts"].startswith("version")
     pol = cp.ClusterPolicy(k["ClusterPolicy"][0], strict=True)
     assert pol.spec.devicePlugin.config.name == "amd-device-plugin-config"
@@ -222,3 +226,48 @@ def test_convert_nvidia_policy(tmp_path):
 def test_check_registry_is_offline_safe():
     ok, why = cfg.check_registry("registry.invalid/amd/x:1", timeout=0.5)
     assert not ok and why
+
+
+# -- self-contained chart: vendored NFD subchart, Chart.lock, OpenShift SCC -----
+
+def test_chart_vendors_nfd_and_installs_offline():
+    with open(os.path.join(CHART, "Chart.yaml")) as f:
+        chart = yaml.safe_load(f)
+    with open(os.path.join(CHART, "Chart.lock")) as f:
+        lock = yaml.safe_load(f)
+    dep = chart["dependencies"][0]
+    with open(os.path.join(CHART, "charts", dep["name"], "Chart.yaml")) as f:
+        sub = yaml.safe_load(f)
+    assert sub["name"] == dep["name"] and sub["version"] == dep["version"]          # helm's presence check
+    assert dep["repository"].startswith("file://charts/")
+    assert lock["dependencies"] == [{k: dep[k] for k in ("name", "version", "repository")}]
+    assert lock["digest"] == gt.chart_lock_digest(chart["dependencies"], lock["dependencies"])
+    k = _by_kind(gt.render_objects(CHART, include_crds=True))
+    conf = [m for m in k["ConfigMap"] if m["metadata"]["name"].endswith("node-feature-discovery-worker-conf")][0]
+    worker_conf = yaml.safe_load(conf["data"]["nfd-worker.conf"])
+    wl = worker_conf["sources"]["pci"]["deviceClassWhitelist"]
+    assert "0380" in wl and "1200" in wl                  # AMD Instinct PF classes (MI300/MI355X)
+    ds = k["DaemonSet"][0]["spec"]["template"]["spec"]
+    assert any(t.get("key") == "amd.com/gpu" for t in ds["tolerations"])
+    crds = {c["metadata"]["name"] for c in k["CustomResourceDefinition"]}
+    assert {"nodefeatures.nfd.k8s-sigs.io", "nodefeaturerules.nfd.k8s-sigs.io", "clusterpolicies.amd.com"} <= crds
+    off = _by_kind(gt.render_objects(CHART, {"nfd": {"enabled": False}}))
+    assert "DaemonSet" not in off and not [d for d in off["Deployment"] if "node-feature" in d["metadata"]["name"]]
+
+
+def test_chart_lock_digest_matches_helm():
+    """The algorithm reproduces a digest Helm itself wrote: the reference's Chart.lock
+    (deployments/gpu-operator/Chart.lock:1-6 over Chart.yaml:19-23)."""
+    repo = "https://kubernetes-sigs.github.io/node-feature-discovery/charts"
+    req = [{"name": "node-feature-discovery", "version": "v0.13.1", "repository": repo, "condition": "nfd.enabled"}]
+    locked = [{"name": "node-feature-discovery", "version": "0.13.1", "repository": repo}]
+    assert gt.chart_lock_digest(req, locked) == \
+        "sha256:8cebf8838e987c231cec03a289deed636e644746464920f799caa35dbcf3bdc6"
+
+
+def test_operator_scc_renders_only_on_openshift():
+    assert "SecurityContextConstraints" not in _by_kind(_objs())
+    k = _by_kind(_objs({"platform": {"openshift": True}}))
+    scc = k["SecurityContextConstraints"][0]
+    assert scc["readOnlyRootFilesystem"] and not scc["allowPrivilegedContainer"] and not scc["allowHostPID"]
+    assert scc["users"] == ["system:serviceaccount:amd-gpu-operator:amd-gpu-operator"]

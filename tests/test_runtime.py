@@ -106,3 +106,34 @@ def test_leader_election_run_invokes_callback():
     assert started.is_set() and e.is_leader.is_set()
     e.stop()
     time.sleep(0.05)
+
+
+def test_aborted_scrape_logs_no_traceback(capfd, caplog):
+    """a client that resets the connection mid-response (an aborted
+    Prometheus scrape) is logged at debug level; socketserver's default handle_error printed a
+    traceback on stderr for every one."""
+    import logging
+    import socket
+    import struct
+    import time as _t
+    from gpu_operator_amd.runtime.manager import _Server
+    body = b"x" * (8 << 20)
+    srv = _Server(("127.0.0.1", 0), {"/metrics": lambda: (200, "text/plain", body)})
+    srv.start()
+    try:
+        with caplog.at_level(logging.DEBUG, logger="amd-gpu-operator.manager"):
+            for _ in range(3):
+                s = socket.create_connection(("127.0.0.1", srv.port))
+                s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
+                s.recv(1024)                                   # the response has started
+                s.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+                s.close()                                      # RST mid-body
+            s = socket.create_connection(("127.0.0.1", srv.port))
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+            s.close()                                          # RST before the request line
+            _t.sleep(0.5)
+    finally:
+        srv.stop()
+    err = capfd.readouterr().err
+    assert "Traceback" not in err and "ConnectionResetError" not in err and "BrokenPipeError" not in err, err
+    assert any("went away" in r.getMessage() for r in caplog.records)
