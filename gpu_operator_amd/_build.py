@@ -87,7 +87,8 @@ def _pyext_name(stem: str) -> str:
     return stem + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
 
 
-GEMM_HEADERS = ["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_fp8_kernels.h"]
+GEMM_HEADERS = ["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h",
+                "hip/gemm_fp8_kernels.h"]
 
 TARGETS: List[Target] = [
     # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.
@@ -118,9 +119,12 @@ TARGETS: List[Target] = [
 LAB_TARGETS: List[Target] = [
     # one library per dtype: an fp8 schedule edit rebuilds only the fp8 lab
     Target("libamdgo_gemm_lab_bf16.so", ["hip/gemm_bf16_lab.hip"], "hip-shared",
-           headers=["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h"]),
+           headers=["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h"]),
     Target("libamdgo_gemm_lab_fp8.so", ["hip/gemm_fp8_lab.hip"], "hip-shared",
            headers=["include/gemm_tile_common.h", "hip/gemm_fp8_kernels.h"]),
+    # the hand-scheduled bf16 K pipeline (w4a) next to v44 (tools/asm_lab.py)
+    Target("libamdgo_gemm_asmlab.so", ["hip/gemm_bf16_asm_lab.hip"], "hip-shared",
+           headers=["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h"]),
 ]
 
 

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""A/B of the hand-scheduled bf16 K pipeline (w4a, native/hip/gemm_bf16_asm_lab.hip) against the
+production v44 and hipBLASLt (torch.matmul), in one process, on the same uniform [-1, 1) data.
+
+1. exactness: every w4a variant's C is compared bit for bit with v44's (same MFMA order);
+2. timing: ``--rounds`` rounds; in each round every implementation is clock-stabilised (back-to-back
+   dispatches until 10 agree within 2 %, >= 30) and then ``--iters`` dispatches are timed between two
+   events. Prints one JSON line per (shape, round) and a best/median summary per shape.
+
+    python tools/asm_lab.py --shapes 8192,4096x4096x16384 --variants 44,100,101,102,103 --rounds 5
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="8192")
+    ap.add_argument("--variants", default="44,100,101,102,103")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--no-blas", action="store_true")
+    ap.add_argument("--one", default=None,
+                    help="profiling mode: dispatch only this variant ('blas' = hipBLASLt) --iters times, no checks")
+    a = ap.parse_args()
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+    lib = ctypes.CDLL(os.path.join(ROOT, "gpu_operator_amd", "_native", "libamdgo_gemm_asmlab.so"))
+    fn = lib.amdgo_asmlab_gemm_bf16
+    fn.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
+    dev = torch.device("cuda", 0)
+    variants = [int(v) for v in a.variants.split(",")]
+
+    def run(v, A, B, C):
+        err = fn(v, A.data_ptr(), B.data_ptr(), C.data_ptr(), A.shape[0], B.shape[0], A.shape[1],
+                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if err:
+            raise RuntimeError(f"variant {v}: hipError {err}")
+
+    for spec in a.shapes.split(","):
+        m, n, k = (int(x) for x in spec.split("x")) if "x" in spec else (int(spec),) * 3
+        A = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 11)
+        B = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 12)
+        if a.one is not None:                 # rocprofv3 --pmc target: the dispatches and nothing else
+            Cx = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+            Bt = B.t()
+            for _ in range(a.iters):
+                if a.one == "blas":
+                    torch.matmul(A, Bt, out=Cx)
+                else:
+                    run(int(a.one), A, B, Cx)
+            torch.cuda.synchronize()
+            continue
+        C = {v: torch.empty((m, n), dtype=torch.bfloat16, device=dev) for v in variants}
+        Cb = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+        ref = None
+        exact = {}
+        for v in variants:
+            run(v, A, B, C[v])
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = C[v]
+                chk = G.verify(A, B, C[v], nrows=16, seed=1)
+                exact["ref_check_ok"] = bool(chk.ok)
+            exact[v] = bool(torch.equal(C[v], ref))
+        print(json.dumps({"shape": spec, "bitwise_equal_to_first": exact}), flush=True)
+        impls = [(str(v), (lambda v=v: run(v, A, B, C[v]))) for v in variants]
+        if not a.no_blas:
+            Bt = B.t()
+            impls.append(("hipblaslt", lambda: torch.matmul(A, Bt, out=Cb)))
+        flop = 2.0 * m * n * k
+        res = {name: [] for name, _ in impls}
+        for r in range(a.rounds):
+            row = {}
+            for name, f in impls:
+                times = []
+                for _ in range(12):                       # stabilise: batches of 10
+                    evs = [torch.cuda.Event(enable_timing=True) for _ in range(11)]
+                    evs[0].record()
+                    for i in range(10):
+                        f()
+                        evs[i + 1].record()
+                    evs[-1].synchronize()
+                    times += [evs[i].elapsed_time(evs[i + 1]) for i in range(10)]
+                    last = sorted(times[-10:])
+                    if len(times) >= 30 and (last[-1] - last[0]) / last[5] < 0.02:
+                        break
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    f()
+                e1.record()
+                e1.synchronize()
+                tf = flop / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e12
+                res[name].append(tf)
+                row[name] = round(tf, 1)
+            print(json.dumps({"shape": spec, "round": r, "tflops": row}), flush=True)
+        summ = {name: {"best": round(max(v), 1), "median": round(statistics.median(v), 1)} for name, v in res.items()}
+        if "hipblaslt" in res:
+            for name in res:
+                summ[name]["ratio_vs_hipblaslt_median"] = round(statistics.median(res[name]) /
+                                                                statistics.median(res["hipblaslt"]), 4)
+        print(json.dumps({"shape": spec, "summary": summ}), flush=True)
+        del A, B, C, Cb
+
+
+if __name__ == "__main__":
+    main()

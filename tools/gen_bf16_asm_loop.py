@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Generate the hand-scheduled K-loop of the bf16 256x256 GEMM (native/hip/gemm_bf16_asm_loop.h).
+
+The production w4s kernel's K-tile schedule (v18: 128 MFMA slots per K-tile, fragment reads,
+16 LDS-DMA pieces, two barriers) is written as C++ that hipcc schedules; what hipcc adds
+around it -- SALU address arithmetic per DMA piece, an ``s_nop 0`` before each piece, lgkmcnt
+ladders, register moves at the back-edge -- is the part of the instruction stream the source
+cannot control (profiles/r2_sched/README.md). Here the whole K pipeline of one workgroup tile
+(prologue DMA of K-tiles 0 and 1, the steady-state loop unrolled over the two LDS buffers, the
+two-tile drain) is one ``asm volatile`` block with physical registers:
+
+  a[0:255]   accumulators (acc m*8+n = a[4(m*8+n) : +3], the w4s layout, read by its epilogue)
+  v[0:63]    R0 = A fragments a0..a7 (v[0:31]) and B fragments b0..b7 (v[32:63]), k-half 0
+  v[64:127]  R1 = the same for k-half 1
+  M0         LDS-DMA destination, advanced 4 KiB per piece (piece p of a wave lands at
+             buffer + p * 4096 + wid * 1024: A pieces 0-7, B pieces 8-15)
+
+and the schedule is data (SCHEDULES below): in MFMA slot i of a K-tile the gap after MFMA i holds
+the ops listed for i. Every gap is kept to <= 2 single-issue instructions (one wave per SIMD: a
+16x16x32 bf16 MFMA leaves 8 of its 16 issue cycles, ~4 per instruction; MI355X_MICROARCH.md).
+Waits are explicit and counted:
+  * lgkmcnt(0) before the "free" barrier: this wave's reads of tile t are done;
+  * vmcnt(n) before the "landed" barrier, n = pieces this K-tile has issued so far: tile t+1's 16
+    pieces (issued one K-tile earlier) have landed in LDS for this wave, the barrier makes that
+    true for all four waves;
+  * lgkmcnt(0) at the end of the K-tile: the next tile's k-half-0 fragments are in registers.
+The MFMA order, operands and accumulators are those of w4s, so results are bitwise identical to
+it (tests/test_gemm_gpu.py checks that).
+
+    python tools/gen_bf16_asm_loop.py          # rewrites native/hip/gemm_bf16_asm_loop.h
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "native", "hip", "gemm_bf16_asm_loop.h")
+
+SLOTS = 128
+PIECE_STRIDE = 0x1000
+
+
+def frag_regs(r: int, isb: bool, x: int) -> str:
+    base = 64 * r + (32 if isb else 0) + 4 * x
+    return f"v[{base}:{base + 3}]"
+
+
+def read_order(j: int):
+    """Read j of a fragment set in consumption order: a0, b0..b7, a1..a7 -> (isb, index)."""
+    if j == 0:
+        return False, 0
+    if j <= 8:
+        return True, j - 1
+    return False, j - 8
+
+
+def mfma(i: int) -> str:
+    r, s = (0, i) if i < 64 else (1, i - 64)
+    acc = s                                   # accumulator m*8+n with m = s >> 3, n = s & 7
+    return (f"v_mfma_f32_16x16x32_bf16 a[{4 * acc}:{4 * acc + 3}], {frag_regs(r, True, s & 7)}, "
+            f"{frag_regs(r, False, s >> 3)}, a[{4 * acc}:{4 * acc + 3}]")
+
+
+class Schedule:
+    """Slot positions of one K-tile (see the module docstring)."""
+
+    def __init__(self, name, r1, w1, b1, dma, m0_lead, w2, b2, r0, vk, w3):
+        self.name = name
+        self.r1 = r1            # slot of R1 read j (k-half 1 of tile t), j = 0..15
+        self.w1, self.b1 = w1, b1   # lgkmcnt(0) slot, free barrier slot
+        self.dma = dma          # slot of DMA piece p (p = 0..15)
+        self.m0_lead = m0_lead  # the M0 update for piece p goes this many slots before it (>= 1)
+        self.w2, self.b2 = w2, b2   # landing vmcnt slot, landing barrier slot
+        self.r0 = r0            # slot of R0 read j (k-half 0 of tile t+1)
+        self.vk = vk            # slot of the K-offset add after the last piece
+        self.w3 = w3            # lgkmcnt(0) slot (the next tile's R0 landed)
+
+    def issued_before_w2(self) -> int:
+        return sum(1 for s in self.dma if s <= self.w2)
+
+
+def make(name, r1=(0, 1), dma=(19, 5), w2=79, r0=(81, 2), w3=126, vk=None):
+    """A schedule from arithmetic progressions: R1 reads j at r1[0] + j*r1[1] (then lgkmcnt(0) and
+    the free barrier right after the last one), DMA piece p at dma[0] + p*dma[1], the landing wait at
+    w2 and its barrier at w2 + 1, R0 reads j at r0[0] + j*r0[1]."""
+    r1s = [r1[0] + j * r1[1] for j in range(16)]
+    w1 = r1s[-1] + 1
+    ds = [dma[0] + p * dma[1] for p in range(16)]
+    r0s = [r0[0] + j * r0[1] for j in range(16)]
+    sc = Schedule(name, r1=r1s, w1=w1, b1=w1 + 1, dma=ds, m0_lead=1, w2=w2, b2=w2 + 1, r0=r0s,
+                  vk=vk if vk is not None else ds[-1] + 2, w3=w3)
+    validate(sc)
+    return sc
+
+
+def validate(sc: "Schedule") -> None:
+    """The protocol's ordering constraints (module docstring) and <= 2 fillers per gap."""
+    assert all(0 <= x < SLOTS for x in sc.r1 + sc.dma + sc.r0 + [sc.w1, sc.b1, sc.w2, sc.b2, sc.vk, sc.w3]), sc.name
+    assert sc.w1 > max(sc.r1) and sc.w1 < 64 and sc.b1 > sc.w1, sc.name           # R1 in before MFMA 64
+    assert min(sc.dma) - sc.m0_lead >= 0 and min(sc.dma) > sc.b1, sc.name          # DMA after the free barrier
+    assert sc.b2 > sc.w2 and min(sc.r0) > sc.b2 and min(sc.r0) >= 64, sc.name      # R0 regs dead after MFMA 63
+    assert max(sc.r0) < sc.w3 < SLOTS and sc.vk > max(sc.dma), sc.name
+    load = {i: 0 for i in range(SLOTS)}
+    for x in sc.r1 + sc.r0 + sc.dma + [d - sc.m0_lead for d in sc.dma] + [sc.w1, sc.b1, sc.w2, sc.b2, sc.vk, sc.w3]:
+        load[x] += 1
+    assert max(load.values()) <= 2, (sc.name, {k: v for k, v in load.items() if v > 2})
+
+
+SCHEDULES = {
+    # v18's placement (the production w4s kernel): R1 burst at slots 0-15, barrier at 17, DMA every
+    # 5th slot from 19, landing barrier at 80, R0 reads every 2nd slot from 81.
+    "v18": make("v18"),
+    # R1 reads every other slot (half the LDS read burst), DMA from slot 35 every 4th
+    "spread": make("spread", r1=(0, 2), dma=(35, 4), w2=99, r0=(101, 1)),
+    # DMA pieces early and dense after the free barrier (more landing time), R0 reads late
+    "early": make("early", dma=(18, 3), w2=68, r0=(71, 3)),
+    "spread3": make("spread3", r1=(0, 3), dma=(48, 4), w2=100, r0=(102, 1)),
+    "spread_d5": make("spread_d5", r1=(0, 2), dma=(34, 5), w2=96, r0=(98, 1)),
+    "v18_r1": make("v18_r1", r0=(81, 1)),
+    "v18_d4": make("v18_d4", dma=(19, 4), w2=80, r0=(82, 2)),
+    "late_land": make("late_land", dma=(18, 3), w2=100, r0=(102, 1)),
+    "v18_d6": make("v18_d6", dma=(19, 6), w2=98, r0=(100, 1)),
+    "v18_d6b": make("v18_d6b", dma=(19, 6), w2=80, r0=(82, 2)),
+    "v18_d5_late": make("v18_d5_late", w2=96, r0=(98, 1)),
+}
+
+
+# schedules the persistent kernel is generated for (its SC index = position here)
+PERSISTENT = ["v18", "v18_d6b", "v18_d5_late"]
+
+
+def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) -> List[str]:
+    """One K-tile: MFMAs on tile t (buffer ``cur``), R1 reads from ``cur``, DMA of tile t+2 into
+    ``cur``, R0 reads of tile t+1 from the other buffer. ``nxt_tile``: the DMA fetches the next
+    output tile's K-tile instead (persistent kernel drain: operands nA / nB / nvoff / nkstep)."""
+    rA, rB, voff, kstep = ("%[nA]", "%[nB]", "%[nvoff]", "%[nkstep]") if nxt_tile else \
+        ("%[rA]", "%[rB]", "%[voff]", "%[kstep]")
+    nxt = 1 - cur
+    gap: Dict[int, List[str]] = {i: [] for i in range(SLOTS)}
+    for j, s in enumerate(sc.r1):
+        isb, x = read_order(j)
+        gap[s].append(f"ds_read_b128 {frag_regs(1, isb, x)}, %[{'rb' if isb else 'ra'}{cur}1] offset:{x * 2048}")
+    gap[sc.w1].append("s_waitcnt lgkmcnt(0)")
+    gap[sc.b1].append("s_barrier")
+    if dma:
+        for p, s in enumerate(sc.dma):
+            lead = s - sc.m0_lead
+            gap[lead].append(f"s_mov_b32 m0, %[m0b{cur}]" if p == 0 else f"s_add_u32 m0, m0, {PIECE_STRIDE:#x}")
+            gap[s].append(f"buffer_load_dwordx4 {voff}, {rB if p >= 8 else rA}, %[s{p & 7}] offen lds")
+        gap[sc.vk].append(f"v_add_u32_e32 {voff}, {kstep}, {voff}")
+    if nx:
+        n = sc.issued_before_w2() if dma else 0
+        gap[sc.w2].append(f"s_waitcnt vmcnt({n})")
+        gap[sc.b2].append("s_barrier")
+        for j, s in enumerate(sc.r0):
+            isb, x = read_order(j)
+            gap[s].append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}{nxt}0] offset:{x * 2048}")
+        gap[sc.w3].append("s_waitcnt lgkmcnt(0)")
+    out = []
+    for i in range(SLOTS):
+        out.append(mfma(i))
+        out += gap[i]
+    return out
+
+
+def prologue() -> List[str]:
+    """DMA K-tiles 0 and 1 into buffers 0 and 1, wait for tile 0, read its k-half 0."""
+    out = ["s_nop 4"]                 # SGPR operands fresh from readfirstlane -> buffer descriptor use
+    for buf in (0, 1):
+        for p in range(16):
+            out.append(f"s_mov_b32 m0, %[m0b{buf}]" if p == 0 else f"s_add_u32 m0, m0, {PIECE_STRIDE:#x}")
+            out.append("s_nop 0")     # M0 write -> LDS-DMA
+            out.append(f"buffer_load_dwordx4 %[voff], %[{'rB' if p >= 8 else 'rA'}], %[s{p & 7}] offen lds")
+        out.append("v_add_u32_e32 %[voff], %[kstep], %[voff]")
+    out += ["s_waitcnt vmcnt(16)", "s_barrier"]
+    for j in range(16):
+        isb, x = read_order(j)
+        out.append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}00] offset:{x * 2048}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    return out
+
+
+def kloop(sc: Schedule) -> List[str]:
+    out = prologue()
+    out.append(".Lw4a_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4a_loop_%="]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    return out
+
+
+def kloop_persistent(sc: Schedule) -> List[str]:
+    """The K pipeline of one output tile of the persistent kernel (w4ap). Uniform branches on
+    %[flags] bit 0 (this workgroup's first tile: issue K-tiles 0 and 1 here; later tiles had them
+    issued by the previous tile's drain and retired by its epilogue) and bit 1 (a next tile: drain
+    with its K-tiles 0 and 1 DMA'd into the buffers as they free up, else the plain drain)."""
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lw4ap_entry_%="]
+    out += [x for x in prologue() if not x.startswith("ds_read") and x != "s_waitcnt lgkmcnt(0)"
+            and x != "s_barrier"]
+    out.append(".Lw4ap_entry_%=:")
+    out.append("s_barrier")
+    for j in range(16):
+        isb, x = read_order(j)
+        out.append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}00] offset:{x * 2048}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    out.append(".Lw4ap_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4ap_loop_%="]
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lw4ap_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True)
+    out += body(sc, 1, dma=True, nx=False, nxt_tile=True)
+    out += ["s_branch .Lw4ap_done_%=", ".Lw4ap_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    out.append(".Lw4ap_done_%=:")
+    return out
+
+
+def audit(lines: List[str]) -> Dict[str, int]:
+    gaps, cur, worst = [], 0, 0
+    for ln in lines:
+        if ln.startswith("v_mfma"):
+            gaps.append(cur)
+            cur = 0
+        elif not ln.startswith("."):
+            cur += 1
+    return {"max_fillers_per_gap": max(gaps[1:]), "mfmas": sum(ln.startswith("v_mfma") for ln in lines)}
+
+
+def render() -> str:
+    parts = ["// GENERATED by tools/gen_bf16_asm_loop.py -- do not edit by hand.",
+             "// The hand-scheduled K pipeline of gemm_bf16_256x256_w4a (gemm_bf16_kernels.h): one asm",
+             "// string per schedule; operands are named in gemm_bf16_kernels.h (W4A_LOOP).",
+             "#pragma once", ""]
+    sel = []
+    for idx, (name, sc) in enumerate(SCHEDULES.items()):
+        sel.append(f"if constexpr (SC == {idx}) W4A_LOOP(W4A_ASM_{name.upper()});")
+    parts.append("// schedule index -> asm text (SC template parameter of gemm_bf16_256x256_w4a)")
+    parts.append("#define W4A_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(sel))
+    parts.append("")
+    parts.append("// " + ", ".join(f"{i} = {n}" for i, n in enumerate(SCHEDULES)))
+    parts.append("")
+    psel = [f"if constexpr (SC == {i}) W4AP_LOOP(W4AP_ASM_{n.upper()});" for i, n in enumerate(PERSISTENT)]
+    parts.append("// persistent kernel (gemm_bf16_256x256_w4ap): schedule index -> asm text")
+    parts.append("#define W4AP_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(psel))
+    parts.append("// " + ", ".join(f"{i} = {n}" for i, n in enumerate(PERSISTENT)))
+    parts.append("")
+    for name in PERSISTENT:
+        lines = kloop_persistent(SCHEDULES[name])
+        parts.append(f"#define W4AP_ASM_{name.upper()} \\")
+        for ln in lines:
+            parts.append(f'  "{ln}\\n\\t" \\')
+        parts.append('  ""')
+        parts.append("")
+    for name, sc in SCHEDULES.items():
+        lines = kloop(sc)
+        a = audit(lines)
+        parts.append(f"// {name}: {a['mfmas']} MFMAs per tile pipeline text, <= {a['max_fillers_per_gap']} "
+                     f"instructions per MFMA gap")
+        parts.append(f"#define W4A_ASM_{name.upper()} \\")
+        for ln in lines:
+            parts.append(f'  "{ln}\\n\\t" \\')
+        parts.append('  ""')
+        parts.append("")
+    return "\n".join(parts)
+
+
+if __name__ == "__main__":
+    with open(OUT, "w") as f:
+        f.write(render())
+    print(f"wrote {OUT}")
