@@ -31,6 +31,9 @@
 
 #include "gemm_bf16_kernels.h"
 
+// v50's K-tile schedule: index into W4AP_LOOP_SELECT (gemm_bf16_asm_loop.h)
+#define W4AP_PRODUCTION_SC 2
+
 static int g_variant = 0;
 
 // Persistent grid: one workgroup per CU (the 160 KiB LDS admits one), a multiple of the 8 XCDs,
@@ -63,6 +66,8 @@ static int resolve_variant(int M, int N, int K) {
   if (v == 48 && !sq) v = 47;
   if ((v == 47 || v == 48) && cus != 256) v = 42;
   if (v == 25 && persistent_grid(nwg) < NXCD) v = 44;
+  // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups
+  if (v == 50 && (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg) < NXCD)) v = 44;
   if ((v == 44 || v == 45) && cus != 256) v = 42;       // serpentine K assumes 32 co-resident WGs / XCD
   // K not a power of two: A-panel DMA instructions read rows 32 apart (PA, v47 / v48). At a 24 KiB
   // row stride adjacent rows cost 8-11 % (12288^3 1405 -> 1557 TF, 8192^2x12288 1457 -> 1579,
@@ -79,7 +84,7 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
-  if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48)
+  if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50)
     return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
@@ -123,6 +128,10 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
     case 45:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true>), dim3(nwg), dim3(W4_THREADS),
                          0, s, a, b, c, M, N, K);
+      break;
+    case 50:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_PRODUCTION_SC, true>), dim3(persistent_grid(nwg)),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {
       dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);

@@ -37,6 +37,8 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4A_CASE(108, 8, 32)
     W4A_CASE(109, 9, 32)
     W4A_CASE(110, 10, 32)
+    W4A_CASE(111, 11, 32)
+    W4A_CASE(112, 12, 32)
     W4A_CASE(120, 0, 0)
 #define W4AP_CASE(V, SC, SERP)                                                                             \
     case V: {                                                                                             \
@@ -49,6 +51,16 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4AP_CASE(131, 1, true)
     W4AP_CASE(132, 2, true)
     W4AP_CASE(133, 0, false)
+    W4AP_CASE(134, 3, true)
+    W4AP_CASE(135, 4, true)
+    W4AP_CASE(136, 5, true)
+    W4AP_CASE(137, 6, true)
+    W4AP_CASE(138, 7, true)
+    W4AP_CASE(139, 8, true)
+    W4AP_CASE(140, 9, true)
+    W4AP_CASE(141, 10, true)
+    W4AP_CASE(142, 11, true)
+    W4AP_CASE(143, 12, true)
     default:
       return (int)hipErrorInvalidValue;
   }

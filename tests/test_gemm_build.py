@@ -59,7 +59,8 @@ def asm_lab(tmp_path_factory):
 @pytest.fixture(scope="module", params=["production", "lab"])
 def w4(request):
     asm = request.getfixturevalue("asm" if request.param == "production" else "asm_lab")
-    return _kernels(asm, "gemm_bf16_256x256_w4")
+    # the hand-scheduled asm K pipeline (w4a/w4ap) has no compiler loop: audited separately below
+    return [k for k in _kernels(asm, "gemm_bf16_256x256_w4") if not re.match(r"\w*w4ap?I", k[0])]
 
 
 def test_production_library_kernel_set(asm):
@@ -169,6 +170,41 @@ def test_w4_accumulators_pinned(w4):
         # w4sp adds its peeled first iteration of every tile
         name = body.split(":", 1)[0]
         assert len(re.findall(r"v_mfma_f32_16x16x32_bf16", body)) == (8 if "w4sp" in name else 6) * 64
+
+
+def _audit_asm_pipeline(body, st):
+    assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+    assert st["NumVgprs"] <= 256, st
+    _no_compiler_agpr_access(body)
+    mfma = len(re.findall(r"v_mfma_f32_16x16x32_bf16", body))
+    reads = body.count("ds_read_b128")
+    dma = len(re.findall(r"buffer_load_dwordx4 .* lds", body))
+    # every K-tile in the asm block is 128 MFMAs fed by 32 fragment reads and 16 LDS-DMA pieces;
+    # the persistent form adds the epilogue reads of the next tile's prologue
+    assert mfma % 128 == 0 and mfma >= 3 * 128, mfma
+    assert reads >= 32 * (mfma // 128) and dma >= 16 * (mfma // 128 - 2), (reads, dma)
+    # the loop itself is one asm block: hipcc inserted no hazard padding into it
+    for blk in re.findall(r";;#ASMSTART(.*?);;#ASMEND", body, re.S):
+        if blk.count("v_mfma") >= 128:
+            assert "s_cbranch" in blk and "s_barrier" in blk
+    return mfma
+
+
+def test_w4ap_production_pipeline(asm):
+    """Production v50: the persistent asm K pipeline, one instantiation (W4AP_PRODUCTION_SC)."""
+    kernels = _kernels(asm, "gemm_bf16_256x256_w4apI")
+    assert len(kernels) == 1
+    body, st = kernels[0]
+    assert _audit_asm_pipeline(body, st) == 6 * 128
+
+
+def test_w4a_lab_pipelines(tmp_path_factory):
+    """Every lab schedule of the asm K pipeline keeps the same register/occupancy contract."""
+    asm = _compile(tmp_path_factory, "gemm_bf16_asm_lab.hip")
+    kernels = _kernels(asm, "gemm_bf16_256x256_w4a")
+    assert len(kernels) >= 10
+    for body, st in kernels:
+        _audit_asm_pipeline(body, st)
 
 
 def test_w4_main_loop_shape(w4):

@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -136,3 +136,26 @@ def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
         want = {44: 42, 45: 42, 47: 42, 48: 42}.get(want, want)
     assert G.get_variant() == 0
     assert G.resolve_variant(m, n, k) == want
+
+
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (4096, 4096, 4096), (2048, 4096, 512)])
+def test_asm_pipeline_is_bitwise_v44(cuda_device, m, n, k):
+    """v50 (the hand-scheduled asm K pipeline, persistent) issues the MFMAs of v44 in the same
+    per-accumulator order, with the same serpentine K per dispatch wave: the outputs are equal bit
+    for bit, not only within tolerance."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    a = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=cuda_device), 5)
+    bt = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=cuda_device), 6)
+    old = G.get_variant()
+    try:
+        G.set_variant(44)
+        c44 = G.gemm_bf16(a, bt)
+        G.set_variant(50)
+        assert G.resolve_variant(m, n, k) == 50
+        c50 = G.gemm_bf16(a, bt)
+    finally:
+        G.set_variant(old)
+    torch.cuda.synchronize()
+    assert torch.equal(c44, c50)

@@ -20,6 +20,50 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+class PowerMeter:
+    """Average shader clock and socket power over a timed window, sampled from the PMFW gpu_metrics
+    table (devices.read_gpu_metrics) every millisecond by a thread; None where it is unreadable."""
+
+    def __init__(self):
+        import threading
+        self.threading = threading
+        try:
+            from gpu_operator_amd import devices
+            self.read = lambda: devices.read_gpu_metrics("/")[0]
+            self.read()
+        except Exception:  # noqa: BLE001 - diagnostics only
+            self.read = None
+
+    def start(self):
+        if self.read is None:
+            return
+        self.samples, self.stop_ev = [], self.threading.Event()
+
+        def loop():
+            while not self.stop_ev.is_set():
+                try:
+                    m = self.read()
+                    clk = [c for c in m["gfxclk_mhz"] if c > 0] if isinstance(m["gfxclk_mhz"], list) else [m["gfxclk_mhz"]]
+                    if clk:
+                        self.samples.append((sum(clk) / len(clk), m["socket_power_w"]))
+                except Exception:  # noqa: BLE001
+                    pass
+                self.stop_ev.wait(0.001)
+        self.t = self.threading.Thread(target=loop, daemon=True)
+        self.t.start()
+
+    def stop(self):
+        if self.read is None:
+            return None
+        self.stop_ev.set()
+        self.t.join()
+        s = [x for x in self.samples if x[0] > 0]
+        if not s:
+            return None
+        return {"gfxclk_mhz": round(sum(x[0] for x in s) / len(s)), "socket_w": round(sum(x[1] for x in s) / len(s), 1),
+                "samples": len(s)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="8192")
@@ -37,6 +81,7 @@ def main():
     fn.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in a.variants.split(",")]
+    pm = PowerMeter()
 
     def run(v, A, B, C):
         err = fn(v, A.data_ptr(), B.data_ptr(), C.data_ptr(), A.shape[0], B.shape[0], A.shape[1],
@@ -77,8 +122,9 @@ def main():
             impls.append(("hipblaslt", lambda: torch.matmul(A, Bt, out=Cb)))
         flop = 2.0 * m * n * k
         res = {name: [] for name, _ in impls}
+        power = {}
         for r in range(a.rounds):
-            row = {}
+            row, prow = {}, {}
             for name, f in impls:
                 times = []
                 for _ in range(12):                       # stabilise: batches of 10
@@ -93,20 +139,30 @@ def main():
                     if len(times) >= 30 and (last[-1] - last[0]) / last[5] < 0.02:
                         break
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                pm.start()
                 e0.record()
                 for _ in range(a.iters):
                     f()
                 e1.record()
                 e1.synchronize()
+                pw = pm.stop()
                 tf = flop / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e12
                 res[name].append(tf)
                 row[name] = round(tf, 1)
-            print(json.dumps({"shape": spec, "round": r, "tflops": row}), flush=True)
+                if pw:
+                    power.setdefault(name, []).append(pw)
+                    prow[name] = pw
+            print(json.dumps({"shape": spec, "round": r, "tflops": row, "power": prow}), flush=True)
         summ = {name: {"best": round(max(v), 1), "median": round(statistics.median(v), 1)} for name, v in res.items()}
         if "hipblaslt" in res:
             for name in res:
                 summ[name]["ratio_vs_hipblaslt_median"] = round(statistics.median(res[name]) /
                                                                 statistics.median(res["hipblaslt"]), 4)
+        for name, pws in power.items():
+            summ[name]["gfxclk_mhz"] = round(statistics.median(p["gfxclk_mhz"] for p in pws))
+            summ[name]["socket_w"] = round(statistics.median(p["socket_w"] for p in pws), 1)
+            summ[name]["mj_per_gemm"] = round(statistics.median(p["socket_w"] for p in pws) * flop
+                                              / (statistics.median(res[name]) * 1e12) * 1e3, 3)
         print(json.dumps({"shape": spec, "summary": summ}), flush=True)
         del A, B, C, Cb
 

@@ -55,18 +55,23 @@ def read_order(j: int):
     return False, j - 8
 
 
-def mfma(i: int) -> str:
+def mfma(i: int, bout: bool = False) -> str:
+    """MFMA slot i: k-half i >> 6; A-outer (m = s >> 3, n = s & 7: the A fragment stays in srcB for
+    8 MFMAs) or B-outer (n = s >> 3, m = s & 7: the B fragment stays in srcA for 8 MFMAs). Each
+    accumulator m*8+n gets the same k sequence either way, so the results are identical."""
     r, s = (0, i) if i < 64 else (1, i - 64)
-    acc = s                                   # accumulator m*8+n with m = s >> 3, n = s & 7
-    return (f"v_mfma_f32_16x16x32_bf16 a[{4 * acc}:{4 * acc + 3}], {frag_regs(r, True, s & 7)}, "
-            f"{frag_regs(r, False, s >> 3)}, a[{4 * acc}:{4 * acc + 3}]")
+    m, n = (s & 7, s >> 3) if bout else (s >> 3, s & 7)
+    acc = m * 8 + n
+    return (f"v_mfma_f32_16x16x32_bf16 a[{4 * acc}:{4 * acc + 3}], {frag_regs(r, True, n)}, "
+            f"{frag_regs(r, False, m)}, a[{4 * acc}:{4 * acc + 3}]")
 
 
 class Schedule:
     """Slot positions of one K-tile (see the module docstring)."""
 
-    def __init__(self, name, r1, w1, b1, dma, m0_lead, w2, b2, r0, vk, w3):
+    def __init__(self, name, r1, w1, b1, dma, m0_lead, w2, b2, r0, vk, w3, bout=False):
         self.name = name
+        self.bout = bout        # B-outer MFMA order (see mfma())
         self.r1 = r1            # slot of R1 read j (k-half 1 of tile t), j = 0..15
         self.w1, self.b1 = w1, b1   # lgkmcnt(0) slot, free barrier slot
         self.dma = dma          # slot of DMA piece p (p = 0..15)
@@ -80,16 +85,16 @@ class Schedule:
         return sum(1 for s in self.dma if s <= self.w2)
 
 
-def make(name, r1=(0, 1), dma=(19, 5), w2=79, r0=(81, 2), w3=126, vk=None):
+def make(name, r1=(0, 1), dma=(19, 5), w2=79, r0=(81, 2), w3=126, vk=None, bout=False, w1_gap=1):
     """A schedule from arithmetic progressions: R1 reads j at r1[0] + j*r1[1] (then lgkmcnt(0) and
     the free barrier right after the last one), DMA piece p at dma[0] + p*dma[1], the landing wait at
     w2 and its barrier at w2 + 1, R0 reads j at r0[0] + j*r0[1]."""
     r1s = [r1[0] + j * r1[1] for j in range(16)]
-    w1 = r1s[-1] + 1
+    w1 = r1s[-1] + w1_gap                  # lgkmcnt(0): w1_gap MFMAs after the last R1 read
     ds = [dma[0] + p * dma[1] for p in range(16)]
     r0s = [r0[0] + j * r0[1] for j in range(16)]
     sc = Schedule(name, r1=r1s, w1=w1, b1=w1 + 1, dma=ds, m0_lead=1, w2=w2, b2=w2 + 1, r0=r0s,
-                  vk=vk if vk is not None else ds[-1] + 2, w3=w3)
+                  vk=vk if vk is not None else ds[-1] + 2, w3=w3, bout=bout)
     validate(sc)
     return sc
 
@@ -123,11 +128,25 @@ SCHEDULES = {
     "v18_d6": make("v18_d6", dma=(19, 6), w2=98, r0=(100, 1)),
     "v18_d6b": make("v18_d6b", dma=(19, 6), w2=80, r0=(82, 2)),
     "v18_d5_late": make("v18_d5_late", w2=96, r0=(98, 1)),
+    # the same placements with the B fragment held in srcA across 8 MFMAs (hipBLASLt's order)
+    "v18_d6b_bout": make("v18_d6b_bout", dma=(19, 6), w2=80, r0=(82, 2), bout=True),
+    "v18_d5_late_bout": make("v18_d5_late_bout", w2=96, r0=(98, 1), bout=True),
+    # the R1 reads' lgkmcnt(0) a few MFMAs after the last read (the LDS latency under the read
+    # burst of all four waves), then the free barrier and the DMA
+    "g4": make("g4", w1_gap=4, dma=(22, 5), w2=98, r0=(100, 1)),
+    "g6": make("g6", w1_gap=6, dma=(24, 5), w2=100, r0=(102, 1)),
+    "g8": make("g8", w1_gap=8, dma=(26, 5), w2=102, r0=(104, 1)),
+    "sp2g6": make("sp2g6", r1=(0, 2), w1_gap=6, dma=(39, 4), w2=100, r0=(102, 1)),
+    "g6d6": make("g6d6", w1_gap=6, dma=(24, 6), w2=86, r0=(88, 2)),
+    "g4d6": make("g4d6", w1_gap=4, dma=(22, 6), w2=86, r0=(88, 2)),
+    "g2d6": make("g2d6", w1_gap=2, dma=(20, 6), w2=84, r0=(86, 2)),
+    "sp2g4d5": make("sp2g4d5", r1=(0, 2), w1_gap=4, dma=(37, 5), w2=100, r0=(102, 1)),
 }
 
 
 # schedules the persistent kernel is generated for (its SC index = position here)
-PERSISTENT = ["v18", "v18_d6b", "v18_d5_late"]
+PERSISTENT = ["v18", "v18_d6b", "v18_d5_late", "v18_d6b_bout", "v18_d5_late_bout", "g4", "g6", "g8", "sp2g6",
+              "g6d6", "g4d6", "g2d6", "sp2g4d5"]
 
 
 def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) -> List[str]:
@@ -159,7 +178,7 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) ->
         gap[sc.w3].append("s_waitcnt lgkmcnt(0)")
     out = []
     for i in range(SLOTS):
-        out.append(mfma(i))
+        out.append(mfma(i, sc.bout))
         out += gap[i]
     return out
 
