@@ -19,10 +19,15 @@
 // Only numerically exact, measured production kernels are reachable from here. The variant is an
 // API argument (amdgo_gemm_set_variant), never read from the environment; superseded generations
 // and knock-out timings live in the tools-only gemm_bf16_lab.hip.
-//   0  = automatic (default): v44; v25 for K <= 4096 with >= 2 tiles per CU; v45 for >= 8 dispatch
-//        waves with K >= 8192 on 16x16-tile multiples; v42 / v18 on devices without 256 CUs.
+//   0  = automatic (default): on the 256-CU MI355X with a power-of-two K >= 256, the persistent asm
+//        K pipeline -- v50, v51 (square raster: >= 8 dispatch waves, K >= 8192, 16x16-tile
+//        multiples), v52 (one or two dispatch waves, K >= 8192); otherwise v44, v25 for K <= 4096
+//        with >= 2 tiles per CU, v45 for >= 8 dispatch waves with K >= 8192 on 16x16-tile
+//        multiples; v42 / v18 on devices without 256 CUs.
 //   47 / 48 = v44 / v45 with permuted A-panel DMA rows (PA), the default when K is not a power of two.
-//   18 / 25 / 42 / 44 / 45 / 47 / 48 = that kernel pinned (no automatic switch; still falls back to a kernel
+//   50 / 51 / 52 = the asm pipeline: w4ap (gemm_bf16_kernels.h) with the g4 schedule, g4 on the square
+//        raster, the g6d6 schedule (tools/gen_bf16_asm_loop.py generates gemm_bf16_asm_loop.h).
+//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
 // Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
 // add per K-tile, loop-invariant soffsets; 17 fewer SALU per K-tile, +0.6-0.8 % at 8192^3 and
@@ -31,8 +36,13 @@
 
 #include "gemm_bf16_kernels.h"
 
-// v50's K-tile schedule: index into W4AP_LOOP_SELECT (gemm_bf16_asm_loop.h)
-#define W4AP_PRODUCTION_SC 2
+// K-tile schedules of the persistent asm pipeline (gemm_bf16_asm_loop.h, tools/gen_bf16_asm_loop.py):
+// g4 waits for the last R1 fragment read 4 MFMAs after it is issued (not 1), which takes the
+// lgkmcnt stall out of the free barrier; g6d6 also spaces the DMA pieces 6 MFMAs apart, which
+// spreads the HBM requests of a one-wave grid whose workgroups run in lockstep.
+// profiles/r3_asm/asm8_summary.jsonl, asm9_summary.jsonl
+#define W4AP_SC_MAIN W4AP_SC_G4
+#define W4AP_SC_LONGK W4AP_SC_G6D6
 
 static int g_variant = 0;
 
@@ -51,7 +61,17 @@ static int resolve_variant(int M, int N, int K) {
   const int cus = device_cu_count();
   const bool sq = (M / BM) % 16 == 0 && (N / BN) % 16 == 0;
   int v = g_variant;
-  if (v == 0) {
+  const bool pow2k = (K & (K - 1)) == 0;
+  if (v == 0 && cus == 256 && pow2k && K >= 4 * BK && persistent_grid(nwg) >= NXCD) {
+    // The hand-scheduled asm K pipeline, persistent (profiles/r3_asm/): v50 everywhere it runs,
+    // ahead of v44 and v25 on every measured shape (8192^3 +2-3 %, 8192^2x2048 +7 %,
+    // 16384^2x1024 +14 % over v44); its square-raster form v51 for >= 8 dispatch waves with long K
+    // (16384^3 1.01x hipBLASLt, v45 0.98x); the DMA-spaced schedule v52 for one or two dispatch
+    // waves with long K (4096^2x16384 +0.9 %, 4096x8192x8192 +1.7 % over v50).
+    v = 50;
+    if (sq && nwg >= 8 * cus && K >= 128 * BK) v = 51;
+    else if (nwg <= 2 * cus && K >= 128 * BK) v = 52;
+  } else if (v == 0) {
     v = 44;
     // Short K (K-loop of <= 64 K-tiles) with several tiles per CU: the persistent v25 hides each
     // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %;
@@ -66,14 +86,16 @@ static int resolve_variant(int M, int N, int K) {
   if (v == 48 && !sq) v = 47;
   if ((v == 47 || v == 48) && cus != 256) v = 42;
   if (v == 25 && persistent_grid(nwg) < NXCD) v = 44;
-  // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups
-  if (v == 50 && (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg) < NXCD)) v = 44;
+  // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups; its square raster
+  // (v51) needs exactly 256 workgroups over 16x16 super-tiles
+  if ((v == 50 || v == 51 || v == 52) && (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg) < NXCD)) v = 44;
+  if (v == 51 && (!sq || cus != 256)) v = 50;
   if ((v == 44 || v == 45) && cus != 256) v = 42;       // serpentine K assumes 32 co-resident WGs / XCD
   // K not a power of two: A-panel DMA instructions read rows 32 apart (PA, v47 / v48). At a 24 KiB
   // row stride adjacent rows cost 8-11 % (12288^3 1405 -> 1557 TF, 8192^2x12288 1457 -> 1579,
   // 12288^2x10240 +5 %); at power-of-two K it is neutral (8192) or worse (16384: -8 %).
   // profiles/r2_sched/sweep_pa.jsonl
-  if (g_variant == 0 && (K & (K - 1)) != 0) {
+  if (g_variant == 0 && !pow2k) {
     if (v == 44) v = 47;
     else if (v == 45) v = 48;
   }
@@ -84,7 +106,8 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
-  if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50)
+  if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50 &&
+      v != 51 && v != 52)
     return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
@@ -102,7 +125,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   const int nwg = (M / BM) * (N / BN);
   switch (resolve_variant(M, N, K)) {
     case 18:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 25:
@@ -110,27 +133,35 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 42:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true, false, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 44:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 47:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true, true>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true, true>), dim3(nwg),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 48:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true, true>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, true, true>), dim3(nwg),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 45:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true>), dim3(nwg), dim3(W4_THREADS),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, true>), dim3(nwg), dim3(W4_THREADS),
                          0, s, a, b, c, M, N, K);
       break;
     case 50:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_PRODUCTION_SC, true>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true>), dim3(persistent_grid(nwg)),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 51:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, true>), dim3(256), dim3(W4_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 52:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true>), dim3(persistent_grid(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {

@@ -69,8 +69,6 @@ __host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
 
 // RSPAN / DSPAN: the 16 fragment reads / DMA pieces of a block are spread over its first
 // RSPAN / DSPAN groups of 4 MFMAs (16 = evenly; smaller = earlier, more latency slack).
-// KO (profiling only, wrong results): bit0 drops the per-tile wait+barrier, bit1 the DMA, bit2
-// the fragment reads -- knock-out timings that price each component.
 
 // v18: v10's data layout with the schedule reshaped around the K-tile instead of two halves.
 // Knock-out cycle accounting of v10 (profiles/r1_gemm_v10/README.md) priced its DMA at 13 % of
@@ -84,14 +82,10 @@ __host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
 //                    iteration's pieces) landed, this iteration's stay in flight -- then a barrier
 //   slots B2+1 ..    read R0 <- tile t+1 kk0, spread over RS slots
 // Barriers sit between two MFMAs so the matrix pipe has queued work while the wave waits.
-// KO (lab knock-out timings only, wrong results): bit0 drops the lgkmcnt(0) before the free barrier,
-// bit1 the landing vmcnt (keeps lgkmcnt(0)), bit2 the free barrier, bit3 the landing barrier, bit4
-// the steady-state DMA pieces, bit5 the fragment reads of the loop, bit6 the XOR chunk permutation
-// of the DMA's global addresses (lanes read their row's chunks in order; the LDS image is then wrong),
-// bit7 (A) / bit8 (B) DMA instructions that read rows rblk + 32 g instead of 8 rblk + g (timing of
-// the row grouping; the LDS image is then a row permutation of the right one).
+// (The round-2 knock-out timings that priced each of these parts are recorded in
+// profiles/r2_sched/README.md; the knock-out builds themselves were retired from the tree.)
 template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
-          bool SQ = false, int KO = 0, bool VK = false, bool PA = false>
+          bool SQ = false, bool VK = false, bool PA = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
@@ -116,7 +110,7 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)gB, 0, panel_bytes, 0x00020000);
   const int par = wid & 1;
   const uint32_t voff = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
-                        (uint32_t)(((lane & 7) ^ ((KO & 64) ? 0 : ((par * 4 + (lane >> 4)) & 7))) * 16);
+                        (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
   const uint32_t voff_p = (uint32_t)(lane >> 3) * 32u * (uint32_t)K * 2u +
                           (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
   auto dma_piece = [&](int i, int k0, char* buf) {
@@ -127,7 +121,7 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     // 8 rblk + g, so its 8 rows are 32 rows apart instead of adjacent (at a 24 KiB row stride,
     // K = 12288, adjacent rows cost 10 %); LDS slot s then holds panel row 32 (s & 7) + (s >> 3),
     // which the epilogue's row mapping undoes. B keeps adjacent rows: its slots are C columns.
-    if ((((KO & 128) || PA) && i < 8) || ((KO & 256) && i >= 8)) {
+    if (PA && i < 8) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= 8 ? rB : rA, (lds_void*)lds, 16, voff_p + (uint32_t)k0 * 2u,
                                                (uint32_t)rblk * (uint32_t)K * 2u, 0, 0);
       return;
@@ -173,18 +167,18 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
       constexpr int i = decltype(I)::value;
       if constexpr (i < 64) w4_mfma<i>(R0.b[i & 7], R0.a[i >> 3]);
       else w4_mfma<i - 64>(R1.b[i & 7], R1.a[(i - 64) >> 3]);
-      if constexpr (i < 16 && !(KO & 32)) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
-      if constexpr (i == B1 - 1 && !(KO & 1)) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-      if constexpr (dm && i == B1 && !(KO & 4)) __builtin_amdgcn_s_barrier();
-      if constexpr (dm && !(KO & 16) && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
+      if constexpr (i < 16) read_frag(R1, cur, 1, std::integral_constant<int, i>{});
+      if constexpr (i == B1 - 1) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      if constexpr (dm && i == B1) __builtin_amdgcn_s_barrier();
+      if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
       if constexpr (nx && i == B2 - 1) {
-        constexpr int issued = (KO & 2) ? 63 : !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
+        constexpr int issued = !dm ? 0 : (B2 - 1 < D0 ? 0 : ((B2 - 1 - D0) / DS + 1 > 16 ? 16 : (B2 - 1 - D0) / DS + 1));
         // vmcnt(issued) lgkmcnt(0): vmcnt low 4 bits [3:0], high 2 bits [15:14]; expcnt 7
         __builtin_amdgcn_s_waitcnt((issued & 15) | ((issued >> 4) << 14) | 0x70);
       }
-      if constexpr (nx && i == B2 && !(KO & 8)) __builtin_amdgcn_s_barrier();
+      if constexpr (nx && i == B2) __builtin_amdgcn_s_barrier();
       constexpr int jr0 = w4s_r0_at(B2, RS, i);
-      if constexpr (nx && jr0 >= 0 && !(KO & 32)) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
+      if constexpr (nx && jr0 >= 0) read_frag(R0, nxt, 0, std::integral_constant<int, jr0>{});
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -739,7 +733,10 @@ gemm_bf16_256x256_w4a(const __bf16* __restrict__ A, const __bf16* __restrict__ B
                  [nkstep] "s"(nkstep), [m0b0] "s"(m0b0), [m0b1] "s"(m0b1), [flags] "s"(flags)                    \
                : "memory", "scc", W4A_VCLOBBERS, W4_AGPR_CLOBBERS)
 
-template <int SC = 0, bool SERP = true>
+// SQ: the square cross-XCD raster of v45 instead -- gridDim is exactly 256 (one workgroup per CU),
+// workgroup b's i-th tile is dispatch-wave index i * 256 + b of tile_coords_sq, so every round of
+// 256 co-resident tiles is one 16x16 super-tile (host: tiles_m and tiles_n multiples of 16).
+template <int SC = 0, bool SERP = true, bool SQ = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
@@ -748,13 +745,24 @@ gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ 
   const int tiles_m = M / BM;
   const int tiles_n = N / BN;
   const int nwg = tiles_m * tiles_n;
-  const int xcd = blockIdx.x % NXCD;
-  const int per = gridDim.x / NXCD;
-  const int q = nwg / NXCD, rem = nwg % NXCD;
-  const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
-  const int t_end = t_begin + q + (xcd < rem ? 1 : 0);
-  int tile = t_begin + (int)(blockIdx.x / NXCD);
+  int tile, per, t_end;
+  if constexpr (SQ) {
+    tile = (int)blockIdx.x;
+    per = (int)gridDim.x;
+    t_end = nwg;
+  } else {
+    const int xcd = blockIdx.x % NXCD;
+    per = gridDim.x / NXCD;
+    const int q = nwg / NXCD, rem = nwg % NXCD;
+    const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+    t_end = t_begin + q + (xcd < rem ? 1 : 0);
+    tile = t_begin + (int)(blockIdx.x / NXCD);
+  }
   if (tile >= t_end) return;                              // uniform over the workgroup
+  auto coords = [&](int t, int& m, int& n) {
+    if constexpr (SQ) tile_coords_sq(t, tiles_n, m, n);
+    else tile_coords(t, tiles_m, tiles_n, m, n);
+  };
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -798,7 +806,7 @@ gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ 
   char* const stg = smem + LDS_BYTES + wid * 8192;
 
   int tm, tn;
-  tile_coords(tile, tiles_m, tiles_n, tm, tn);
+  coords(tile, tm, tn);
   bool rev = false;
   w4a_u32x4 sA = mk_rs(A + (size_t)tm * BM * K), sB = mk_rs(Bt + (size_t)tn * BN * K);
   uint32_t voff_k = voff0(rev);
@@ -814,7 +822,7 @@ gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ 
     int ntm = tm, ntn = tn;
     w4a_u32x4 nA = sA, nB = sB;
     if (hasnext) {
-      tile_coords(next, tiles_m, tiles_n, ntm, ntn);
+      coords(next, ntm, ntn);
       nA = mk_rs(A + (size_t)ntm * BM * K);
       nB = mk_rs(Bt + (size_t)ntn * BN * K);
     }

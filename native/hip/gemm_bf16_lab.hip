@@ -9,9 +9,8 @@
 // one barrier apart, half-tile LDS ring), 4 = v3 with buffer_load...lds staging, 5 = v4 with an
 // LDS-staged, fully coalesced epilogue, 6-9 = v5 phase/knob variants; 10-14 = one wave per SIMD with
 // a 128x128 wave tile; 15-17 = half-tile ring; 18/19 = the K-tile schedule; 20-24 = knock-outs;
-// 80-85 = v44 knock-outs (KO bits of w4s: 1 lgkmcnt, 2 landing vmcnt, 4 free barrier, 8 landing
-// barrier, 16 DMA, 32 fragment reads, 64 DMA chunk order; 84 = 1|4, 85 = 15, 86 = 16, 87 = 32,
-// 88 = 63, 89 = 64);
+// (the v44 knock-outs 80-89 and the row-grouping timings 95-97 were retired once priced:
+// profiles/r2_sched/README.md);
 // 25-27 = persistent; 30-35 = barrier-placement sweep; 40/41 = serpentine K, 42/43 = loop rotation,
 // 44 = both (production default), 45 = 44 + square raster. Measured: profiles/r1_gemm_v4/,
 // profiles/r1_s2_gemm/, profiles/r1_s6_sq/.
@@ -1138,33 +1137,15 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
     hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true>), dim3(nwg), dim3(W4_THREADS),
                        0, s, a, b, c, M, N, K);
   } else if (v >= 90 && v <= 94 && kk) {            // v44 + VK (90); DMA spacing 6 / 7 slots (91-94)
-    auto kern = v == 90 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true>
-              : v == 91 ? gemm_bf16_256x256_w4s<17, 19, 6, 80, 40, 32, true, false, 0, true>
-              : v == 92 ? gemm_bf16_256x256_w4s<17, 19, 7, 80, 40, 32, true, false, 0, true>
-              : v == 93 ? gemm_bf16_256x256_w4s<17, 19, 6, 96, 24, 32, true, false, 0, true>
-                        : gemm_bf16_256x256_w4s<17, 18, 6, 64, 48, 32, true, false, 0, true>;
+    auto kern = v == 90 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true>
+              : v == 91 ? gemm_bf16_256x256_w4s<17, 19, 6, 80, 40, 32, true, false, true>
+              : v == 92 ? gemm_bf16_256x256_w4s<17, 19, 7, 80, 40, 32, true, false, true>
+              : v == 93 ? gemm_bf16_256x256_w4s<17, 19, 6, 96, 24, 32, true, false, true>
+                        : gemm_bf16_256x256_w4s<17, 18, 6, 64, 48, 32, true, false, true>;
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
   } else if ((v == 98 && kk && (M / BM) % 16 == 0 && (N / BN) % 16 == 0) || (v == 99 && kk)) {   // + PA
-    auto kern = v == 98 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 0, true, true>
-                        : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 0, true, true>;
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
-  } else if (v >= 95 && v <= 97 && kk) {            // v45+VK with permuted DMA row grouping (WRONG results)
-    if ((M / BM) % 16 || (N / BN) % 16) return (int)hipErrorInvalidValue;
-    auto kern = v == 95 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 128, true>
-              : v == 96 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 256, true>
-                        : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, 384, true>;
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
-  } else if (v >= 80 && v <= 89 && kk) {            // v44 knock-outs (WRONG results by design)
-    auto kern = v == 89 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 64>
-              : v == 86 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 16>
-              : v == 87 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 32>
-              : v == 88 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 63>
-              : v == 80 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 1>
-              : v == 81 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 2>
-              : v == 82 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 4>
-              : v == 83 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 8>
-              : v == 84 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 5>
-                        : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, 15>;
+    auto kern = v == 98 ? gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, true, true>
+                        : gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true, true>;
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
   } else if ((v == 70 || v == 71) && kk) {            // w4t, B-outer MFMA operand order
     auto kern = v == 70 ? gemm_bf16_256x256_w4t<W4SchedV18, 32, true, false, false, 0, true>
@@ -1192,7 +1173,7 @@ int amdgo_lab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, in
   return (int)hipGetLastError();
 }
 
-// 1 if variant v produces correct results (everything except the knock-out timings 20-24, 80-85).
-int amdgo_lab_variant_is_exact(int v) { return !(v >= 20 && v <= 24) && !(v >= 80 && v <= 89) && !(v >= 95 && v <= 97); }
+// 1 if variant v produces correct results (everything except the knock-out timings 20-24).
+int amdgo_lab_variant_is_exact(int v) { return !(v >= 20 && v <= 24); }
 
 }  // extern "C"

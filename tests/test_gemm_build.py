@@ -191,11 +191,12 @@ def _audit_asm_pipeline(body, st):
 
 
 def test_w4ap_production_pipeline(asm):
-    """Production v50: the persistent asm K pipeline, one instantiation (W4AP_PRODUCTION_SC)."""
+    """Production v50 / v51 / v52: the persistent asm K pipeline (main schedule, its square-raster
+    form, the long-K schedule)."""
     kernels = _kernels(asm, "gemm_bf16_256x256_w4apI")
-    assert len(kernels) == 1
-    body, st = kernels[0]
-    assert _audit_asm_pipeline(body, st) == 6 * 128
+    assert len(kernels) == 3
+    for body, st in kernels:
+        assert _audit_asm_pipeline(body, st) == 6 * 128
 
 
 def test_w4a_lab_pipelines(tmp_path_factory):
@@ -212,10 +213,6 @@ def test_w4_main_loop_shape(w4):
         ko = re.match(r"\w*w4ILi\d+ELi\d+ELi(\d+)E", body)
         if ko and int(ko.group(1)):
             continue                        # knock-out profiling builds drop parts on purpose
-        # w4s knock-outs (lab 80-89): KO is the 9th template argument, after SQ
-        ko_s = re.match(r"\w*w4sI(?:Li-?\d+E){6}Lb[01]ELb[01]ELi(\d+)E", body)
-        if ko_s and int(ko_s.group(1)):
-            continue
         loop = re.search(r"; =>\s*This Inner Loop Header.*?\n(.*?)s_cbranch_scc\d \.LBB", body, re.S)
         assert loop, "main loop not found"
         text = loop.group(1)

@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -95,7 +95,7 @@ def test_smoke_vector_add(cuda_device):
 
 
 def test_default_dispatch_square_raster_covers_every_tile(cuda_device):
-    """12288x12288x8192 (48x48 tiles, 9 dispatch waves) takes the square cross-XCD raster (v45)
+    """12288x12288x8192 (48x48 tiles, 9 dispatch waves) takes the square cross-XCD raster (v51)
     under the default variant; one checked row per tile row covers every output tile."""
     import torch
     from gpu_operator_amd.ops import gemm as G
@@ -116,24 +116,25 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
     assert G.get_variant() == 0
 
 
-@pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 44), (16384, 16384, 1024, 25), (8192, 8192, 4096, 25),
+@pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 50), (16384, 16384, 1024, 50), (8192, 8192, 4096, 50),
                                         (12288, 12288, 12288, 48), (8192, 8192, 12288, 47),
-                                        (12288, 12288, 8192, 45), (4096, 4096, 4096, 44),
-                                        (256, 256, 64, 0), (300, 256, 256, 0)])
+                                        (12288, 12288, 8192, 51), (16384, 16384, 16384, 51),
+                                        (4096, 4096, 16384, 52), (4096, 8192, 8192, 52), (4096, 4096, 4096, 50),
+                                        (8192, 8192, 128, 25), (256, 256, 64, 0), (300, 256, 256, 0)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""
     import torch
     from gpu_operator_amd.ops import gemm as G
 
     if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
-        want = {44: 42, 45: 42, 47: 42, 48: 42}.get(want, want)
+        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42}.get(want, want)
     assert G.get_variant() == 0
     assert G.resolve_variant(m, n, k) == want
 
@@ -159,3 +160,32 @@ def test_asm_pipeline_is_bitwise_v44(cuda_device, m, n, k):
         G.set_variant(old)
     torch.cuda.synchronize()
     assert torch.equal(c44, c50)
+
+
+@pytest.mark.parametrize("m,n,k", [(4096, 8192, 256), (8192, 8192, 1024), (4096, 4096, 2048)])
+def test_asm_square_raster_is_bitwise_v45(cuda_device, m, n, k):
+    """v51 (persistent asm pipeline on the square cross-XCD raster) walks the tiles of v45 in the
+    same rounds of 256 with the same serpentine K per round: bitwise-equal outputs."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
+        pytest.skip("square raster needs the 256-CU MI355X")
+    a = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=cuda_device), 7)
+    bt = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=cuda_device), 8)
+    old = G.get_variant()
+    try:
+        G.set_variant(45)
+        c45 = G.gemm_bf16(a, bt)
+        G.set_variant(51)
+        assert G.resolve_variant(m, n, k) == 51
+        c51 = G.gemm_bf16(a, bt)
+        G.set_variant(52)
+        c52 = G.gemm_bf16(a, bt)
+        G.set_variant(50)
+        c50 = G.gemm_bf16(a, bt)
+    finally:
+        G.set_variant(old)
+    torch.cuda.synchronize()
+    assert torch.equal(c45, c51)
+    assert torch.equal(c50, c52)      # same pipeline, different instruction placement

@@ -17,7 +17,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 LAB_DIR = os.path.join(ROOT, "gpu_operator_amd", "_native")
-KNOCKOUT_BF16 = tuple(range(20, 25)) + tuple(range(80, 90)) + (95, 96, 97)   # timings with deliberately wrong results
+KNOCKOUT_BF16 = tuple(range(20, 25))   # timings with deliberately wrong results
 _LIBS = {}
 
 

@@ -269,6 +269,9 @@ def render() -> str:
     parts.append("#define W4AP_LOOP_SELECT(SC) \\")
     parts.append("  " + " else \\\n  ".join(psel))
     parts.append("// " + ", ".join(f"{i} = {n}" for i, n in enumerate(PERSISTENT)))
+    parts.append("// by name (the production dispatch refers to schedules this way)")
+    for i, n in enumerate(PERSISTENT):
+        parts.append(f"#define W4AP_SC_{n.upper()} {i}")
     parts.append("")
     for name in PERSISTENT:
         lines = kloop_persistent(SCHEDULES[name])
