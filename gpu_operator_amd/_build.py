@@ -88,7 +88,7 @@ def _pyext_name(stem: str) -> str:
 
 
 GEMM_HEADERS = ["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h",
-                "hip/gemm_fp8_kernels.h"]
+                "hip/gemm_fp8_kernels.h", "hip/gemm_fp8_asm_loop.h", "hip/gemm_w4ap.h"]
 
 TARGETS: List[Target] = [
     # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.

@@ -8,7 +8,12 @@
 //   45  = w4s v45 (production for big square grids: v44 + square cross-XCD raster)
 //   130 + SC = w4ap (persistent) with persistent schedule SC, serpentine K; 133 = schedule 0 without
 //   150 / 151 = w4ap square raster (SQ) with persistent schedule 5 / 9; 152 = 150 without serpentine K
+// amdgo_asmlab_gemm_fp8 (fp8 e4m3 operands):
+//   15 / 16 / 18 = production q16 (serpentine K), q16 square raster, persistent q16p
+//   200 + SC = q16ap (persistent asm pipeline) with fp8 schedule SC (gemm_fp8_asm_loop.h), linear K
+//   210 + SC = q16ap with serpentine K; 220 + SC = q16ap square raster, serpentine K
 #include "gemm_bf16_kernels.h"
+#include "gemm_fp8_kernels.h"
 
 extern "C" {
 
@@ -76,6 +81,10 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4AP_CASE(141, 10, true)
     W4AP_CASE(142, 11, true)
     W4AP_CASE(143, 12, true)
+    W4AP_CASE(144, 13, true)
+    W4AP_CASE(145, 14, true)
+    W4AP_CASE(146, 15, true)
+    W4AP_CASE(147, 16, true)
 #define W4APSQ_CASE(V, SC, SERP)                                                                           \
     case V:                                                                                               \
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;    \
@@ -85,6 +94,63 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4APSQ_CASE(150, 5, true)
     W4APSQ_CASE(151, 9, true)
     W4APSQ_CASE(152, 5, false)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
+  if (M % F8_BM || N % F8_BN || K % (2 * F8_BK) || K < 4 * F8_BK) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const auto* a = (const uint8_t*)A;
+  const auto* b = (const uint8_t*)Bt;
+  auto* c = (__bf16*)C;
+  const int nwg = (M / F8_BM) * (N / F8_BN);
+  const int cus = device_cu_count();
+  const int g = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;
+  const bool sq = (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0 && cus == 256;
+  switch (v) {
+    case 15:
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, 32, false, 2, 2, true>), dim3(nwg),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 16:
+      if (!sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, 32, true, 2, 2, true>), dim3(nwg),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 18:
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16p<>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+#define F8AP_CASE(V, SC, SERP, SQ)                                                                         \
+    case V:                                                                                               \
+      if (g < NXCD || (SQ && !sq)) return (int)hipErrorInvalidValue;                                      \
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<SC, SERP, SQ>), dim3(SQ ? 256 : g), dim3(F8_THREADS), 0, s, \
+                         a, b, c, M, N, K);                                                               \
+      break;
+    F8AP_CASE(200, 0, false, false)
+    F8AP_CASE(201, 1, false, false)
+    F8AP_CASE(202, 2, false, false)
+    F8AP_CASE(203, 3, false, false)
+    F8AP_CASE(204, 4, false, false)
+    F8AP_CASE(205, 5, false, false)
+    F8AP_CASE(206, 6, false, false)
+    F8AP_CASE(210, 0, true, false)
+    F8AP_CASE(211, 1, true, false)
+    F8AP_CASE(212, 2, true, false)
+    F8AP_CASE(213, 3, true, false)
+    F8AP_CASE(214, 4, true, false)
+    F8AP_CASE(215, 5, true, false)
+    F8AP_CASE(216, 6, true, false)
+    F8AP_CASE(220, 0, true, true)
+    F8AP_CASE(221, 1, true, true)
+    F8AP_CASE(222, 2, true, true)
+    F8AP_CASE(223, 3, true, true)
+    F8AP_CASE(224, 4, true, true)
+    F8AP_CASE(225, 5, true, true)
+    F8AP_CASE(226, 6, true, true)
     default:
       return (int)hipErrorInvalidValue;
   }

@@ -16,7 +16,7 @@
 #include <stdint.h>
 
 #include "gemm_tile_common.h"
-#include "gemm_bf16_asm_loop.h"
+#include "gemm_w4ap.h"
 
 namespace {
 
@@ -589,17 +589,6 @@ gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ B
 // accumulators as w4s: the results are bitwise those of v44. SC selects the schedule (the index list
 // is in gemm_bf16_asm_loop.h). Host guarantees: K % 128 == 0 and K >= 256 (an even number of
 // K-tiles, at least one loop trip).
-#define W4A_VCLOBBERS                                                                                       \
-  "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", \
-  "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31",   \
-  "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46",   \
-  "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61",   \
-  "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76",   \
-  "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",   \
-  "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105",    \
-  "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118",    \
-  "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127"
-
 #define W4A_LOOP(TEXT)                                                                                       \
   asm volatile("s_mov_b32 %[m0save], m0\n\t" TEXT "s_mov_b32 m0, %[m0save]"                                  \
                : [voff] "+v"(voff_k), [cnt] "+s"(trips), [m0save] "=&s"(m0save)                               \
@@ -608,8 +597,6 @@ gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ B
                  [s1] "s"(so[1]), [s2] "s"(so[2]), [s3] "s"(so[3]), [s4] "s"(so[4]), [s5] "s"(so[5]),           \
                  [s6] "s"(so[6]), [s7] "s"(so[7]), [rA] "s"(sA), [rB] "s"(sB), [m0b0] "s"(m0b0), [m0b1] "s"(m0b1) \
                : "memory", "scc", W4A_VCLOBBERS, W4_AGPR_CLOBBERS)
-
-typedef uint32_t w4a_u32x4 __attribute__((ext_vector_type(4)));
 
 template <int SC = 0, int SERP = 32, bool SQ = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
@@ -713,178 +700,13 @@ gemm_bf16_256x256_w4a(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   }
 }
 
-// w4ap: w4a made persistent (the v25 structure with the asm K pipeline). gridDim = one workgroup per
-// CU (a multiple of 8); XCD x owns a contiguous run of output tiles that its workgroups walk in
-// strides of gridDim / 8, so the 32 co-resident tiles of an XCD are neighbours in the grouped
-// raster. The K stream runs on across tiles: the last two K-tiles of a tile DMA the next tile's
-// K-tiles 0 and 1 into the buffers they free (drain with %[nA] / %[nB] / %[nvoff]), and the
-// epilogue stages each wave's 128x128 sub-tile through a private 8 KiB slice of the 32 KiB of LDS
-// beyond the K buffers -- no workgroup barrier, overlapping the in-flight DMA; its vmcnt(0) before
-// the first C store retires those DMAs, so the next tile starts with a barrier and its fragment
-// reads. SERP: odd tiles of a workgroup walk K backwards (they start on the K-slices the previous
-// tile left in L2). Host guarantees as w4a, plus gridDim % 8 == 0.
-#define W4AP_LOOP(TEXT)                                                                                       \
-  asm volatile("s_mov_b32 %[m0save], m0\n\t" TEXT "s_mov_b32 m0, %[m0save]"                                   \
-               : [voff] "+v"(voff_k), [nvoff] "+v"(nvoff), [cnt] "+s"(trips), [m0save] "=&s"(m0save)           \
-               : [ra00] "v"(ra00), [rb00] "v"(rb00), [ra01] "v"(ra01), [rb01] "v"(rb01), [ra10] "v"(ra10),       \
-                 [rb10] "v"(rb10), [ra11] "v"(ra11), [rb11] "v"(rb11), [kstep] "s"(kstep), [s0] "s"(so[0]),      \
-                 [s1] "s"(so[1]), [s2] "s"(so[2]), [s3] "s"(so[3]), [s4] "s"(so[4]), [s5] "s"(so[5]),            \
-                 [s6] "s"(so[6]), [s7] "s"(so[7]), [rA] "s"(sA), [rB] "s"(sB), [nA] "s"(nA), [nB] "s"(nB),       \
-                 [nkstep] "s"(nkstep), [m0b0] "s"(m0b0), [m0b1] "s"(m0b1), [flags] "s"(flags)                    \
-               : "memory", "scc", W4A_VCLOBBERS, W4_AGPR_CLOBBERS)
-
-// SQ: the square cross-XCD raster of v45 instead -- gridDim is exactly 256 (one workgroup per CU),
-// workgroup b's i-th tile is dispatch-wave index i * 256 + b of tile_coords_sq, so every round of
-// 256 co-resident tiles is one 16x16 super-tile (host: tiles_m and tiles_n multiples of 16).
+// w4ap (v50-v52): w4a made persistent; the frame is shared with the fp8 kernel (gemm_w4ap.h).
 template <int SC = 0, bool SERP = true, bool SQ = false>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES + 4 * 8192];
-
-  const int tiles_m = M / BM;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  int tile, per, t_end;
-  if constexpr (SQ) {
-    tile = (int)blockIdx.x;
-    per = (int)gridDim.x;
-    t_end = nwg;
-  } else {
-    const int xcd = blockIdx.x % NXCD;
-    per = gridDim.x / NXCD;
-    const int q = nwg / NXCD, rem = nwg % NXCD;
-    const int t_begin = (xcd < rem) ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
-    t_end = t_begin + q + (xcd < rem ? 1 : 0);
-    tile = t_begin + (int)(blockIdx.x / NXCD);
-  }
-  if (tile >= t_end) return;                              // uniform over the workgroup
-  auto coords = [&](int t, int& m, int& n) {
-    if constexpr (SQ) tile_coords_sq(t, tiles_n, m, n);
-    else tile_coords(t, tiles_m, tiles_n, m, n);
-  };
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-  const uint32_t panel_bytes = (uint32_t)BM * (uint32_t)K * 2u;
-  auto mk_rs = [&](const __bf16* base) {
-    const uint64_t p = (uint64_t)(uintptr_t)base;
-    w4a_u32x4 r;
-    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)p);
-    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-    r[2] = panel_bytes;
-    r[3] = 0x00020000u;
-    return r;
-  };
-  const int par = wid & 1;
-  const int ktiles = K / BK;
-  const uint32_t lane_dma = (uint32_t)(lane >> 3) * (uint32_t)K * 2u +
-                            (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
-  // the lane offset of a tile's first DMA K-tile, and its K step, by walking direction
-  auto voff0 = [&](bool rev) { return lane_dma + (uint32_t)((rev ? ktiles - 1 : 0) * BK * 2); };
-  auto kst = [&](bool rev) { return rev ? -2 * BK : 2 * BK; };
-  uint32_t so[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    so[i] = __builtin_amdgcn_readfirstlane((uint32_t)((i << 2) + wid) * 8u * (uint32_t)K * 2u);
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
-  const uint32_t m0b0 = lds0 + (uint32_t)wid * 1024u, m0b1 = m0b0 + (uint32_t)BUF_BYTES;
-  int lane_off[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int r = lane & 15;
-    const int c = kk * 4 + (lane >> 4);
-    lane_off[kk] = r * ROW_BYTES + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-  const uint32_t a_base = lds0 + (uint32_t)(wr * 128 * ROW_BYTES);
-  const uint32_t b_base = lds0 + (uint32_t)(PANEL_BYTES + wc * 128 * ROW_BYTES);
-  const uint32_t ra00 = a_base + lane_off[0], rb00 = b_base + lane_off[0];
-  const uint32_t ra01 = a_base + lane_off[1], rb01 = b_base + lane_off[1];
-  const uint32_t ra10 = ra00 + BUF_BYTES, rb10 = rb00 + BUF_BYTES;
-  const uint32_t ra11 = ra01 + BUF_BYTES, rb11 = rb01 + BUF_BYTES;
-  char* const stg = smem + LDS_BYTES + wid * 8192;
-
-  int tm, tn;
-  coords(tile, tm, tn);
-  bool rev = false;
-  w4a_u32x4 sA = mk_rs(A + (size_t)tm * BM * K), sB = mk_rs(Bt + (size_t)tn * BN * K);
-  uint32_t voff_k = voff0(rev);
-  int kstep = kst(rev);
-  uint32_t first = 1;
-
-  asm volatile("" ::: W4_AGPR_CLOBBERS);
-  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
-  for (;;) {
-    const int next = tile + per;
-    const uint32_t hasnext = __builtin_amdgcn_readfirstlane(next < t_end ? 1u : 0u);
-    const bool nrev = SERP && !rev;
-    int ntm = tm, ntn = tn;
-    w4a_u32x4 nA = sA, nB = sB;
-    if (hasnext) {
-      coords(next, ntm, ntn);
-      nA = mk_rs(A + (size_t)ntm * BM * K);
-      nB = mk_rs(Bt + (size_t)ntn * BN * K);
-    }
-    uint32_t nvoff = voff0(nrev);
-    const int nkstep = kst(nrev);
-    uint32_t trips = __builtin_amdgcn_readfirstlane((uint32_t)((ktiles - 2) >> 1));
-    uint32_t m0save;
-    const uint32_t flags = __builtin_amdgcn_readfirstlane(first | (hasnext << 1));
-    W4AP_LOOP_SELECT(SC)
-
-    // wave-private epilogue (the K buffers may be receiving the next tile's DMA): 4 passes of
-    // 2 fragment rows = 32 C rows x 128 columns through this wave's 8 KiB, accumulators zeroed
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA D -> accvgpr reads
-    static_for<0, 4>([&](auto S) {
-      constexpr int s = decltype(S)::value;
-      static_for<0, 16>([&](auto I) {
-        constexpr int u = decltype(I)::value;
-        constexpr int mm = u >> 3, n = u & 7;
-        constexpr int i = (2 * s + mm) * 8 + n;                    // accumulator index m*8+n
-        float x0, x1, x2, x3;
-        asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
-                     "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
-                     "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
-                     "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
-                     : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
-                     : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
-        const int r = mm * 16 + (lane & 15);
-        const int g = n * 4 + (lane >> 4);
-        bf16x4 v;
-        v[0] = (__bf16)x0;
-        v[1] = (__bf16)x1;
-        v[2] = (__bf16)x2;
-        v[3] = (__bf16)x3;
-        *reinterpret_cast<bf16x4*>(stg + r * 256 + ((g ^ (r & 15)) << 3)) = v;
-      });
-      asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
-      if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA landed
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int r = k * 4 + (lane >> 4);
-        const int ch = lane & 15;
-        const int sw = r & 15;
-        const int pg = (2 * ch) ^ sw;
-        const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
-        uint4 v = raw;
-        if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-        *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + wr * 128 + s * 32 + r) * N + tn * BN + wc * 128 + ch * 8) = v;
-      }
-      asm volatile("" ::: "memory");
-    });
-    if (!hasnext) break;
-    tile = next;
-    tm = ntm;
-    tn = ntn;
-    sA = nA;
-    sB = nB;
-    rev = nrev;
-    voff_k = nvoff;                 // the drain advanced it past the next tile's K-tiles 0 and 1
-    kstep = nkstep;
-    first = 0;
-  }
+  __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
+  w4ap_run<SC, SERP, SQ, false>((const char*)A, (const char*)Bt, C, M, N, K, smem);
 }
 
 // v25/v26: v18 made persistent. gridDim = one workgroup per CU; XCD x (= blockIdx % 8) owns a

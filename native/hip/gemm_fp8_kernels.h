@@ -39,6 +39,7 @@
 #include <stdint.h>
 
 #include "gemm_tile_common.h"
+#include "gemm_w4ap.h"
 
 namespace {
 
@@ -387,7 +388,8 @@ gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
       constexpr int ai = (blk & 1) * 4 + (aslow ? (w >> 2) : (w & 3));
       f8q_mfma<ai * 8 + bi>(FB[bi], FA[ai]);                      // accumulator m*8+n
       // A1 (a4..7) at slots 0..7, B1 (b4..7) at 8..15: one fragment per two slots
-      if constexpr (i < 16 && (i & 1) == 0) read_frag(i < 8 ? FA[4 + i / 2] : FB[4 + (i - 8) / 2], i >= 8, 4 + (i & 7) / 2, cur);
+      if constexpr (i < 8 && (i & 1) == 0) read_frag(FA[4 + i / 2], false, 4 + i / 2, cur);
+      if constexpr (i >= 8 && i < 16 && (i & 1) == 0) read_frag(FB[4 + (i - 8) / 2], true, 4 + (i - 8) / 2, cur);
       if constexpr (i == W1) __builtin_amdgcn_s_waitcnt(0xC07F);                 // lgkmcnt(0)
       if constexpr (dm && i == W1 + 1) __builtin_amdgcn_s_barrier();
       if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, dk, cur);
@@ -776,7 +778,8 @@ gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__
       constexpr int bi = (blk >> 1) * 4 + (aslow ? (w & 3) : (w >> 2));
       constexpr int ai = (blk & 1) * 4 + (aslow ? (w >> 2) : (w & 3));
       f8q_mfma<ai * 8 + bi>(FB[bi], FA[ai]);
-      if constexpr (i < 16 && (i & 1) == 0) read_frag(i < 8 ? FA[4 + i / 2] : FB[4 + (i - 8) / 2], i >= 8, 4 + (i & 7) / 2, cur);
+      if constexpr (i < 8 && (i & 1) == 0) read_frag(FA[4 + i / 2], false, 4 + i / 2, cur);
+      if constexpr (i >= 8 && i < 16 && (i & 1) == 0) read_frag(FB[4 + (i - 8) / 2], true, 4 + (i - 8) / 2, cur);
       if constexpr (i == W1) __builtin_amdgcn_s_waitcnt(0xC07F);                 // lgkmcnt(0)
       if constexpr (dm && i == W1 + 1) __builtin_amdgcn_s_barrier();
       if constexpr (dm && i >= D0 && (i - D0) % DS == 0 && (i - D0) / DS < 16) dma_piece((i - D0) / DS, ra, rb, dk, cur);
@@ -899,6 +902,18 @@ gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__
     rA = nA;
     rB = nB;
   }
+}
+
+// q16ap (fp8 v20-v22): the persistent asm-pipeline frame of the bf16 v50 (gemm_w4ap.h) around the
+// q16 K-tile body as one hand-scheduled asm block per output tile (tools/gen_fp8_asm_loop.py,
+// gemm_fp8_asm_loop.h): the same MFMAs, operands and accumulators as q16p, waits computed per
+// fragment instead of hipcc's, no per-piece SALU address arithmetic or s_nop.
+template <int SC = 0, bool SERP = false, bool SQ = false>
+__global__ void __launch_bounds__(F8_THREADS, 1)
+gemm_fp8_256x256_q16ap(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
+                       __bf16* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
+  w4ap_run<SC, SERP, SQ, true>((const char*)A, (const char*)Bt, C, M, N, K, smem);
 }
 
 // OCP e4m3fn -> f32 in software (independent of the matrix cores): bias 7, no infinities,

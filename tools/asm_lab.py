@@ -71,13 +71,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--no-blas", action="store_true")
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8: e4m3 operands through amdgo_asmlab_gemm_fp8, hipBLASLt via torch._scaled_mm")
     ap.add_argument("--one", default=None,
                     help="profiling mode: dispatch only this variant ('blas' = hipBLASLt) --iters times, no checks")
     a = ap.parse_args()
     import torch
     from gpu_operator_amd.ops import gemm as G
     lib = ctypes.CDLL(os.path.join(ROOT, "gpu_operator_amd", "_native", "libamdgo_gemm_asmlab.so"))
-    fn = lib.amdgo_asmlab_gemm_bf16
+    f8 = a.dtype == "fp8"
+    fn = lib.amdgo_asmlab_gemm_fp8 if f8 else lib.amdgo_asmlab_gemm_bf16
     fn.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in a.variants.split(",")]
@@ -91,14 +94,25 @@ def main():
 
     for spec in a.shapes.split(","):
         m, n, k = (int(x) for x in spec.split("x")) if "x" in spec else (int(spec),) * 3
-        A = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 11)
-        B = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 12)
+        if f8:
+            A = G.fill_uniform_fp8_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device=dev), 11)
+            B = G.fill_uniform_fp8_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device=dev), 12)
+            one = torch.ones((), dtype=torch.float32, device=dev)
+
+            def blas(out, Bt):
+                return torch._scaled_mm(A, Bt, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+        else:
+            A = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 11)
+            B = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 12)
+
+            def blas(out, Bt):
+                return torch.matmul(A, Bt, out=out)
         if a.one is not None:                 # rocprofv3 --pmc target: the dispatches and nothing else
             Cx = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
             Bt = B.t()
             for _ in range(a.iters):
                 if a.one == "blas":
-                    torch.matmul(A, Bt, out=Cx)
+                    blas(Cx, Bt)
                 else:
                     run(int(a.one), A, B, Cx)
             torch.cuda.synchronize()
@@ -119,7 +133,7 @@ def main():
         impls = [(str(v), (lambda v=v: run(v, A, B, C[v]))) for v in variants]
         if not a.no_blas:
             Bt = B.t()
-            impls.append(("hipblaslt", lambda: torch.matmul(A, Bt, out=Cb)))
+            impls.append(("hipblaslt", lambda: blas(Cb, Bt)))
         flop = 2.0 * m * n * k
         res = {name: [] for name, _ in impls}
         power = {}

@@ -81,6 +81,10 @@ class Schedule:
         self.vk = vk            # slot of the K-offset add after the last piece
         self.w3 = w3            # lgkmcnt(0) slot (the next tile's R0 landed)
 
+    @property
+    def merged(self) -> bool:
+        return self.w2 is None
+
     def issued_before_w2(self) -> int:
         return sum(1 for s in self.dma if s <= self.w2)
 
@@ -88,12 +92,15 @@ class Schedule:
 def make(name, r1=(0, 1), dma=(19, 5), w2=79, r0=(81, 2), w3=126, vk=None, bout=False, w1_gap=1):
     """A schedule from arithmetic progressions: R1 reads j at r1[0] + j*r1[1] (then lgkmcnt(0) and
     the free barrier right after the last one), DMA piece p at dma[0] + p*dma[1], the landing wait at
-    w2 and its barrier at w2 + 1, R0 reads j at r0[0] + j*r0[1]."""
+    w2 and its barrier at w2 + 1, R0 reads j at r0[0] + j*r0[1].
+    w2 = None: ONE barrier per K-tile -- the free wait becomes vmcnt(0) lgkmcnt(0), so the barrier
+    after it also publishes tile t+1 (DMA'd during the previous K-tile) and R0 of tile t+1 may be
+    read any time after MFMA 63."""
     r1s = [r1[0] + j * r1[1] for j in range(16)]
     w1 = r1s[-1] + w1_gap                  # lgkmcnt(0): w1_gap MFMAs after the last R1 read
     ds = [dma[0] + p * dma[1] for p in range(16)]
     r0s = [r0[0] + j * r0[1] for j in range(16)]
-    sc = Schedule(name, r1=r1s, w1=w1, b1=w1 + 1, dma=ds, m0_lead=1, w2=w2, b2=w2 + 1, r0=r0s,
+    sc = Schedule(name, r1=r1s, w1=w1, b1=w1 + 1, dma=ds, m0_lead=1, w2=w2, b2=None if w2 is None else w2 + 1, r0=r0s,
                   vk=vk if vk is not None else ds[-1] + 2, w3=w3, bout=bout)
     validate(sc)
     return sc
@@ -101,13 +108,15 @@ def make(name, r1=(0, 1), dma=(19, 5), w2=79, r0=(81, 2), w3=126, vk=None, bout=
 
 def validate(sc: "Schedule") -> None:
     """The protocol's ordering constraints (module docstring) and <= 2 fillers per gap."""
-    assert all(0 <= x < SLOTS for x in sc.r1 + sc.dma + sc.r0 + [sc.w1, sc.b1, sc.w2, sc.b2, sc.vk, sc.w3]), sc.name
+    land = [] if sc.merged else [sc.w2, sc.b2]
+    assert all(0 <= x < SLOTS for x in sc.r1 + sc.dma + sc.r0 + [sc.w1, sc.b1, sc.vk, sc.w3] + land), sc.name
     assert sc.w1 > max(sc.r1) and sc.w1 < 64 and sc.b1 > sc.w1, sc.name           # R1 in before MFMA 64
     assert min(sc.dma) - sc.m0_lead >= 0 and min(sc.dma) > sc.b1, sc.name          # DMA after the free barrier
-    assert sc.b2 > sc.w2 and min(sc.r0) > sc.b2 and min(sc.r0) >= 64, sc.name      # R0 regs dead after MFMA 63
+    assert min(sc.r0) >= 64, sc.name                                                # R0 regs dead after MFMA 63
+    assert sc.merged or (sc.b2 > sc.w2 and min(sc.r0) > sc.b2), sc.name
     assert max(sc.r0) < sc.w3 < SLOTS and sc.vk > max(sc.dma), sc.name
     load = {i: 0 for i in range(SLOTS)}
-    for x in sc.r1 + sc.r0 + sc.dma + [d - sc.m0_lead for d in sc.dma] + [sc.w1, sc.b1, sc.w2, sc.b2, sc.vk, sc.w3]:
+    for x in sc.r1 + sc.r0 + sc.dma + [d - sc.m0_lead for d in sc.dma] + [sc.w1, sc.b1, sc.vk, sc.w3] + land:
         load[x] += 1
     assert max(load.values()) <= 2, (sc.name, {k: v for k, v in load.items() if v > 2})
 
@@ -141,12 +150,17 @@ SCHEDULES = {
     "g4d6": make("g4d6", w1_gap=4, dma=(22, 6), w2=86, r0=(88, 2)),
     "g2d6": make("g2d6", w1_gap=2, dma=(20, 6), w2=84, r0=(86, 2)),
     "sp2g4d5": make("sp2g4d5", r1=(0, 2), w1_gap=4, dma=(37, 5), w2=100, r0=(102, 1)),
+    # one barrier per K-tile (w2=None): the landing of tile t+1 is published by the free barrier
+    "m4": make("m4", w1_gap=4, dma=(22, 5), w2=None, r0=(100, 1)),
+    "m4d4": make("m4d4", w1_gap=4, dma=(22, 4), w2=None, r0=(88, 1)),
+    "m4d3": make("m4d3", w1_gap=4, dma=(22, 3), w2=None, r0=(72, 1)),
+    "m6d4": make("m6d4", w1_gap=6, dma=(24, 4), w2=None, r0=(90, 1)),
 }
 
 
 # schedules the persistent kernel is generated for (its SC index = position here)
 PERSISTENT = ["v18", "v18_d6b", "v18_d5_late", "v18_d6b_bout", "v18_d5_late_bout", "g4", "g6", "g8", "sp2g6",
-              "g6d6", "g4d6", "g2d6", "sp2g4d5"]
+              "g6d6", "g4d6", "g2d6", "sp2g4d5", "m4", "m4d4", "m4d3", "m6d4"]
 
 
 def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) -> List[str]:
@@ -160,7 +174,7 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) ->
     for j, s in enumerate(sc.r1):
         isb, x = read_order(j)
         gap[s].append(f"ds_read_b128 {frag_regs(1, isb, x)}, %[{'rb' if isb else 'ra'}{cur}1] offset:{x * 2048}")
-    gap[sc.w1].append("s_waitcnt lgkmcnt(0)")
+    gap[sc.w1].append("s_waitcnt vmcnt(0) lgkmcnt(0)" if sc.merged else "s_waitcnt lgkmcnt(0)")
     gap[sc.b1].append("s_barrier")
     if dma:
         for p, s in enumerate(sc.dma):
@@ -169,9 +183,10 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) ->
             gap[s].append(f"buffer_load_dwordx4 {voff}, {rB if p >= 8 else rA}, %[s{p & 7}] offen lds")
         gap[sc.vk].append(f"v_add_u32_e32 {voff}, {kstep}, {voff}")
     if nx:
-        n = sc.issued_before_w2() if dma else 0
-        gap[sc.w2].append(f"s_waitcnt vmcnt({n})")
-        gap[sc.b2].append("s_barrier")
+        if not sc.merged:
+            n = sc.issued_before_w2() if dma else 0
+            gap[sc.w2].append(f"s_waitcnt vmcnt({n})")
+            gap[sc.b2].append("s_barrier")
         for j, s in enumerate(sc.r0):
             isb, x = read_order(j)
             gap[s].append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}{nxt}0] offset:{x * 2048}")
