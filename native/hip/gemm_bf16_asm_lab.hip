@@ -7,11 +7,17 @@
 //   25  = w4sp v25 (production for short K: persistent, VK)
 //   45  = w4s v45 (production for big square grids: v44 + square cross-XCD raster)
 //   130 + SC = w4ap (persistent) with persistent schedule SC, serpentine K; 133 = schedule 0 without
+//   170 / 171 / 172 / 173 = w4ap with the fused epilogue (EPI=2): g4 serpentine K, g6d6 serpentine, g4 linear,
+//   g4 square raster
+//   160 / 161 = knock-outs (wrong C): 136 without its epilogue / without the epilogue's global stores
 //   150 / 151 = w4ap square raster (SQ) with persistent schedule 5 / 9; 152 = 150 without serpentine K
 // amdgo_asmlab_gemm_fp8 (fp8 e4m3 operands):
 //   15 / 16 / 18 = production q16 (serpentine K), q16 square raster, persistent q16p
 //   200 + SC = q16ap (persistent asm pipeline) with fp8 schedule SC (gemm_fp8_asm_loop.h), linear K
 //   210 + SC = q16ap with serpentine K; 220 + SC = q16ap square raster, serpentine K
+//   240 / 241 / 242 / 243 = q16ap with the fused epilogue (EPI=2): p linear, s1d3 serpentine, p serpentine,
+//   p square raster
+//   230 / 231 = knock-outs: 200 without its epilogue / without the epilogue's global stores
 #include "gemm_bf16_kernels.h"
 #include "gemm_fp8_kernels.h"
 
@@ -94,6 +100,35 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4APSQ_CASE(150, 5, true)
     W4APSQ_CASE(151, 9, true)
     W4APSQ_CASE(152, 5, false)
+    case 173:     // EF square raster, g4, serpentine K
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4, true, true, 2>), dim3(256), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 160: {   // knock-out: v50 (schedule g4, serpentine K) without the epilogue's C stores
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<5, true, false, 1>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 170:     // EF: fused epilogue (EPI=2), schedule g4, serpentine K
+    case 171:     // EF: schedule g6d6
+    case 172: {   // EF: g4, linear K
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      if (v == 170)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4, true, false, 2>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      else if (v == 171)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G6D6, true, false, 2>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4, false, false, 2>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 161: {   // knock-out: v50 with the epilogue but without its global C stores
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<5, true, false, 3>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
     default:
       return (int)hipErrorInvalidValue;
   }
@@ -151,6 +186,30 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     F8AP_CASE(224, 4, true, true)
     F8AP_CASE(225, 5, true, true)
     F8AP_CASE(226, 6, true, true)
+    case 240:     // EF: fused epilogue (EPI=2), schedule p, linear K
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_P, false, false, 2>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 241:     // EF: schedule s1d3, serpentine K
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_S1D3, true, false, 2>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 242:     // EF: schedule p, serpentine K
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_P, true, false, 2>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 243:     // EF: schedule p, square raster, serpentine K
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_P, true, true, 2>), dim3(256), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 231:     // knock-out: 200 with the epilogue but without its global C stores
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<0, false, false, 3>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 230:     // knock-out: q16ap schedule p, linear K, without the epilogue
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<0, false, false, 1>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
     default:
       return (int)hipErrorInvalidValue;
   }

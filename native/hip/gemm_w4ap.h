@@ -28,6 +28,9 @@
 #include "gemm_tile_common.h"
 #include "gemm_bf16_asm_loop.h"
 #include "gemm_fp8_asm_loop.h"
+#ifndef F8EF_LOOP_SELECT
+#define F8EF_LOOP_SELECT(SC) static_assert(SC < 0, "no fp8 fused-epilogue schedule generated");
+#endif
 
 namespace {
 
@@ -41,6 +44,11 @@ namespace {
   "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105",    \
   "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118",    \
   "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127"
+
+#define W4EF_VCLOBBERS                                                                                      \
+  "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236",     \
+  "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249",     \
+  "v250", "v251", "v252", "v253", "v254", "v255"
 
 typedef uint32_t w4a_u32x4 __attribute__((ext_vector_type(4)));
 
@@ -61,8 +69,27 @@ constexpr int W4AP_LDS = 2 * W4AP_BUF + 4 * W4AP_EPI_WAVE;   // 160 KiB
                  [nkstep] "s"(nkstep), [m0b0] "s"(m0b0), [m0b1] "s"(m0b1), [flags] "s"(flags)                    \
                : "memory", "scc", W4A_VCLOBBERS, W4_AGPR_CLOBBERS)
 
+// The fused-epilogue pipeline (EPI=2, tools/gen_bf16_asm_loop.py EF): permuted B-fragment lane offsets
+// (rbe / rbo), the per-row-block C lane offsets cv0..cv7 and the tile's C corner sC; v[224:255] are its
+// epilogue temps.
+#define W4EF_LOOP(TEXT)                                                                                       \
+  asm volatile("s_mov_b32 %[m0save], m0\n\t" TEXT "s_mov_b32 m0, %[m0save]"                                   \
+               : [voff] "+v"(voff_k), [nvoff] "+v"(nvoff), [cnt] "+s"(trips), [m0save] "=&s"(m0save)           \
+               : [ra00] "v"(ra00), [ra01] "v"(ra01), [ra10] "v"(ra10), [ra11] "v"(ra11), [rbe00] "v"(rbe00),    \
+                 [rbo00] "v"(rbo00), [rbe01] "v"(rbe01), [rbo01] "v"(rbo01), [rbe10] "v"(rbe10),                \
+                 [rbo10] "v"(rbo10), [rbe11] "v"(rbe11), [rbo11] "v"(rbo11), [kstep] "s"(kstep), [s0] "s"(so[0]), \
+                 [s1] "s"(so[1]), [s2] "s"(so[2]), [s3] "s"(so[3]), [s4] "s"(so[4]), [s5] "s"(so[5]),            \
+                 [s6] "s"(so[6]), [s7] "s"(so[7]), [rA] "s"(sA), [rB] "s"(sB), [nA] "s"(nA), [nB] "s"(nB),       \
+                 [nkstep] "s"(nkstep), [m0b0] "s"(m0b0), [m0b1] "s"(m0b1), [flags] "s"(flags), [cv0] "v"(cv[0]), \
+                 [cv1] "v"(cv[1]), [cv2] "v"(cv[2]), [cv3] "v"(cv[3]), [cv4] "v"(cv[4]), [cv5] "v"(cv[5]),       \
+                 [cv6] "v"(cv[6]), [cv7] "v"(cv[7]), [sC] "s"(sC)                                               \
+               : "memory", "scc", W4A_VCLOBBERS, W4EF_VCLOBBERS, W4_AGPR_CLOBBERS)
+
 // A, Bt: K-major operands (element size 1 for F8, else 2); C: bf16; smem: W4AP_LDS bytes.
-template <int SC, bool SERP, bool SQ, bool F8>
+// EPI: 0 = the staged epilogue below; 2 = the fused epilogue (the C tile leaves through the last
+// K-tile's MFMA shadow, generated asm); knock-outs (lab only, wrong C): 1 = no epilogue at all,
+// 3 = the staged epilogue without its global stores (prices the stores against the rest).
+template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
                                          __bf16* __restrict__ C, int M, int N, int K, char* smem) {
   constexpr int ESZ = F8 ? 1 : 2;
@@ -130,6 +157,28 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   const uint32_t ra01 = a_base + lane_off[1], rb01 = b_base + lane_off[1];
   const uint32_t ra10 = ra00 + W4AP_BUF, rb10 = rb00 + W4AP_BUF;
   const uint32_t ra11 = ra01 + W4AP_BUF, rb11 = rb01 + W4AP_BUF;
+  // EF (EPI=2): B fragment x, row rho reads panel row 32(x>>1) + 4(x&1) + 8(rho>>2) + (rho&3); even and
+  // odd fragments differ in bit 1 of the chunk swizzle, so each has its own lane offset (the fragment's
+  // 4 KiB step is the read's immediate offset). Lane (g, r) of accumulator pair (m, 2p), (m, 2p+1) then
+  // holds C row 16m + r, columns 32p + 8g .. +7: cv[m] is that row's byte offset from the wave's corner.
+  uint32_t rbe00 = 0, rbo00 = 0, rbe01 = 0, rbo01 = 0, rbe10 = 0, rbo10 = 0, rbe11 = 0, rbo11 = 0;
+  uint32_t cv[8] = {};
+  if constexpr (EPI == 2) {
+    const int rho = lane & 15;
+    const int re = 8 * (rho >> 2) + (rho & 3);
+    uint32_t pe[2], po[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      pe[kk] = b_base + (uint32_t)(re * W4AP_ROW + ((c ^ ((re >> 1) & 7)) << 4));
+      po[kk] = b_base + (uint32_t)((re + 4) * W4AP_ROW + ((c ^ (((re + 4) >> 1) & 7)) << 4));
+    }
+    rbe00 = pe[0]; rbo00 = po[0]; rbe01 = pe[1]; rbo01 = po[1];
+    rbe10 = pe[0] + W4AP_BUF; rbo10 = po[0] + W4AP_BUF; rbe11 = pe[1] + W4AP_BUF; rbo11 = po[1] + W4AP_BUF;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      cv[m] = (uint32_t)(16 * m + rho) * (uint32_t)N * 2u + (uint32_t)(16 * (lane >> 4));
+  }
   char* const stg = smem + 2 * W4AP_BUF + wid * W4AP_EPI_WAVE;
 
   int tm, tn;
@@ -141,7 +190,8 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   uint32_t first = 1;
 
   asm volatile("" ::: W4_AGPR_CLOBBERS);
-  static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
+  if constexpr (EPI != 2)     // EF: every tile's first K-tile starts its accumulators with src C = 0
+    static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
   for (;;) {
     const int next = tile + per;
     const uint32_t hasnext = __builtin_amdgcn_readfirstlane(next < t_end ? 1u : 0u);
@@ -158,7 +208,17 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     uint32_t trips = __builtin_amdgcn_readfirstlane((uint32_t)((ktiles - 2) >> 1));
     uint32_t m0save;
     const uint32_t flags = __builtin_amdgcn_readfirstlane(first | (hasnext << 1));
-    if constexpr (F8) {
+    if constexpr (EPI == 2) {
+      // this tile's C corner for the fused epilogue's stores (wave-uniform)
+      const uint64_t cc = (uint64_t)(uintptr_t)(C + (size_t)(tm * W4AP_TILE + wr * 128) * N + tn * W4AP_TILE + wc * 128);
+      const uint64_t sC = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cc >> 32)) << 32) |
+                          __builtin_amdgcn_readfirstlane((uint32_t)cc);
+      if constexpr (F8) {
+        F8EF_LOOP_SELECT(SC)
+      } else {
+        W4EF_LOOP_SELECT(SC)
+      }
+    } else if constexpr (F8) {
       F8AP_LOOP_SELECT(SC)
     } else {
       W4AP_LOOP_SELECT(SC)
@@ -167,6 +227,11 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     // wave-private epilogue (the K buffers may be receiving the next tile's DMA): 4 passes of
     // 2 fragment rows = 32 C rows x 128 columns through this wave's 8 KiB, accumulators zeroed
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    if constexpr (EPI == 2) {
+      // the asm block stored C; its stores and the next tile's DMA are waited for by count in the next block
+    } else if constexpr (EPI == 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
     if constexpr (F8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     else asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA D -> accvgpr reads
     static_for<0, 4>([&](auto S) {
@@ -202,11 +267,16 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
         uint4 v = raw;
         if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-        *reinterpret_cast<uint4*>(C + (size_t)(tm * W4AP_TILE + wr * 128 + s * 32 + r) * N + tn * W4AP_TILE +
-                                  wc * 128 + ch * 8) = v;
+        if constexpr (EPI == 3) {        // knock-out: keep the value live, skip the global store
+          asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+        } else {
+          *reinterpret_cast<uint4*>(C + (size_t)(tm * W4AP_TILE + wr * 128 + s * 32 + r) * N + tn * W4AP_TILE +
+                                    wc * 128 + ch * 8) = v;
+        }
       }
       asm volatile("" ::: "memory");
     });
+    }
     if (!hasnext) break;
     tile = next;
     tm = ntm;

@@ -182,6 +182,14 @@ def _audit_asm_pipeline(body, st):
     # every K-tile in the asm block is 128 MFMAs fed by 32 fragment reads and 16 LDS-DMA pieces;
     # the persistent form adds the epilogue reads of the next tile's prologue
     assert mfma % 128 == 0 and mfma >= 3 * 128, mfma
+    name = body.split(":", 1)[0]
+    if re.search(r"w4apILi\d+ELb\dELb\dELi2E", name):
+        # fused epilogue (EPI=2): peeled first K-tile pair, loop, two drains whose last K-tiles read
+        # only k-half 1 and store the C tile (32 pair stores each); no compiler epilogue
+        assert mfma == 8 * 128 and reads == 16 + 6 * 32 + 2 * 16, (mfma, reads)
+        assert body.count("global_store_dwordx4") == 2 * 32, body.count("global_store_dwordx4")
+        assert body.count("v_accvgpr_read_b32") == 2 * 256
+        return mfma
     assert reads >= 32 * (mfma // 128) and dma >= 16 * (mfma // 128 - 2), (reads, dma)
     # the loop itself is one asm block: hipcc inserted no hazard padding into it
     for blk in re.findall(r";;#ASMSTART(.*?);;#ASMEND", body, re.S):
@@ -205,7 +213,17 @@ def test_w4a_lab_pipelines(tmp_path_factory):
     kernels = _kernels(asm, "gemm_bf16_256x256_w4a")
     assert len(kernels) >= 10
     for body, st in kernels:
+        if re.search(r"w4apILi\d+ELb\dELb\dELi[13]E", body.split(":", 1)[0]):
+            continue                        # knock-out builds (EPI 1 / 3) drop the epilogue on purpose
         _audit_asm_pipeline(body, st)
+    # the fused-epilogue fp8 kernels: 4 K-tile pairs of 64 MFMAs, C stored from the asm block
+    ef8 = [k for k in _kernels(asm, "gemm_fp8_256x256_q16apI") if re.search(r"Lb\dELb\dELi2E", k[0].split(":", 1)[0])]
+    assert len(ef8) >= 3
+    for body, st in ef8:
+        assert st["NumAgprs"] == 256 and st["ScratchSize"] == 0 and st["Occupancy"] == 1, st
+        _no_compiler_agpr_access(body)
+        assert len(re.findall(r"v_mfma_f32_16x16x128_f8f6f4", body)) == 8 * 64
+        assert body.count("global_store_dwordx4") == 2 * 32 and body.count("v_accvgpr_read_b32") == 2 * 256
 
 
 def test_w4_main_loop_shape(w4):

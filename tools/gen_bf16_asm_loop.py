@@ -254,6 +254,274 @@ def kloop_persistent(sc: Schedule) -> List[str]:
     return out
 
 
+# ---------------------------------------------------------------------------------------------------
+# Fused epilogue (w4ap EPI=2, "EF"): the C tile leaves through the last K-tile's MFMA shadow.
+#
+# The staged epilogue (gemm_w4ap.h, EPI=0) runs after the K pipeline: 256 accvgpr reads, 256 zeroing
+# writes, an LDS round trip and 32 row stores per wave, none of it under an MFMA -- the lab prices it
+# at 4-5 % of an 8192^3 GEMM (profiles/r3_s2). Here:
+#   * B fragment x reads Bt rows 32(x>>1) + 4(x&1) + 8(rho>>2) + (rho&3) for fragment row rho (even /
+#     odd fragments through their own lane offsets rbe / rbo), so a lane of accumulator pair
+#     (m, 2p), (m, 2p+1) holds 8 consecutive C columns 32p + 8g .. +7 of row 16m + (lane & 15):
+#     one 16-byte global store per pair, straight from registers;
+#   * the last K-tile runs its MFMAs so the finals (k-half 1) spread over slots 20..127 -- k-half 0
+#     of accumulators 0..19 first, then k-half 1 interleaved with the rest of k-half 0 (each
+#     accumulator still gets k-half 0 before k-half 1: bitwise the same sums) -- and each final is
+#     followed (>= 3 MFMAs later: the XDL-write -> VALU-read distance) by 4 v_accvgpr_read, 2
+#     v_cvt_pk_bf16_f32 and, per pair, one global_store_dwordx4 in the gaps;
+#   * the next tile's first K-tile issues its k-half-0 MFMAs with src C = 0 (no zeroing writes);
+#   * waits: the entry waits vmcnt(16 + stores) (K-tile 0 landed: younger are K-tile 1's 16 pieces and
+#     this tile's stores), the first K-tile's landing wait counts the stores issued after the last
+#     K-tile-1 piece, so stores have the rest of that K-tile to complete.
+# Physical temps: v[224:239] accumulator reads (4 sets), v[240:255] packed pairs (4 sets).
+EF_T, EF_NT = 224, 4
+EF_P, EF_NP = 240, 4
+EF_FIRST_KH1 = 20          # first slot of a k-half-1 MFMA in the last K-tile (R1 landed at w1 <= 19)
+EF_HAZ = 3                 # accvgpr reads of an accumulator >= this many MFMAs after its final
+
+
+def b_read(r: int, x: int, buf: int) -> str:
+    """EF: B fragment x of k-half r from buffer buf through the permuted lane offsets."""
+    par = "e" if x % 2 == 0 else "o"
+    return f"ds_read_b128 {frag_regs(r, True, x)}, %[rb{par}{buf}{r}] offset:{(x >> 1) * 4096}"
+
+
+def ef_last_order() -> List[tuple]:
+    """(k-half, acc) per slot of the last K-tile: finals spread over slots 20..127."""
+    order = [(0, i) for i in range(EF_FIRST_KH1)]
+    n0, n1 = EF_FIRST_KH1, 0
+    span = SLOTS - EF_FIRST_KH1
+    for s in range(EF_FIRST_KH1, SLOTS):
+        want1 = -(-(s - EF_FIRST_KH1 + 1) * 64 // span)        # ceil: k-half-1 MFMAs due by slot s
+        if (n1 < want1 and n1 < n0) or n0 == 64:
+            order.append((1, n1))
+            n1 += 1
+        else:
+            order.append((0, n0))
+            n0 += 1
+    assert n0 == 64 and n1 == 64 and len(order) == SLOTS
+    first = {}
+    for s, (kh, acc) in enumerate(order):
+        if kh == 0:
+            first[acc] = s
+        else:
+            assert first[acc] < s, acc
+    return order
+
+
+def mfma_op(kh: int, acc: int, zero_c: bool = False) -> str:
+    m, n = acc >> 3, acc & 7
+    c = "0" if zero_c else f"a[{4 * acc}:{4 * acc + 3}]"
+    return f"v_mfma_f32_16x16x32_bf16 a[{4 * acc}:{4 * acc + 3}], {frag_regs(kh, True, n)}, {frag_regs(kh, False, m)}, {c}"
+
+
+def ef_epilogue(order: List[tuple], load: Dict[int, int], cap: int):
+    """Place the epilogue of the last K-tile: returns ({slot: [ops]}, tail ops). Greedy: each op goes
+    to the earliest gap at or after it is ready with fewer than ``cap`` instructions (existing fillers
+    counted by ``load``); what does not fit before the last MFMA runs after it."""
+    final = {acc: s for s, (kh, acc) in enumerate(order) if kh == 1}
+    gaps: Dict[int, List[str]] = {i: [] for i in range(SLOTS)}
+    tail: List[str] = []
+    used = dict(load)
+    where = {}                                   # op id -> position (slot, or SLOTS + tail index)
+
+    def put(op: str, ready: int, key) -> int:
+        for s in range(max(ready, 0), SLOTS):
+            if used.get(s, 0) < cap:
+                gaps[s].append(op)
+                used[s] = used.get(s, 0) + 1
+                where[key] = s
+                return s
+        tail.append(op)
+        where[key] = SLOTS + len(tail)
+        return SLOTS + len(tail)
+
+    accs = sorted(final, key=lambda a: final[a])
+    pair_done = {}
+    tset = 0
+    pset_of = {}
+    npairs = 0
+    last_store_pos = {}                          # P set -> position of its last store
+    last_cvt_pos = {}                            # T set -> position of its last cvt
+    for acc in accs:
+        t = EF_T + 4 * (tset % EF_NT)
+        ready = max(final[acc] + EF_HAZ, last_cvt_pos.get(tset % EF_NT, -1))
+        for k in range(4):
+            ready = put(f"v_accvgpr_read_b32 v{t + k}, a{4 * acc + k}", ready, ("r", acc, k))
+        pair = acc >> 1
+        if pair not in pset_of:
+            pset_of[pair] = npairs % EF_NP
+            npairs += 1
+        ps = pset_of[pair]
+        pbase = EF_P + 4 * ps + 2 * (acc & 1)
+        ready = max(ready, last_store_pos.get(ps, -1))
+        for k in range(2):
+            ready = put(f"v_cvt_pk_bf16_f32 v{pbase + k}, v{t + 2 * k}, v{t + 2 * k + 1}", ready, ("c", acc, k))
+        last_cvt_pos[tset % EF_NT] = ready
+        tset += 1
+        pair_done.setdefault(pair, []).append(ready)
+        if len(pair_done[pair]) == 2:
+            m, p = pair >> 2, pair & 3
+            pos = put(f"global_store_dwordx4 %[cv{m}], v[{EF_P + 4 * ps}:{EF_P + 4 * ps + 3}], %[sC] offset:{64 * p}",
+                      max(pair_done[pair]), ("s", pair))
+            last_store_pos[ps] = pos + 1             # the next cvt into this set at least one op later
+    return gaps, tail
+
+
+def ef_check(lines: List[str]) -> None:
+    """Static audit of the EF last K-tile text: every accumulator read >= EF_HAZ MFMAs (or a
+    16-wait-state pad) after its final MFMA, read -> cvt -> store register flow without a clobber
+    in between, every pair stored exactly once."""
+    import re
+    mf = 0
+    final_at = {}
+    pad = {}
+    treg = {}          # v reg -> (acc, k) last written by an accvgpr read
+    pword = {}         # v reg -> acc of its last cvt
+    stored = set()
+    for ln in lines:
+        if ln.startswith("v_mfma"):
+            mf += 1
+            mm = re.match(r"v_mfma_f32_16x16x32_bf16 a\[(\d+):\d+\], v\[(\d+):", ln)
+            acc = int(mm.group(1)) // 4
+            kh = 1 if int(mm.group(2)) >= 64 else 0
+            if kh == 1:
+                final_at[acc] = mf
+            continue
+        if ln.startswith("s_nop"):
+            pad[mf] = pad.get(mf, 0) + int(ln.split()[1]) + 1
+            continue
+        mm = re.match(r"v_accvgpr_read_b32 v(\d+), a(\d+)", ln)
+        if mm:
+            acc = int(mm.group(2)) // 4
+            assert acc in final_at, ("read before final", acc)
+            dist = mf - final_at[acc]
+            assert dist >= EF_HAZ or pad.get(mf, 0) >= 16, ("hazard", acc, dist)
+            treg[int(mm.group(1))] = (acc, int(mm.group(2)) % 4)
+            continue
+        mm = re.match(r"v_cvt_pk_bf16_f32 v(\d+), v(\d+), v(\d+)", ln)
+        if mm:
+            d, s0, s1 = (int(x) for x in mm.groups())
+            (a0, k0), (a1, k1) = treg[s0], treg[s1]
+            assert a0 == a1 and k1 == k0 + 1 and k0 % 2 == 0, ln
+            assert (d - EF_P) % 4 == 2 * (a0 & 1) + k0 // 2, ln
+            pword[d] = a0
+            continue
+        mm = re.match(r"global_store_dwordx4 %\[cv(\d)\], v\[(\d+):\d+\], %\[sC\] offset:(\d+)", ln)
+        if mm:
+            m, base, off = int(mm.group(1)), int(mm.group(2)), int(mm.group(3))
+            accs = [pword[base + k] for k in range(4)]
+            p = off // 64
+            want = [m * 8 + 2 * p, m * 8 + 2 * p, m * 8 + 2 * p + 1, m * 8 + 2 * p + 1]
+            assert accs == want, (ln, accs, want)
+            stored.add((m, p))
+    assert len(stored) == 32, len(stored)
+
+
+def body_ef(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, zero_c: bool = False,
+            w2_extra: int = 0, last: bool = False, cap: int = 5):
+    """body() for the EF kernel: permuted B reads, optional src-C-zero first K-tile, extra landing-wait
+    count, and (last) the fused epilogue with the spread-final MFMA order. Returns (lines, stores issued
+    after the last DMA piece)."""
+    assert not sc.bout
+    rA, rB, voff, kstep = ("%[nA]", "%[nB]", "%[nvoff]", "%[nkstep]") if nxt_tile else \
+        ("%[rA]", "%[rB]", "%[voff]", "%[kstep]")
+    nxt = 1 - cur
+    gap: Dict[int, List[str]] = {i: [] for i in range(SLOTS)}
+    for j, s in enumerate(sc.r1):
+        isb, x = read_order(j)
+        gap[s].append(b_read(1, x, cur) if isb else f"ds_read_b128 {frag_regs(1, False, x)}, %[ra{cur}1] offset:{x * 2048}")
+    gap[sc.w1].append("s_waitcnt vmcnt(0) lgkmcnt(0)" if sc.merged else "s_waitcnt lgkmcnt(0)")
+    gap[sc.b1].append("s_barrier")
+    if dma:
+        for p, s in enumerate(sc.dma):
+            lead = s - sc.m0_lead
+            gap[lead].append(f"s_mov_b32 m0, %[m0b{cur}]" if p == 0 else f"s_add_u32 m0, m0, {PIECE_STRIDE:#x}")
+            gap[s].append(f"buffer_load_dwordx4 {voff}, {rB if p >= 8 else rA}, %[s{p & 7}] offen lds")
+        gap[sc.vk].append(f"v_add_u32_e32 {voff}, {kstep}, {voff}")
+    if nx:
+        assert not last
+        if not sc.merged:
+            n = (sc.issued_before_w2() if dma else 0) + w2_extra
+            gap[sc.w2].append(f"s_waitcnt vmcnt({n})")
+            gap[sc.b2].append("s_barrier")
+        for j, s in enumerate(sc.r0):
+            isb, x = read_order(j)
+            gap[s].append(b_read(0, x, nxt) if isb else f"ds_read_b128 {frag_regs(0, False, x)}, %[ra{nxt}0] offset:{x * 2048}")
+        gap[sc.w3].append("s_waitcnt lgkmcnt(0)")
+    if last:
+        order = ef_last_order()
+        load = {i: len(gap[i]) for i in range(SLOTS)}
+        egap, tail = ef_epilogue(order, load, cap)
+        for i in range(SLOTS):
+            gap[i] += egap[i]
+    else:
+        order = [(i >> 6, i & 63) for i in range(SLOTS)]
+        tail = []
+    out = []
+    for i in range(SLOTS):
+        kh, acc = order[i]
+        out.append(mfma_op(kh, acc, zero_c and kh == 0))
+        out += gap[i]
+    if tail:
+        out += ["s_nop 7", "s_nop 7"] + tail
+    late = 0
+    if last and dma:
+        seen_last_piece = False
+        for ln in out:
+            if ln.startswith("buffer_load"):
+                seen_last_piece = True
+                late = 0
+            elif ln.startswith("global_store") and seen_last_piece:
+                late += 1
+    elif last:
+        late = sum(ln.startswith("global_store") for ln in out)
+    return out, late
+
+
+def kloop_persistent_ef(sc: Schedule, cap: int = 5) -> List[str]:
+    """kloop_persistent() with the fused epilogue (EPI=2). %[flags] bit 0: first tile of this
+    workgroup (prologue DMA, then vmcnt(0): nothing older is in flight); bit 1: a next tile (the drain
+    DMAs its K-tiles 0 and 1)."""
+    last_nx, late_nx = body_ef(sc, 1, dma=True, nx=False, nxt_tile=True, last=True, cap=cap)
+    last_no, late_no = body_ef(sc, 1, dma=False, nx=False, last=True, cap=cap)
+    ef_check(last_nx)
+    ef_check(last_no)
+    stores = sum(ln.startswith("global_store") for ln in last_nx)
+    assert stores == 32 and 16 + stores <= 63
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lw4ef_entry_%="]
+    out += [x for x in prologue() if not x.startswith("ds_read") and x != "s_waitcnt lgkmcnt(0)"
+            and x != "s_barrier" and not x.startswith("s_waitcnt vmcnt")]
+    out.append("s_waitcnt vmcnt(0)")
+    out.append(".Lw4ef_entry_%=:")
+    out.append(f"s_waitcnt vmcnt({16 + stores})")        # K-tile 0 landed (K-tile 1 + the stores younger)
+    out.append("s_barrier")
+    for j in range(16):
+        isb, x = read_order(j)
+        out.append(b_read(0, x, 0) if isb else f"ds_read_b128 {frag_regs(0, False, x)}, %[ra00] offset:{x * 2048}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += body_ef(sc, 0, dma=True, nx=True, zero_c=True, w2_extra=late_nx)[0]
+    out += body_ef(sc, 1, dma=True, nx=True)[0]
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4ef_drain_%="]
+    out.append(".Lw4ef_loop_%=:")
+    out += body_ef(sc, 0, dma=True, nx=True)[0]
+    out += body_ef(sc, 1, dma=True, nx=True)[0]
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4ef_loop_%="]
+    out.append(".Lw4ef_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lw4ef_last_%="]
+    out += body_ef(sc, 0, dma=True, nx=True, nxt_tile=True)[0]
+    out += last_nx
+    out += ["s_branch .Lw4ef_done_%=", ".Lw4ef_last_%=:"]
+    out += body_ef(sc, 0, dma=False, nx=True)[0]
+    out += last_no
+    out.append(".Lw4ef_done_%=:")
+    return out
+
+
+# schedules the fused-epilogue kernel is generated for (index = EF SC)
+EF = ["g4", "g6d6"]
+
+
 def audit(lines: List[str]) -> Dict[str, int]:
     gaps, cur, worst = [], 0, 0
     for ln in lines:
@@ -288,6 +556,21 @@ def render() -> str:
     for i, n in enumerate(PERSISTENT):
         parts.append(f"#define W4AP_SC_{n.upper()} {i}")
     parts.append("")
+    esel = [f"if constexpr (SC == {i}) W4EF_LOOP(W4EF_ASM_{n.upper()});" for i, n in enumerate(EF)]
+    parts.append("// fused-epilogue persistent kernel (w4ap EPI=2): schedule index -> asm text")
+    parts.append("#define W4EF_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(esel))
+    parts.append("// " + ", ".join(f"{i} = {n}" for i, n in enumerate(EF)))
+    for i, n in enumerate(EF):
+        parts.append(f"#define W4EF_SC_{n.upper()} {i}")
+    parts.append("")
+    for name in EF:
+        lines = kloop_persistent_ef(SCHEDULES[name])
+        parts.append(f"#define W4EF_ASM_{name.upper()} \\")
+        for ln in lines:
+            parts.append(f'  "{ln}\\n\\t" \\')
+        parts.append('  ""')
+        parts.append("")
     for name in PERSISTENT:
         lines = kloop_persistent(SCHEDULES[name])
         parts.append(f"#define W4AP_ASM_{name.upper()} \\")

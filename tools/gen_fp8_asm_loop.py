@@ -58,10 +58,11 @@ def operands(i: int, aslow: bool):
     return bi, ai
 
 
-def mfma(i: int, aslow: bool) -> str:
+def mfma(i: int, aslow: bool, zero_c: bool = False) -> str:
     bi, ai = operands(i, aslow)
     q = ai * 8 + bi
-    return f"v_mfma_f32_16x16x128_f8f6f4 a[{4 * q}:{4 * q + 3}], {frag(True, bi)}, {frag(False, ai)}, a[{4 * q}:{4 * q + 3}]"
+    c = "0" if zero_c else f"a[{4 * q}:{4 * q + 3}]"
+    return f"v_mfma_f32_16x16x128_f8f6f4 a[{4 * q}:{4 * q + 3}], {frag(True, bi)}, {frag(False, ai)}, {c}"
 
 
 def last_use(aslow: bool) -> Dict[tuple, int]:
@@ -167,14 +168,24 @@ SCHEDULES["md3"] = make("md3", r1=list(range(16)), w1=19, dma=[21 + 3 * p for p 
 PERSISTENT = list(SCHEDULES)
 
 
-def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) -> List[str]:
+def rd(isb: bool, x: int, h: int, buf: int, ef: bool) -> str:
+    """ds_read of fragment half (isb, x, h) from buffer buf; ef: B through the permuted lane offsets
+    (gemm_w4ap.h EPI=2: fragment x reads Bt rows 32(x>>1) + 4(x&1) + 8(rho>>2) + (rho&3))."""
+    if ef and isb:
+        return f"ds_read_b128 {half(isb, x, h)}, %[rb{'e' if x % 2 == 0 else 'o'}{buf}{h}] offset:{(x >> 1) * 4096}"
+    return f"ds_read_b128 {half(isb, x, h)}, %[{'rb' if isb else 'ra'}{buf}{h}] offset:{x * 2048}"
+
+
+def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, ef: bool = False,
+         zero_c: bool = False, w2_extra: int = 0, last: bool = False, cap: int = 7) -> List[str]:
+    """One K-tile. EF kernel (ef): permuted B reads; zero_c: src C = 0 (the tile's first K-tile);
+    w2_extra: stores younger than the landing pieces; last: the fused epilogue in the gaps."""
     rA, rB, voff, kstep = ("%[nA]", "%[nB]", "%[nvoff]", "%[nkstep]") if nxt_tile else \
         ("%[rA]", "%[rB]", "%[voff]", "%[kstep]")
     nxt = 1 - cur
     gap: Dict[int, List[tuple]] = {i: [] for i in range(SLOTS)}
     for (isb, x, h), s in zip(R1_ORDER, sc.r1):
-        gap[s].append(("read", (isb, x), f"ds_read_b128 {half(isb, x, h)}, %[{'rb' if isb else 'ra'}{cur}{h}] "
-                                         f"offset:{x * 2048}"))
+        gap[s].append(("read", (isb, x), rd(isb, x, h, cur, ef)))
     gap[sc.w1].append(("lgk0", None, "s_waitcnt vmcnt(0) lgkmcnt(0)" if sc.merged else "s_waitcnt lgkmcnt(0)"))
     gap[sc.b1].append(("op", None, "s_barrier"))
     if dma:
@@ -185,13 +196,19 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) ->
         gap[sc.vk].append(("op", None, f"v_add_u32_e32 {voff}, {kstep}, {voff}"))
     if nx:
         if not sc.merged:
-            n = sc.issued_before_w2() if dma else 0
+            n = (sc.issued_before_w2() if dma else 0) + w2_extra
             gap[sc.w2].append(("op", None, f"s_waitcnt vmcnt({n})"))
             gap[sc.b2].append(("op", None, "s_barrier"))
         for (isb, x, h), s in zip(R0_ORDER, sc.r0):
-            gap[s].append(("read", None, f"ds_read_b128 {half(isb, x, h)}, %[{'rb' if isb else 'ra'}{nxt}{h}] "
-                                         f"offset:{x * 2048}"))
+            gap[s].append(("read", None, rd(isb, x, h, nxt, ef)))
     gap[sc.w3].append(("lgk0", None, "s_waitcnt lgkmcnt(0)"))
+    tail: List[str] = []
+    if last:
+        assert ef and not nx
+        load = {i: len(gap[i]) for i in range(SLOTS)}
+        egap, tail = ef_epilogue([operands(i, sc.aslow) for i in range(SLOTS)], load, cap)
+        for i in range(SLOTS):
+            gap[i] += [("op", None, t) for t in egap[i]]
     # simulate the LDS queue: before each MFMA, wait for the reads of this K-tile it consumes
     out: List[str] = []
     queue: List[object] = []           # in-flight LDS reads in issue order (fragment key or None)
@@ -203,13 +220,15 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) ->
             n = len(queue) - last - 1
             out.append(f"s_waitcnt lgkmcnt({n})")
             queue = queue[last + 1:]
-        out.append(mfma(i, sc.aslow))
+        out.append(mfma(i, sc.aslow, zero_c))
         for kind, key, text in gap[i]:
             out.append(text)
             if kind == "read":
                 queue.append(key)
             elif kind == "lgk0":
                 queue = []
+    if tail:
+        out += ["s_nop 7", "s_nop 7"] + tail
     return out
 
 
@@ -253,6 +272,139 @@ def kloop_persistent(sc: Schedule) -> List[str]:
     return out
 
 
+# ---------------------------------------------------------------------------------------------------
+# Fused epilogue (w4ap EPI=2, "EF"; the bf16 design in tools/gen_bf16_asm_loop.py). In the fp8 K-tile
+# every accumulator gets exactly one MFMA, so in the last K-tile each slot finalises one accumulator:
+# its 4 accvgpr reads (>= EF_HAZ MFMAs later: 16x16x128 f8 is an 8-pass XDL op), 2 cvts and, per
+# accumulator pair (bi even / odd, same ai), one 16-byte store go into the following gaps.
+EF_T, EF_NT = 224, 4
+EF_P, EF_NP = 240, 4
+EF_HAZ = 2
+
+
+def ef_epilogue(order: List[tuple], load: Dict[int, int], cap: int):
+    """order: (bi, ai) per slot. Same greedy placement as the bf16 generator."""
+    final = {ai * 8 + bi: s for s, (bi, ai) in enumerate(order)}
+    gaps: Dict[int, List[str]] = {i: [] for i in range(SLOTS)}
+    tail: List[str] = []
+    used = dict(load)
+
+    def put(op: str, ready: int) -> int:
+        for s in range(max(ready, 0), SLOTS):
+            if used.get(s, 0) < cap:
+                gaps[s].append(op)
+                used[s] = used.get(s, 0) + 1
+                return s
+        tail.append(op)
+        return SLOTS + len(tail)
+
+    pair_done, pset_of, last_store, last_cvt = {}, {}, {}, {}
+    for n_acc, acc in enumerate(sorted(final, key=lambda a: final[a])):
+        ts = n_acc % EF_NT
+        t = EF_T + 4 * ts
+        ready = max(final[acc] + EF_HAZ, last_cvt.get(ts, -1))
+        for k in range(4):
+            ready = put(f"v_accvgpr_read_b32 v{t + k}, a{4 * acc + k}", ready)
+        pair = acc >> 1
+        if pair not in pset_of:
+            pset_of[pair] = len(pset_of) % EF_NP
+        ps = pset_of[pair]
+        pbase = EF_P + 4 * ps + 2 * (acc & 1)
+        ready = max(ready, last_store.get(ps, -1))
+        for k in range(2):
+            ready = put(f"v_cvt_pk_bf16_f32 v{pbase + k}, v{t + 2 * k}, v{t + 2 * k + 1}", ready)
+        last_cvt[ts] = ready
+        pair_done.setdefault(pair, []).append(ready)
+        if len(pair_done[pair]) == 2:
+            m, p = pair >> 2, pair & 3
+            pos = put(f"global_store_dwordx4 %[cv{m}], v[{EF_P + 4 * ps}:{EF_P + 4 * ps + 3}], %[sC] offset:{64 * p}",
+                      max(pair_done[pair]))
+            last_store[ps] = pos + 1
+    return gaps, tail
+
+
+def ef_check(lines: List[str]) -> None:
+    """Static audit of an EF last K-tile (see the bf16 generator's ef_check)."""
+    import re
+    mf, final_at, pad, treg, pword, stored = 0, {}, {}, {}, {}, set()
+    for ln in lines:
+        if ln.startswith("v_mfma"):
+            mf += 1
+            final_at[int(re.match(r"v_mfma\S* a\[(\d+):", ln).group(1)) // 4] = mf
+            continue
+        if ln.startswith("s_nop"):
+            pad[mf] = pad.get(mf, 0) + int(ln.split()[1]) + 1
+            continue
+        mm = re.match(r"v_accvgpr_read_b32 v(\d+), a(\d+)", ln)
+        if mm:
+            acc = int(mm.group(2)) // 4
+            assert acc in final_at and (mf - final_at[acc] >= EF_HAZ or pad.get(mf, 0) >= 16), ("hazard", acc)
+            treg[int(mm.group(1))] = (acc, int(mm.group(2)) % 4)
+            continue
+        mm = re.match(r"v_cvt_pk_bf16_f32 v(\d+), v(\d+), v(\d+)", ln)
+        if mm:
+            d, s0, s1 = (int(x) for x in mm.groups())
+            (a0, k0), (a1, k1) = treg[s0], treg[s1]
+            assert a0 == a1 and k1 == k0 + 1 and k0 % 2 == 0 and (d - EF_P) % 4 == 2 * (a0 & 1) + k0 // 2, ln
+            pword[d] = a0
+            continue
+        mm = re.match(r"global_store_dwordx4 %\[cv(\d)\], v\[(\d+):\d+\], %\[sC\] offset:(\d+)", ln)
+        if mm:
+            m, base, p = int(mm.group(1)), int(mm.group(2)), int(mm.group(3)) // 64
+            q = m * 8 + 2 * p
+            assert [pword[base + k] for k in range(4)] == [q, q, q + 1, q + 1], ln
+            stored.add((m, p))
+    assert len(stored) == 32, len(stored)
+
+
+def late_stores(lines: List[str]) -> int:
+    """Stores issued after the last DMA piece of a K-tile text."""
+    late = 0
+    for ln in lines:
+        if ln.startswith("buffer_load"):
+            late = 0
+        elif ln.startswith("global_store"):
+            late += 1
+    return late
+
+
+def kloop_persistent_ef(sc: Schedule, cap: int = 7) -> List[str]:
+    last_nx = body(sc, 1, dma=True, nx=False, nxt_tile=True, ef=True, last=True, cap=cap)
+    last_no = body(sc, 1, dma=False, nx=False, ef=True, last=True, cap=cap)
+    ef_check(last_nx)
+    ef_check(last_no)
+    stores = sum(ln.startswith("global_store") for ln in last_nx)
+    assert stores == 32
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lf8ef_entry_%="]
+    out += prologue()
+    out += ["s_waitcnt vmcnt(0)"]
+    out.append(".Lf8ef_entry_%=:")
+    out.append(f"s_waitcnt vmcnt({16 + stores})")
+    out.append("s_barrier")
+    out += [rd(isb, x, h, 0, True) for isb, x, h in R0_ORDER]
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += body(sc, 0, dma=True, nx=True, ef=True, zero_c=True, w2_extra=late_stores(last_nx))
+    out += body(sc, 1, dma=True, nx=True, ef=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8ef_drain_%="]
+    out.append(".Lf8ef_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True, ef=True)
+    out += body(sc, 1, dma=True, nx=True, ef=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8ef_loop_%="]
+    out.append(".Lf8ef_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lf8ef_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True, ef=True)
+    out += last_nx
+    out += ["s_branch .Lf8ef_done_%=", ".Lf8ef_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True, ef=True)
+    out += last_no
+    out.append(".Lf8ef_done_%=:")
+    return out
+
+
+# schedules the fused-epilogue kernel is generated for (index = EF SC)
+EF = ["p", "s1d3"]
+
+
 def audit(lines: List[str]) -> Dict[str, int]:
     gaps, cur = [], 0
     for ln in lines:
@@ -276,6 +428,21 @@ def render() -> str:
     for i, n in enumerate(PERSISTENT):
         parts.append(f"#define F8AP_SC_{n.upper()} {i}")
     parts.append("")
+    esel = [f"if constexpr (SC == {i}) W4EF_LOOP(F8EF_ASM_{n.upper()});" for i, n in enumerate(EF)]
+    parts.append("// fused-epilogue persistent kernel (q16ap EPI=2): schedule index -> asm text (W4EF_LOOP)")
+    parts.append("#define F8EF_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(esel))
+    parts.append("// " + ", ".join(f"{i} = {n}" for i, n in enumerate(EF)))
+    for i, n in enumerate(EF):
+        parts.append(f"#define F8EF_SC_{n.upper()} {i}")
+    parts.append("")
+    for name in EF:
+        lines = kloop_persistent_ef(SCHEDULES[name])
+        parts.append(f"#define F8EF_ASM_{name.upper()} \\")
+        for ln in lines:
+            parts.append(f'  "{ln}\\n\\t" \\')
+        parts.append('  ""')
+        parts.append("")
     for name in PERSISTENT:
         lines = kloop_persistent(SCHEDULES[name])
         a = audit(lines)
