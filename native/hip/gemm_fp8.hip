@@ -11,8 +11,15 @@
 //       v17 (q16 without serpentine K) on devices without 256 CUs; v18 (persistent q16: the next
 //       tile's prologue DMA under the current tile's last K-tiles) for 2048 <= K <= 8192 with >= 4
 //       tiles per CU (8192^3 +0.7-1.2 %, 16384^2x4096 +2.9 %; profiles/r2_fp8_q16/sweep_q16p*.jsonl).
-//   10 / 15 / 16 / 17 / 18 = that kernel pinned (no automatic switch; falls back when the shape or
-//       the device cannot run it).
+//   20 / 21 (round 3, the default on the 256-CU MI355X for K a multiple of 256, K >= 512): q16ap, the
+//       q16 K-tile body as one hand-scheduled asm block per output tile in the persistent frame of
+//       the bf16 v50 (gemm_w4ap.h, tools/gen_fp8_asm_loop.py): v20 schedule p, linear K; v21 the same
+//       on the square cross-XCD raster with serpentine K, for >= 8 dispatch waves on 16x16-tile
+//       multiples. Against hipBLASLt fp8 on MI355X (profiles/r3_s2/): 8192^3 1.005-1.021x (q16p
+//       0.974-0.981x), 4096^3 1.04x, 16384^3 1.03x (v21), 16384^2x2048 1.05x (v21), 16384^2x1024
+//       1.09x (v21), 16384x8192x8192 1.00x.
+//   10 / 15 / 16 / 17 / 18 / 20 / 21 = that kernel pinned (no automatic switch; falls back when the
+//       shape or the device cannot run it).
 // q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
 // (profiles/r2_fp8_q16/): 8192^3 +5.3 %, 16384^3 +3.1 %, 4096^3 +4.1 %, 16384x8192x8192 +2.2 %.
 // Fast path: M % 256 == 0, N % 256 == 0, K % 128 == 0, K >= 256; otherwise the generic kernel.
@@ -32,7 +39,10 @@ static int resolve_fp8_variant(int M, int N, int K) {
   const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;     // persistent grid: one WG per CU
   const bool sq = (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0;
   int v = g_fp8_variant;
-  if (v == 0) {
+  const bool ap_ok = cus == 256 && K % (2 * F8_BK) == 0 && K >= 4 * F8_BK && pgrid >= NXCD;
+  if (v == 0 && ap_ok) {
+    v = (sq && nwg >= 8 * cus) ? 21 : 20;
+  } else if (v == 0) {
     v = sq ? 16 : 15;
     // Short K (<= 12 K-tiles) with several tiles per CU: the persistent block-scaled kernel hides
     // each tile's prologue and epilogue under the neighbouring K-loops; up to 64 K-tiles with >= 4
@@ -41,6 +51,8 @@ static int resolve_fp8_variant(int M, int N, int K) {
     if (K <= 12 * F8_BK && nwg >= 2 * cus) v = 10;
     else if (K <= 64 * F8_BK && nwg >= 4 * cus) v = 18;
   }
+  if ((v == 20 || v == 21) && !ap_ok) v = sq ? 16 : 15;
+  if (v == 21 && !sq) v = 20;
   if (v == 16 && !sq) v = 15;
   if ((v == 10 || v == 18) && pgrid < NXCD) v = 15;
   if ((v == 15 || v == 16) && cus != 256) v = 17;   // serpentine K assumes 32 co-resident tiles per XCD
@@ -51,7 +63,8 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
-  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18) return (int)hipErrorInvalidValue;
+  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21)
+    return (int)hipErrorInvalidValue;
   g_fp8_variant = v;
   return 0;
 }
@@ -75,6 +88,14 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
       break;
     case 18:
       hipLaunchKernelGGL((gemm_fp8_256x256_q16p<>), dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 20:
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, false, false>), dim3(pgrid), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 21:
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, true, true>), dim3(256), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
       break;
     case 15:
       hipLaunchKernelGGL(Q16(32, false), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
