@@ -9,6 +9,7 @@
 //   130 + SC = w4ap (persistent) with persistent schedule SC, serpentine K; 133 = schedule 0 without
 //   170 / 171 / 172 / 173 = w4ap with the fused epilogue (EPI=2): g4 serpentine K, g6d6 serpentine, g4 linear,
 //   g4 square raster
+//   162 = v50 (136) with nontemporal C stores; 174 = 170 with nontemporal stores
 //   160 / 161 = knock-outs (wrong C): 136 without its epilogue / without the epilogue's global stores
 //   150 / 151 = w4ap square raster (SQ) with persistent schedule 5 / 9; 152 = 150 without serpentine K
 // amdgo_asmlab_gemm_fp8 (fp8 e4m3 operands):
@@ -17,6 +18,7 @@
 //   210 + SC = q16ap with serpentine K; 220 + SC = q16ap square raster, serpentine K
 //   240 / 241 / 242 / 243 = q16ap with the fused epilogue (EPI=2): p linear, s1d3 serpentine, p serpentine,
 //   p square raster
+//   232 = 200 with nontemporal C stores; 244 = 240 with nontemporal stores
 //   230 / 231 = knock-outs: 200 without its epilogue / without the epilogue's global stores
 #include "gemm_bf16_kernels.h"
 #include "gemm_fp8_kernels.h"
@@ -112,6 +114,7 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     }
     case 170:     // EF: fused epilogue (EPI=2), schedule g4, serpentine K
     case 171:     // EF: schedule g6d6
+    case 174:     // EF g4 with nontemporal stores
     case 172: {   // EF: g4, linear K
       const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
       if (g < NXCD) return (int)hipErrorInvalidValue;
@@ -119,8 +122,16 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
         hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4, true, false, 2>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       else if (v == 171)
         hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G6D6, true, false, 2>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      else if (v == 174)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4_NT, true, false, 2>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       else
         hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4, false, false, 2>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 162: {   // v50 with nontemporal C stores in the staged epilogue
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<5, true, false, 4>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     }
     case 161: {   // knock-out: v50 with the epilogue but without its global C stores
@@ -201,6 +212,14 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     case 243:     // EF: schedule p, square raster, serpentine K
       if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_P, true, true, 2>), dim3(256), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 232:     // 200 with nontemporal C stores
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<0, false, false, 4>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 244:     // EF p with nontemporal stores
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_P_NT, false, false, 2>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 231:     // knock-out: 200 with the epilogue but without its global C stores
       if (g < NXCD) return (int)hipErrorInvalidValue;

@@ -258,7 +258,7 @@ gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
     const int gr = PA ? 32 * (r & 7) + (r >> 3) : r;           // LDS slot -> panel row (PA)
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + gr) * N + tn * BN + ch * 8) = v;
+    store_c16(C + (size_t)(tm * BM + gr) * N + tn * BN + ch * 8, v);
   }
 }
 // w4t: the w4s kernel with the whole K-tile schedule taken from a schedule class SC, so the
@@ -578,7 +578,7 @@ gemm_bf16_256x256_w4t(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+    store_c16(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8, v);
   }
 }
 
@@ -696,7 +696,7 @@ gemm_bf16_256x256_w4a(const __bf16* __restrict__ A, const __bf16* __restrict__ B
     const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8) = v;
+    store_c16(C + (size_t)(tm * BM + r) * N + tn * BN + ch * 8, v);
   }
 }
 
@@ -859,7 +859,7 @@ gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ 
         const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
         uint4 v = raw;
         if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * BM + wr * 128 + s * 32 + r) * N + tn_ * BN + wc * 128 + ch * 8) = v;
+        store_c16(C + (size_t)(tm_ * BM + wr * 128 + s * 32 + r) * N + tn_ * BN + wc * 128 + ch * 8, v);
       }
       asm volatile("" ::: "memory");
     });

@@ -13,7 +13,8 @@
 //       tiles per CU (8192^3 +0.7-1.2 %, 16384^2x4096 +2.9 %; profiles/r2_fp8_q16/sweep_q16p*.jsonl).
 //   20 / 21 (round 3, the default on the 256-CU MI355X for K a multiple of 256, K >= 512): q16ap, the
 //       q16 K-tile body as one hand-scheduled asm block per output tile in the persistent frame of
-//       the bf16 v50 (gemm_w4ap.h, tools/gen_fp8_asm_loop.py): v20 schedule p, linear K; v21 the same
+//       the bf16 v50 (gemm_w4ap.h, tools/gen_fp8_asm_loop.py), nontemporal C stores (4096^3 +4.9 %,
+//       16384^2x1024 +6.6 %): v20 schedule p, linear K; v21 the same
 //       on the square cross-XCD raster with serpentine K, for >= 8 dispatch waves on 16x16-tile
 //       multiples. Against hipBLASLt fp8 on MI355X (profiles/r3_s2/): 8192^3 1.005-1.021x (q16p
 //       0.974-0.981x), 4096^3 1.04x, 16384^3 1.03x (v21), 16384^2x2048 1.05x (v21), 16384^2x1024
@@ -90,11 +91,11 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
       hipLaunchKernelGGL((gemm_fp8_256x256_q16p<>), dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 20:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, false, false>), dim3(pgrid), dim3(F8_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, false, false, W4AP_EPI_STAGED_NT>), dim3(pgrid), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 21:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, true, true>), dim3(256), dim3(F8_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, true, true, W4AP_EPI_STAGED_NT>), dim3(256), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 15:

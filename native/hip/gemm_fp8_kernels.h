@@ -260,7 +260,7 @@ gemm_fp8_256x256_w4s(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
     const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * F8_BM + r) * N + tn * F8_BN + ch * 8) = v;
+    store_c16(C + (size_t)(tm * F8_BM + r) * N + tn * F8_BN + ch * 8, v);
   }
 }
 
@@ -465,7 +465,7 @@ gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
     const uint4 raw = *reinterpret_cast<const uint4*>(smem + r * CROW + ((pg & ~1) << 3));
     uint4 v = raw;
     if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-    *reinterpret_cast<uint4*>(C + (size_t)(tm * F8_BM + r) * N + tn * F8_BN + ch * 8) = v;
+    store_c16(C + (size_t)(tm * F8_BM + r) * N + tn * F8_BN + ch * 8, v);
   }
 }
 
@@ -633,8 +633,8 @@ gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__
         const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
         uint4 v = raw;
         if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * F8_BM + wr * 128 + im * 32 + r) * N + tn_ * F8_BN +
-                                  wc * 128 + ch * 8) = v;
+        store_c16(C + (size_t)(tm_ * F8_BM + wr * 128 + im * 32 + r) * N + tn_ * F8_BN +
+                                  wc * 128 + ch * 8, v);
       }
       asm volatile("" ::: "memory");
     });
@@ -837,8 +837,8 @@ gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__
         const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
         uint4 v = raw;
         if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
-        *reinterpret_cast<uint4*>(C + (size_t)(tm_ * F8_BM + wr * 128 + p * 32 + r) * N + tn_ * F8_BN +
-                                  wc * 128 + ch * 8) = v;
+        store_c16(C + (size_t)(tm_ * F8_BM + wr * 128 + p * 32 + r) * N + tn_ * F8_BN +
+                                  wc * 128 + ch * 8, v);
       }
       asm volatile("" ::: "memory");
     });

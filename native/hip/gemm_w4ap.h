@@ -85,10 +85,18 @@ constexpr int W4AP_LDS = 2 * W4AP_BUF + 4 * W4AP_EPI_WAVE;   // 160 KiB
                  [cv6] "v"(cv[6]), [cv7] "v"(cv[7]), [sC] "s"(sC)                                               \
                : "memory", "scc", W4A_VCLOBBERS, W4EF_VCLOBBERS, W4_AGPR_CLOBBERS)
 
+// Epilogue forms (EPI template argument of w4ap_run and its kernels).
+constexpr int W4AP_EPI_STAGED = 0;      // LDS-staged row stores
+constexpr int W4AP_EPI_KO_NONE = 1;     // lab knock-out: no epilogue (wrong C)
+constexpr int W4AP_EPI_FUSED = 2;       // C stored from the last K-tile's MFMA gaps (generated asm)
+constexpr int W4AP_EPI_KO_NOSTORE = 3;  // lab knock-out: staged epilogue without the global stores
+constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores: production (profiles/r3_s2/)
+
 // A, Bt: K-major operands (element size 1 for F8, else 2); C: bf16; smem: W4AP_LDS bytes.
 // EPI: 0 = the staged epilogue below; 2 = the fused epilogue (the C tile leaves through the last
 // K-tile's MFMA shadow, generated asm); knock-outs (lab only, wrong C): 1 = no epilogue at all,
-// 3 = the staged epilogue without its global stores (prices the stores against the rest).
+// 3 = the staged epilogue without its global stores (prices the stores against the rest);
+// 4 = the staged epilogue with nontemporal stores.
 template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
                                          __bf16* __restrict__ C, int M, int N, int K, char* smem) {
@@ -211,8 +219,9 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     if constexpr (EPI == 2) {
       // this tile's C corner for the fused epilogue's stores (wave-uniform)
       const uint64_t cc = (uint64_t)(uintptr_t)(C + (size_t)(tm * W4AP_TILE + wr * 128) * N + tn * W4AP_TILE + wc * 128);
-      const uint64_t sC = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cc >> 32)) << 32) |
-                          __builtin_amdgcn_readfirstlane((uint32_t)cc);
+      // readfirstlane returns int: widen through uint32_t, or bit 31 of the low word sign-extends
+      const uint64_t sC = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cc >> 32)) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cc);
       if constexpr (F8) {
         F8EF_LOOP_SELECT(SC)
       } else {
@@ -269,6 +278,11 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
         if constexpr (EPI == 3) {        // knock-out: keep the value live, skip the global store
           asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+        } else if constexpr (EPI == 4) {   // nontemporal (streaming) C stores: global_store ... nt
+          w4a_u32x4 nv;
+          nv[0] = v.x; nv[1] = v.y; nv[2] = v.z; nv[3] = v.w;
+          __builtin_nontemporal_store(nv, reinterpret_cast<w4a_u32x4*>(C + (size_t)(tm * W4AP_TILE + wr * 128 + s * 32 + r) * N +
+                                                                       tn * W4AP_TILE + wc * 128 + ch * 8));
         } else {
           *reinterpret_cast<uint4*>(C + (size_t)(tm * W4AP_TILE + wr * 128 + s * 32 + r) * N + tn * W4AP_TILE +
                                     wc * 128 + ch * 8) = v;

@@ -107,4 +107,16 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// A 16-byte C store with the nontemporal (streaming) hint: `global_store_dwordx4 ... nt`. The C tile is
+// written once and never re-read by the kernel; streaming it keeps the write-allocated lines from
+// filling L2 under the operand panels and shortens the wait on the stores (the next tile's landing
+// wait, the end-of-kernel release): persistent asm pipeline +1.1 % at 8192^3, +6.3 % with one
+// dispatch wave (4096^2x16384), fp8 +4.9 % at 4096^3 (profiles/r3_s2/nt_*.jsonl).
+__device__ __forceinline__ void store_c16(void* p, uint4 v) {
+  typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+  u32x4_nt x;
+  x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4_nt*>(p));
+}
+
 }  // namespace

@@ -519,7 +519,8 @@ def kloop_persistent_ef(sc: Schedule, cap: int = 5) -> List[str]:
 
 
 # schedules the fused-epilogue kernel is generated for (index = EF SC)
-EF = ["g4", "g6d6"]
+EF = ["g4", "g6d6", "g4_nt"]
+# a name ending in _nt: the same schedule with nontemporal C stores (global_store ... nt)
 
 
 def audit(lines: List[str]) -> Dict[str, int]:
@@ -565,7 +566,9 @@ def render() -> str:
         parts.append(f"#define W4EF_SC_{n.upper()} {i}")
     parts.append("")
     for name in EF:
-        lines = kloop_persistent_ef(SCHEDULES[name])
+        lines = kloop_persistent_ef(SCHEDULES[name.split("_")[0]])
+        if name.endswith("_nt"):
+            lines = [ln + " nt" if ln.startswith("global_store") else ln for ln in lines]
         parts.append(f"#define W4EF_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')

@@ -402,7 +402,8 @@ def kloop_persistent_ef(sc: Schedule, cap: int = 7) -> List[str]:
 
 
 # schedules the fused-epilogue kernel is generated for (index = EF SC)
-EF = ["p", "s1d3"]
+EF = ["p", "s1d3", "p_nt"]
+# a name ending in _nt: the same schedule with nontemporal C stores (global_store ... nt)
 
 
 def audit(lines: List[str]) -> Dict[str, int]:
@@ -437,7 +438,9 @@ def render() -> str:
         parts.append(f"#define F8EF_SC_{n.upper()} {i}")
     parts.append("")
     for name in EF:
-        lines = kloop_persistent_ef(SCHEDULES[name])
+        lines = kloop_persistent_ef(SCHEDULES[name.split("_")[0]])
+        if name.endswith("_nt"):
+            lines = [ln + " nt" if ln.startswith("global_store") else ln for ln in lines]
         parts.append(f"#define F8EF_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
