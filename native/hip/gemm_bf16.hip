@@ -21,7 +21,7 @@
 // and knock-out timings live in the tools-only gemm_bf16_lab.hip.
 //   0  = automatic (default): on the 256-CU MI355X with a power-of-two K >= 256, the persistent asm
 //        K pipeline -- v50, v51 (square raster: >= 8 dispatch waves, K >= 8192, 16x16-tile
-//        multiples), v52 (one or two dispatch waves, K >= 8192); otherwise v44, v25 for K <= 4096
+//        multiples), v52 (one or two dispatch waves, K >= 32768); otherwise v44, v25 for K <= 4096
 //        with >= 2 tiles per CU, v45 for >= 8 dispatch waves with K >= 8192 on 16x16-tile
 //        multiples; v42 / v18 on devices without 256 CUs.
 //   47 / 48 = v44 / v45 with permuted A-panel DMA rows (PA), the default when K is not a power of two.
@@ -70,10 +70,11 @@ static int resolve_variant(int M, int N, int K) {
     // ahead of v44 and v25 on every measured shape (8192^3 +2-3 %, 8192^2x2048 +7 %,
     // 16384^2x1024 +14 % over v44); its square-raster form v51 for >= 8 dispatch waves with long K
     // (16384^3 1.01x hipBLASLt, v45 0.98x); the DMA-spaced schedule v52 for one or two dispatch
-    // waves with long K (4096^2x16384 +0.9 %, 4096x8192x8192 +1.7 % over v50).
+    // waves with very long K (with nontemporal C stores: 4096^2x32768 +1.0 % over v50, but v50 ahead
+    // at 4096^2x16384 by 1.9 % and at 4096x8192x8192 by 0.5 %; profiles/r3_s2/longk_bf16.jsonl).
     v = 50;
     if (sq && nwg >= 8 * cus && K >= 128 * BK) v = 51;
-    else if (nwg <= 2 * cus && K >= 128 * BK) v = 52;
+    else if (nwg <= 2 * cus && K >= 512 * BK) v = 52;
   } else if (v == 0) {
     v = 44;
     // Short K (K-loop of <= 64 K-tiles) with several tiles per CU: the persistent v25 hides each

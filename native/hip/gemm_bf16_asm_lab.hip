@@ -6,9 +6,11 @@
 //   120 = w4a schedule 0 without serpentine K
 //   25  = w4sp v25 (production for short K: persistent, VK)
 //   45  = w4s v45 (production for big square grids: v44 + square cross-XCD raster)
+// (every w4ap / q16ap case below uses the production nontemporal-store epilogue unless it says otherwise)
 //   130 + SC = w4ap (persistent) with persistent schedule SC, serpentine K; 133 = schedule 0 without
 //   170 / 171 / 172 / 173 = w4ap with the fused epilogue (EPI=2): g4 serpentine K, g6d6 serpentine, g4 linear,
 //   g4 square raster
+//   180 / 181 / 182 = relaxed first landing wait (_rw): g4 (= v50 + rw), g6d6 (v52 + rw), g4 square raster (v51 + rw)
 //   162 = v50 (136) with nontemporal C stores; 174 = 170 with nontemporal stores
 //   160 / 161 = knock-outs (wrong C): 136 without its epilogue / without the epilogue's global stores
 //   150 / 151 = w4ap square raster (SQ) with persistent schedule 5 / 9; 152 = 150 without serpentine K
@@ -18,6 +20,8 @@
 //   210 + SC = q16ap with serpentine K; 220 + SC = q16ap square raster, serpentine K
 //   240 / 241 / 242 / 243 = q16ap with the fused epilogue (EPI=2): p linear, s1d3 serpentine, p serpentine,
 //   p square raster
+//   250 / 251 / 252 / 253 = q16ap relaxed first landing wait: p linear (v20 + rw), s1d3 serpentine, p square
+//   raster (v21 + rw), p serpentine
 //   232 = 200 with nontemporal C stores; 244 = 240 with nontemporal stores
 //   230 / 231 = knock-outs: 200 without its epilogue / without the epilogue's global stores
 #include "gemm_bf16_kernels.h"
@@ -72,7 +76,7 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     case V: {                                                                                             \
       const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;                   \
       if (g < NXCD) return (int)hipErrorInvalidValue;                                                     \
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<SC, SERP>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K); \
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<SC, SERP, false, W4AP_EPI_STAGED_NT>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K); \
       break;                                                                                              \
     }
     W4AP_CASE(130, 0, true)
@@ -93,15 +97,18 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4AP_CASE(145, 14, true)
     W4AP_CASE(146, 15, true)
     W4AP_CASE(147, 16, true)
+    W4AP_CASE(180, W4AP_SC_G4_RW, true)
+    W4AP_CASE(181, W4AP_SC_G6D6_RW, true)
 #define W4APSQ_CASE(V, SC, SERP)                                                                           \
     case V:                                                                                               \
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;    \
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<SC, SERP, true>), dim3(256), dim3(W4_THREADS), 0, s, a, b, c, \
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<SC, SERP, true, W4AP_EPI_STAGED_NT>), dim3(256), dim3(W4_THREADS), 0, s, a, b, c, \
                          M, N, K);                                                                        \
       break;
     W4APSQ_CASE(150, 5, true)
     W4APSQ_CASE(151, 9, true)
     W4APSQ_CASE(152, 5, false)
+    W4APSQ_CASE(182, W4AP_SC_G4_RW, true)
     case 173:     // EF square raster, g4, serpentine K
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4, true, true, 2>), dim3(256), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
@@ -173,7 +180,7 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
 #define F8AP_CASE(V, SC, SERP, SQ)                                                                         \
     case V:                                                                                               \
       if (g < NXCD || (SQ && !sq)) return (int)hipErrorInvalidValue;                                      \
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<SC, SERP, SQ>), dim3(SQ ? 256 : g), dim3(F8_THREADS), 0, s, \
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<SC, SERP, SQ, W4AP_EPI_STAGED_NT>), dim3(SQ ? 256 : g), dim3(F8_THREADS), 0, s, \
                          a, b, c, M, N, K);                                                               \
       break;
     F8AP_CASE(200, 0, false, false)
@@ -197,6 +204,10 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     F8AP_CASE(224, 4, true, true)
     F8AP_CASE(225, 5, true, true)
     F8AP_CASE(226, 6, true, true)
+    F8AP_CASE(250, F8AP_SC_P_RW, false, false)
+    F8AP_CASE(251, F8AP_SC_S1D3_RW, true, false)
+    F8AP_CASE(252, F8AP_SC_P_RW, true, true)
+    F8AP_CASE(253, F8AP_SC_P_RW, true, false)
     case 240:     // EF: fused epilogue (EPI=2), schedule p, linear K
       if (g < NXCD) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_P, false, false, 2>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);

@@ -126,7 +126,8 @@ def test_production_variant_set_is_closed(cuda_device):
 @pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 50), (16384, 16384, 1024, 50), (8192, 8192, 4096, 50),
                                         (12288, 12288, 12288, 48), (8192, 8192, 12288, 47),
                                         (12288, 12288, 8192, 51), (16384, 16384, 16384, 51),
-                                        (4096, 4096, 16384, 52), (4096, 8192, 8192, 52), (4096, 4096, 4096, 50),
+                                        (4096, 4096, 16384, 50), (4096, 8192, 8192, 50), (4096, 4096, 32768, 52),
+                                        (4096, 4096, 4096, 50),
                                         (8192, 8192, 128, 25), (256, 256, 64, 0), (300, 256, 256, 0)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""

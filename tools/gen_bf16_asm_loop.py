@@ -160,10 +160,11 @@ SCHEDULES = {
 
 # schedules the persistent kernel is generated for (its SC index = position here)
 PERSISTENT = ["v18", "v18_d6b", "v18_d5_late", "v18_d6b_bout", "v18_d5_late_bout", "g4", "g6", "g8", "sp2g6",
-              "g6d6", "g4d6", "g2d6", "sp2g4d5", "m4", "m4d4", "m4d3", "m6d4"]
+              "g6d6", "g4d6", "g2d6", "sp2g4d5", "m4", "m4d4", "m4d3", "m6d4", "g4_rw", "g6d6_rw"]
+# a name ending in _rw: that schedule in kloop_persistent_rw (relaxed first landing wait)
 
 
-def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) -> List[str]:
+def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, w2_extra: int = 0) -> List[str]:
     """One K-tile: MFMAs on tile t (buffer ``cur``), R1 reads from ``cur``, DMA of tile t+2 into
     ``cur``, R0 reads of tile t+1 from the other buffer. ``nxt_tile``: the DMA fetches the next
     output tile's K-tile instead (persistent kernel drain: operands nA / nB / nvoff / nkstep)."""
@@ -184,7 +185,7 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False) ->
         gap[sc.vk].append(f"v_add_u32_e32 {voff}, {kstep}, {voff}")
     if nx:
         if not sc.merged:
-            n = sc.issued_before_w2() if dma else 0
+            n = (sc.issued_before_w2() if dma else 0) + w2_extra
             gap[sc.w2].append(f"s_waitcnt vmcnt({n})")
             gap[sc.b2].append("s_barrier")
         for j, s in enumerate(sc.r0):
@@ -223,6 +224,40 @@ def kloop(sc: Schedule) -> List[str]:
     out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4a_loop_%="]
     out += body(sc, 0, dma=False, nx=True)
     out += body(sc, 1, dma=False, nx=False)
+    return out
+
+
+def kloop_persistent_rw(sc: Schedule, stores: int = 32) -> List[str]:
+    """kloop_persistent() for the staged epilogue with a relaxed first landing wait ("_rw"): the
+    previous tile's epilogue issued ``stores`` C stores after waiting for this tile's K-tiles 0 and 1
+    (vmcnt(0)), so the first K-tile's landing wait (K-tile 1) skips them -- vmcnt(16 + stores) -- and
+    the stores have until the second K-tile's landing wait to complete. The first tile of a workgroup
+    waits for both prologue K-tiles (vmcnt(0)), so the relaxed count is exact there too."""
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lw4rw_entry_%="]
+    out += [x for x in prologue() if not x.startswith("ds_read") and x != "s_waitcnt lgkmcnt(0)"
+            and x != "s_barrier" and not x.startswith("s_waitcnt vmcnt")]
+    out.append("s_waitcnt vmcnt(0)")
+    out.append(".Lw4rw_entry_%=:")
+    out.append("s_barrier")
+    for j in range(16):
+        isb, x = read_order(j)
+        out.append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}00] offset:{x * 2048}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += body(sc, 0, dma=True, nx=True, w2_extra=stores)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4rw_drain_%="]
+    out.append(".Lw4rw_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4rw_loop_%="]
+    out.append(".Lw4rw_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lw4rw_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True)
+    out += body(sc, 1, dma=True, nx=False, nxt_tile=True)
+    out += ["s_branch .Lw4rw_done_%=", ".Lw4rw_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    out.append(".Lw4rw_done_%=:")
     return out
 
 
@@ -575,7 +610,7 @@ def render() -> str:
         parts.append('  ""')
         parts.append("")
     for name in PERSISTENT:
-        lines = kloop_persistent(SCHEDULES[name])
+        lines = kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else kloop_persistent(SCHEDULES[name])
         parts.append(f"#define W4AP_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')

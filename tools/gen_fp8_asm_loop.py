@@ -165,7 +165,8 @@ SCHEDULES["m"] = make("m", r1=list(range(16)), w1=19, dma=[21 + 2 * p for p in r
 SCHEDULES["md3"] = make("md3", r1=list(range(16)), w1=19, dma=[21 + 3 * p for p in range(14)] + [61, 63],
                         w2=None, r0=_M_R0)
 
-PERSISTENT = list(SCHEDULES)
+PERSISTENT = list(SCHEDULES) + ["p_rw", "s1d3_rw"]
+# a name ending in _rw: that schedule in kloop_persistent_rw (relaxed first landing wait)
 
 
 def rd(isb: bool, x: int, h: int, buf: int, ef: bool) -> str:
@@ -246,6 +247,35 @@ def prologue() -> List[str]:
 def r0_reads(buf: int) -> List[str]:
     return [f"ds_read_b128 {half(isb, x, h)}, %[{'rb' if isb else 'ra'}{buf}{h}] offset:{x * 2048}"
             for isb, x, h in R0_ORDER]
+
+
+def kloop_persistent_rw(sc: Schedule, stores: int = 32) -> List[str]:
+    """kloop_persistent() with the relaxed first landing wait (tools/gen_bf16_asm_loop.py
+    kloop_persistent_rw): the previous tile's staged-epilogue stores are skipped by the first K-tile's
+    landing wait; the first tile waits for both prologue K-tiles."""
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lf8rw_entry_%="]
+    out += prologue()
+    out += ["s_waitcnt vmcnt(0)"]
+    out.append(".Lf8rw_entry_%=:")
+    out.append("s_barrier")
+    out += r0_reads(0)
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += body(sc, 0, dma=True, nx=True, w2_extra=stores)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8rw_drain_%="]
+    out.append(".Lf8rw_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8rw_loop_%="]
+    out.append(".Lf8rw_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lf8rw_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True)
+    out += body(sc, 1, dma=True, nx=False, nxt_tile=True)
+    out += ["s_branch .Lf8rw_done_%=", ".Lf8rw_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    out.append(".Lf8rw_done_%=:")
+    return out
 
 
 def kloop_persistent(sc: Schedule) -> List[str]:
@@ -447,7 +477,7 @@ def render() -> str:
         parts.append('  ""')
         parts.append("")
     for name in PERSISTENT:
-        lines = kloop_persistent(SCHEDULES[name])
+        lines = kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else kloop_persistent(SCHEDULES[name])
         a = audit(lines)
         parts.append(f"// {name}: {a['mfmas']} MFMAs, <= {a['max_fillers_per_gap']} instructions per MFMA gap")
         parts.append(f"#define F8AP_ASM_{name.upper()} \\")
