@@ -11,6 +11,7 @@
 //   170 / 171 / 172 / 173 = w4ap with the fused epilogue (EPI=2): g4 serpentine K, g6d6 serpentine, g4 linear,
 //   g4 square raster
 //   180 / 181 / 182 = relaxed first landing wait (_rw): g4 (= v50 + rw), g6d6 (v52 + rw), g4 square raster (v51 + rw)
+//   190 / 191 / 192 / 193 = VP DMA form: g4 (= v50 in VP form), g4 + PA, g6d6 VP, g4 + PA linear K
 //   162 = v50 (136) with nontemporal C stores; 174 = 170 with nontemporal stores
 //   160 / 161 = knock-outs (wrong C): 136 without its epilogue / without the epilogue's global stores
 //   150 / 151 = w4ap square raster (SQ) with persistent schedule 5 / 9; 152 = 150 without serpentine K
@@ -22,6 +23,7 @@
 //   p square raster
 //   250 / 251 / 252 / 253 = q16ap relaxed first landing wait: p linear (v20 + rw), s1d3 serpentine, p square
 //   raster (v21 + rw), p serpentine
+//   260 / 261 / 262 / 263 = q16ap VP form: p linear (= v20 in VP form), p + PA, p + PA square raster, s1d3 + PA serp
 //   232 = 200 with nontemporal C stores; 244 = 240 with nontemporal stores
 //   230 / 231 = knock-outs: 200 without its epilogue / without the epilogue's global stores
 #include "gemm_bf16_kernels.h"
@@ -98,6 +100,18 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4AP_CASE(146, 15, true)
     W4AP_CASE(147, 16, true)
     W4AP_CASE(180, W4AP_SC_G4_RW, true)
+#define W4VP_CASE(V, SC, SERP, DM)                                                                         \
+    case V: {                                                                                             \
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;                   \
+      if (g < NXCD) return (int)hipErrorInvalidValue;                                                     \
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<SC, SERP, false, W4AP_EPI_STAGED_NT, DM>), dim3(g), dim3(W4_THREADS), 0, s, \
+                         a, b, c, M, N, K);                                                               \
+      break;                                                                                              \
+    }
+    W4VP_CASE(190, W4VP_SC_G4, true, 1)
+    W4VP_CASE(191, W4VP_SC_G4, true, 2)
+    W4VP_CASE(192, W4VP_SC_G6D6, true, 1)
+    W4VP_CASE(193, W4VP_SC_G4, false, 2)
     W4AP_CASE(181, W4AP_SC_G6D6_RW, true)
 #define W4APSQ_CASE(V, SC, SERP)                                                                           \
     case V:                                                                                               \
@@ -205,6 +219,16 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     F8AP_CASE(225, 5, true, true)
     F8AP_CASE(226, 6, true, true)
     F8AP_CASE(250, F8AP_SC_P_RW, false, false)
+#define F8VP_CASE(V, SC, SERP, SQ, DM)                                                                     \
+    case V:                                                                                               \
+      if (g < NXCD || (SQ && !sq)) return (int)hipErrorInvalidValue;                                      \
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<SC, SERP, SQ, W4AP_EPI_STAGED_NT, DM>), dim3(SQ ? 256 : g), dim3(F8_THREADS), \
+                         0, s, a, b, c, M, N, K);                                                         \
+      break;
+    F8VP_CASE(260, F8VP_SC_P, false, false, 1)
+    F8VP_CASE(261, F8VP_SC_P, false, false, 2)
+    F8VP_CASE(262, F8VP_SC_P, true, true, 2)
+    F8VP_CASE(263, F8VP_SC_S1D3, true, false, 2)
     F8AP_CASE(251, F8AP_SC_S1D3_RW, true, false)
     F8AP_CASE(252, F8AP_SC_P_RW, true, true)
     F8AP_CASE(253, F8AP_SC_P_RW, true, false)

@@ -701,12 +701,12 @@ gemm_bf16_256x256_w4a(const __bf16* __restrict__ A, const __bf16* __restrict__ B
 }
 
 // w4ap (v50-v52): w4a made persistent; the frame is shared with the fp8 kernel (gemm_w4ap.h).
-template <int SC = 0, bool SERP = true, bool SQ = false, int EPI = 0>
+template <int SC = 0, bool SERP = true, bool SQ = false, int EPI = 0, int DM = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
-  w4ap_run<SC, SERP, SQ, false, EPI>((const char*)A, (const char*)Bt, C, M, N, K, smem);
+  w4ap_run<SC, SERP, SQ, false, EPI, DM>((const char*)A, (const char*)Bt, C, M, N, K, smem);
 }
 
 // v25/v26: v18 made persistent. gridDim = one workgroup per CU; XCD x (= blockIdx % 8) owns a

@@ -908,12 +908,12 @@ gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__
 // q16 K-tile body as one hand-scheduled asm block per output tile (tools/gen_fp8_asm_loop.py,
 // gemm_fp8_asm_loop.h): the same MFMAs, operands and accumulators as q16p, waits computed per
 // fragment instead of hipcc's, no per-piece SALU address arithmetic or s_nop.
-template <int SC = 0, bool SERP = false, bool SQ = false, int EPI = 0>
+template <int SC = 0, bool SERP = false, bool SQ = false, int EPI = 0, int DM = 0>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_q16ap(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
-  w4ap_run<SC, SERP, SQ, true, EPI>((const char*)A, (const char*)Bt, C, M, N, K, smem);
+  w4ap_run<SC, SERP, SQ, true, EPI, DM>((const char*)A, (const char*)Bt, C, M, N, K, smem);
 }
 
 // OCP e4m3fn -> f32 in software (independent of the matrix cores): bias 7, no infinities,

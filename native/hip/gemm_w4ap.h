@@ -52,6 +52,20 @@ namespace {
 
 typedef uint32_t w4a_u32x4 __attribute__((ext_vector_type(4)));
 
+// The VP DMA form (DM >= 1; tools/gen_*_asm_loop.py to_vp): piece p's lane offset is its own VGPR
+// vp[p] and the DMA'd K-tile's byte offset one SGPR (koff, nkoff for the next tile).
+#define W4VP_LOOP(TEXT)                                                                                       \
+  asm volatile("s_mov_b32 %[m0save], m0\n\t" TEXT "s_mov_b32 m0, %[m0save]"                                   \
+               : [koff] "+s"(koff), [nkoff] "+s"(nkoff), [cnt] "+s"(trips), [m0save] "=&s"(m0save)              \
+               : [ra00] "v"(ra00), [rb00] "v"(rb00), [ra01] "v"(ra01), [rb01] "v"(rb01), [ra10] "v"(ra10),       \
+                 [rb10] "v"(rb10), [ra11] "v"(ra11), [rb11] "v"(rb11), [kstep] "s"(kstep), [vp0] "v"(vp[0]),     \
+                 [vp1] "v"(vp[1]), [vp2] "v"(vp[2]), [vp3] "v"(vp[3]), [vp4] "v"(vp[4]), [vp5] "v"(vp[5]),        \
+                 [vp6] "v"(vp[6]), [vp7] "v"(vp[7]), [vp8] "v"(vp[8]), [vp9] "v"(vp[9]), [vp10] "v"(vp[10]),      \
+                 [vp11] "v"(vp[11]), [vp12] "v"(vp[12]), [vp13] "v"(vp[13]), [vp14] "v"(vp[14]),                 \
+                 [vp15] "v"(vp[15]), [rA] "s"(sA), [rB] "s"(sB), [nA] "s"(nA), [nB] "s"(nB), [nkstep] "s"(nkstep), \
+                 [m0b0] "s"(m0b0), [m0b1] "s"(m0b1), [flags] "s"(flags)                                          \
+               : "memory", "scc", W4A_VCLOBBERS, W4_AGPR_CLOBBERS)
+
 constexpr int W4AP_TILE = 256;                     // output tile edge
 constexpr int W4AP_ROW = 128;                      // bytes per staged K-row (one K-tile)
 constexpr int W4AP_PANEL = W4AP_TILE * W4AP_ROW;   // 32 KiB per operand per K-tile
@@ -93,11 +107,14 @@ constexpr int W4AP_EPI_KO_NOSTORE = 3;  // lab knock-out: staged epilogue withou
 constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores: production (profiles/r3_s2/)
 
 // A, Bt: K-major operands (element size 1 for F8, else 2); C: bf16; smem: W4AP_LDS bytes.
+// DM (DMA form): 0 = one lane offset + per-row-block SGPR soffsets, SC indexes W4AP/F8AP schedules;
+// 1 = VP (per-piece VGPR lane offsets, SGPR K offset), SC indexes the VP schedules; 2 = VP with the
+// A-panel pieces reading rows 32 apart (PA; the epilogue maps LDS slot s to C row 32 (s & 7) + (s >> 3)).
 // EPI: 0 = the staged epilogue below; 2 = the fused epilogue (the C tile leaves through the last
 // K-tile's MFMA shadow, generated asm); knock-outs (lab only, wrong C): 1 = no epilogue at all,
 // 3 = the staged epilogue without its global stores (prices the stores against the rest);
 // 4 = the staged epilogue with nontemporal stores.
-template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0>
+template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
                                          __bf16* __restrict__ C, int M, int N, int K, char* smem) {
   constexpr int ESZ = F8 ? 1 : 2;
@@ -148,6 +165,18 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
 #pragma unroll
   for (int i = 0; i < 8; ++i)
     so[i] = __builtin_amdgcn_readfirstlane((uint32_t)((i << 2) + wid) * 8u * row_bytes);
+  static_assert(DM == 0 || EPI != W4AP_EPI_FUSED, "the fused epilogue uses the DM 0 DMA form");
+  uint32_t vp[16] = {};
+  if constexpr (DM >= 1) {
+    const uint32_t chunk = (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const uint32_t rblk = (uint32_t)(((p & 7) << 2) + wid);
+      vp[p] = (DM == 2 && p < 8) ? (uint32_t)(lane >> 3) * 32u * row_bytes + chunk + rblk * row_bytes
+                                 : (uint32_t)(lane >> 3) * row_bytes + chunk + rblk * 8u * row_bytes;
+    }
+  }
+  auto koff0 = [&](bool rev) { return __builtin_amdgcn_readfirstlane((uint32_t)((rev ? ktiles - 1 : 0) * W4AP_ROW)); };
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
   const uint32_t m0b0 = lds0 + (uint32_t)wid * 1024u, m0b1 = m0b0 + (uint32_t)W4AP_BUF;
   // a lane's two 16-byte chunks of row (lane & 15) of a 16-row fragment: kk*4 + g for bf16 k-half
@@ -194,6 +223,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   bool rev = false;
   w4a_u32x4 sA = mk_rs(A + (size_t)tm * panel_bytes), sB = mk_rs(Bt + (size_t)tn * panel_bytes);
   uint32_t voff_k = voff0(rev);
+  uint32_t koff = koff0(rev);
   int kstep = kst(rev);
   uint32_t first = 1;
 
@@ -212,6 +242,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       nB = mk_rs(Bt + (size_t)ntn * panel_bytes);
     }
     uint32_t nvoff = voff0(nrev);
+    uint32_t nkoff = koff0(nrev);
     const int nkstep = kst(nrev);
     uint32_t trips = __builtin_amdgcn_readfirstlane((uint32_t)((ktiles - 2) >> 1));
     uint32_t m0save;
@@ -227,6 +258,10 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       } else {
         W4EF_LOOP_SELECT(SC)
       }
+    } else if constexpr (DM >= 1 && F8) {
+      F8VP_LOOP_SELECT(SC)
+    } else if constexpr (DM >= 1) {
+      W4VP_LOOP_SELECT(SC)
     } else if constexpr (F8) {
       F8AP_LOOP_SELECT(SC)
     } else {
@@ -276,16 +311,15 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
         uint4 v = raw;
         if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+        const int slot = wr * 128 + s * 32 + r;                        // the tile row's LDS slot
+        const int crow = DM == 2 ? 32 * (slot & 7) + (slot >> 3) : slot; // PA: slot -> panel row
+        __bf16* const dst = C + (size_t)(tm * W4AP_TILE + crow) * N + tn * W4AP_TILE + wc * 128 + ch * 8;
         if constexpr (EPI == 3) {        // knock-out: keep the value live, skip the global store
           asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
         } else if constexpr (EPI == 4) {   // nontemporal (streaming) C stores: global_store ... nt
-          w4a_u32x4 nv;
-          nv[0] = v.x; nv[1] = v.y; nv[2] = v.z; nv[3] = v.w;
-          __builtin_nontemporal_store(nv, reinterpret_cast<w4a_u32x4*>(C + (size_t)(tm * W4AP_TILE + wr * 128 + s * 32 + r) * N +
-                                                                       tn * W4AP_TILE + wc * 128 + ch * 8));
+          store_c16(dst, v);
         } else {
-          *reinterpret_cast<uint4*>(C + (size_t)(tm * W4AP_TILE + wr * 128 + s * 32 + r) * N + tn * W4AP_TILE +
-                                    wc * 128 + ch * 8) = v;
+          *reinterpret_cast<uint4*>(dst) = v;
         }
       }
       asm volatile("" ::: "memory");
@@ -299,6 +333,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     sB = nB;
     rev = nrev;
     voff_k = nvoff;                 // the drain advanced it past the next tile's K-tiles 0 and 1
+    koff = nkoff;
     kstep = nkstep;
     first = 0;
   }

@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -116,7 +116,7 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
@@ -124,7 +124,8 @@ def test_production_variant_set_is_closed(cuda_device):
 
 
 @pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 50), (16384, 16384, 1024, 50), (8192, 8192, 4096, 50),
-                                        (12288, 12288, 12288, 48), (8192, 8192, 12288, 47),
+                                        (12288, 12288, 12288, 53), (8192, 8192, 12288, 53), (8192, 8192, 8256, 47),
+                                        (12288, 12288, 8256, 48),
                                         (12288, 12288, 8192, 51), (16384, 16384, 16384, 51),
                                         (4096, 4096, 16384, 50), (4096, 8192, 8192, 50), (4096, 4096, 32768, 52),
                                         (4096, 4096, 4096, 50),
@@ -135,12 +136,12 @@ def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     from gpu_operator_amd.ops import gemm as G
 
     if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
-        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42}.get(want, want)
+        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42, 53: 42}.get(want, want)
     assert G.get_variant() == 0
     assert G.resolve_variant(m, n, k) == want
 
 
-@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (4096, 4096, 4096), (2048, 4096, 512)])
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (4096, 4096, 4096), (2048, 4096, 512), (4096, 4096, 3072)])
 def test_asm_pipeline_is_bitwise_v44(cuda_device, m, n, k):
     """v50 (the hand-scheduled asm K pipeline, persistent) issues the MFMAs of v44 in the same
     per-accumulator order, with the same serpentine K per dispatch wave: the outputs are equal bit
@@ -157,10 +158,14 @@ def test_asm_pipeline_is_bitwise_v44(cuda_device, m, n, k):
         G.set_variant(50)
         assert G.resolve_variant(m, n, k) == 50
         c50 = G.gemm_bf16(a, bt)
+        G.set_variant(53)            # the same pipeline in the VP DMA form: same MFMA order
+        assert G.resolve_variant(m, n, k) == 53
+        c53 = G.gemm_bf16(a, bt)
     finally:
         G.set_variant(old)
     torch.cuda.synchronize()
     assert torch.equal(c44, c50)
+    assert torch.equal(c44, c53)
 
 
 @pytest.mark.parametrize("m,n,k", [(4096, 8192, 256), (8192, 8192, 1024), (4096, 4096, 2048)])

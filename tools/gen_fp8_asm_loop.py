@@ -29,6 +29,7 @@ tile, flags) is the bf16 one: gemm_w4ap.h runs both.
 from __future__ import annotations
 
 import os
+import re
 from typing import Dict, List
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -436,6 +437,34 @@ EF = ["p", "s1d3", "p_nt"]
 # a name ending in _nt: the same schedule with nontemporal C stores (global_store ... nt)
 
 
+# ---------------------------------------------------------------------------------------------------
+# VP DMA form (frame DM >= 1, gemm_w4ap.h): piece p's whole lane offset (row block, row, chunk) is its
+# own VGPR %[vp<p>], fixed for the kernel, and the K byte offset of the DMA'd K-tile is one SGPR
+# (%[koff], %[nkoff] for the next tile) used as the soffset: one SALU add per K-tile instead of a VALU
+# add, no per-piece row-block SGPRs, and A and B pieces may use different row maps -- DM = 2 reads each
+# A-panel DMA instruction's 8 rows 32 apart (PA: K not a power of two, see gemm_bf16.hip v47).
+VP = ["p", "s1d3"]
+
+
+def to_vp(lines: List[str]) -> List[str]:
+    out = []
+    for ln in lines:
+        m = re.match(r"buffer_load_dwordx4 %\[(n?)voff\], %\[([rn])([AB])\], %\[s(\d)\] offen lds", ln)
+        if m:
+            piece = int(m.group(4)) + (8 if m.group(3) == "B" else 0)
+            assert (m.group(1) == "n") == (m.group(2) == "n"), ln
+            out.append(f"buffer_load_dwordx4 %[vp{piece}], %[{m.group(2)}{m.group(3)}], %[{m.group(1)}koff] offen lds")
+            continue
+        m = re.match(r"v_add_u32_e32 %\[(n?)voff\], %\[(n?)kstep\], %\[(n?)voff\]", ln)
+        if m:
+            n = m.group(1)
+            out.append(f"s_add_u32 %[{n}koff], %[{n}koff], %[{n}kstep]")
+            continue
+        assert "voff" not in ln and "%[s" not in ln, ln
+        out.append(ln)
+    return out
+
+
 def audit(lines: List[str]) -> Dict[str, int]:
     gaps, cur = [], 0
     for ln in lines:
@@ -472,6 +501,20 @@ def render() -> str:
         if name.endswith("_nt"):
             lines = [ln + " nt" if ln.startswith("global_store") else ln for ln in lines]
         parts.append(f"#define F8EF_ASM_{name.upper()} \\")
+        for ln in lines:
+            parts.append(f'  "{ln}\\n\\t" \\')
+        parts.append('  ""')
+        parts.append("")
+    vsel = [f"if constexpr (SC == {i}) W4VP_LOOP(F8VP_ASM_{n.upper()});" for i, n in enumerate(VP)]
+    parts.append("// VP DMA form (frame DM >= 1): schedule index -> asm text (W4VP_LOOP)")
+    parts.append("#define F8VP_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(vsel))
+    for i, n in enumerate(VP):
+        parts.append(f"#define F8VP_SC_{n.upper()} {i}")
+    parts.append("")
+    for name in VP:
+        lines = to_vp(kloop_persistent(SCHEDULES[name]))
+        parts.append(f"#define F8VP_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
         parts.append('  ""')
