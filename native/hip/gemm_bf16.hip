@@ -24,12 +24,12 @@
 //        multiples), v52 (one or two dispatch waves, K >= 32768); otherwise v44, v25 for K <= 4096
 //        with >= 2 tiles per CU, v45 for >= 8 dispatch waves with K >= 8192 on 16x16-tile
 //        multiples; v42 / v18 on devices without 256 CUs.
-//   53 = the asm pipeline (g4) in the VP DMA form (gemm_w4ap.h DM 1): the default when K is not a power
-//        of two (an even number of K-tiles, >= 4).
+//   53 / 54 = the asm pipeline (g4) in the VP DMA form (gemm_w4ap.h DM 1), linear / square raster: the
+//        default when K is not a power of two (an even number of K-tiles, >= 4).
 //   47 / 48 = v44 / v45 with permuted A-panel DMA rows (PA), the default for other K not a power of two.
 //   50 / 51 / 52 = the asm pipeline: w4ap (gemm_bf16_kernels.h) with the g4 schedule, g4 on the square
 //        raster, the g6d6 schedule (tools/gen_bf16_asm_loop.py generates gemm_bf16_asm_loop.h).
-//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 = that kernel pinned (no automatic switch; still falls back to a kernel
+//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
 // Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
 // add per K-tile, loop-invariant soffsets; 17 fewer SALU per K-tile, +0.6-0.8 % at 8192^3 and
@@ -70,8 +70,10 @@ static int resolve_variant(int M, int N, int K) {
   if (v == 0 && cus == 256 && !pow2k && K % (2 * BK) == 0 && K >= 4 * BK && persistent_grid(nwg) >= NXCD) {
     // K not a power of two: the asm pipeline in the VP DMA form (per-piece VGPR lane offsets, the K
     // offset in one SGPR): 12288^3 1.02x hipBLASLt (v48 0.98x, the DM-0 asm form 0.88x),
-    // 8192^2x12288 1.07x (v47 1.02x), 12288^2x10240 1.03x (v48 1.03x); profiles/r3_s2/vp_bf16.jsonl
-    v = 53;
+    // 8192^2x12288 1.07x (v47 1.02x), 12288^2x10240 1.03x (v48 1.03x); profiles/r3_s2/vp_bf16.jsonl.
+    // v54 = the same on the square cross-XCD raster for >= 8 dispatch waves on 16x16-tile multiples:
+    // 12288^3 1.05x (v53 1.03x), 12288^2x10240 1.07x (v53 1.04x); profiles/r3_s2/vpsq_bf16.jsonl
+    v = (sq && nwg >= 8 * cus) ? 54 : 53;
   } else if (v == 0 && cus == 256 && pow2k && K >= 4 * BK && persistent_grid(nwg) >= NXCD) {
     // The hand-scheduled asm K pipeline, persistent (profiles/r3_asm/): v50 everywhere it runs,
     // ahead of v44 and v25 on every measured shape (8192^3 +2-3 %, 8192^2x2048 +7 %,
@@ -99,8 +101,10 @@ static int resolve_variant(int M, int N, int K) {
   if (v == 25 && persistent_grid(nwg) < NXCD) v = 44;
   // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups; its square raster
   // (v51) needs exactly 256 workgroups over 16x16 super-tiles
-  if ((v == 50 || v == 51 || v == 52 || v == 53) && (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg) < NXCD))
+  if ((v == 50 || v == 51 || v == 52 || v == 53 || v == 54) &&
+      (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg) < NXCD))
     v = 44;
+  if (v == 54 && (!sq || cus != 256)) v = 53;
   if (v == 51 && (!sq || cus != 256)) v = 50;
   if ((v == 44 || v == 45) && cus != 256) v = 42;       // serpentine K assumes 32 co-resident WGs / XCD
   // K not a power of two: A-panel DMA instructions read rows 32 apart (PA, v47 / v48). At a 24 KiB
@@ -119,7 +123,7 @@ extern "C" {
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
   if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50 &&
-      v != 51 && v != 52 && v != 53)
+      v != 51 && v != 52 && v != 53 && v != 54)
     return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
@@ -175,6 +179,10 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
     case 53:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4, true, false, W4AP_EPI_STAGED_NT, 1>), dim3(persistent_grid(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 54:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4, true, true, W4AP_EPI_STAGED_NT, 1>), dim3(256), dim3(W4_THREADS),
+                         0, s, a, b, c, M, N, K);
       break;
     case 52:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_NT>), dim3(persistent_grid(nwg)),

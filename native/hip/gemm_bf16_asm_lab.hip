@@ -12,6 +12,7 @@
 //   g4 square raster
 //   180 / 181 / 182 = relaxed first landing wait (_rw): g4 (= v50 + rw), g6d6 (v52 + rw), g4 square raster (v51 + rw)
 //   190 / 191 / 192 / 193 = VP DMA form: g4 (= v50 in VP form), g4 + PA, g6d6 VP, g4 + PA linear K
+//   194 / 195 = VP DMA form on the square raster (g4), without / with PA
 //   162 = v50 (136) with nontemporal C stores; 174 = 170 with nontemporal stores
 //   160 / 161 = knock-outs (wrong C): 136 without its epilogue / without the epilogue's global stores
 //   150 / 151 = w4ap square raster (SQ) with persistent schedule 5 / 9; 152 = 150 without serpentine K
@@ -123,6 +124,16 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
     W4APSQ_CASE(151, 9, true)
     W4APSQ_CASE(152, 5, false)
     W4APSQ_CASE(182, W4AP_SC_G4_RW, true)
+    case 194:     // VP DMA form on the square raster (g4, serpentine K); 195 = the same with PA
+    case 195:
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      if (v == 194)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4, true, true, W4AP_EPI_STAGED_NT, 1>), dim3(256), dim3(W4_THREADS), 0,
+                           s, a, b, c, M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4, true, true, W4AP_EPI_STAGED_NT, 2>), dim3(256), dim3(W4_THREADS), 0,
+                           s, a, b, c, M, N, K);
+      break;
     case 173:     // EF square raster, g4, serpentine K
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4, true, true, 2>), dim3(256), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);

@@ -199,10 +199,11 @@ def _audit_asm_pipeline(body, st):
 
 
 def test_w4ap_production_pipeline(asm):
-    """Production v50 / v51 / v52 / v53: the persistent asm K pipeline (main schedule, its square-raster
-    form, the long-K schedule, the VP DMA form for K not a power of two)."""
+    """Production v50 / v51 / v52 / v53 / v54: the persistent asm K pipeline (main schedule, its
+    square-raster form, the long-K schedule, the VP DMA form for K not a power of two, linear and
+    square raster)."""
     kernels = _kernels(asm, "gemm_bf16_256x256_w4apI")
-    assert len(kernels) == 4
+    assert len(kernels) == 5
     for body, st in kernels:
         assert _audit_asm_pipeline(body, st) == 6 * 128
 

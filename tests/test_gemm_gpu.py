@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -94,6 +94,24 @@ def test_smoke_vector_add(cuda_device):
     assert smoke.smoke(n=1_000_003, device=str(cuda_device))
 
 
+def test_vp_square_raster_covers_every_tile(cuda_device):
+    """12288x12288x10240 (K not a power of two; 48x48 tiles, 9 dispatch waves) takes the VP-form asm
+    pipeline on the square raster (v54) under the default variant; one checked row per tile row."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    m = n = 12288
+    k = 10240
+    if torch.cuda.get_device_properties(cuda_device).multi_processor_count == 256:
+        assert G.resolve_variant(m, n, k) == 54
+    a = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=cuda_device), 13)
+    bt = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=cuda_device), 14)
+    c = G.gemm_bf16(a, bt)
+    rows = torch.tensor([tm * 256 + (tm * 41) % 256 for tm in range(m // 256)], device=cuda_device)
+    ref = a[rows].float() @ bt.float().t()
+    torch.testing.assert_close(c[rows].float(), ref, atol=0.15, rtol=1e-2)
+
+
 def test_default_dispatch_square_raster_covers_every_tile(cuda_device):
     """12288x12288x8192 (48x48 tiles, 9 dispatch waves) takes the square cross-XCD raster (v51)
     under the default variant; one checked row per tile row covers every output tile."""
@@ -116,7 +134,7 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
@@ -124,7 +142,7 @@ def test_production_variant_set_is_closed(cuda_device):
 
 
 @pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 50), (16384, 16384, 1024, 50), (8192, 8192, 4096, 50),
-                                        (12288, 12288, 12288, 53), (8192, 8192, 12288, 53), (8192, 8192, 8256, 47),
+                                        (12288, 12288, 12288, 54), (8192, 8192, 12288, 53), (8192, 8192, 8256, 47),
                                         (12288, 12288, 8256, 48),
                                         (12288, 12288, 8192, 51), (16384, 16384, 16384, 51),
                                         (4096, 4096, 16384, 50), (4096, 8192, 8192, 50), (4096, 4096, 32768, 52),
@@ -136,7 +154,7 @@ def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     from gpu_operator_amd.ops import gemm as G
 
     if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
-        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42, 53: 42}.get(want, want)
+        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42, 53: 42, 54: 42}.get(want, want)
     assert G.get_variant() == 0
     assert G.resolve_variant(m, n, k) == want
 
@@ -190,8 +208,11 @@ def test_asm_square_raster_is_bitwise_v45(cuda_device, m, n, k):
         c52 = G.gemm_bf16(a, bt)
         G.set_variant(50)
         c50 = G.gemm_bf16(a, bt)
+        G.set_variant(54)            # v51 in the VP DMA form
+        c54 = G.gemm_bf16(a, bt)
     finally:
         G.set_variant(old)
     torch.cuda.synchronize()
     assert torch.equal(c45, c51)
+    assert torch.equal(c45, c54)
     assert torch.equal(c50, c52)      # same pipeline, different instruction placement
