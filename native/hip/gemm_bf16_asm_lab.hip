@@ -13,6 +13,8 @@
 //   180 / 181 / 182 = relaxed first landing wait (_rw): g4 (= v50 + rw), g6d6 (v52 + rw), g4 square raster (v51 + rw)
 //   190 / 191 / 192 / 193 = VP DMA form: g4 (= v50 in VP form), g4 + PA, g6d6 VP, g4 + PA linear K
 //   194 / 195 = VP DMA form on the square raster (g4), without / with PA
+//   196 / 264 = deferred C stores (EPI 7): bf16 g4 serpentine (v50 + DS), fp8 p linear (v20 + DS); K >= 8 K-tiles
+//   163 / 164 = knock-outs: production epilogue storing only the first quarter / half of C; 233 = fp8 quarter
 //   162 = v50 (136) with nontemporal C stores; 174 = 170 with nontemporal stores
 //   160 / 161 = knock-outs (wrong C): 136 without its epilogue / without the epilogue's global stores
 //   150 / 151 = w4ap square raster (SQ) with persistent schedule 5 / 9; 152 = 150 without serpentine K
@@ -166,6 +168,23 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<5, true, false, 4>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     }
+    case 163:     // knock-outs of the production epilogue: only the first quarter (163) / half (164) of C stored
+    case 164: {
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      if (v == 163)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<5, true, false, 5>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<5, true, false, 6>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 196: {   // deferred C stores (EPI 7): v50 (g4, serpentine K) storing quarters 1-3 in the next K-loop
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD || K < 8 * 2 * BK) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4DS_SC_G4, true, false, W4AP_EPI_DEFERRED>), dim3(g), dim3(W4_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    }
     case 161: {   // knock-out: v50 with the epilogue but without its global C stores
       const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
       if (g < NXCD) return (int)hipErrorInvalidValue;
@@ -266,6 +285,15 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     case 244:     // EF p with nontemporal stores
       if (g < NXCD) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8EF_SC_P_NT, false, false, 2>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 233:     // knock-out: 200 with nontemporal stores of only the first quarter of C
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<0, false, false, 5>), dim3(g), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 264:     // deferred C stores (EPI 7): v20 (p, linear K)
+      if (g < NXCD || K < 8 * 2 * F8_BK) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8DS_SC_P, false, false, W4AP_EPI_DEFERRED>), dim3(g), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
       break;
     case 231:     // knock-out: 200 with the epilogue but without its global C stores
       if (g < NXCD) return (int)hipErrorInvalidValue;

@@ -52,6 +52,27 @@ namespace {
 
 typedef uint32_t w4a_u32x4 __attribute__((ext_vector_type(4)));
 
+// The deferred-store form (EPI 7; tools/gen_*_asm_loop.py kloop_persistent_ds): the previous tile's
+// C quarters 1-2 in h0..h15, quarter 3 in the wave's staging LDS (stgl: this lane's 16-byte slot), stored
+// through vcur (advanced by s8N = 4 C rows per store) from the previous tile's corner sCp.
+#define W4DS_LOOP(TEXT)                                                                                       \
+  asm volatile("s_mov_b32 %[m0save], m0\n\t" TEXT "s_mov_b32 m0, %[m0save]"                                   \
+               : [voff] "+v"(voff_k), [nvoff] "+v"(nvoff), [cnt] "+s"(trips), [m0save] "=&s"(m0save),          \
+                 [vcur] "+v"(vcur)                                                                             \
+               : [ra00] "v"(ra00), [rb00] "v"(rb00), [ra01] "v"(ra01), [rb01] "v"(rb01), [ra10] "v"(ra10),       \
+                 [rb10] "v"(rb10), [ra11] "v"(ra11), [rb11] "v"(rb11), [kstep] "s"(kstep), [s0] "s"(so[0]),      \
+                 [s1] "s"(so[1]), [s2] "s"(so[2]), [s3] "s"(so[3]), [s4] "s"(so[4]), [s5] "s"(so[5]),            \
+                 [s6] "s"(so[6]), [s7] "s"(so[7]), [rA] "s"(sA), [rB] "s"(sB), [nA] "s"(nA), [nB] "s"(nB),       \
+                 [nkstep] "s"(nkstep), [m0b0] "s"(m0b0), [m0b1] "s"(m0b1), [flags] "s"(flags), [h0] "v"(held[0]), \
+                 [h1] "v"(held[1]), [h2] "v"(held[2]), [h3] "v"(held[3]), [h4] "v"(held[4]), [h5] "v"(held[5]),  \
+                 [h6] "v"(held[6]), [h7] "v"(held[7]), [h8] "v"(held[8]), [h9] "v"(held[9]),                     \
+                 [h10] "v"(held[10]), [h11] "v"(held[11]), [h12] "v"(held[12]), [h13] "v"(held[13]),             \
+                 [h14] "v"(held[14]), [h15] "v"(held[15]), [stgl] "v"(stgl), [s8N] "s"(s8N), [sCp] "s"(sCp)      \
+               : "memory", "scc", W4A_VCLOBBERS, W4DS_VCLOBBERS, W4_AGPR_CLOBBERS)
+#define W4DS_VCLOBBERS                                                                                      \
+  "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252",     \
+  "v253", "v254", "v255"
+
 // The VP DMA form (DM >= 1; tools/gen_*_asm_loop.py to_vp): piece p's lane offset is its own VGPR
 // vp[p] and the DMA'd K-tile's byte offset one SGPR (koff, nkoff for the next tile).
 #define W4VP_LOOP(TEXT)                                                                                       \
@@ -105,6 +126,7 @@ constexpr int W4AP_EPI_KO_NONE = 1;     // lab knock-out: no epilogue (wrong C)
 constexpr int W4AP_EPI_FUSED = 2;       // C stored from the last K-tile's MFMA gaps (generated asm)
 constexpr int W4AP_EPI_KO_NOSTORE = 3;  // lab knock-out: staged epilogue without the global stores
 constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores: production (profiles/r3_s2/)
+constexpr int W4AP_EPI_DEFERRED = 7;    // staged nt, quarters 1-3 of C stored during the next tile's K-loop
 
 // A, Bt: K-major operands (element size 1 for F8, else 2); C: bf16; smem: W4AP_LDS bytes.
 // DM (DMA form): 0 = one lane offset + per-row-block SGPR soffsets, SC indexes W4AP/F8AP schedules;
@@ -113,7 +135,8 @@ constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores: productio
 // EPI: 0 = the staged epilogue below; 2 = the fused epilogue (the C tile leaves through the last
 // K-tile's MFMA shadow, generated asm); knock-outs (lab only, wrong C): 1 = no epilogue at all,
 // 3 = the staged epilogue without its global stores (prices the stores against the rest);
-// 4 = the staged epilogue with nontemporal stores.
+// 4 = the staged epilogue with nontemporal stores; 5 / 6 = lab knock-outs of 4 that store only the first
+// quarter / half of the tile (price the store burst by its size).
 template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
                                          __bf16* __restrict__ C, int M, int N, int K, char* smem) {
@@ -165,7 +188,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
 #pragma unroll
   for (int i = 0; i < 8; ++i)
     so[i] = __builtin_amdgcn_readfirstlane((uint32_t)((i << 2) + wid) * 8u * row_bytes);
-  static_assert(DM == 0 || EPI != W4AP_EPI_FUSED, "the fused epilogue uses the DM 0 DMA form");
+  static_assert(DM == 0 || (EPI != W4AP_EPI_FUSED && EPI != W4AP_EPI_DEFERRED), "EPI 2 / 7 use the DM 0 DMA form");
   uint32_t vp[16] = {};
   if constexpr (DM >= 1) {
     const uint32_t chunk = (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
@@ -217,6 +240,18 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       cv[m] = (uint32_t)(16 * m + rho) * (uint32_t)N * 2u + (uint32_t)(16 * (lane >> 4));
   }
   char* const stg = smem + 2 * W4AP_BUF + wid * W4AP_EPI_WAVE;
+  // EPI 7: the held C quarters, the lane's LDS slot of the staged quarter, the store offset walker
+  w4a_u32x4 held[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) held[i] = w4a_u32x4{0u, 0u, 0u, 0u};
+  const uint32_t stgl = (uint32_t)(uintptr_t)stg + (uint32_t)lane * 16u;
+  const uint32_t s8N = __builtin_amdgcn_readfirstlane((uint32_t)N * 8u);
+  const uint32_t vcur0 = (uint32_t)(32 + (lane >> 4)) * (uint32_t)N * 2u + (uint32_t)(lane & 15) * 16u;
+  auto corner = [&](int tm_, int tn_) {
+    const uint64_t cc = (uint64_t)(uintptr_t)(C + (size_t)(tm_ * W4AP_TILE + wr * 128) * N + tn_ * W4AP_TILE + wc * 128);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cc >> 32)) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cc);
+  };
 
   int tm, tn;
   coords(tile, tm, tn);
@@ -226,6 +261,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   uint32_t koff = koff0(rev);
   int kstep = kst(rev);
   uint32_t first = 1;
+  uint64_t sCp = corner(tm, tn);    // the first tile's deferred stores write its own corner (overwritten later)
 
   asm volatile("" ::: W4_AGPR_CLOBBERS);
   if constexpr (EPI != 2)     // EF: every tile's first K-tile starts its accumulators with src C = 0
@@ -257,6 +293,13 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         F8EF_LOOP_SELECT(SC)
       } else {
         W4EF_LOOP_SELECT(SC)
+      }
+    } else if constexpr (EPI == W4AP_EPI_DEFERRED) {
+      uint32_t vcur = vcur0;
+      if constexpr (F8) {
+        F8DS_LOOP_SELECT(SC)
+      } else {
+        W4DS_LOOP_SELECT(SC)
       }
     } else if constexpr (DM >= 1 && F8) {
       F8VP_LOOP_SELECT(SC)
@@ -302,6 +345,36 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       });
       asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
       if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA landed
+      if constexpr (EPI == W4AP_EPI_DEFERRED) {
+        // quarter 0 now; with a next tile, quarters 1-2 stay in registers (held) and quarter 3 in this
+        // wave's staging LDS, lane-linear, for the next tile's K-loop to store (W4DS_LOOP)
+        uint4 vv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = k * 4 + (lane >> 4);
+          const int sw = r & 15;
+          const int pg = (2 * (lane & 15)) ^ sw;
+          const uint4 raw = *reinterpret_cast<const uint4*>(stg + r * 256 + ((pg & ~1) << 3));
+          vv[k] = raw;
+          if (sw & 1) { vv[k].x = raw.z; vv[k].y = raw.w; vv[k].z = raw.x; vv[k].w = raw.y; }
+        }
+        if (s == 0 || !hasnext) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int r = k * 4 + (lane >> 4);
+            store_c16(C + (size_t)(tm * W4AP_TILE + wr * 128 + s * 32 + r) * N + tn * W4AP_TILE + wc * 128 +
+                          (lane & 15) * 8, vv[k]);
+          }
+        } else if constexpr (s == 1 || s == 2) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            held[(s - 1) * 8 + k] = w4a_u32x4{vv[k].x, vv[k].y, vv[k].z, vv[k].w};
+        } else {
+          asm volatile("" ::: "memory");   // every read of the staging above is issued before these writes
+#pragma unroll
+          for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(stg + k * 1024 + lane * 16) = vv[k];
+        }
+      } else
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int r = k * 4 + (lane >> 4);
@@ -314,9 +387,9 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         const int slot = wr * 128 + s * 32 + r;                        // the tile row's LDS slot
         const int crow = DM == 2 ? 32 * (slot & 7) + (slot >> 3) : slot; // PA: slot -> panel row
         __bf16* const dst = C + (size_t)(tm * W4AP_TILE + crow) * N + tn * W4AP_TILE + wc * 128 + ch * 8;
-        if constexpr (EPI == 3) {        // knock-out: keep the value live, skip the global store
+        if constexpr (EPI == 3 || (EPI == 5 && s > 0) || (EPI == 6 && s > 1)) {   // knock-outs: skip the store
           asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-        } else if constexpr (EPI == 4) {   // nontemporal (streaming) C stores: global_store ... nt
+        } else if constexpr (EPI == 4 || EPI == 5 || EPI == 6) {   // nontemporal (streaming) C stores
           store_c16(dst, v);
         } else {
           *reinterpret_cast<uint4*>(dst) = v;
@@ -325,6 +398,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       asm volatile("" ::: "memory");
     });
     }
+    if constexpr (EPI == W4AP_EPI_DEFERRED) sCp = corner(tm, tn);   // the next tile stores this tile's rest
     if (!hasnext) break;
     tile = next;
     tm = ntm;

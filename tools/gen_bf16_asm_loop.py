@@ -165,7 +165,8 @@ PERSISTENT = ["v18", "v18_d6b", "v18_d5_late", "v18_d6b_bout", "v18_d5_late_bout
 # a name ending in _rw: that schedule in kloop_persistent_rw (relaxed first landing wait)
 
 
-def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, w2_extra: int = 0) -> List[str]:
+def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, w2_extra: int = 0,
+         extra: Dict[int, List[str]] = None) -> List[str]:
     """One K-tile: MFMAs on tile t (buffer ``cur``), R1 reads from ``cur``, DMA of tile t+2 into
     ``cur``, R0 reads of tile t+1 from the other buffer. ``nxt_tile``: the DMA fetches the next
     output tile's K-tile instead (persistent kernel drain: operands nA / nB / nvoff / nkstep)."""
@@ -193,6 +194,8 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, w2
             isb, x = read_order(j)
             gap[s].append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}{nxt}0] offset:{x * 2048}")
         gap[sc.w3].append("s_waitcnt lgkmcnt(0)")
+    for i, ops in (extra or {}).items():
+        gap[i] += ops
     out = []
     for i in range(SLOTS):
         out.append(mfma(i, sc.bout))
@@ -260,6 +263,70 @@ def kloop_persistent_rw(sc: Schedule, stores: int = 32) -> List[str]:
     out += body(sc, 1, dma=False, nx=False)
     out.append(".Lw4rw_done_%=:")
     return out
+
+
+# Deferred C stores (frame EPI 7, gemm_w4ap.h): the staged epilogue stores only the first quarter of
+# the tile (8 stores per wave); the other 24 go out from the next tile's first 6 K-tiles, 4 at the
+# start of each (before its DMA pieces, so the next landing wait but one is the first to need them):
+# 16 from VGPRs the epilogue left in %[h0..h15], 8 from the wave's staging LDS, read into v[240:255]
+# at the end of the K-tile before. Knock-outs priced the burst: storing a quarter of C at the tile
+# boundary costs 0.2 %, all of it 1.5 % (bf16 8192^3; fp8 0.4 % / 3.3 %; profiles/r3_s2/).
+DS_PEEL = 6                          # K-tiles carrying deferred stores (3 loop pairs)
+DS_STORE_SLOTS = (1, 3, 5, 7)        # store slots in a carrying K-tile (add of %[vcur] one slot later)
+DS_LDS_SLOTS = (116, 117, 118, 119)  # ds_reads for the next K-tile's LDS-held stores (w3 covers them)
+DS_EPI_STORES = 8                    # stores the staged epilogue itself issues (pass 0)
+
+
+def ds_ops(j: int, store_slots=DS_STORE_SLOTS, lds_slots=DS_LDS_SLOTS) -> Dict[int, List[str]]:
+    """Deferred-store ops of carrying K-tile j (0-based within the tile)."""
+    ops: Dict[int, List[str]] = {}
+    for n, sl in enumerate(store_slots):
+        item = 4 * j + n
+        data = f"%[h{item}]" if item < 16 else f"v[{240 + 4 * n}:{243 + 4 * n}]"
+        ops.setdefault(sl, []).append(f"global_store_dwordx4 %[vcur], {data}, %[sCp] nt")
+        ops.setdefault(sl + 1, []).append("v_add_u32_e32 %[vcur], %[s8N], %[vcur]")
+    if j + 1 < DS_PEEL and 4 * (j + 1) >= 16:        # the next K-tile stores from LDS: read it now
+        for n, sl in enumerate(lds_slots):
+            k = 4 * (j + 1) - 16 + n
+            ops.setdefault(sl, []).append(f"ds_read_b128 v[{240 + 4 * n}:{243 + 4 * n}], %[stgl] offset:{k * 1024}")
+    return ops
+
+
+def kloop_persistent_ds(sc: Schedule) -> List[str]:
+    """kloop_persistent() with the deferred stores in the first DS_PEEL K-tiles (host: >= 8 K-tiles).
+    Landing waits: the first K-tile's skips the epilogue's 8 stores and its own 4 (the first tile of a
+    workgroup waits for both prologue K-tiles instead), every carrying K-tile's skips its own 4."""
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lw4ds_entry_%="]
+    out += [x for x in prologue() if not x.startswith("ds_read") and x != "s_waitcnt lgkmcnt(0)"
+            and x != "s_barrier" and not x.startswith("s_waitcnt vmcnt")]
+    out.append("s_waitcnt vmcnt(0)")
+    out.append(".Lw4ds_entry_%=:")
+    out.append("s_barrier")
+    for j in range(16):
+        isb, x = read_order(j)
+        out.append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}00] offset:{x * 2048}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    for j in range(DS_PEEL):
+        extra = len(DS_STORE_SLOTS) + (DS_EPI_STORES if j == 0 else 0)
+        out += body(sc, j % 2, dma=True, nx=True, w2_extra=extra, extra=ds_ops(j))
+    out += [f"s_sub_u32 %[cnt], %[cnt], {DS_PEEL // 2}", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4ds_drain_%="]
+    out.append(".Lw4ds_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4ds_loop_%="]
+    out.append(".Lw4ds_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lw4ds_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True)
+    out += body(sc, 1, dma=True, nx=False, nxt_tile=True)
+    out += ["s_branch .Lw4ds_done_%=", ".Lw4ds_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    out.append(".Lw4ds_done_%=:")
+    assert sum(ln.startswith("global_store") for ln in out) == 24
+    return out
+
+
+DS = ["g4"]
 
 
 def kloop_persistent(sc: Schedule) -> List[str]:
@@ -634,6 +701,20 @@ def render() -> str:
         if name.endswith("_nt"):
             lines = [ln + " nt" if ln.startswith("global_store") else ln for ln in lines]
         parts.append(f"#define W4EF_ASM_{name.upper()} \\")
+        for ln in lines:
+            parts.append(f'  "{ln}\\n\\t" \\')
+        parts.append('  ""')
+        parts.append("")
+    dsel = [f"if constexpr (SC == {i}) W4DS_LOOP(W4DS_ASM_{n.upper()});" for i, n in enumerate(DS)]
+    parts.append("// deferred-store form (frame EPI 7): schedule index -> asm text (W4DS_LOOP)")
+    parts.append("#define W4DS_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(dsel))
+    for i, n in enumerate(DS):
+        parts.append(f"#define W4DS_SC_{n.upper()} {i}")
+    parts.append("")
+    for name in DS:
+        lines = kloop_persistent_ds(SCHEDULES[name])
+        parts.append(f"#define W4DS_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
         parts.append('  ""')

@@ -179,7 +179,8 @@ def rd(isb: bool, x: int, h: int, buf: int, ef: bool) -> str:
 
 
 def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, ef: bool = False,
-         zero_c: bool = False, w2_extra: int = 0, last: bool = False, cap: int = 7) -> List[str]:
+         zero_c: bool = False, w2_extra: int = 0, last: bool = False, cap: int = 7,
+         extra: Dict[int, List[str]] = None) -> List[str]:
     """One K-tile. EF kernel (ef): permuted B reads; zero_c: src C = 0 (the tile's first K-tile);
     w2_extra: stores younger than the landing pieces; last: the fused epilogue in the gaps."""
     rA, rB, voff, kstep = ("%[nA]", "%[nB]", "%[nvoff]", "%[nkstep]") if nxt_tile else \
@@ -204,6 +205,8 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, ef
         for (isb, x, h), s in zip(R0_ORDER, sc.r0):
             gap[s].append(("read", None, rd(isb, x, h, nxt, ef)))
     gap[sc.w3].append(("lgk0", None, "s_waitcnt lgkmcnt(0)"))
+    for i, ops in (extra or {}).items():
+        gap[i] += [("read", None, t) if t.startswith("ds_read") else ("op", None, t) for t in ops]
     tail: List[str] = []
     if last:
         assert ef and not nx
@@ -277,6 +280,61 @@ def kloop_persistent_rw(sc: Schedule, stores: int = 32) -> List[str]:
     out += body(sc, 1, dma=False, nx=False)
     out.append(".Lf8rw_done_%=:")
     return out
+
+
+# Deferred C stores (frame EPI 7; the bf16 generator documents the protocol). fp8 K-tile: stores at
+# the odd slots 1..7 (no R1 reads there, before the first DMA piece at 18), the LDS reads for the next
+# K-tile at 51..57 (after the R0 reads; the K-tile's closing lgkmcnt(0) covers them).
+DS_PEEL = 6
+DS_STORE_SLOTS = (1, 3, 5, 7)
+DS_ADD_SLOTS = (9, 11, 13, 15)
+DS_LDS_SLOTS = (51, 53, 55, 57)
+DS_EPI_STORES = 8
+
+
+def ds_ops(j: int) -> Dict[int, List[str]]:
+    ops: Dict[int, List[str]] = {}
+    for n, (sl, al) in enumerate(zip(DS_STORE_SLOTS, DS_ADD_SLOTS)):
+        item = 4 * j + n
+        data = f"%[h{item}]" if item < 16 else f"v[{240 + 4 * n}:{243 + 4 * n}]"
+        ops.setdefault(sl, []).append(f"global_store_dwordx4 %[vcur], {data}, %[sCp] nt")
+        ops.setdefault(sl + 1, []).append("v_add_u32_e32 %[vcur], %[s8N], %[vcur]")
+    if j + 1 < DS_PEEL and 4 * (j + 1) >= 16:
+        for n, sl in enumerate(DS_LDS_SLOTS):
+            k = 4 * (j + 1) - 16 + n
+            ops.setdefault(sl, []).append(f"ds_read_b128 v[{240 + 4 * n}:{243 + 4 * n}], %[stgl] offset:{k * 1024}")
+    return ops
+
+
+def kloop_persistent_ds(sc: Schedule) -> List[str]:
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lf8ds_entry_%="]
+    out += prologue()
+    out += ["s_waitcnt vmcnt(0)"]
+    out.append(".Lf8ds_entry_%=:")
+    out.append("s_barrier")
+    out += r0_reads(0)
+    out.append("s_waitcnt lgkmcnt(0)")
+    for j in range(DS_PEEL):
+        extra = len(DS_STORE_SLOTS) + (DS_EPI_STORES if j == 0 else 0)
+        out += body(sc, j % 2, dma=True, nx=True, w2_extra=extra, extra=ds_ops(j))
+    out += [f"s_sub_u32 %[cnt], %[cnt], {DS_PEEL // 2}", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8ds_drain_%="]
+    out.append(".Lf8ds_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8ds_loop_%="]
+    out.append(".Lf8ds_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lf8ds_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True)
+    out += body(sc, 1, dma=True, nx=False, nxt_tile=True)
+    out += ["s_branch .Lf8ds_done_%=", ".Lf8ds_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    out.append(".Lf8ds_done_%=:")
+    assert sum(ln.startswith("global_store") for ln in out) == 24
+    return out
+
+
+DS = ["p"]
 
 
 def kloop_persistent(sc: Schedule) -> List[str]:
@@ -501,6 +559,20 @@ def render() -> str:
         if name.endswith("_nt"):
             lines = [ln + " nt" if ln.startswith("global_store") else ln for ln in lines]
         parts.append(f"#define F8EF_ASM_{name.upper()} \\")
+        for ln in lines:
+            parts.append(f'  "{ln}\\n\\t" \\')
+        parts.append('  ""')
+        parts.append("")
+    dsel = [f"if constexpr (SC == {i}) W4DS_LOOP(F8DS_ASM_{n.upper()});" for i, n in enumerate(DS)]
+    parts.append("// deferred-store form (frame EPI 7): schedule index -> asm text (W4DS_LOOP)")
+    parts.append("#define F8DS_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(dsel))
+    for i, n in enumerate(DS):
+        parts.append(f"#define F8DS_SC_{n.upper()} {i}")
+    parts.append("")
+    for name in DS:
+        lines = kloop_persistent_ds(SCHEDULES[name])
+        parts.append(f"#define F8DS_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
         parts.append('  ""')
