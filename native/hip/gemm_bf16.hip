@@ -43,11 +43,14 @@
 // lgkmcnt stall out of the free barrier; g6d6 also spaces the DMA pieces 6 MFMAs apart, which
 // spreads the HBM requests of a one-wave grid whose workgroups run in lockstep.
 // profiles/r3_asm/asm8_summary.jsonl, asm9_summary.jsonl
+// Every tile's first K-tile starts its accumulators with src C = 0 (the *_zc schedules, EPI 8), so the
+// epilogue reads the accumulators without writing zeros back: 8192^3 +0.8 %, 8192^2x2048 +1.4 %
+// (profiles/r3_s2/zc_bf16.jsonl).
 // The C tile leaves through nontemporal (streaming) stores: the next tile's first landing wait and
 // the end-of-kernel release no longer wait on C lines allocated in L2 (8192^3 +1.1 %, one dispatch
 // wave 4096^2x16384 +6.3 %; profiles/r3_s2/nt_*.jsonl).
-#define W4AP_SC_MAIN W4AP_SC_G4
-#define W4AP_SC_LONGK W4AP_SC_G6D6
+#define W4AP_SC_MAIN W4AP_SC_G4_ZC
+#define W4AP_SC_LONGK W4AP_SC_G6D6_ZC
 
 static int g_variant = 0;
 
@@ -169,23 +172,23 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          0, s, a, b, c, M, N, K);
       break;
     case 50:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_NT>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 51:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, true, W4AP_EPI_STAGED_NT>), dim3(256), dim3(W4_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 53:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4, true, false, W4AP_EPI_STAGED_NT, 1>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 1>), dim3(persistent_grid(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 54:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4, true, true, W4AP_EPI_STAGED_NT, 1>), dim3(256), dim3(W4_THREADS),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC, 1>), dim3(256), dim3(W4_THREADS),
                          0, s, a, b, c, M, N, K);
       break;
     case 52:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_NT>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {

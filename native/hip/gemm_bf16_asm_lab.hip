@@ -13,6 +13,7 @@
 //   180 / 181 / 182 = relaxed first landing wait (_rw): g4 (= v50 + rw), g6d6 (v52 + rw), g4 square raster (v51 + rw)
 //   190 / 191 / 192 / 193 = VP DMA form: g4 (= v50 in VP form), g4 + PA, g6d6 VP, g4 + PA linear K
 //   194 / 195 = VP DMA form on the square raster (g4), without / with PA
+//   197 / 198 / 265 / 266 = ZC (EPI 8, src C = 0 first K-tile): bf16 v50 / v51, fp8 v20 / v21 forms
 //   196 / 264 = deferred C stores (EPI 7): bf16 g4 serpentine (v50 + DS), fp8 p linear (v20 + DS); K >= 8 K-tiles
 //   163 / 164 = knock-outs: production epilogue storing only the first quarter / half of C; 233 = fp8 quarter
 //   162 = v50 (136) with nontemporal C stores; 174 = 170 with nontemporal stores
@@ -185,6 +186,18 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
                          a, b, c, M, N, K);
       break;
     }
+    case 197: {   // ZC (EPI 8): v50 with src C = 0 in each tile's first K-tile, epilogue without zeroing writes
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC>), dim3(g), dim3(W4_THREADS), 0,
+                         s, a, b, c, M, N, K);
+      break;
+    }
+    case 198:     // ZC on the square raster (v51 + ZC)
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(W4_THREADS), 0,
+                         s, a, b, c, M, N, K);
+      break;
     case 161: {   // knock-out: v50 with the epilogue but without its global C stores
       const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
       if (g < NXCD) return (int)hipErrorInvalidValue;
@@ -293,6 +306,16 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     case 264:     // deferred C stores (EPI 7): v20 (p, linear K)
       if (g < NXCD || K < 8 * 2 * F8_BK) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8DS_SC_P, false, false, W4AP_EPI_DEFERRED>), dim3(g), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 265:     // ZC (EPI 8): v20 with src C = 0 in each tile's first K-tile
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, false, false, W4AP_EPI_STAGED_ZC>), dim3(g), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 266:     // ZC square raster (v21 + ZC)
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 231:     // knock-out: 200 with the epilogue but without its global C stores

@@ -15,8 +15,9 @@
 //       q16 K-tile body as one hand-scheduled asm block per output tile in the persistent frame of
 //       the bf16 v50 (gemm_w4ap.h, tools/gen_fp8_asm_loop.py), nontemporal C stores (4096^3 +4.9 %,
 //       16384^2x1024 +6.6 %): v20 schedule p, linear K; v21 the same
-//       on the square cross-XCD raster with serpentine K, for >= 8 dispatch waves on 16x16-tile
-//       multiples. Against hipBLASLt fp8 on MI355X (profiles/r3_s2/): 8192^3 1.005-1.021x (q16p
+//       on the square cross-XCD raster with serpentine K, for >= 2 dispatch waves on 16x16-tile
+//       multiples (8192^2x2048 1.03x vs v20 0.98x, 16384^2x4096 1.01x vs 0.99x; profiles/r3_s2/zc_fp8.jsonl).
+//       Both start each tile's accumulators with src C = 0 (the p_zc schedule, EPI 8; 8192^2x2048 +3.9 %). Against hipBLASLt fp8 on MI355X (profiles/r3_s2/): 8192^3 1.005-1.021x (q16p
 //       0.974-0.981x), 4096^3 1.04x, 16384^3 1.03x (v21), 16384^2x2048 1.05x (v21), 16384^2x1024
 //       1.09x (v21), 16384x8192x8192 1.00x.
 //   10 / 15 / 16 / 17 / 18 / 20 / 21 = that kernel pinned (no automatic switch; falls back when the
@@ -42,7 +43,7 @@ static int resolve_fp8_variant(int M, int N, int K) {
   int v = g_fp8_variant;
   const bool ap_ok = cus == 256 && K % (2 * F8_BK) == 0 && K >= 4 * F8_BK && pgrid >= NXCD;
   if (v == 0 && ap_ok) {
-    v = (sq && nwg >= 8 * cus) ? 21 : 20;
+    v = (sq && nwg >= 2 * cus) ? 21 : 20;
   } else if (v == 0) {
     v = sq ? 16 : 15;
     // Short K (<= 12 K-tiles) with several tiles per CU: the persistent block-scaled kernel hides
@@ -91,11 +92,11 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
       hipLaunchKernelGGL((gemm_fp8_256x256_q16p<>), dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 20:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, false, false, W4AP_EPI_STAGED_NT>), dim3(pgrid), dim3(F8_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, false, false, W4AP_EPI_STAGED_ZC>), dim3(pgrid), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 21:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P, true, true, W4AP_EPI_STAGED_NT>), dim3(256), dim3(F8_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 15:

@@ -127,6 +127,8 @@ constexpr int W4AP_EPI_FUSED = 2;       // C stored from the last K-tile's MFMA 
 constexpr int W4AP_EPI_KO_NOSTORE = 3;  // lab knock-out: staged epilogue without the global stores
 constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores: production (profiles/r3_s2/)
 constexpr int W4AP_EPI_DEFERRED = 7;    // staged nt, quarters 1-3 of C stored during the next tile's K-loop
+constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile starts accumulators with src C = 0,
+                                        // so the epilogue only reads them (generated *_zc schedules)
 
 // A, Bt: K-major operands (element size 1 for F8, else 2); C: bf16; smem: W4AP_LDS bytes.
 // DM (DMA form): 0 = one lane offset + per-row-block SGPR soffsets, SC indexes W4AP/F8AP schedules;
@@ -264,7 +266,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   uint64_t sCp = corner(tm, tn);    // the first tile's deferred stores write its own corner (overwritten later)
 
   asm volatile("" ::: W4_AGPR_CLOBBERS);
-  if constexpr (EPI != 2)     // EF: every tile's first K-tile starts its accumulators with src C = 0
+  if constexpr (EPI != 2 && EPI != W4AP_EPI_STAGED_ZC)   // EF / ZC: the first K-tile uses src C = 0
     static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
   for (;;) {
     const int next = tile + per;
@@ -319,8 +321,11 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     } else if constexpr (EPI == 1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-    if constexpr (F8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    else asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA D -> accvgpr reads
+    // last MFMA D -> accvgpr reads. ZC reads in pass order, whose first accumulators took their last
+    // MFMA >= 16 MFMAs before the end of the K-tile (g4 / p orders), so it needs no pad
+    if constexpr (EPI == W4AP_EPI_STAGED_ZC) {
+    } else if constexpr (F8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    else asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     static_for<0, 4>([&](auto S) {
       constexpr int s = decltype(S)::value;
       static_for<0, 16>([&](auto I) {
@@ -328,12 +333,18 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         constexpr int mm = u >> 3, n = u & 7;
         constexpr int i = (2 * s + mm) * 8 + n;                    // accumulator index m*8+n
         float x0, x1, x2, x3;
-        asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
-                     "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
-                     "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
-                     "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
-                     : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
-                     : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+        if constexpr (EPI == W4AP_EPI_STAGED_ZC)
+          asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                       "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                       : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                       : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+        else
+          asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                       "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7\n\t"
+                       "v_accvgpr_write_b32 a%c4, 0\n\tv_accvgpr_write_b32 a%c5, 0\n\t"
+                       "v_accvgpr_write_b32 a%c6, 0\n\tv_accvgpr_write_b32 a%c7, 0"
+                       : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                       : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
         const int r = mm * 16 + (lane & 15);
         const int g = n * 4 + (lane >> 4);
         bf16x4 v;
@@ -389,7 +400,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         __bf16* const dst = C + (size_t)(tm * W4AP_TILE + crow) * N + tn * W4AP_TILE + wc * 128 + ch * 8;
         if constexpr (EPI == 3 || (EPI == 5 && s > 0) || (EPI == 6 && s > 1)) {   // knock-outs: skip the store
           asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-        } else if constexpr (EPI == 4 || EPI == 5 || EPI == 6) {   // nontemporal (streaming) C stores
+        } else if constexpr (EPI == 4 || EPI == 5 || EPI == 6 || EPI == W4AP_EPI_STAGED_ZC) {   // nontemporal stores
           store_c16(dst, v);
         } else {
           *reinterpret_cast<uint4*>(dst) = v;

@@ -205,7 +205,9 @@ def test_w4ap_production_pipeline(asm):
     kernels = _kernels(asm, "gemm_bf16_256x256_w4apI")
     assert len(kernels) == 5
     for body, st in kernels:
-        assert _audit_asm_pipeline(body, st) == 6 * 128
+        # the zc schedules (every production form) peel the first K-tile pair (src C = 0): 8 bodies
+        assert _audit_asm_pipeline(body, st) == 8 * 128
+        assert "v_accvgpr_write" not in body      # src C = 0 instead of zeroing writes
 
 
 def test_w4a_lab_pipelines(tmp_path_factory):

@@ -154,7 +154,8 @@ def test_fp8_production_variant_set_is_closed(cuda_device):
     assert G.get_fp8_variant() == 0
     cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
     if cus == 256:       # MI355X: the persistent asm pipeline
-        assert G.resolve_fp8_variant(8192, 8192, 8192) == 20
+        assert G.resolve_fp8_variant(8192, 8192, 8192) == 21
+        assert G.resolve_fp8_variant(8192, 8192 + 256, 8192) == 20     # not 16x16-tile multiples
         assert G.resolve_fp8_variant(16384, 16384, 16384) == 21
         assert G.resolve_fp8_variant(16384, 16384, 1024) == 21
         assert G.resolve_fp8_variant(4096, 4096, 4096) == 20

@@ -56,15 +56,16 @@ def read_order(j: int):
     return False, j - 8
 
 
-def mfma(i: int, bout: bool = False) -> str:
+def mfma(i: int, bout: bool = False, zero_c: bool = False) -> str:
     """MFMA slot i: k-half i >> 6; A-outer (m = s >> 3, n = s & 7: the A fragment stays in srcB for
     8 MFMAs) or B-outer (n = s >> 3, m = s & 7: the B fragment stays in srcA for 8 MFMAs). Each
     accumulator m*8+n gets the same k sequence either way, so the results are identical."""
     r, s = (0, i) if i < 64 else (1, i - 64)
     m, n = (s & 7, s >> 3) if bout else (s >> 3, s & 7)
     acc = m * 8 + n
+    c = "0" if zero_c and r == 0 else f"a[{4 * acc}:{4 * acc + 3}]"     # zero_c: a tile's first k-half
     return (f"v_mfma_f32_16x16x32_bf16 a[{4 * acc}:{4 * acc + 3}], {frag_regs(r, True, n)}, "
-            f"{frag_regs(r, False, m)}, a[{4 * acc}:{4 * acc + 3}]")
+            f"{frag_regs(r, False, m)}, {c}")
 
 
 class Schedule:
@@ -161,12 +162,14 @@ SCHEDULES = {
 
 # schedules the persistent kernel is generated for (its SC index = position here)
 PERSISTENT = ["v18", "v18_d6b", "v18_d5_late", "v18_d6b_bout", "v18_d5_late_bout", "g4", "g6", "g8", "sp2g6",
-              "g6d6", "g4d6", "g2d6", "sp2g4d5", "m4", "m4d4", "m4d3", "m6d4", "g4_rw", "g6d6_rw"]
+              "g6d6", "g4d6", "g2d6", "sp2g4d5", "m4", "m4d4", "m4d3", "m6d4", "g4_rw", "g6d6_rw", "g4_zc",
+              "g6d6_zc"]
+# a name ending in _zc: kloop_persistent_zc (first K-tile with src C = 0; frame EPI 8)
 # a name ending in _rw: that schedule in kloop_persistent_rw (relaxed first landing wait)
 
 
 def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, w2_extra: int = 0,
-         extra: Dict[int, List[str]] = None) -> List[str]:
+         extra: Dict[int, List[str]] = None, zero_c: bool = False) -> List[str]:
     """One K-tile: MFMAs on tile t (buffer ``cur``), R1 reads from ``cur``, DMA of tile t+2 into
     ``cur``, R0 reads of tile t+1 from the other buffer. ``nxt_tile``: the DMA fetches the next
     output tile's K-tile instead (persistent kernel drain: operands nA / nB / nvoff / nkstep)."""
@@ -198,7 +201,7 @@ def body(sc: Schedule, cur: int, dma: bool, nx: bool, nxt_tile: bool = False, w2
         gap[i] += ops
     out = []
     for i in range(SLOTS):
-        out.append(mfma(i, sc.bout))
+        out.append(mfma(i, sc.bout, zero_c))
         out += gap[i]
     return out
 
@@ -327,6 +330,36 @@ def kloop_persistent_ds(sc: Schedule) -> List[str]:
 
 
 DS = ["g4"]
+
+
+def kloop_persistent_zc(sc: Schedule) -> List[str]:
+    """kloop_persistent() whose first K-tile issues its k-half-0 MFMAs with src C = 0 (frame EPI 8): the
+    epilogue reads the accumulators without writing 256 zeros back, and nothing zeroes them at start."""
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lw4zc_entry_%="]
+    out += [x for x in prologue() if not x.startswith("ds_read") and x != "s_waitcnt lgkmcnt(0)"
+            and x != "s_barrier"]
+    out.append(".Lw4zc_entry_%=:")
+    out.append("s_barrier")
+    for j in range(16):
+        isb, x = read_order(j)
+        out.append(f"ds_read_b128 {frag_regs(0, isb, x)}, %[{'rb' if isb else 'ra'}00] offset:{x * 2048}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += body(sc, 0, dma=True, nx=True, zero_c=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4zc_drain_%="]
+    out.append(".Lw4zc_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4zc_loop_%="]
+    out.append(".Lw4zc_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lw4zc_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True)
+    out += body(sc, 1, dma=True, nx=False, nxt_tile=True)
+    out += ["s_branch .Lw4zc_done_%=", ".Lw4zc_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    out.append(".Lw4zc_done_%=:")
+    return out
 
 
 def kloop_persistent(sc: Schedule) -> List[str]:
@@ -632,7 +665,7 @@ EF = ["g4", "g6d6", "g4_nt"]
 # (%[koff], %[nkoff] for the next tile) used as the soffset: one SALU add per K-tile instead of a VALU
 # add, no per-piece row-block SGPRs, and A and B pieces may use different row maps -- DM = 2 reads each
 # A-panel DMA instruction's 8 rows 32 apart (PA: K not a power of two, see gemm_bf16.hip v47).
-VP = ["g4", "g6d6"]
+VP = ["g4", "g6d6", "g4_zc"]   # _zc: from kloop_persistent_zc (frame EPI 8)
 
 
 def to_vp(lines: List[str]) -> List[str]:
@@ -727,14 +760,15 @@ def render() -> str:
         parts.append(f"#define W4VP_SC_{n.upper()} {i}")
     parts.append("")
     for name in VP:
-        lines = to_vp(kloop_persistent(SCHEDULES[name]))
+        lines = to_vp(kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
         parts.append(f"#define W4VP_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
         parts.append('  ""')
         parts.append("")
     for name in PERSISTENT:
-        lines = kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else kloop_persistent(SCHEDULES[name])
+        lines = (kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else
+                 kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
         parts.append(f"#define W4AP_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')

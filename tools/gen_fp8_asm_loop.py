@@ -166,7 +166,8 @@ SCHEDULES["m"] = make("m", r1=list(range(16)), w1=19, dma=[21 + 2 * p for p in r
 SCHEDULES["md3"] = make("md3", r1=list(range(16)), w1=19, dma=[21 + 3 * p for p in range(14)] + [61, 63],
                         w2=None, r0=_M_R0)
 
-PERSISTENT = list(SCHEDULES) + ["p_rw", "s1d3_rw"]
+PERSISTENT = list(SCHEDULES) + ["p_rw", "s1d3_rw", "p_zc"]
+# a name ending in _zc: kloop_persistent_zc (first K-tile with src C = 0; frame EPI 8)
 # a name ending in _rw: that schedule in kloop_persistent_rw (relaxed first landing wait)
 
 
@@ -335,6 +336,33 @@ def kloop_persistent_ds(sc: Schedule) -> List[str]:
 
 
 DS = ["p"]
+
+
+def kloop_persistent_zc(sc: Schedule) -> List[str]:
+    """kloop_persistent() whose first K-tile starts every accumulator with src C = 0 (frame EPI 8)."""
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lf8zc_entry_%="]
+    out += prologue()
+    out += ["s_waitcnt vmcnt(16)"]
+    out.append(".Lf8zc_entry_%=:")
+    out.append("s_barrier")
+    out += r0_reads(0)
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += body(sc, 0, dma=True, nx=True, zero_c=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8zc_drain_%="]
+    out.append(".Lf8zc_loop_%=:")
+    out += body(sc, 0, dma=True, nx=True)
+    out += body(sc, 1, dma=True, nx=True)
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lf8zc_loop_%="]
+    out.append(".Lf8zc_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lf8zc_last_%="]
+    out += body(sc, 0, dma=True, nx=True, nxt_tile=True)
+    out += body(sc, 1, dma=True, nx=False, nxt_tile=True)
+    out += ["s_branch .Lf8zc_done_%=", ".Lf8zc_last_%=:"]
+    out += body(sc, 0, dma=False, nx=True)
+    out += body(sc, 1, dma=False, nx=False)
+    out.append(".Lf8zc_done_%=:")
+    return out
 
 
 def kloop_persistent(sc: Schedule) -> List[str]:
@@ -592,7 +620,8 @@ def render() -> str:
         parts.append('  ""')
         parts.append("")
     for name in PERSISTENT:
-        lines = kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else kloop_persistent(SCHEDULES[name])
+        lines = (kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else
+                 kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
         a = audit(lines)
         parts.append(f"// {name}: {a['mfmas']} MFMAs, <= {a['max_fillers_per_gap']} instructions per MFMA gap")
         parts.append(f"#define F8AP_ASM_{name.upper()} \\")
