@@ -14,6 +14,7 @@
 //   190 / 191 / 192 / 193 = VP DMA form: g4 (= v50 in VP form), g4 + PA, g6d6 VP, g4 + PA linear K
 //   194 / 195 = VP DMA form on the square raster (g4), without / with PA
 //   197 / 198 / 265 / 266 = ZC (EPI 8, src C = 0 first K-tile): bf16 v50 / v51, fp8 v20 / v21 forms
+//   211-214 = 197 with store cache policy sc1 nt / sc0 sc1 / sc0 sc1 nt / sc0 nt
 //   196 / 264 = deferred C stores (EPI 7): bf16 g4 serpentine (v50 + DS), fp8 p linear (v20 + DS); K >= 8 K-tiles
 //   163 / 164 = knock-outs: production epilogue storing only the first quarter / half of C; 233 = fp8 quarter
 //   162 = v50 (136) with nontemporal C stores; 174 = 170 with nontemporal stores
@@ -191,6 +192,15 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
       if (g < NXCD) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC>), dim3(g), dim3(W4_THREADS), 0,
                          s, a, b, c, M, N, K);
+      break;
+    }
+    case 211: case 212: case 213: case 214: {   // 197 with store policy sc1 nt / sc0 sc1 / sc0 sc1 nt / sc0 nt
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      if (v == 211) hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, 11>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      if (v == 212) hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, 12>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      if (v == 213) hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, 13>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      if (v == 214) hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, 14>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     }
     case 198:     // ZC on the square raster (v51 + ZC)

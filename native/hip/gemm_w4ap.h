@@ -138,7 +138,8 @@ constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile 
 // K-tile's MFMA shadow, generated asm); knock-outs (lab only, wrong C): 1 = no epilogue at all,
 // 3 = the staged epilogue without its global stores (prices the stores against the rest);
 // 4 = the staged epilogue with nontemporal stores; 5 / 6 = lab knock-outs of 4 that store only the first
-// quarter / half of the tile (price the store burst by its size).
+// quarter / half of the tile (price the store burst by its size); 11-14 = ZC with other store
+// cache-policy bits (lab, store_c16_pol).
 template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
                                          __bf16* __restrict__ C, int M, int N, int K, char* smem) {
@@ -266,7 +267,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   uint64_t sCp = corner(tm, tn);    // the first tile's deferred stores write its own corner (overwritten later)
 
   asm volatile("" ::: W4_AGPR_CLOBBERS);
-  if constexpr (EPI != 2 && EPI != W4AP_EPI_STAGED_ZC)   // EF / ZC: the first K-tile uses src C = 0
+  if constexpr (EPI != 2 && EPI != W4AP_EPI_STAGED_ZC && !(EPI >= 11 && EPI <= 14))   // EF / ZC: src C = 0
     static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
   for (;;) {
     const int next = tile + per;
@@ -323,7 +324,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     } else {
     // last MFMA D -> accvgpr reads. ZC reads in pass order, whose first accumulators took their last
     // MFMA >= 16 MFMAs before the end of the K-tile (g4 / p orders), so it needs no pad
-    if constexpr (EPI == W4AP_EPI_STAGED_ZC) {
+    if constexpr (EPI == W4AP_EPI_STAGED_ZC || (EPI >= 11 && EPI <= 14)) {
     } else if constexpr (F8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     else asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     static_for<0, 4>([&](auto S) {
@@ -333,7 +334,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         constexpr int mm = u >> 3, n = u & 7;
         constexpr int i = (2 * s + mm) * 8 + n;                    // accumulator index m*8+n
         float x0, x1, x2, x3;
-        if constexpr (EPI == W4AP_EPI_STAGED_ZC)
+        if constexpr (EPI == W4AP_EPI_STAGED_ZC || (EPI >= 11 && EPI <= 14))
           asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
                        "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
                        : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
@@ -402,6 +403,8 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
           asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
         } else if constexpr (EPI == 4 || EPI == 5 || EPI == 6 || EPI == W4AP_EPI_STAGED_ZC) {   // nontemporal stores
           store_c16(dst, v);
+        } else if constexpr (EPI >= 11 && EPI <= 14) {   // lab: other cache-policy bits (store_c16_pol)
+          store_c16_pol<EPI - 10>(dst, v);
         } else {
           *reinterpret_cast<uint4*>(dst) = v;
         }
