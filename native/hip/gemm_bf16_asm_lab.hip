@@ -34,6 +34,55 @@
 #include "gemm_bf16_kernels.h"
 #include "gemm_fp8_kernels.h"
 
+namespace {
+
+// Lab: a 16-byte C store with explicit gfx950 cache-policy bits (POL: 1 = "sc1 nt", 2 = "sc0 sc1",
+// 3 = "sc0 sc1 nt", 4 = "sc0 nt"), to price the store path against store_c16's plain "nt".
+template <int POL>
+__device__ __forceinline__ void store_c16_pol(void* p, uint4 v) {
+  typedef unsigned int u32x4_p __attribute__((ext_vector_type(4)));
+  u32x4_p x;
+  x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" :: "v"(p), "v"(x) : "memory");
+  else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(x) : "memory");
+  else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" :: "v"(p), "v"(x) : "memory");
+  else asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" :: "v"(p), "v"(x) : "memory");
+}
+
+// Lab epilogue forms of the persistent frame (W4apEpi, gemm_w4ap.h): knock-outs that price the
+// epilogue (wrong C) and store-policy variants. Production kernels never instantiate these.
+constexpr int EPI_KO_NONE = 1;      // no epilogue at all
+constexpr int EPI_KO_NOSTORE = 3;   // staged epilogue without the global stores
+constexpr int EPI_KO_QUARTER = 5;   // nt stores of only the first quarter of C
+constexpr int EPI_KO_HALF = 6;      // ... the first half
+
+template <int EPI, int STORED_PASSES, bool ZC>
+struct W4apEpiLab {
+  static constexpr bool run = STORED_PASSES >= 0;
+  static constexpr bool zc = ZC;
+  template <int S>
+  static __device__ __forceinline__ void store(__bf16* dst, uint4 v) {
+    if constexpr (S < STORED_PASSES) store_c16(dst, v);
+    else asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));   // keep the value live
+  }
+};
+template <> struct W4apEpi<EPI_KO_NONE> : W4apEpiLab<EPI_KO_NONE, -1, false> {};
+template <> struct W4apEpi<EPI_KO_NOSTORE> : W4apEpiLab<EPI_KO_NOSTORE, 0, false> {};
+template <> struct W4apEpi<EPI_KO_QUARTER> : W4apEpiLab<EPI_KO_QUARTER, 1, false> {};
+template <> struct W4apEpi<EPI_KO_HALF> : W4apEpiLab<EPI_KO_HALF, 2, false> {};
+template <int P>
+struct W4apEpiPol {                 // ZC with the store cache-policy bits of store_c16_pol<P>
+  static constexpr bool run = true, zc = true;
+  template <int S>
+  static __device__ __forceinline__ void store(__bf16* dst, uint4 v) { store_c16_pol<P>(dst, v); }
+};
+template <> struct W4apEpi<11> : W4apEpiPol<1> {};
+template <> struct W4apEpi<12> : W4apEpiPol<2> {};
+template <> struct W4apEpi<13> : W4apEpiPol<3> {};
+template <> struct W4apEpi<14> : W4apEpiPol<4> {};
+
+}  // namespace
+
 extern "C" {
 
 int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {

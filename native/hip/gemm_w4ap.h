@@ -122,24 +122,30 @@ constexpr int W4AP_LDS = 2 * W4AP_BUF + 4 * W4AP_EPI_WAVE;   // 160 KiB
 
 // Epilogue forms (EPI template argument of w4ap_run and its kernels).
 constexpr int W4AP_EPI_STAGED = 0;      // LDS-staged row stores
-constexpr int W4AP_EPI_KO_NONE = 1;     // lab knock-out: no epilogue (wrong C)
 constexpr int W4AP_EPI_FUSED = 2;       // C stored from the last K-tile's MFMA gaps (generated asm)
-constexpr int W4AP_EPI_KO_NOSTORE = 3;  // lab knock-out: staged epilogue without the global stores
-constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores: production (profiles/r3_s2/)
+constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores (profiles/r3_s2/)
 constexpr int W4AP_EPI_DEFERRED = 7;    // staged nt, quarters 1-3 of C stored during the next tile's K-loop
 constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile starts accumulators with src C = 0,
                                         // so the epilogue only reads them (generated *_zc schedules)
+
+// What the staged epilogue does for an EPI value. The tools-only lab library specialises this for its
+// knock-out forms (native/hip/gemm_bf16_asm_lab.hip); the production forms are the primary template.
+template <int EPI>
+struct W4apEpi {
+  static constexpr bool run = true;                         // run the staged epilogue at all
+  static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC;     // the K-loop zeroes the accumulators (src C = 0)
+  template <int S>                                          // pass S's 16-byte C store
+  static __device__ __forceinline__ void store(__bf16* dst, uint4 v) {
+    if constexpr (EPI == W4AP_EPI_STAGED) *reinterpret_cast<uint4*>(dst) = v;
+    else store_c16(dst, v);
+  }
+};
 
 // A, Bt: K-major operands (element size 1 for F8, else 2); C: bf16; smem: W4AP_LDS bytes.
 // DM (DMA form): 0 = one lane offset + per-row-block SGPR soffsets, SC indexes W4AP/F8AP schedules;
 // 1 = VP (per-piece VGPR lane offsets, SGPR K offset), SC indexes the VP schedules; 2 = VP with the
 // A-panel pieces reading rows 32 apart (PA; the epilogue maps LDS slot s to C row 32 (s & 7) + (s >> 3)).
-// EPI: 0 = the staged epilogue below; 2 = the fused epilogue (the C tile leaves through the last
-// K-tile's MFMA shadow, generated asm); knock-outs (lab only, wrong C): 1 = no epilogue at all,
-// 3 = the staged epilogue without its global stores (prices the stores against the rest);
-// 4 = the staged epilogue with nontemporal stores; 5 / 6 = lab knock-outs of 4 that store only the first
-// quarter / half of the tile (price the store burst by its size); 11-14 = ZC with other store
-// cache-policy bits (lab, store_c16_pol).
+// EPI: the W4AP_EPI_* forms above (W4apEpi says what the staged epilogue does for each).
 template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
                                          __bf16* __restrict__ C, int M, int N, int K, char* smem) {
@@ -267,7 +273,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   uint64_t sCp = corner(tm, tn);    // the first tile's deferred stores write its own corner (overwritten later)
 
   asm volatile("" ::: W4_AGPR_CLOBBERS);
-  if constexpr (EPI != 2 && EPI != W4AP_EPI_STAGED_ZC && !(EPI >= 11 && EPI <= 14))   // EF / ZC: src C = 0
+  if constexpr (EPI != W4AP_EPI_FUSED && !W4apEpi<EPI>::zc)   // EF / ZC: the first K-tile uses src C = 0
     static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
   for (;;) {
     const int next = tile + per;
@@ -319,12 +325,12 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     if constexpr (EPI == 2) {
       // the asm block stored C; its stores and the next tile's DMA are waited for by count in the next block
-    } else if constexpr (EPI == 1) {
+    } else if constexpr (!W4apEpi<EPI>::run) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
     // last MFMA D -> accvgpr reads. ZC reads in pass order, whose first accumulators took their last
     // MFMA >= 16 MFMAs before the end of the K-tile (g4 / p orders), so it needs no pad
-    if constexpr (EPI == W4AP_EPI_STAGED_ZC || (EPI >= 11 && EPI <= 14)) {
+    if constexpr (W4apEpi<EPI>::zc) {
     } else if constexpr (F8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     else asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     static_for<0, 4>([&](auto S) {
@@ -334,7 +340,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         constexpr int mm = u >> 3, n = u & 7;
         constexpr int i = (2 * s + mm) * 8 + n;                    // accumulator index m*8+n
         float x0, x1, x2, x3;
-        if constexpr (EPI == W4AP_EPI_STAGED_ZC || (EPI >= 11 && EPI <= 14))
+        if constexpr (W4apEpi<EPI>::zc)
           asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
                        "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
                        : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
@@ -399,15 +405,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         const int slot = wr * 128 + s * 32 + r;                        // the tile row's LDS slot
         const int crow = DM == 2 ? 32 * (slot & 7) + (slot >> 3) : slot; // PA: slot -> panel row
         __bf16* const dst = C + (size_t)(tm * W4AP_TILE + crow) * N + tn * W4AP_TILE + wc * 128 + ch * 8;
-        if constexpr (EPI == 3 || (EPI == 5 && s > 0) || (EPI == 6 && s > 1)) {   // knock-outs: skip the store
-          asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-        } else if constexpr (EPI == 4 || EPI == 5 || EPI == 6 || EPI == W4AP_EPI_STAGED_ZC) {   // nontemporal stores
-          store_c16(dst, v);
-        } else if constexpr (EPI >= 11 && EPI <= 14) {   // lab: other cache-policy bits (store_c16_pol)
-          store_c16_pol<EPI - 10>(dst, v);
-        } else {
-          *reinterpret_cast<uint4*>(dst) = v;
-        }
+        W4apEpi<EPI>::template store<s>(dst, v);
       }
       asm volatile("" ::: "memory");
     });

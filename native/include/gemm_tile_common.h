@@ -119,17 +119,4 @@ __device__ __forceinline__ void store_c16(void* p, uint4 v) {
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4_nt*>(p));
 }
 
-// Lab: a 16-byte C store with explicit gfx950 cache-policy bits (POL: 1 = "sc1 nt", 2 = "sc0 sc1",
-// 3 = "sc0 sc1 nt", 4 = "sc0 nt"), to price the store path against store_c16's plain "nt".
-template <int POL>
-__device__ __forceinline__ void store_c16_pol(void* p, uint4 v) {
-  typedef unsigned int u32x4_p __attribute__((ext_vector_type(4)));
-  u32x4_p x;
-  x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-  if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" :: "v"(p), "v"(x) : "memory");
-  else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(x) : "memory");
-  else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" :: "v"(p), "v"(x) : "memory");
-  else asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" :: "v"(p), "v"(x) : "memory");
-}
-
 }  // namespace
