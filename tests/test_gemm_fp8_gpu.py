@@ -33,7 +33,8 @@ def fp8_variant(request):
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 512), (1024, 1024, 1024),
                                    (2048, 512, 4096), (768, 2304, 640), (256, 512, 384),
                                    (4608, 4608, 512),     # > 256 tiles: serpentine waves reverse K
-                                   (4096, 8192, 256), (8192, 4096, 384)])   # 16x16-tile super-tiles (v16)
+                                   (4096, 8192, 256), (8192, 4096, 384),    # 16x16-tile super-tiles (v16)
+                                   (4096, 8192, 512), (8192, 8192, 768)])   # v21: 2 / 4 dispatch waves, 4 / 6 K-tiles
 def test_fp8_fast_path_matches_fp32_reference(cuda_device, fp8_variant, m, n, k):
     import torch
     from gpu_operator_amd.ops import gemm as G
