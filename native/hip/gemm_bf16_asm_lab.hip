@@ -14,6 +14,7 @@
 //   190 / 191 / 192 / 193 = VP DMA form: g4 (= v50 in VP form), g4 + PA, g6d6 VP, g4 + PA linear K
 //   194 / 195 = VP DMA form on the square raster (g4), without / with PA
 //   197 / 198 / 265 / 266 = ZC (EPI 8, src C = 0 first K-tile): bf16 v50 / v51, fp8 v20 / v21 forms
+//   199 = direct epilogue (EPI 9: EF layout, stores from the accumulators, no LDS staging)
 //   211-214 = 197 with store cache policy sc1 nt / sc0 sc1 / sc0 sc1 nt / sc0 nt
 //   196 / 264 = deferred C stores (EPI 7): bf16 g4 serpentine (v50 + DS), fp8 p linear (v20 + DS); K >= 8 K-tiles
 //   163 / 164 = knock-outs: production epilogue storing only the first quarter / half of C; 233 = fp8 quarter
@@ -250,6 +251,13 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
       if (v == 212) hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, 12>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       if (v == 213) hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, 13>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       if (v == 214) hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, 14>), dim3(g), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 199: {   // direct epilogue (EPI 9): EF fragment layout, C stored from the accumulators after the loop
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4EF_SC_G4_POST, true, false, W4AP_EPI_DIRECT>), dim3(g), dim3(W4_THREADS), 0,
+                         s, a, b, c, M, N, K);
       break;
     }
     case 198:     // ZC on the square raster (v51 + ZC)

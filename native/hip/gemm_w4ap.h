@@ -125,6 +125,8 @@ constexpr int W4AP_EPI_STAGED = 0;      // LDS-staged row stores
 constexpr int W4AP_EPI_FUSED = 2;       // C stored from the last K-tile's MFMA gaps (generated asm)
 constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores (profiles/r3_s2/)
 constexpr int W4AP_EPI_DEFERRED = 7;    // staged nt, quarters 1-3 of C stored during the next tile's K-loop
+constexpr int W4AP_EPI_DIRECT = 9;      // EF fragment layout, src C = 0 first K-tile, C stored straight from the
+                                        // accumulators after the K-loop (no LDS staging; bf16)
 constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile starts accumulators with src C = 0,
                                         // so the epilogue only reads them (generated *_zc schedules)
 
@@ -232,7 +234,9 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   // holds C row 16m + r, columns 32p + 8g .. +7: cv[m] is that row's byte offset from the wave's corner.
   uint32_t rbe00 = 0, rbo00 = 0, rbe01 = 0, rbo01 = 0, rbe10 = 0, rbo10 = 0, rbe11 = 0, rbo11 = 0;
   uint32_t cv[8] = {};
-  if constexpr (EPI == 2) {
+  constexpr bool EFL = EPI == W4AP_EPI_FUSED || EPI == W4AP_EPI_DIRECT;   // the EF fragment layout
+  static_assert(!(EPI == W4AP_EPI_DIRECT && F8), "EPI 9 is generated for bf16 only");
+  if constexpr (EFL) {
     const int rho = lane & 15;
     const int re = 8 * (rho >> 2) + (rho & 3);
     uint32_t pe[2], po[2];
@@ -273,7 +277,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   uint64_t sCp = corner(tm, tn);    // the first tile's deferred stores write its own corner (overwritten later)
 
   asm volatile("" ::: W4_AGPR_CLOBBERS);
-  if constexpr (EPI != W4AP_EPI_FUSED && !W4apEpi<EPI>::zc)   // EF / ZC: the first K-tile uses src C = 0
+  if constexpr (!EFL && !W4apEpi<EPI>::zc)   // EF / direct / ZC: the first K-tile uses src C = 0
     static_for<0, 256>([&](auto R) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(R)::value)); });
   for (;;) {
     const int next = tile + per;
@@ -292,7 +296,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     uint32_t trips = __builtin_amdgcn_readfirstlane((uint32_t)((ktiles - 2) >> 1));
     uint32_t m0save;
     const uint32_t flags = __builtin_amdgcn_readfirstlane(first | (hasnext << 1));
-    if constexpr (EPI == 2) {
+    if constexpr (EFL) {
       // this tile's C corner for the fused epilogue's stores (wave-uniform)
       const uint64_t cc = (uint64_t)(uintptr_t)(C + (size_t)(tm * W4AP_TILE + wr * 128) * N + tn * W4AP_TILE + wc * 128);
       // readfirstlane returns int: widen through uint32_t, or bit 31 of the low word sign-extends
@@ -325,6 +329,28 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     if constexpr (EPI == 2) {
       // the asm block stored C; its stores and the next tile's DMA are waited for by count in the next block
+    } else if constexpr (EPI == W4AP_EPI_DIRECT) {
+      // accumulator pair (m, 2p), (m, 2p+1): lane (g, r) holds C row 16m + r, columns 32p + 8g .. +7
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the next tile's DMA landed
+      __bf16* const cw = C + (size_t)(tm * W4AP_TILE + wr * 128 + (lane & 15)) * N + tn * W4AP_TILE + wc * 128 +
+                         8 * (lane >> 4);
+      static_for<0, 32>([&](auto Q) {
+        constexpr int m = decltype(Q)::value >> 2, p = decltype(Q)::value & 3;
+        constexpr int a0 = 4 * (m * 8 + 2 * p);
+        float x[8];
+        asm volatile("v_accvgpr_read_b32 %0, a%c8\n\tv_accvgpr_read_b32 %1, a%c9\n\t"
+                     "v_accvgpr_read_b32 %2, a%c10\n\tv_accvgpr_read_b32 %3, a%c11\n\t"
+                     "v_accvgpr_read_b32 %4, a%c12\n\tv_accvgpr_read_b32 %5, a%c13\n\t"
+                     "v_accvgpr_read_b32 %6, a%c14\n\tv_accvgpr_read_b32 %7, a%c15"
+                     : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7])
+                     : "i"(a0), "i"(a0 + 1), "i"(a0 + 2), "i"(a0 + 3), "i"(a0 + 4), "i"(a0 + 5), "i"(a0 + 6),
+                       "i"(a0 + 7));
+        typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+        bf16x8 b;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b[e] = (__bf16)x[e];
+        store_c16(cw + (size_t)(16 * m) * N + 32 * p, __builtin_bit_cast(uint4, b));
+      });
     } else if constexpr (!W4apEpi<EPI>::run) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {

@@ -183,6 +183,12 @@ def _audit_asm_pipeline(body, st):
     # the persistent form adds the epilogue reads of the next tile's prologue
     assert mfma % 128 == 0 and mfma >= 3 * 128, mfma
     name = body.split(":", 1)[0]
+    if re.search(r"w4apILi\d+ELb\dELb\dELi9E", name):
+        # direct epilogue (EPI 9): the EF fragment layout with standard bodies; C stored after the block
+        # straight from the accumulators (32 pair stores, 256 accumulator reads, no LDS staging)
+        assert mfma == 8 * 128 and reads == 16 + 6 * 32 + 2 * 16, (mfma, reads)
+        assert body.count("global_store_dwordx4") == 32 and body.count("v_accvgpr_read_b32") == 256
+        return mfma
     if re.search(r"w4apILi\d+ELb\dELb\dELi2E", name):
         # fused epilogue (EPI=2): peeled first K-tile pair, loop, two drains whose last K-tiles read
         # only k-half 1 and store the C tile (32 pair stores each); no compiler epilogue

@@ -654,8 +654,40 @@ def kloop_persistent_ef(sc: Schedule, cap: int = 5) -> List[str]:
     return out
 
 
+def kloop_persistent_efp(sc: Schedule) -> List[str]:
+    """The EF fragment layout (permuted B reads: a lane of an accumulator pair holds 8 consecutive C
+    columns) with the standard K-tile bodies and src C = 0 in each tile's first K-tile; the C tile
+    is stored after the block straight from the accumulators, no LDS staging (frame EPI 9)."""
+    out = ["s_nop 4", "s_bitcmp0_b32 %[flags], 0", "s_cbranch_scc1 .Lw4efp_entry_%="]
+    out += [x for x in prologue() if not x.startswith("ds_read") and x != "s_waitcnt lgkmcnt(0)"
+            and x != "s_barrier"]
+    out.append(".Lw4efp_entry_%=:")
+    out.append("s_barrier")
+    for j in range(16):
+        isb, x = read_order(j)
+        out.append(b_read(0, x, 0) if isb else f"ds_read_b128 {frag_regs(0, False, x)}, %[ra00] offset:{x * 2048}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += body_ef(sc, 0, dma=True, nx=True, zero_c=True)[0]
+    out += body_ef(sc, 1, dma=True, nx=True)[0]
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4efp_drain_%="]
+    out.append(".Lw4efp_loop_%=:")
+    out += body_ef(sc, 0, dma=True, nx=True)[0]
+    out += body_ef(sc, 1, dma=True, nx=True)[0]
+    out += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 .Lw4efp_loop_%="]
+    out.append(".Lw4efp_drain_%=:")
+    out += ["s_bitcmp0_b32 %[flags], 1", "s_cbranch_scc1 .Lw4efp_last_%="]
+    out += body_ef(sc, 0, dma=True, nx=True, nxt_tile=True)[0]
+    out += body_ef(sc, 1, dma=True, nx=False, nxt_tile=True)[0]
+    out += ["s_branch .Lw4efp_done_%=", ".Lw4efp_last_%=:"]
+    out += body_ef(sc, 0, dma=False, nx=True)[0]
+    out += body_ef(sc, 1, dma=False, nx=False)[0]
+    out.append(".Lw4efp_done_%=:")
+    assert not any(ln.startswith("global_store") for ln in out)
+    return out
+
+
 # schedules the fused-epilogue kernel is generated for (index = EF SC)
-EF = ["g4", "g6d6", "g4_nt"]
+EF = ["g4", "g6d6", "g4_nt", "g4_post"]   # _post: kloop_persistent_efp (frame EPI 9)
 # a name ending in _nt: the same schedule with nontemporal C stores (global_store ... nt)
 
 
@@ -730,7 +762,8 @@ def render() -> str:
         parts.append(f"#define W4EF_SC_{n.upper()} {i}")
     parts.append("")
     for name in EF:
-        lines = kloop_persistent_ef(SCHEDULES[name.split("_")[0]])
+        lines = (kloop_persistent_efp(SCHEDULES[name.split("_")[0]]) if name.endswith("_post") else
+                 kloop_persistent_ef(SCHEDULES[name.split("_")[0]]))
         if name.endswith("_nt"):
             lines = [ln + " nt" if ln.startswith("global_store") else ln for ln in lines]
         parts.append(f"#define W4EF_ASM_{name.upper()} \\")
