@@ -14,6 +14,7 @@
 //   190 / 191 / 192 / 193 = VP DMA form: g4 (= v50 in VP form), g4 + PA, g6d6 VP, g4 + PA linear K
 //   194 / 195 = VP DMA form on the square raster (g4), without / with PA
 //   197 / 198 / 265 / 266 = ZC (EPI 8, src C = 0 first K-tile): bf16 v50 / v51, fp8 v20 / v21 forms
+//   200 / 267 / 268 = WG512 epilogue (EPI 10: workgroup-shared staging, 2 x 512-byte rows per store): bf16 v50, fp8 v20 / v21
 //   199 = direct epilogue (EPI 9: EF layout, stores from the accumulators, no LDS staging)
 //   211-214 = 197 with store cache policy sc1 nt / sc0 sc1 / sc0 sc1 nt / sc0 nt
 //   196 / 264 = deferred C stores (EPI 7): bf16 g4 serpentine (v50 + DS), fp8 p linear (v20 + DS); K >= 8 K-tiles
@@ -260,6 +261,13 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
                          s, a, b, c, M, N, K);
       break;
     }
+    case 200: {   // WG512 epilogue (EPI 10): ZC, workgroup-shared staging, 2 x 512 B rows per store
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, W4AP_EPI_WG512>), dim3(g), dim3(W4_THREADS), 0,
+                         s, a, b, c, M, N, K);
+      break;
+    }
     case 198:     // ZC on the square raster (v51 + ZC)
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(W4_THREADS), 0,
@@ -383,6 +391,16 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     case 266:     // ZC square raster (v21 + ZC)
       if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 267:     // WG512 epilogue (EPI 10) for v20 (p_zc, linear K)
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, false, false, W4AP_EPI_WG512>), dim3(g), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 268:     // WG512 epilogue for v21 (square raster)
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_WG512>), dim3(256), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 231:     // knock-out: 200 with the epilogue but without its global C stores

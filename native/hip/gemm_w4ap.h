@@ -127,6 +127,8 @@ constexpr int W4AP_EPI_STAGED_NT = 4;   // staged, nontemporal stores (profiles/
 constexpr int W4AP_EPI_DEFERRED = 7;    // staged nt, quarters 1-3 of C stored during the next tile's K-loop
 constexpr int W4AP_EPI_DIRECT = 9;      // EF fragment layout, src C = 0 first K-tile, C stored straight from the
                                         // accumulators after the K-loop (no LDS staging; bf16)
+constexpr int W4AP_EPI_WG512 = 10;      // ZC; the workgroup stages 512-byte C rows (both column halves) through
+                                        // the shared 32 KiB, 2 barriers per pass: one store = 2 full rows
 constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile starts accumulators with src C = 0,
                                         // so the epilogue only reads them (generated *_zc schedules)
 
@@ -135,7 +137,7 @@ constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile 
 template <int EPI>
 struct W4apEpi {
   static constexpr bool run = true;                         // run the staged epilogue at all
-  static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC;     // the K-loop zeroes the accumulators (src C = 0)
+  static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC || EPI == W4AP_EPI_WG512;   // K-loop zeroes (src C = 0)
   template <int S>                                          // pass S's 16-byte C store
   static __device__ __forceinline__ void store(__bf16* dst, uint4 v) {
     if constexpr (EPI == W4AP_EPI_STAGED) *reinterpret_cast<uint4*>(dst) = v;
@@ -385,11 +387,32 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         v[1] = (__bf16)x1;
         v[2] = (__bf16)x2;
         v[3] = (__bf16)x3;
-        *reinterpret_cast<bf16x4*>(stg + r * 256 + ((g ^ (r & 15)) << 3)) = v;
+        if constexpr (EPI == W4AP_EPI_WG512) {
+          // shared staging [wr][32 rows][512 B]: column group c (8 B) of row r at c ^ (r & 31)
+          const int c = wc * 32 + g;
+          *reinterpret_cast<bf16x4*>(smem + 2 * W4AP_BUF + wr * 16384 + r * 512 + ((c ^ (r & 31)) << 3)) = v;
+        } else {
+          *reinterpret_cast<bf16x4*>(stg + r * 256 + ((g ^ (r & 15)) << 3)) = v;
+        }
       });
       asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
       if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA landed
-      if constexpr (EPI == W4AP_EPI_DEFERRED) {
+      if constexpr (EPI == W4AP_EPI_WG512) {
+        __syncthreads();                  // both column halves of every row staged
+        // wave w stores rows (w & 1) * 16 .. +15 of row block w >> 1: one store = 2 rows x 512 B
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = (wid & 1) * 16 + 2 * k + (lane >> 5);
+          const int sw = r & 31;
+          const int pg = (2 * (lane & 31)) ^ sw;
+          const uint4 raw = *reinterpret_cast<const uint4*>(smem + 2 * W4AP_BUF + (wid >> 1) * 16384 + r * 512 +
+                                                            ((pg & ~1) << 3));
+          uint4 v = raw;
+          if (sw & 1) { v.x = raw.z; v.y = raw.w; v.z = raw.x; v.w = raw.y; }
+          store_c16(C + (size_t)(tm * W4AP_TILE + (wid >> 1) * 128 + s * 32 + r) * N + tn * W4AP_TILE + (lane & 31) * 8, v);
+        }
+        __syncthreads();                  // the staging is free for the next pass
+      } else if constexpr (EPI == W4AP_EPI_DEFERRED) {
         // quarter 0 now; with a next tile, quarters 1-2 stay in registers (held) and quarter 3 in this
         // wave's staging LDS, lane-linear, for the next tile's K-loop to store (W4DS_LOOP)
         uint4 vv[8];
