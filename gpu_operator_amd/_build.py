@@ -87,8 +87,11 @@ def _pyext_name(stem: str) -> str:
     return stem + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
 
 
+# Production builds read the generated headers with the shipped schedules only; the lab libraries
+# read the *_lab.h headers (every schedule), which mask the production ones (tools/gen_*_asm_loop.py).
 GEMM_HEADERS = ["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h",
                 "hip/gemm_fp8_kernels.h", "hip/gemm_fp8_asm_loop.h", "hip/gemm_w4ap.h"]
+LAB_HEADERS = GEMM_HEADERS + ["hip/gemm_bf16_asm_loop_lab.h", "hip/gemm_fp8_asm_loop_lab.h"]
 
 TARGETS: List[Target] = [
     # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.
@@ -118,13 +121,10 @@ TARGETS: List[Target] = [
 # (tools/gemm_lab.py). Never loaded by the validator; built on request (`--lab`).
 LAB_TARGETS: List[Target] = [
     # one library per dtype: an fp8 schedule edit rebuilds only the fp8 lab
-    Target("libamdgo_gemm_lab_bf16.so", ["hip/gemm_bf16_lab.hip"], "hip-shared",
-           headers=["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h"]),
-    Target("libamdgo_gemm_lab_fp8.so", ["hip/gemm_fp8_lab.hip"], "hip-shared",
-           headers=["include/gemm_tile_common.h", "hip/gemm_fp8_kernels.h"]),
+    Target("libamdgo_gemm_lab_bf16.so", ["hip/gemm_bf16_lab.hip"], "hip-shared", headers=LAB_HEADERS),
+    Target("libamdgo_gemm_lab_fp8.so", ["hip/gemm_fp8_lab.hip"], "hip-shared", headers=LAB_HEADERS),
     # the hand-scheduled bf16 K pipeline (w4a) next to v44 (tools/asm_lab.py)
-    Target("libamdgo_gemm_asmlab.so", ["hip/gemm_bf16_asm_lab.hip"], "hip-shared",
-           headers=["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h"]),
+    Target("libamdgo_gemm_asmlab.so", ["hip/gemm_bf16_asm_lab.hip"], "hip-shared", headers=LAB_HEADERS),
 ]
 
 

@@ -56,28 +56,28 @@ static int g_variant = 0;
 
 // Persistent grid: one workgroup per CU (the 160 KiB LDS admits one), a multiple of the 8 XCDs,
 // never more workgroups than tiles. 0 when the device or the tile count is too small.
-static int persistent_grid(int nwg) {
-  const int cus = device_cu_count();
+static int persistent_grid(int nwg, hipStream_t s) {
+  const int cus = device_cu_count(s);
   const int g = nwg < cus ? nwg : cus;
   return (g / NXCD) * NXCD;
 }
 
-// The kernel amdgo_gemm_bf16 runs for this shape on this device (0 = generic).
-static int resolve_variant(int M, int N, int K) {
+// The kernel amdgo_gemm_bf16 runs for this shape on the device of stream `s` (0 = generic).
+static int resolve_variant(int M, int N, int K, hipStream_t s) {
   if (M % BM || N % BN || K % BK || K < 2 * BK) return 0;
   const int nwg = (M / BM) * (N / BN);
-  const int cus = device_cu_count();
+  const int cus = device_cu_count(s);
   const bool sq = (M / BM) % 16 == 0 && (N / BN) % 16 == 0;
   int v = g_variant;
   const bool pow2k = (K & (K - 1)) == 0;
-  if (v == 0 && cus == 256 && !pow2k && K % (2 * BK) == 0 && K >= 4 * BK && persistent_grid(nwg) >= NXCD) {
+  if (v == 0 && cus == 256 && !pow2k && K % (2 * BK) == 0 && K >= 4 * BK && persistent_grid(nwg, s) >= NXCD) {
     // K not a power of two: the asm pipeline in the VP DMA form (per-piece VGPR lane offsets, the K
     // offset in one SGPR): 12288^3 1.02x hipBLASLt (v48 0.98x, the DM-0 asm form 0.88x),
     // 8192^2x12288 1.07x (v47 1.02x), 12288^2x10240 1.03x (v48 1.03x); profiles/r3_s2/vp_bf16.jsonl.
     // v54 = the same on the square cross-XCD raster for >= 8 dispatch waves on 16x16-tile multiples:
     // 12288^3 1.05x (v53 1.03x), 12288^2x10240 1.07x (v53 1.04x); profiles/r3_s2/vpsq_bf16.jsonl
     v = (sq && nwg >= 8 * cus) ? 54 : 53;
-  } else if (v == 0 && cus == 256 && pow2k && K >= 4 * BK && persistent_grid(nwg) >= NXCD) {
+  } else if (v == 0 && cus == 256 && pow2k && K >= 4 * BK && persistent_grid(nwg, s) >= NXCD) {
     // The hand-scheduled asm K pipeline, persistent (profiles/r3_asm/): v50 everywhere it runs,
     // ahead of v44 and v25 on every measured shape (8192^3 +2-3 %, 8192^2x2048 +7 %,
     // 16384^2x1024 +14 % over v44); its square-raster form v51 for >= 8 dispatch waves with long K
@@ -101,11 +101,11 @@ static int resolve_variant(int M, int N, int K) {
   if (v == 45 && !sq) v = 44;                           // square raster needs 16x16 super-tiles
   if (v == 48 && !sq) v = 47;
   if ((v == 47 || v == 48) && cus != 256) v = 42;
-  if (v == 25 && persistent_grid(nwg) < NXCD) v = 44;
+  if (v == 25 && persistent_grid(nwg, s) < NXCD) v = 44;
   // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups; its square raster
   // (v51) needs exactly 256 workgroups over 16x16 super-tiles
   if ((v == 50 || v == 51 || v == 52 || v == 53 || v == 54) &&
-      (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg) < NXCD))
+      (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg, s) < NXCD))
     v = 44;
   if (v == 54 && (!sq || cus != 256)) v = 53;
   if (v == 51 && (!sq || cus != 256)) v = 50;
@@ -132,7 +132,7 @@ int amdgo_gemm_set_variant(int v) {
   return 0;
 }
 int amdgo_gemm_get_variant() { return g_variant; }
-int amdgo_gemm_resolve_variant(int M, int N, int K) { return resolve_variant(M, N, K); }
+int amdgo_gemm_resolve_variant(int M, int N, int K) { return resolve_variant(M, N, K, nullptr); }
 
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
@@ -142,13 +142,13 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   const auto* b = (const __bf16*)Bt;
   auto* c = (__bf16*)C;
   const int nwg = (M / BM) * (N / BN);
-  switch (resolve_variant(M, N, K)) {
+  switch (resolve_variant(M, N, K, s)) {
     case 18:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 25:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, false, true>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, false, true>), dim3(persistent_grid(nwg, s)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 42:
@@ -172,7 +172,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          0, s, a, b, c, M, N, K);
       break;
     case 50:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg, s)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 51:
@@ -180,7 +180,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          a, b, c, M, N, K);
       break;
     case 53:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 1>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 1>), dim3(persistent_grid(nwg, s)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 54:
@@ -188,7 +188,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          0, s, a, b, c, M, N, K);
       break;
     case 52:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg, s)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {

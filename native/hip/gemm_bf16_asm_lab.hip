@@ -33,6 +33,8 @@
 //   260 / 261 / 262 / 263 = q16ap VP form: p linear (= v20 in VP form), p + PA, p + PA square raster, s1d3 + PA serp
 //   232 = 200 with nontemporal C stores; 244 = 240 with nontemporal stores
 //   230 / 231 = knock-outs: 200 without its epilogue / without the epilogue's global stores
+#include "gemm_bf16_asm_loop_lab.h"  // every schedule (masks the production header)
+#include "gemm_fp8_asm_loop_lab.h"  // every schedule (masks the production header)
 #include "gemm_bf16_kernels.h"
 #include "gemm_fp8_kernels.h"
 

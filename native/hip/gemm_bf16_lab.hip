@@ -16,6 +16,7 @@
 // profiles/r1_s2_gemm/, profiles/r1_s6_sq/.
 #include <stdlib.h>
 
+#include "gemm_bf16_asm_loop_lab.h"  // every schedule (masks the production header)
 #include "gemm_bf16_kernels.h"
 
 namespace {

@@ -34,10 +34,11 @@ static int g_fp8_variant = 0;
 // landing wait at 34, B0' reads from slot 35, A0' reads from 43 (block 2 walks A0 slowly).
 #define Q16(SERP, SQ) (gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, SERP, SQ, 2, 2, true>)
 
-static int resolve_fp8_variant(int M, int N, int K) {
+// The kernel amdgo_gemm_fp8 runs for this shape on the device of stream `s` (0 = generic).
+static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
   if (M % F8_BM || N % F8_BN || K % F8_BK || K < 2 * F8_BK) return 0;
   const int nwg = (M / F8_BM) * (N / F8_BN);
-  const int cus = device_cu_count();
+  const int cus = device_cu_count(s);
   const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;     // persistent grid: one WG per CU
   const bool sq = (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0;
   int v = g_fp8_variant;
@@ -71,7 +72,7 @@ int amdgo_gemm_fp8_set_variant(int v) {
   return 0;
 }
 int amdgo_gemm_fp8_get_variant() { return g_fp8_variant; }
-int amdgo_gemm_fp8_resolve_variant(int M, int N, int K) { return resolve_fp8_variant(M, N, K); }
+int amdgo_gemm_fp8_resolve_variant(int M, int N, int K) { return resolve_fp8_variant(M, N, K, nullptr); }
 
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
@@ -81,9 +82,9 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
   const auto* b = (const uint8_t*)Bt;
   auto* c = (__bf16*)C;
   const int nwg = (M / F8_BM) * (N / F8_BN);
-  const int cus = device_cu_count();
+  const int cus = device_cu_count(s);
   const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;
-  switch (resolve_fp8_variant(M, N, K)) {
+  switch (resolve_fp8_variant(M, N, K, s)) {
     case 10:
       hipLaunchKernelGGL((gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>), dim3(pgrid), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);

@@ -4,6 +4,7 @@
 //   rotated at slot B1, 9 = 4 with both, 10 / 11 = persistent with the schedules of 4 / 3,
 //   12 = 10 with serpentine K, 13 = 9 with the square cross-XCD raster; 20-37 = q16 placements;
 //   40 / 41 = persistent q16 (41: serpentine K).
+#include "gemm_fp8_asm_loop_lab.h"  // every schedule (masks the production header)
 #include "gemm_fp8_kernels.h"
 
 extern "C" {

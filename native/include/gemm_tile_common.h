@@ -85,18 +85,27 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Host: compute units of the current device (cached per device; 256 on MI355X). The serpentine-K
-// variants assume NXCD x 32 co-resident workgroups (one per CU) and are only picked at 256.
-inline int device_cu_count() {
+// Host: compute units of the device a launch on `stream` runs on (cached per device; 256 on MI355X,
+// 32 on a CPX partition). The stream's device, not the calling thread's current one: a process that
+// drives several devices (or an SPX GPU next to CPX partitions) launches on streams of devices other
+// than the current one, and a grid sized for the wrong device over- or under-fills by up to 8x. A null
+// stream is the current device's. The serpentine-K variants assume NXCD x 32 co-resident workgroups
+// (one per CU) and are only picked at 256.
+inline int device_cu_count(hipStream_t stream = nullptr) {
   static int cus[64] = {0};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
+  if (stream != nullptr) {
+    if (hipStreamGetDevice(stream, &dev) != hipSuccess) return 0;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    return 0;
   }
-  return cus[dev];
+  if (dev < 0 || dev >= 64) return 0;
+  int n = __atomic_load_n(&cus[dev], __ATOMIC_RELAXED);
+  if (n == 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    __atomic_store_n(&cus[dev], n, __ATOMIC_RELAXED);
+  }
+  return n;
 }
 
 template <int B, int E, typename F>

@@ -298,3 +298,32 @@ def test_fp8_q16_kernel_audit(asm_fp8_lab):
     kernels = _kernels(asm_fp8_lab, "gemm_fp8_256x256_q16I")
     assert len(kernels) == 18
     _audit_q16(kernels)
+
+
+@pytest.mark.parametrize("gen,headers", [
+    ("gen_bf16_asm_loop.py", ["gemm_bf16_asm_loop.h", "gemm_bf16_asm_loop_lab.h"]),
+    ("gen_fp8_asm_loop.py", ["gemm_fp8_asm_loop.h", "gemm_fp8_asm_loop_lab.h"]),
+])
+def test_generated_asm_headers_match_generator(tmp_path, gen, headers):
+    """The checked-in K-pipeline headers are exactly what their generator emits today: a generator
+    edit committed without regenerating (or a hand-edited header) fails here."""
+    subprocess.run(["python3", os.path.join(ROOT, "tools", gen), "--out-dir", str(tmp_path)], check=True,
+                   capture_output=True, timeout=300)
+    for h in headers:
+        want = (tmp_path / h).read_bytes()
+        have = open(os.path.join(ROOT, "native", "hip", h), "rb").read()
+        assert have == want, f"native/hip/{h} differs from tools/{gen} output: regenerate it"
+
+
+def test_production_asm_headers_carry_only_shipped_schedules():
+    """Production builds (libamdgo_hip.so, amd-gemm-validate) read the small headers; only the lab
+    sources include the *_lab.h headers (which carry every schedule)."""
+    hip = os.path.join(ROOT, "native", "hip")
+    prod = [open(os.path.join(hip, h)).read() for h in ("gemm_bf16_asm_loop.h", "gemm_fp8_asm_loop.h")]
+    assert sum(p.count("\n") for p in prod) < 10000
+    asm_defs = sorted(re.findall(r"^#define (\w+_ASM_\w+) \\", "\n".join(prod), re.M))
+    assert asm_defs == ["F8AP_ASM_P_ZC", "W4AP_ASM_G4_ZC", "W4AP_ASM_G6D6_ZC", "W4VP_ASM_G4_ZC"]
+    for f in os.listdir(hip):
+        text = open(os.path.join(hip, f), errors="replace").read()
+        if "_asm_loop_lab.h\"" in text and not f.endswith("_lab.h"):
+            assert f.endswith("_lab.hip"), f"{f} includes a lab header"

@@ -27,7 +27,13 @@ Waits are explicit and counted:
 The MFMA order, operands and accumulators are those of w4s, so results are bitwise identical to
 it (tests/test_gemm_gpu.py checks that).
 
-    python tools/gen_bf16_asm_loop.py          # rewrites native/hip/gemm_bf16_asm_loop.h
+    python tools/gen_bf16_asm_loop.py               # rewrites both headers in native/hip/
+    python tools/gen_bf16_asm_loop.py --out-dir D   # writes them to D (tests/test_gemm_build.py drift check)
+
+Two headers: ``gemm_bf16_asm_loop.h`` carries only the shipped schedules (SHIPPED below, the ones
+gemm_bf16.hip dispatches), ``gemm_bf16_asm_loop_lab.h`` every schedule, for the tools-only lab
+libraries (which include it before gemm_bf16_kernels.h; it then masks the production header). A
+schedule keeps its SC index in both, so production kernel names do not change.
 """
 from __future__ import annotations
 
@@ -37,6 +43,8 @@ from typing import Dict, List
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "native", "hip", "gemm_bf16_asm_loop.h")
+LAB_OUT = os.path.join(ROOT, "native", "hip", "gemm_bf16_asm_loop_lab.h")
+LAB_GUARD = "AMDGO_BF16_ASM_LOOP_LAB"
 
 SLOTS = 128
 PIECE_STRIDE = 0x1000
@@ -732,9 +740,10 @@ def audit(lines: List[str]) -> Dict[str, int]:
 
 def render() -> str:
     parts = ["// GENERATED by tools/gen_bf16_asm_loop.py -- do not edit by hand.",
-             "// The hand-scheduled K pipeline of gemm_bf16_256x256_w4a (gemm_bf16_kernels.h): one asm",
-             "// string per schedule; operands are named in gemm_bf16_kernels.h (W4A_LOOP).",
-             "#pragma once", ""]
+             "// LAB header: every schedule of the hand-scheduled K pipeline of gemm_bf16_256x256_w4a / w4ap",
+             "// (gemm_bf16_kernels.h, gemm_w4ap.h), one asm string per schedule. Only the tools-only lab",
+             "// libraries include it (before gemm_bf16_kernels.h); production builds gemm_bf16_asm_loop.h.",
+             "#pragma once", f"#define {LAB_GUARD} 1", ""]
     sel = []
     for idx, (name, sc) in enumerate(SCHEDULES.items()):
         sel.append(f"if constexpr (SC == {idx}) W4A_LOOP(W4A_ASM_{name.upper()});")
@@ -793,15 +802,14 @@ def render() -> str:
         parts.append(f"#define W4VP_SC_{n.upper()} {i}")
     parts.append("")
     for name in VP:
-        lines = to_vp(kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
+        lines = vp_lines(name)
         parts.append(f"#define W4VP_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
         parts.append('  ""')
         parts.append("")
     for name in PERSISTENT:
-        lines = (kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else
-                 kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
+        lines = ap_lines(name)
         parts.append(f"#define W4AP_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
@@ -820,7 +828,64 @@ def render() -> str:
     return "\n".join(parts)
 
 
+# The schedules gemm_bf16.hip dispatches: v50 / v51 W4AP g4_zc, v52 W4AP g6d6_zc, v53 / v54 W4VP g4_zc.
+SHIPPED = {"W4AP": ["g4_zc", "g6d6_zc"], "W4VP": ["g4_zc"]}
+
+
+def ap_lines(name: str) -> List[str]:
+    return (kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else
+            kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
+
+
+def vp_lines(name: str) -> List[str]:
+    return to_vp(kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
+
+
+def _asm_define(macro: str, lines: List[str]) -> List[str]:
+    return [f"#define {macro} \\"] + [f'  "{ln}\\n\\t" \\' for ln in lines] + ['  ""', ""]
+
+
+def render_production() -> str:
+    """The shipped schedules only, at their lab SC indices; every other family or index is a
+    compile-time error naming the lab header."""
+    lab_only = 'static_assert(SC < 0, "lab-only schedule: include gemm_bf16_asm_loop_lab.h first");'
+    parts = ["// GENERATED by tools/gen_bf16_asm_loop.py -- do not edit by hand.",
+             "// PRODUCTION header: the K-pipeline schedules gemm_bf16.hip dispatches (SHIPPED in the generator),",
+             "// at the SC indices they have in the lab header gemm_bf16_asm_loop_lab.h, which carries every",
+             "// schedule and, when included first, masks this one.",
+             "#pragma once", f"#ifndef {LAB_GUARD}", ""]
+    for fam in ("W4A", "W4EF", "W4DS"):
+        parts.append(f"#define {fam}_LOOP_SELECT(SC) {lab_only}")
+    parts.append("")
+    for fam, names in (("W4AP", PERSISTENT), ("W4VP", VP)):
+        sel = [f"if constexpr (SC == {names.index(n)}) {fam}_LOOP({fam}_ASM_{n.upper()});" for n in SHIPPED[fam]]
+        parts.append(f"#define {fam}_LOOP_SELECT(SC) \\")
+        parts.append("  " + " else \\\n  ".join(sel + [lab_only]))
+        for n in SHIPPED[fam]:
+            parts.append(f"#define {fam}_SC_{n.upper()} {names.index(n)}")
+        parts.append("")
+    for n in SHIPPED["W4AP"]:
+        parts += _asm_define(f"W4AP_ASM_{n.upper()}", ap_lines(n))
+    for n in SHIPPED["W4VP"]:
+        parts += _asm_define(f"W4VP_ASM_{n.upper()}", vp_lines(n))
+    parts.append(f"#endif  // {LAB_GUARD}")
+    return "\n".join(parts) + "\n"
+
+
+def write_all(out_dir: str = "") -> List[str]:
+    outs = []
+    for path, text in ((OUT, render_production()), (LAB_OUT, render())):
+        if out_dir:
+            path = os.path.join(out_dir, os.path.basename(path))
+        with open(path, "w") as f:
+            f.write(text)
+        outs.append(path)
+    return outs
+
+
 if __name__ == "__main__":
-    with open(OUT, "w") as f:
-        f.write(render())
-    print(f"wrote {OUT}")
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out-dir", default="", help="write the headers here instead of native/hip/")
+    for p in write_all(ap.parse_args().out_dir):
+        print(f"wrote {p}")

@@ -24,7 +24,11 @@ of tile t+2 then overwrites), the DMA pieces, and the landing wait (vmcnt(pieces
 + s_barrier: tile t+1 is in LDS). The persistent frame (operands, drain into the next output
 tile, flags) is the bf16 one: gemm_w4ap.h runs both.
 
-    python tools/gen_fp8_asm_loop.py          # rewrites native/hip/gemm_fp8_asm_loop.h
+    python tools/gen_fp8_asm_loop.py               # rewrites both headers in native/hip/
+    python tools/gen_fp8_asm_loop.py --out-dir D   # writes them to D (tests/test_gemm_build.py drift check)
+
+Two headers, as for bf16 (tools/gen_bf16_asm_loop.py): ``gemm_fp8_asm_loop.h`` with the shipped
+schedules only (SHIPPED below), ``gemm_fp8_asm_loop_lab.h`` with every schedule for the lab libraries.
 """
 from __future__ import annotations
 
@@ -34,6 +38,8 @@ from typing import Dict, List
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "native", "hip", "gemm_fp8_asm_loop.h")
+LAB_OUT = os.path.join(ROOT, "native", "hip", "gemm_fp8_asm_loop_lab.h")
+LAB_GUARD = "AMDGO_FP8_ASM_LOOP_LAB"
 
 SLOTS = 64
 PIECE_STRIDE = 0x1000
@@ -564,9 +570,10 @@ def audit(lines: List[str]) -> Dict[str, int]:
 
 def render() -> str:
     parts = ["// GENERATED by tools/gen_fp8_asm_loop.py -- do not edit by hand.",
-             "// The hand-scheduled K pipeline of the persistent fp8 GEMM (gemm_fp8_256x256_q16ap,",
-             "// gemm_fp8_kernels.h; frame and operands in gemm_w4ap.h, W4AP_LOOP).",
-             "#pragma once", ""]
+             "// LAB header: every schedule of the hand-scheduled K pipeline of the persistent fp8 GEMM",
+             "// (gemm_fp8_256x256_q16ap, gemm_fp8_kernels.h; frame and operands in gemm_w4ap.h, W4AP_LOOP).",
+             "// Only the tools-only lab libraries include it; production builds gemm_fp8_asm_loop.h.",
+             "#pragma once", f"#define {LAB_GUARD} 1", ""]
     sel = [f"if constexpr (SC == {i}) W4AP_LOOP(F8AP_ASM_{n.upper()});" for i, n in enumerate(PERSISTENT)]
     parts.append("#define F8AP_LOOP_SELECT(SC) \\")
     parts.append("  " + " else \\\n  ".join(sel))
@@ -620,8 +627,7 @@ def render() -> str:
         parts.append('  ""')
         parts.append("")
     for name in PERSISTENT:
-        lines = (kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else
-                 kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
+        lines = ap_lines(name)
         a = audit(lines)
         parts.append(f"// {name}: {a['mfmas']} MFMAs, <= {a['max_fillers_per_gap']} instructions per MFMA gap")
         parts.append(f"#define F8AP_ASM_{name.upper()} \\")
@@ -632,7 +638,53 @@ def render() -> str:
     return "\n".join(parts)
 
 
+# The schedule gemm_fp8.hip dispatches: v20 / v21 F8AP p_zc.
+SHIPPED = {"F8AP": ["p_zc"]}
+
+
+def ap_lines(name: str) -> List[str]:
+    return (kloop_persistent_rw(SCHEDULES[name[:-3]]) if name.endswith("_rw") else
+            kloop_persistent_zc(SCHEDULES[name[:-3]]) if name.endswith("_zc") else kloop_persistent(SCHEDULES[name]))
+
+
+def render_production() -> str:
+    """The shipped schedule only, at its lab SC index; every other family or index is a
+    compile-time error naming the lab header."""
+    lab_only = 'static_assert(SC < 0, "lab-only schedule: include gemm_fp8_asm_loop_lab.h first");'
+    parts = ["// GENERATED by tools/gen_fp8_asm_loop.py -- do not edit by hand.",
+             "// PRODUCTION header: the K-pipeline schedule gemm_fp8.hip dispatches (SHIPPED in the generator),",
+             "// at the SC index it has in the lab header gemm_fp8_asm_loop_lab.h, which carries every",
+             "// schedule and, when included first, masks this one.",
+             "#pragma once", f"#ifndef {LAB_GUARD}", ""]
+    for fam in ("F8EF", "F8DS", "F8VP"):
+        parts.append(f"#define {fam}_LOOP_SELECT(SC) {lab_only}")
+    sel = [f"if constexpr (SC == {PERSISTENT.index(n)}) W4AP_LOOP(F8AP_ASM_{n.upper()});" for n in SHIPPED["F8AP"]]
+    parts.append("#define F8AP_LOOP_SELECT(SC) \\")
+    parts.append("  " + " else \\\n  ".join(sel + [lab_only]))
+    for n in SHIPPED["F8AP"]:
+        parts.append(f"#define F8AP_SC_{n.upper()} {PERSISTENT.index(n)}")
+    parts.append("")
+    for n in SHIPPED["F8AP"]:
+        parts.append(f"#define F8AP_ASM_{n.upper()} \\")
+        parts += [f'  "{ln}\\n\\t" \\' for ln in ap_lines(n)] + ['  ""', ""]
+    parts.append(f"#endif  // {LAB_GUARD}")
+    return "\n".join(parts) + "\n"
+
+
+def write_all(out_dir: str = "") -> List[str]:
+    outs = []
+    for path, text in ((OUT, render_production()), (LAB_OUT, render())):
+        if out_dir:
+            path = os.path.join(out_dir, os.path.basename(path))
+        with open(path, "w") as f:
+            f.write(text)
+        outs.append(path)
+    return outs
+
+
 if __name__ == "__main__":
-    with open(OUT, "w") as f:
-        f.write(render())
-    print("wrote", OUT)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out-dir", default="", help="write the headers here instead of native/hip/")
+    for p in write_all(ap.parse_args().out_dir):
+        print("wrote", p)

@@ -3,6 +3,12 @@
 set -e
 OUT=gpurun_out/${1:-round}
 mkdir -p $OUT
+# read-only evidence for the partition round trip (tests/test_node_agents_gpu.py): who we are, whether
+# root is available without a password, and whether the compute-partition attributes are writable
+{ id; sudo -n true 2>&1 && echo "sudo: ok" || echo "sudo: not available"
+  for f in /sys/bus/pci/devices/*/current_compute_partition /sys/bus/pci/devices/*/current_memory_partition; do
+    [ -e "$f" ] || continue; ls -l "$f"; echo "  value=$(cat "$f") writable=$([ -w "$f" ] && echo yes || echo no)"; done
+} > $OUT/partition_permissions.log 2>&1 || true
 echo "pytest -m gpu"; timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 tail -3 $OUT/pytest_gpu.log
 echo "smoke"; timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
