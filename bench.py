@@ -177,6 +177,11 @@ def main(argv=None) -> int:
                   step_ms_median=res["median_ms"], step_ms_p90=res["p90_ms"])
     if res["median_ms"]:
         extras["per_gpu_tflops_at_median"] = _r(G.tflops(m, n, k, res["median_ms"] / 1e3))
+    # the headline takes the slowest rank's clock (MAX over ranks); each rank's own loop shows
+    # whether one GPU is slow
+    rank_tf = [G.tflops(m, n, k, t / args.steps) for t in res["per_rank_s"]]
+    extras.update(per_rank_tflops_min=_r(min(rank_tf)), per_rank_tflops_max=_r(max(rank_tf)),
+                  slowest_rank=int(min(range(len(rank_tf)), key=lambda i: rank_tf[i])))
 
     if not args.no_extras:
         if not cpu:
@@ -253,6 +258,16 @@ class Ctx:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, x: float):
+        """Every rank's value, in rank order (one all-gather of a float64 scalar)."""
+        if not self.distributed:
+            return [x]
+        torch = self.torch
+        mine = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        out = [torch.zeros_like(mine) for _ in range(self.world)]
+        self.dist.all_gather(out, mine)
+        return [float(t.item()) for t in out]
+
     def stabilise(self, step, min_dispatches=50, window=10, tol=0.02, batch=10):
         """Issue back-to-back dispatches in batches of ``batch`` (event between each) until the
         last ``window`` per-dispatch times spread by < ``tol`` of their median, with at least
@@ -295,12 +310,14 @@ class Ctx:
             if evs:
                 evs[i + 1].record()
         self.sync()
+        own = time.perf_counter() - t0          # this rank's own loop, before it waits for the others
         self.barrier()
         self.sync()
         elapsed = self.max_over_ranks(time.perf_counter() - t0)
+        per_rank = self.gather(own)
         per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else []
         med, p90 = _pct(per, 0.5), _pct(per, 0.9)
-        return {"elapsed_s": elapsed, "stabilise_dispatches": n_stab, "stabilise_spread": spread,
+        return {"elapsed_s": elapsed, "per_rank_s": per_rank, "stabilise_dispatches": n_stab, "stabilise_spread": spread,
                 "median_ms": round(med, 4) if med is not None else None,
                 "p90_ms": round(p90, 4) if p90 is not None else None}
 

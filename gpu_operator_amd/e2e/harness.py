@@ -171,7 +171,9 @@ class E2E:
             spec.setdefault("driver", {})["enabled"] = False      # the host's preinstalled amdgpu
         v = spec.setdefault("validator", {})
         env = [{"name": "HIP_VALIDATION_MODE", "value": self.hip_mode}]
-        v.setdefault("hip", {})["env"] = list(env)
+        # on CPU the GEMM pod is planned (free / tenant-held GPUs), scheduled and run, without GEMMs
+        v.setdefault("hip", {})["env"] = list(env) + (
+            [{"name": "GEMM_VALIDATION_MODE", "value": "dry-run"}] if self.hip_mode == "skip" else [])
         # on CPU the fabric pod is still planned, scheduled and run (topology check on the fake
         # sysfs), without the collective
         v.setdefault("rccl", {})["env"] = list(env) + (
@@ -672,23 +674,36 @@ class E2E:
                 "privileged": bool((c0.get("securityContext") or {}).get("privileged")),
                 "env": {k: env[k] for k in ("RCCL_RANKS", "AMD_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES") if k in env}}
 
+    def _validation_pod_env(self, app: str) -> Dict[str, str]:
+        pods = [p for p in self.backing.list("v1", "Pod", NS) if o.get_labels(p).get("app") == app]
+        if not pods:
+            return {}
+        c0 = pods[-1]["spec"]["initContainers"][0]
+        return {e["name"]: e.get("value") for e in c0.get("env") or []}
+
     def restart_validator(self) -> Dict:
         """Delete the validator pod (a restart, as after an upgrade or a node reboot) and wait for
         the DaemonSet's replacement to re-run the chain and write a fresh rccl-ready."""
         before = (self._barrier("rccl-ready") or {}).get("ts", 0.0)
+        t = time.monotonic()
         for p in self.operand_pods():
             if o.name(p).startswith("amd-operator-validator"):
                 self.backing.delete("v1", "Pod", o.name(p), NS)
         self._wait("a fresh rccl-ready from the restarted validator",
                    lambda: (self._barrier("rccl-ready") or {}).get("ts", 0.0) > before)
         self._wait("the validator Ready again", self.all_ready)
-        return {"rccl-ready": self._barrier("rccl-ready"), "rccl_pod": self._rccl_pod_shape()}
+        env = self._validation_pod_env("amd-hip-validator")
+        return {"rccl-ready": self._barrier("rccl-ready"), "rccl_pod": self._rccl_pod_shape(),
+                "hip-ready": self._barrier("hip-ready"), "ready_s": round(time.monotonic() - t, 3),
+                "hip_pod_env": {k: env[k] for k in ("GEMM_DEVICES", "GEMM_PROBE_DEVICES", "GEMM_DRY_RUN") if k in env}}
 
-    def _gpu_job(self, name: str) -> None:
+    def _gpu_job(self, name: str, gpus: int = 1) -> None:
         pod = self.workload_pod()
         pod["metadata"]["name"] = name
+        pod["metadata"]["labels"] = {"app": name}
         pod["spec"]["restartPolicy"] = "Never"
         pod["spec"]["containers"][0]["command"] = ["sleep", "600"]
+        pod["spec"]["containers"][0]["resources"] = {"limits": {GPU: gpus}}
         if not any(o.name(n) == "default" for n in self.backing.list("v1", "Namespace")):
             self.backing.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "default"}})
         self.backing.create(pod)
@@ -721,6 +736,78 @@ class E2E:
             self._gpu_job("gpu-busy")
             out["busy"] = self.step("validator-restart[busy]", self.restart_validator)
             self.backing.delete("v1", "Pod", "gpu-busy", "default")
+        except Exception as e:  # noqa: BLE001 - reported in the result
+            self.result["error"] = f"{type(e).__name__}: {e}"
+            self.result["logs_dir"] = self.base
+            self.keep = True
+        finally:
+            self.teardown()
+        self.result.update(out)
+        self.result.update(ok=all(s.get("ok") for s in self.steps) and "error" not in self.result, steps=self.steps)
+        return self.result
+
+    def _tenant_race(self) -> Dict:
+        """A tenant scheduled between the validator's busy check and its fabric pod: the kubelet
+        holds the fabric pod's admission until a 1-GPU tenant runs, then admits it -- the
+        validator must fall back to topology-only in seconds, not wait out the pod timeout."""
+        released = threading.Event()
+        seen = threading.Event()
+        errs: List[str] = []
+        old = {p["metadata"]["uid"] for p in self.backing.list("v1", "Pod", NS)
+               if o.get_labels(p).get("app") == "amd-rccl-validator"}
+
+        def hold(p):
+            return o.get_labels(p).get("app") == "amd-rccl-validator" and not released.is_set()
+
+        def start_tenant():
+            try:
+                self._gpu_job("tenant-race", gpus=1)
+            except Exception as e:  # noqa: BLE001 - reported in the step's result
+                errs.append(f"{type(e).__name__}: {e}")
+            finally:
+                released.set()
+
+        def on_event(ev):
+            if ev.type == "ADDED" and o.get_labels(ev.obj).get("app") == "amd-rccl-validator" and \
+                    ev.obj["metadata"]["uid"] not in old and not seen.is_set():
+                seen.set()
+                threading.Thread(target=start_tenant, daemon=True).start()
+        self.kubelet.hold_admission = hold
+        stop = self.backing.watch("v1", "Pod", on_event, namespace=NS)
+        try:
+            out = self.restart_validator()
+        finally:
+            stop()
+            self.kubelet.hold_admission = None
+            released.set()
+        out["tenant_started_after_busy_check"] = seen.is_set()
+        if errs:
+            raise StepFailed(f"the racing tenant did not start: {errs}")
+        return out
+
+    def run_tenant_cases(self) -> Dict[str, Any]:
+        """The validator beside tenants, on real processes: (i) a pod holds 2 GPUs
+        -- the HIP pod's full sweep gets the 6 free GPUs, the 2 held ones a probe; (ii) pods hold all
+        8 -- the probe only; (iii) a tenant lands between the fabric busy check and the fabric pod --
+        topology-only. The validator reaches Ready in each."""
+        self.setup()
+        out: Dict[str, Any] = {}
+        try:
+            self.step("install-operator", self.install_operator)
+            self.step("verify-operator", lambda: self.verify_operator("install"))
+            env = self._validation_pod_env("amd-hip-validator")
+            out["idle"] = {"hip-ready": self._barrier("hip-ready"), "rccl-ready": self._barrier("rccl-ready"),
+                           "hip_pod_env": {k: env[k] for k in ("GEMM_DEVICES", "GEMM_PROBE_DEVICES") if k in env}}
+            self._gpu_job("tenant-a", gpus=2)
+            out["two-held"] = self.step("validator-restart[2 GPUs held]", self.restart_validator)
+            self._gpu_job("tenant-b", gpus=6)
+            out["all-held"] = self.step("validator-restart[8 GPUs held]", self.restart_validator)
+            for name in ("tenant-a", "tenant-b"):
+                self.backing.delete("v1", "Pod", name, "default")
+            self._wait("the tenants gone", lambda: not [p for p in self.backing.list("v1", "Pod", "default")
+                                                        if o.name(p).startswith("tenant-")])
+            out["race"] = self.step("validator-restart[tenant before the fabric pod]", self._tenant_race)
+            self.backing.delete("v1", "Pod", "tenant-race", "default")
         except Exception as e:  # noqa: BLE001 - reported in the result
             self.result["error"] = f"{type(e).__name__}: {e}"
             self.result["logs_dir"] = self.base
@@ -939,6 +1026,9 @@ def main(argv=None) -> int:
     ap.add_argument("--nodes", type=int, default=1, help="N > 1: that many nodes on fake sysfs (CPU rehearsal)")
     ap.add_argument("--driver-container", action="store_true",
                     help="the driver DaemonSet installs a simulated amdgpu on a fake sysfs (CPU rehearsal)")
+    ap.add_argument("--flow", choices=["reference", "fabric", "tenants"], default="reference",
+                    help="reference: end-to-end.sh; fabric: the fabric pod on node shapes; tenants: the "
+                         "validator beside GPU pods (fake sysfs, no GPU work)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
     if a.nodes > 1:
@@ -954,10 +1044,15 @@ def main(argv=None) -> int:
                 driver="container").run()
         print(json.dumps(r, default=str))
         return 0 if r["ok"] else 1
-    if a.fake_gpus:
+    if a.fake_gpus or a.flow != "reference":
         from ..devices import fakesys
         sys_root = dev_root = str(fakesys.make_node(os.path.join(tempfile.mkdtemp(prefix="amd-e2e-sys-"), "root"),
-                                                    n_gpus=a.fake_gpus))
+                                                    n_gpus=a.fake_gpus or 8))
+    if a.flow != "reference":
+        e = E2E(sys_root=sys_root, dev_root=dev_root, hip_mode="skip", timeout=a.timeout, keep=a.keep)
+        r = e.run_tenant_cases() if a.flow == "tenants" else e.run_fabric_shapes()
+        print(json.dumps(r, default=str))
+        return 0 if r["ok"] else 1
     r = E2E(sys_root=sys_root, dev_root=dev_root, hip_mode=a.hip_mode, timeout=a.timeout, keep=a.keep).run()
     print(json.dumps(r, default=str))
     return 0 if r["ok"] else 1

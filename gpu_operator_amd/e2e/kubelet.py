@@ -45,7 +45,7 @@ import subprocess
 import threading
 import time
 from concurrent import futures
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Callable, Any, Dict, List, Optional, Tuple
 
 from ..k8s import errors
 from ..k8s import objects as o
@@ -179,6 +179,7 @@ class PodRun:
         self.stop_evt = threading.Event()
         self.ready = False
         self.phase = "Pending"
+        self.reason = self.message = ""          # status.reason / message (admission failures)
         self.started_at: Dict[str, float] = {}
         self.thread = threading.Thread(target=self._main, name=f"pod-{self.name}", daemon=True)
 
@@ -207,6 +208,8 @@ class PodRun:
                                  {"type": "PodScheduled", "status": "True"}],
                   "initContainerStatuses": [self._ctr_status(c, True) for c in spec.get("initContainers") or []],
                   "containerStatuses": [self._ctr_status(c, False) for c in spec.get("containers") or []]}
+        if self.reason:
+            status.update(reason=self.reason, message=self.message)
         self.kl.set_status(self.ns, self.name, self.uid, status)
 
     # -- container plumbing ------------------------------------------------------------------
@@ -384,6 +387,10 @@ class PodRun:
             log.exception("pod %s/%s: %s", self.ns, self.name, e)
             self.kl.event(f"{self.name}:error", error=str(e))
             self.phase = "Failed"
+            if str(e).startswith("UnexpectedAdmissionError"):
+                # a nodeName-bound pod whose device request the node cannot serve: the kubelet
+                # rejects it at admission (it is never Pending)
+                self.reason, self.message = "UnexpectedAdmissionError", str(e)
             self.publish()
 
     def _lifecycle(self) -> None:
@@ -545,6 +552,8 @@ class ProcessKubelet:
         # an image's ENV (images are not pulled: the harness says what a tag's config carries)
         self.image_env = image_env or (lambda image: {})
         self.pods: Dict[str, PodRun] = {}
+        # harness hook: pods (not yet running here) for which this returns True are not admitted yet
+        self.hold_admission: Optional[Callable[[Dict], bool]] = None
         self._terminating: set = set()                 # deleted pods whose processes are being killed
         self._lock = threading.Lock()
         self._stop = threading.Event()
@@ -614,7 +623,10 @@ class ProcessKubelet:
         node = self.client.get("v1", "Node", self.node)
         pods = self.client.list("v1", "Pod")
         live = {}
+        hold = self.hold_admission
         for p in pods:
+            if hold is not None and p["metadata"]["uid"] not in self.pods and hold(p):
+                continue                     # the harness orders admissions (race rehearsals)
             spec = p.get("spec") or {}
             if not spec.get("nodeName"):
                 if (p.get("status") or {}).get("phase", "Pending") == "Pending" and self._schedulable(p, node):

@@ -182,9 +182,11 @@ def validate_toolkit(ctx: Context) -> Dict[str, Any]:
 # ---------------------------------------------------------------------------------------------
 # node shape: GPU model, physical GPUs, GPU pods holding devices
 # ---------------------------------------------------------------------------------------------
-GEMM_FLOOR_FRACTION = 0.40     # of the model's dense peak: healthy MI355X runs 0.59-0.65 on random data
+GEMM_FLOOR_FRACTION = 0.50     # of the model's dense peak: healthy MI355X runs 0.63-0.68 on random data
+GEMM_MIN_RELATIVE = 0.85       # of the node median, same dtype and shape: boxes differ ~6 %, GPUs of one box ~2 %
+GEMM_MIN_EFFICIENCY = 0.90     # of N x the 1-GPU figure: independent GEMMs on separate GPUs scale at ~1.0
 BUSBW_FLOOR_FRACTION = 0.25    # of one xGMI link: a healthy 8-GPU mesh runs well above one link
-FABRIC_ANNOTATION = "amd.com/gpu.fabric-validation"
+FABRIC_ANNOTATION = "amd.com/gpu.fabric-validation"   # read for records of older validators only
 
 
 def _validator_env(ctx: Context) -> Dict[str, str]:
@@ -263,6 +265,79 @@ def gpu_pods_on_node(ctx: Context) -> List[str]:
     return sorted(out)
 
 
+def _pod_device_ids(ctx: Context) -> Optional[Dict[str, List[str]]]:
+    """"namespace/name" -> AMD device ids the kubelet allocated to the pod (pod-resources List, the
+    API the metrics exporter attributes GPUs with). None when the socket cannot be queried."""
+    from ..operands import kubeletapi as K
+    sock = ctx.env.get("POD_RESOURCES_SOCKET") or mounts.path(K.POD_RESOURCES_SOCKET)
+    if not os.path.exists(sock):
+        return None
+    try:
+        import grpc
+        with grpc.insecure_channel("unix://" + sock) as ch:
+            resp = K.pod_resources_stub(ch)(K.PR["ListPodResourcesRequest"](), timeout=5.0)
+    except Exception as e:  # noqa: BLE001 - unknown attribution: the caller treats every GPU as held
+        log.info("pod-resources query failed: %s", e)
+        return None
+    out: Dict[str, List[str]] = {}
+    for pr in resp.pod_resources:
+        ids = [did for c in pr.containers for d in c.devices if d.resource_name.startswith("amd.com/")
+               for did in d.device_ids]
+        if ids:
+            out[f"{pr.namespace}/{pr.name}"] = ids
+    return out
+
+
+def _agent_of(device_id: str, gpus: List[Dict[str, Any]]) -> Optional[Dict[str, Any]]:
+    """The KFD agent a device-plugin id names: ``amdgpu-<unique id hex>`` (uuid strategy) or the
+    agent index (index strategy); a time-slicing replica ``<id>::<k>`` is its GPU."""
+    base = device_id.split("::")[0]
+    for g in gpus:
+        if (g.get("unique_id") and base == f"amdgpu-{g['unique_id']:016x}") or base == str(g["index"]):
+            return g
+    return None
+
+
+def held_gpus(ctx: Context, busy: List[str], gpus: Optional[List[Dict[str, Any]]] = None) -> Dict[str, Any]:
+    """Which physical GPUs (PCI functions) the running GPU pods ``busy`` hold. A GPU counts as held
+    when any of its agents (CPX partitions share its HBM and power) is allocated to one of them.
+    Without a device mapping for every busy pod (no pod-resources socket, an unknown id) every GPU
+    is held: the validator never guesses a tenant's GPU is free."""
+    gpus = gpus if gpus is not None else _gpus(ctx)
+    if not busy:
+        return {"held_bdfs": [], "attribution": "none", "by_pod": {}}
+    ids = _pod_device_ids(ctx)
+    by_pod: Dict[str, List[str]] = {}
+    unmapped = []
+    for pod in busy:
+        agents = [_agent_of(d, gpus) for d in (ids or {}).get(pod, [])]
+        if ids is None or not agents or any(a is None for a in agents):
+            unmapped.append(pod)
+            continue
+        by_pod[pod] = sorted({a["pci_bdf"] for a in agents})
+    if unmapped:
+        return {"held_bdfs": sorted({g["pci_bdf"] for g in gpus}), "attribution": "unattributed",
+                "unattributed_pods": unmapped[:16], "by_pod": by_pod}
+    return {"held_bdfs": sorted({b for v in by_pod.values() for b in v}), "attribution": "pod-resources",
+            "by_pod": by_pod}
+
+
+def hip_plan(ctx: Context, busy: List[str], gpus: Optional[List[Dict[str, Any]]] = None) -> Dict[str, Any]:
+    """The HIP validation plan for this node: the full stabilised GEMM sweep on the GPUs no pod
+    holds (``full``: HIP indices, None = every GPU), a correctness-only probe on the held ones
+    (``probe``). Reference: the plugin workload asks the scheduler for exactly 1 GPU
+    (validator/main.go:978-983) and the CUDA pod runs a microsecond vectorAdd
+    (validator/cuda-workload-validation.yaml:20) -- neither touches a GPU someone else was given."""
+    gpus = gpus if gpus is not None else _gpus(ctx)
+    held = held_gpus(ctx, busy, gpus)
+    if not busy:
+        return {"full": None, "probe": [], **held}
+    hb = set(held["held_bdfs"])
+    order = sorted(gpus, key=lambda g: g["index"])
+    return {"full": [g["index"] for g in order if g["pci_bdf"] not in hb],
+            "probe": [g["index"] for g in order if g["pci_bdf"] in hb], **held}
+
+
 def _env_float(ctx: Context, key: str) -> Optional[float]:
     v = ctx.env.get(key, "")
     if v == "":
@@ -312,9 +387,19 @@ def _dtype_key(name: str) -> str:
 
 def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
     agg = [r for r in results if r.get("event") == "aggregate"]
-    per = [r for r in results if r.get("event") == "gemm"]
+    per = [r for r in results if r.get("event") == "gemm" and not r.get("probe")]
+    probe = [r for r in results if r.get("event") == "gemm" and r.get("probe")]
     smoke = [r for r in results if r.get("event") == "hip-smoke"]
-    out: Dict[str, Any] = {"gemm": per, "aggregate": agg}
+    out: Dict[str, Any] = {"gemm": per, "aggregate": agg,
+                           "uniformity": [r for r in results if r.get("event") == "uniformity"]}
+    plan = next((r for r in results if r.get("event") == "plan"), None)
+    if plan is not None:
+        out["plan"] = plan
+    if probe:
+        # tenant-held GPUs: correctness only; a GPU whose HBM the tenant holds is skipped, not failed
+        out["probe"] = [{"device": r.get("device"), "ok": bool(r.get("ok")),
+                         **({"skipped": "busy: " + str(r.get("error", "out of memory"))} if r.get("oom") else {}),
+                         **({"error": r["error"]} if r.get("error") and not r.get("oom") else {})} for r in probe]
     if agg:
         # headline: bf16 before fp8, the largest shape, then the most GPUs
         head = max(agg, key=lambda r: (_dtype_key(r.get("dtype", "bf16")) == "bf16", r["m"] * r["n"] * r["k"],
@@ -340,52 +425,113 @@ def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
     return out
 
 
-def gate_gemm(info: Dict[str, Any], floors: Dict[str, float], busy: List[str]) -> List[str]:
-    """Why a GEMM result must not open hip-ready: failed checks, and (on a node no GPU pod is
-    sharing) any GPU below its dtype's floor. Also checked in the pod (``--min-tflops``); done
-    here again so an older workload image cannot pass a slow GPU."""
-    bad = [f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('error', 'check failed')}"
-           for r in info["gemm"] if not r.get("ok")]
-    bad += [f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: not ok" for r in info["aggregate"]
-            if r.get("ok") is False and not bad]
-    if info.get("smoke_ok") is False:
-        bad.append("hip-smoke failed")
-    if not busy:
-        for r in info["gemm"]:
-            floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0)
-            if r.get("ok") and floor and r.get("tflops", 0.0) < floor:
-                bad.append(f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('tflops')} TFLOP/s "
-                           f"below the {floor} floor")
-        for r in info["aggregate"]:          # the slowest GPU of each set (per-GPU lines may be cut)
-            floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0)
-            slow = r.get("min_gpu_tflops", r.get("per_gpu_tflops", 0.0))
-            if floor and slow < floor and not bad:
-                bad.append(f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: slowest GPU {slow} TFLOP/s "
-                           f"below the {floor} floor")
+def floor_applies(m: int, n: int, k: int) -> bool:
+    """The per-GPU floors are fractions of the dense peak: they apply to shapes that can reach it --
+    a full dispatch wave of 256x256 tiles and K >= 4096 (the same rule as amd-gemm-validate)."""
+    return (m or 0) * (n or 0) >= 256 * 256 * 256 and (k or 0) >= 4096
+
+
+def _relative_outliers(per: List[Dict[str, Any]], frac: float) -> List[str]:
+    """GPUs whose best TFLOP/s is below ``frac`` x the node's (upper) median at the same dtype and
+    shape: a 40 %-slow GPU passes any absolute floor loose enough for every box, not this."""
+    if not frac:
+        return []
+    best: Dict[tuple, Dict[Any, float]] = {}
+    for r in per:
+        if not r.get("ok") or not r.get("tflops"):
+            continue
+        key = (_dtype_key(r.get("dtype", "bf16")), r.get("m"), r.get("n"), r.get("k"))
+        d = best.setdefault(key, {})
+        d[r.get("device")] = max(d.get(r.get("device"), 0.0), float(r["tflops"]))
+    bad = []
+    for (dt, m, n, k), d in sorted(best.items(), key=lambda kv: str(kv[0])):
+        if len(d) < 2:
+            continue
+        med = sorted(d.values())[len(d) // 2]
+        for dev, t in sorted(d.items(), key=lambda kv: str(kv[0])):
+            if t < frac * med:
+                bad.append(f"gemm {dt} {m}x{n}x{k} device {dev}: {t:.1f} TFLOP/s is {t / med:.2f}x the node median "
+                           f"{med:.1f} (floor {frac:g}x)")
     return bad
 
 
-def _hip_env(ctx: Context, floors: Dict[str, float], busy: List[str]) -> Dict[str, str]:
+def gate_gemm(info: Dict[str, Any], floors: Dict[str, float], busy: List[str] = (),
+              min_relative: float = GEMM_MIN_RELATIVE, min_efficiency: float = GEMM_MIN_EFFICIENCY) -> List[str]:
+    """Why a GEMM result must not open hip-ready: failed checks, any GPU of the full run below its
+    dtype's floor, below ``min_relative`` x the node median, or a scaling step below
+    ``min_efficiency``; on probed (tenant-held) GPUs a failed correctness check -- an allocation
+    failure there is a busy skip. Also checked in the pod (--min-tflops, --min-relative,
+    --min-efficiency); done here again so an older workload image cannot pass a slow GPU. The full
+    run only ever covers GPUs no pod holds (hip_plan), so the floors apply to all of it."""
+    bad = [f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('error', 'check failed')}"
+           for r in info["gemm"] if not r.get("ok")]
+    bad += [f"probe device {p['device']}: {p.get('error', 'check failed')}" for p in info.get("probe", [])
+            if not p["ok"] and "skipped" not in p]
+    bad += [f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: not ok" for r in info["aggregate"]
+            if r.get("ok") is False and not bad and r.get("efficiency_ok") is not False]
+    if info.get("smoke_ok") is False:
+        bad.append("hip-smoke failed")
+    for r in info["gemm"]:
+        floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0)
+        if not floor_applies(r.get("m"), r.get("n"), r.get("k")):
+            continue
+        if r.get("ok") and floor and r.get("tflops", 0.0) < floor:
+            bad.append(f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('tflops')} TFLOP/s "
+                       f"below the {floor} floor")
+    for r in info["aggregate"]:          # the slowest GPU of each set (per-GPU lines may be cut)
+        floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0) if floor_applies(r.get("m"), r.get("n"), r.get("k")) else 0.0
+        slow = r.get("min_gpu_tflops", r.get("per_gpu_tflops", 0.0))
+        if floor and slow < floor and not bad:
+            bad.append(f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: slowest GPU {slow} TFLOP/s "
+                       f"below the {floor} floor")
+        eff = r.get("efficiency")
+        if min_efficiency and eff is not None and (r.get("gpus") or 1) > 1 and eff < min_efficiency:
+            bad.append(f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: scaling efficiency {eff:.3f} "
+                       f"below {min_efficiency:g}")
+    bad += _relative_outliers(info["gemm"], min_relative)
+    bad += [f"uniformity {u.get('dtype')} {u.get('m')}x{u.get('n')}x{u.get('k')}: slow devices "
+            f"{u.get('slow_devices')} (min ratio {u.get('min_ratio')})" for u in info.get("uniformity", [])
+            if u.get("ok") is False]
+    return list(dict.fromkeys(bad))
+
+
+def _hip_env(ctx: Context, floors: Dict[str, float], plan: Dict[str, Any]) -> Dict[str, str]:
     env = _validator_env(ctx)
     for k, v in ctx.env.items():
-        if k.startswith(("GEMM_", "HIP_", "HSA_")) and k != "HIP_VALIDATION_MODE":
+        if k.startswith(("GEMM_", "HIP_", "HSA_")) and k not in ("HIP_VALIDATION_MODE", "GEMM_VALIDATION_MODE"):
             env[k] = v
     env.setdefault("GEMM_SCALING", "1,2,4,8")
-    # beside running GPU pods the numbers measure the sharing: check correctness, gate nothing
-    env["GEMM_MIN_TFLOPS_BF16"] = "0" if busy else f"{floors['bf16']:g}"
-    env["GEMM_MIN_TFLOPS_FP8"] = "0" if busy else f"{floors['fp8']:g}"
+    env["GEMM_MIN_TFLOPS_BF16"] = f"{floors['bf16']:g}"
+    env["GEMM_MIN_TFLOPS_FP8"] = f"{floors['fp8']:g}"
+    env["GEMM_MIN_RELATIVE"] = f"{_gate_value(ctx, 'GEMM_MIN_RELATIVE', GEMM_MIN_RELATIVE):g}"
+    env["GEMM_MIN_EFFICIENCY"] = f"{_gate_value(ctx, 'GEMM_MIN_EFFICIENCY', GEMM_MIN_EFFICIENCY):g}"
+    if plan["full"] is not None:
+        # tenant GPUs stay out of the full sweep: the free ones, or none at all
+        env["GEMM_DEVICES"] = ",".join(map(str, plan["full"])) or "none"
+    if plan["probe"]:
+        env["GEMM_PROBE_DEVICES"] = ",".join(map(str, plan["probe"]))
     return env
 
 
-def _run_local_hip(ctx: Context, floors: Optional[Dict[str, float]] = None) -> List[Dict[str, Any]]:
+def _gate_value(ctx: Context, key: str, default: float) -> float:
+    v = _env_float(ctx, key)
+    return default if v is None else v
+
+
+def _run_local_hip(ctx: Context, floors: Optional[Dict[str, float]] = None,
+                   plan: Optional[Dict[str, Any]] = None) -> List[Dict[str, Any]]:
     """The HIP workload in this process's container (HIP_VALIDATION_MODE=local)."""
     from .workload_main import run_hip
     floors = floors or {}
+    plan = plan or {"full": None, "probe": []}
     t0 = ctx.clock()
     results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run,
                       dtype=ctx.env.get("GEMM_DTYPE", "bf16"), scaling=ctx.env.get("GEMM_SCALING") or None,
                       iters=int(ctx.env.get("GEMM_ITERS", "50")),
-                      min_tflops=floors.get("bf16", 0.0), min_tflops_fp8=floors.get("fp8", 0.0))
+                      min_tflops=floors.get("bf16", 0.0), min_tflops_fp8=floors.get("fp8", 0.0),
+                      devices=plan["full"], probe_devices=plan["probe"],
+                      min_relative=_gate_value(ctx, "GEMM_MIN_RELATIVE", GEMM_MIN_RELATIVE),
+                      min_efficiency=_gate_value(ctx, "GEMM_MIN_EFFICIENCY", GEMM_MIN_EFFICIENCY))
     if ctx.poll_mode:
         # the reference spawns the workload pod and polls its phase every sleep_interval, first
         # right after creating it (validator/main.go:1042-1059): it sees the result at the
@@ -405,27 +551,41 @@ def _local_workload(ctx: Context, mode: str) -> Dict[str, Any]:
 
 
 def validate_hip(ctx: Context) -> Dict[str, Any]:
-    """hip-smoke + the MFMA GEMM probe (bf16 and fp8, 1/2/4/8-GPU sweep), gated on correctness
-    and on per-GPU throughput floors (models/ defaults, spec.validator.hip.env overrides). The
-    reference gates on vectorAdd's exit code alone (validator/main.go:1176-1211)."""
+    """hip-smoke + the MFMA GEMM probe (bf16 and fp8, 1/2/4/8-GPU sweep), gated on correctness, on
+    per-GPU throughput floors (models/ defaults, spec.validator.hip.env overrides), on the node
+    median and on scaling efficiency. Tenant-safe: GPUs that running pods hold (kubelet
+    pod-resources) get a correctness-only probe, never the full sweep (hip_plan). The reference
+    gates on vectorAdd's exit code alone (validator/main.go:1176-1211)."""
     mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
-    if mode == "skip":                  # no GPU work (CPU rehearsals of the node bring-up)
+    # GEMM_VALIDATION_MODE=dry-run (CPU rehearsals with a kubelet): the pod is planned, scheduled
+    # and run, the GEMMs are not; HIP_VALIDATION_MODE=skip without it: nothing is spawned
+    dry = ctx.env.get("GEMM_VALIDATION_MODE", "") == "dry-run"
+    if mode == "skip" and not dry:      # no GPU work (CPU rehearsals of the node bring-up)
         info = {"skipped": True}
         ctx.status.create(S.HIP_READY, info)
         return info
-    floors = gemm_floors(ctx)
+    gpus = _gpus(ctx)
+    floors = gemm_floors(ctx, gpus)
     busy = gpu_pods_on_node(ctx)
+    plan = hip_plan(ctx, busy, gpus)
     if mode == "local":
-        results = _run_local_hip(ctx, {} if busy else floors)
+        results = _run_local_hip(ctx, floors, plan)
     else:
+        env = _hip_env(ctx, floors, plan)
+        if dry:
+            env["GEMM_DRY_RUN"] = "1"
         res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                                 _hip_env(ctx, floors, busy), timeout=ctx.pod_timeout)
+                                 env, timeout=ctx.pod_timeout)
         results = res["results"]
     info = summarize_gemm(results)
     info["floors_tflops"] = floors
+    info["plan"] = {"full": "all" if plan["full"] is None else plan["full"], "probe": plan["probe"],
+                    "attribution": plan["attribution"], **({"busy_pods": busy[:16]} if busy else {})}
     if busy:
-        info["floor_skipped"] = f"{len(busy)} GPU pod(s) running on the node: {busy[:8]}"
-    bad = gate_gemm(info, floors, busy)
+        info["busy"] = f"{len(busy)} GPU pod(s) on the node hold {len(plan['held_bdfs'])} GPU(s) " \
+                       f"({plan['attribution']}): full sweep on {len(plan['full'])} free, probe on {len(plan['probe'])}"
+    bad = gate_gemm(info, floors, busy, min_relative=_gate_value(ctx, "GEMM_MIN_RELATIVE", GEMM_MIN_RELATIVE),
+                    min_efficiency=_gate_value(ctx, "GEMM_MIN_EFFICIENCY", GEMM_MIN_EFFICIENCY))
     if bad:
         raise ValidationError(f"HIP validation failed: {bad[:8]}")
     ctx.status.create(S.HIP_READY, info)
@@ -545,7 +705,12 @@ def run_topology_check(ctx: Context) -> Dict[str, Any]:
     return fabric
 
 
-def _last_full_fabric(node: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+def _last_full_fabric(ctx: Context, node: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    """The last full collective result: the node-local record, else the Node annotation an older
+    validator wrote (read-only: the validator no longer writes Nodes)."""
+    rec = ctx.status.read(S.FABRIC_LAST_FULL)
+    if rec is not None:
+        return rec
     raw = ((node.get("metadata") or {}).get("annotations") or {}).get(FABRIC_ANNOTATION)
     try:
         return json.loads(raw) if raw else None
@@ -554,16 +719,13 @@ def _last_full_fabric(node: Dict[str, Any]) -> Optional[Dict[str, Any]]:
 
 
 def _record_full_fabric(ctx: Context, info: Dict[str, Any]) -> None:
-    """Keep the last full collective result on the Node (survives validator restarts), so a
-    topology-only pass on a busy node can report when the fabric was last measured."""
-    rec = {"ts": round(time.time(), 3), "ranks": info.get("ranks"), "peak_busbw_gbps": info.get("peak_busbw_gbps"),
-           "busbw_by_ranks": {str(k): v for k, v in (info.get("busbw_by_ranks") or {}).items()},
-           "ok": bool(info.get("ok"))}
-    try:
-        ctx.client.patch("v1", "Node", ctx.node_name,
-                         {"metadata": {"annotations": {FABRIC_ANNOTATION: json.dumps(rec, separators=(",", ":"))}}})
-    except Exception as e:  # noqa: BLE001 - bookkeeping only; the barrier carries the result too
-        log.info("recording the fabric result on node %s failed: %s", ctx.node_name, e)
+    """Keep the last full collective result on the node (survives validator restarts), so a
+    topology-only pass on a busy node can report when the fabric was last measured. A node-local
+    file, not a Node annotation: the validator DaemonSet needs no write access to Nodes."""
+    ctx.status.create(S.FABRIC_LAST_FULL, {
+        "ts": round(time.time(), 3), "ranks": info.get("ranks"), "peak_busbw_gbps": info.get("peak_busbw_gbps"),
+        "busbw_by_ranks": {str(k): v for k, v in (info.get("busbw_by_ranks") or {}).items()},
+        "ok": bool(info.get("ok"))})
 
 
 def plan_rccl_pod(ctx: Context, node: Dict[str, Any], phys: List[Dict[str, Any]]) -> Dict[str, Any]:
@@ -630,14 +792,8 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
         ctx.status.create(S.RCCL_READY, info)
         return info
     if busy:
-        fabric = run_topology_check(ctx)
-        if fabric.get("ok") is False:
-            raise ValidationError(f"xGMI topology check failed: {fabric.get('reason', fabric)}")
-        info = {"mode": "topology-only", "physical_gpus": ngpu, "fabric": fabric, "ok": True,
-                "busy_pods": busy[:16], "last_full": _last_full_fabric(node),
-                "reason": f"{len(busy)} GPU pod(s) hold devices: the collective runs when the node is free"}
-        ctx.status.create(S.RCCL_READY, info)
-        return info
+        return _topology_only(ctx, node, ngpu, busy,
+                              f"{len(busy)} GPU pod(s) hold devices: the collective runs when the node is free")
     plan = plan_rccl_pod(ctx, node, phys)
     env = _validator_env(ctx)
     env.update({k: v for k, v in ctx.env.items() if k.startswith(("RCCL_", "NCCL_"))})
@@ -650,9 +806,29 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
     env["RCCL_MIN_BUSBW_GBPS"] = f"{floor:g}"
     if dry:
         env["RCCL_DRY_RUN"] = "1"
-    out = W.run_workload_pod(ctx.client, "rccl-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                             env, timeout=ctx.pod_timeout, gpu_limit=plan["gpu_limit"],
-                             privileged=plan["privileged"])
+
+    def tenant_arrived(pod: Dict[str, Any]) -> Optional[str]:
+        # the busy check above and the pod's start are not atomic: a tenant scheduled in between
+        # leaves a scheduled-shape pod waiting for GPUs it will not get -- give the node back
+        started = any(((cs.get("state") or {}).get("running") or (cs.get("state") or {}).get("terminated"))
+                      for cs in ((pod.get("status") or {}).get("initContainerStatuses") or []))
+        if started:
+            return None
+        now = gpu_pods_on_node(ctx)
+        return f"GPU pod(s) {now[:8]} started before the fabric pod" if now else None
+    try:
+        out = W.run_workload_pod(ctx.client, "rccl-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                                 env, timeout=ctx.pod_timeout, gpu_limit=plan["gpu_limit"],
+                                 privileged=plan["privileged"], abort_check=tenant_arrived)
+    except W.WorkloadAborted as e:
+        return _topology_only(ctx, node, ngpu, gpu_pods_on_node(ctx), f"fabric pod withdrawn: {e}")
+    except W.PodFailed as e:
+        now = gpu_pods_on_node(ctx)
+        if e.admission or now:
+            return _topology_only(ctx, node, ngpu, now, f"fabric pod not admitted beside GPU pod(s): {e}"[:400])
+        raise ValidationError(f"RCCL all-reduce validation failed: {e}")
+    except (RuntimeError, TimeoutError) as e:
+        raise ValidationError(f"RCCL all-reduce validation failed: {e}")
     info = summarize_rccl(out["results"])
     info.update(mode="full", physical_gpus=ngpu, pod_shape=plan["shape"], min_busbw_gbps=floor)
     if plan.get("reason"):
@@ -661,10 +837,31 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
     if info["ok"] and not info["skipped"] and floor and peak is not None and peak < floor:
         info["ok"] = False
         info["error"] = f"peak busBW {peak} GB/s below the {floor} GB/s floor"
+    if plan["privileged"]:
+        # the privileged-all pod holds no GPU resource: the device plugin kept advertising the GPUs,
+        # so a tenant may have started during the collective -- its numbers (and any failure) then
+        # measure the sharing, not the fabric
+        after = gpu_pods_on_node(ctx)
+        if after:
+            return _topology_only(ctx, node, ngpu, after, "GPU pod(s) started during the collective: not measured",
+                                  disturbed={k: info.get(k) for k in ("ok", "peak_busbw_gbps", "error") if k in info})
     if not info["ok"]:
         raise ValidationError(f"RCCL all-reduce validation failed: {info}")
     if not info["skipped"]:
         _record_full_fabric(ctx, info)
+    ctx.status.create(S.RCCL_READY, info)
+    return info
+
+
+def _topology_only(ctx: Context, node: Dict[str, Any], ngpu: int, busy: List[str], reason: str,
+                   **extra) -> Dict[str, Any]:
+    """The fabric check without a collective (a node whose GPUs pods hold): topology and hive from
+    sysfs, plus the last full result with its timestamp."""
+    fabric = run_topology_check(ctx)
+    if fabric.get("ok") is False:
+        raise ValidationError(f"xGMI topology check failed: {fabric.get('reason', fabric)}")
+    info = {"mode": "topology-only", "physical_gpus": ngpu, "fabric": fabric, "ok": True,
+            "busy_pods": busy[:16], "last_full": _last_full_fabric(ctx, node), "reason": reason, **extra}
     ctx.status.create(S.RCCL_READY, info)
     return info
 

@@ -30,6 +30,9 @@ MXGPU_MANAGER_READY = "mxgpu-manager-ready"
 HOST_MXGPU_MANAGER_READY = "host-mxgpu-manager-ready"
 MXGPU_DEVICES_READY = "mxgpu-devices-ready"
 WORKLOAD_TYPE = "workload-type"
+# the last full RCCL fabric result (no "-ready" suffix: it outlives validator restarts, whose preStop
+# removes *-ready; tmpfs, so a reboot -- after which the fabric is measured again -- clears it)
+FABRIC_LAST_FULL = "fabric-last-full"
 
 CONTAINER_CHAIN = [DRIVER_READY, TOOLKIT_READY, HIP_READY, PLUGIN_READY, RCCL_READY]
 

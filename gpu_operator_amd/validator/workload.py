@@ -18,7 +18,7 @@ import logging
 import os
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 import yaml
 
@@ -85,6 +85,23 @@ def prepare_pod(client, template: Dict[str, Any], namespace: str, node: str, env
     return pod
 
 
+class PodFailed(RuntimeError):
+    """The validation pod ended Failed; ``reason`` is the pod's status.reason (the kubelet's
+    admission rejection, e.g. ``UnexpectedAdmissionError`` / ``OutOfamd.com/gpu``, or empty)."""
+
+    def __init__(self, msg: str, reason: str = ""):
+        super().__init__(msg)
+        self.reason = reason
+
+    @property
+    def admission(self) -> bool:
+        return self.reason == "UnexpectedAdmissionError" or self.reason.startswith("OutOf")
+
+
+class WorkloadAborted(RuntimeError):
+    """The caller's abort check fired while the pod was waiting or running; the pod was deleted."""
+
+
 def delete_stale(client, namespace: str, app: str, node: str) -> None:
     for p in client.list("v1", "Pod", namespace, label_selector={"app": app},
                          field_selector=f"spec.nodeName={node}"):
@@ -94,8 +111,10 @@ def delete_stale(client, namespace: str, app: str, node: str) -> None:
             pass
 
 
-def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0) -> Dict[str, Any]:
-    """Block until the pod Succeeds (returns it) or Fails / times out (raises)."""
+def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0,
+                 abort_check: Optional[Callable[[Dict[str, Any]], Optional[str]]] = None) -> Dict[str, Any]:
+    """Block until the pod Succeeds (returns it) or Fails / times out (raises). ``abort_check``
+    sees the current pod at least every 2 s; a non-empty reason raises WorkloadAborted."""
     done = threading.Event()
     state: Dict[str, Any] = {}
 
@@ -119,6 +138,9 @@ def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0) -> D
                 if (cur.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
                     state["pod"] = cur
                     break
+                why = abort_check(cur) if abort_check else None
+                if why:
+                    raise WorkloadAborted(why)
             except errors.NotFound:
                 pass
             remaining = deadline - time.monotonic()
@@ -131,7 +153,10 @@ def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0) -> D
         raise RuntimeError(state["error"])
     pod = state["pod"]
     if pod["status"]["phase"] != "Succeeded":
-        raise RuntimeError(f"pod {name} failed: {termination_message(pod)}")
+        st = pod["status"]
+        why = ": ".join(x for x in (st.get("reason", ""), st.get("message", "")) if x)
+        raise PodFailed(f"pod {name} failed{' (' + why + ')' if why else ''}: {termination_message(pod)}",
+                        reason=st.get("reason", ""))
     return pod
 
 
@@ -159,9 +184,12 @@ def parse_results(msg: str) -> List[Dict[str, Any]]:
 
 def run_workload_pod(client, manifest: str, namespace: str, node: str, env: Dict[str, str],
                      timeout: float = 300.0, gpu_limit: Optional[Dict[str, int]] = None,
-                     privileged: bool = False) -> Dict[str, Any]:
+                     privileged: bool = False,
+                     abort_check: Optional[Callable[[Dict[str, Any]], Optional[str]]] = None) -> Dict[str, Any]:
     """``gpu_limit``: GPU resources the workload container requests through the scheduler;
-    ``privileged``: the container sees every device instead (AMD_VISIBLE_DEVICES=all in ``env``)."""
+    ``privileged``: the container sees every device instead (AMD_VISIBLE_DEVICES=all in ``env``);
+    ``abort_check``: see wait_for_pod -- on an abort the pod is deleted before WorkloadAborted
+    propagates."""
     template = load_pod_spec(manifest)
     pod = prepare_pod(client, template, namespace, node, env)
     for c in pod["spec"].get("initContainers", []):
@@ -173,5 +201,12 @@ def run_workload_pod(client, manifest: str, namespace: str, node: str, env: Dict
     delete_stale(client, namespace, app, node)
     client.create(pod)
     log.info("created validation pod %s/%s", namespace, o.name(pod))
-    done = wait_for_pod(client, namespace, o.name(pod), timeout)
+    try:
+        done = wait_for_pod(client, namespace, o.name(pod), timeout, abort_check=abort_check)
+    except WorkloadAborted:
+        try:
+            client.delete("v1", "Pod", o.name(pod), namespace, grace_period_seconds=0)
+        except errors.NotFound:
+            pass
+        raise
     return {"pod": o.name(pod), "results": parse_results(termination_message(done))}

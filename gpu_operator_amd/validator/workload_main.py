@@ -2,8 +2,15 @@
 
     amd-validator-workload hip  [--gemm-shapes 8192,...] [--gemm-dtype bf16|fp8|both] [--counters]
                                 [--scaling 1,2,4,8] [--min-tflops X] [--min-tflops-fp8 Y]
+                                [--min-relative R] [--min-efficiency E]
+                                [--devices I,J,..|none] [--probe-devices K,L,..]
     amd-validator-workload rccl [--ranks 2,4,8] [--processes N] [--max-bytes N] [--dtype float|bf16]
-                                [--min-busbw GBPS]
+                                [--min-busbw GBPS] [--timeout-s T]
+
+Tenant safety (hip): ``--devices`` are the HIP indices of the GPUs no pod holds -- the full stabilised
+sweep runs there only, with HIP_VISIBLE_DEVICES set to them, so the process never opens a context on
+a tenant's GPU; ``--probe-devices`` are the held GPUs -- one 1024^3 bf16 GEMM each (no stabilisation,
+no sweep, no counters), a correctness probe whose out-of-memory result is reported, not failed.
 
 Runs the native workload binaries (``amd-hip-smoke``, ``amd-gemm-validate``,
 ``amd-rccl-validate``), optionally collects rocprofv3 counters for one GEMM dispatch
@@ -25,6 +32,7 @@ import shutil
 import subprocess
 import sys
 import tempfile
+import time
 from typing import Callable, Dict, List, Optional
 
 BIN_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native", "bin")
@@ -67,11 +75,27 @@ def _json_lines(text: str) -> List[Dict]:
     return out
 
 
-def run_json(cmd: List[str], run: Callable = subprocess.run, timeout: float = 600) -> (int, List[Dict]):
-    p = run(cmd, capture_output=True, text=True, timeout=timeout)
+def run_json(cmd: List[str], run: Callable = subprocess.run, timeout: float = 600,
+             visible: Optional[List[int]] = None) -> (int, List[Dict]):
+    """Run a workload binary and parse its JSON lines. ``visible``: HIP_VISIBLE_DEVICES for the
+    child; the binary then counts devices from 0 and its ``device`` fields are mapped back to the
+    node's HIP indices (``visible_index`` keeps the child's own)."""
+    kw = {}
+    if visible is not None:
+        kw["env"] = dict(os.environ, HIP_VISIBLE_DEVICES=",".join(str(d) for d in visible))
+    p = run(cmd, capture_output=True, text=True, timeout=timeout, **kw)
     if p.stderr:
         sys.stderr.write(p.stderr[-4000:])
-    return p.returncode, _json_lines(p.stdout)
+    lines = _json_lines(p.stdout)
+    if visible is not None:
+        for x in lines:
+            if isinstance(x.get("device"), int) and 0 <= x["device"] < len(visible):
+                x["visible_index"] = x["device"]
+                x["device"] = visible[x["device"]]
+            if isinstance(x.get("slow_devices"), list):
+                x["slow_devices"] = [visible[d] if isinstance(d, int) and 0 <= d < len(visible) else d
+                                     for d in x["slow_devices"]]
+    return p.returncode, lines
 
 
 def _shape_mnk(shape: str):
@@ -79,7 +103,8 @@ def _shape_mnk(shape: str):
     return (parts[0],) * 3 if len(parts) == 1 else tuple(parts[:3])
 
 
-def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "bf16") -> List[Dict]:
+def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "bf16",
+                     visible: Optional[List[int]] = None) -> List[Dict]:
     """One profiled GEMM dispatch of ``dtype`` under rocprofv3 (counters only: no sys/runtime
     traces, which this pool refuses beside --pmc). Adds the expected MFMA op count
     (2·M·N·K / 512) and whether the measured one matches it."""
@@ -92,7 +117,8 @@ def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "b
         cmd = [prof, "--pmc", *spec["mops"], *PMC_COMMON, "--output-format", "csv", "-d", out, "--",
                binary("amd-gemm-validate"), "--shapes", shape, "--iters", "1", "--warmup", "0",
                "--no-stabilise", "--devices", "0", "--check-rows", "1", "--dtype", dtype]
-        p = run(cmd, capture_output=True, text=True, timeout=300)
+        kw = {"env": dict(os.environ, HIP_VISIBLE_DEVICES=",".join(map(str, visible)))} if visible else {}
+        p = run(cmd, capture_output=True, text=True, timeout=300, **kw)
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if p.returncode != 0 or not files:
             return [{"event": "counters", "dtype": dtype, "ok": False,
@@ -118,33 +144,86 @@ def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "b
         shutil.rmtree(out, ignore_errors=True)
 
 
+PROBE_SHAPE = "1024"      # the correctness probe on GPUs a tenant holds: 6 MiB of operands, ~1 ms
+
+
+def _parse_devices(spec: Optional[str]) -> Optional[List[int]]:
+    """"" / None -> None (every visible GPU); "none" -> [] (no GPU); "0,3" -> [0, 3]."""
+    if spec is None or spec.strip() == "":
+        return None
+    if spec.strip() == "none":
+        return []
+    return [int(x) for x in spec.split(",") if x.strip()]
+
+
 def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
             run: Callable = subprocess.run, dtype: str = "bf16", scaling: Optional[str] = None,
-            min_tflops: float = 0.0, min_tflops_fp8: float = 0.0) -> List[Dict]:
+            min_tflops: float = 0.0, min_tflops_fp8: float = 0.0, devices: Optional[List[int]] = None,
+            probe_devices: Optional[List[int]] = None, min_relative: float = 0.0,
+            min_efficiency: float = 0.0, dry_run: bool = False) -> List[Dict]:
     """hip-smoke, then the MFMA GEMM probe in ``dtype`` (bf16, fp8 e4m3fn on the double-rate
     16x16x128 matrix-core path, or both) -- clock-stabilised like bench.py, optionally swept over
-    ``scaling`` GPU counts ("1,2,4,8") and gated on per-GPU floors -- then optionally one
-    counter-collection pass per dtype."""
-    results: List[Dict] = []
-    rc, r = run_json([binary("amd-hip-smoke")], run)
+    ``scaling`` GPU counts ("1,2,4,8") and gated on per-GPU floors, on the node median
+    (``min_relative``) and on scaling efficiency -- then optionally one counter-collection pass per
+    dtype. ``devices`` (None = all) bounds that full run; ``probe_devices`` get the correctness
+    probe only (module docstring)."""
+    results: List[Dict] = [{"event": "plan", "devices": "all" if devices is None else devices,
+                            "probe_devices": probe_devices or []}]
+    if dry_run:
+        # GEMM_DRY_RUN=1 (CPU rehearsals of node bring-up): what this pod was given, no GPU work
+        results[0].update(skipped="dry-run", hip_visible_devices=os.environ.get("HIP_VISIBLE_DEVICES"),
+                          amd_visible_devices=os.environ.get("AMD_VISIBLE_DEVICES"))
+        return results
+    full = devices is None or len(devices) > 0
+    smoke_on = devices if full else (probe_devices or [])[:1]
+    rc, r = run_json([binary("amd-hip-smoke")], run, visible=smoke_on if smoke_on else None)
     results += r or [{"event": "hip-smoke", "ok": False, "rc": rc}]
-    cmd = [binary("amd-gemm-validate"), "--shapes", ",".join(shapes), "--iters", str(iters)]
-    if dtype != "bf16":
-        cmd += ["--dtype", dtype]
-    if scaling:
-        cmd += ["--scaling", scaling]
-    if min_tflops:
-        cmd += ["--min-tflops", f"{min_tflops:g}"]
-    if min_tflops_fp8:
-        cmd += ["--min-tflops-fp8", f"{min_tflops_fp8:g}"]
-    rc, r = run_json(cmd, run, timeout=1200)
-    results += r
-    if rc != 0 and not any(x.get("event") == "gemm" for x in r):
-        results.append({"event": "gemm", "ok": False, "rc": rc})
-    if counters:
+    if full:
+        cmd = [binary("amd-gemm-validate"), "--shapes", ",".join(shapes), "--iters", str(iters)]
+        if dtype != "bf16":
+            cmd += ["--dtype", dtype]
+        if scaling:
+            cmd += ["--scaling", scaling]
+        if min_tflops:
+            cmd += ["--min-tflops", f"{min_tflops:g}"]
+        if min_tflops_fp8:
+            cmd += ["--min-tflops-fp8", f"{min_tflops_fp8:g}"]
+        if min_relative:
+            cmd += ["--min-relative", f"{min_relative:g}"]
+        if min_efficiency:
+            cmd += ["--min-efficiency", f"{min_efficiency:g}"]
+        rc, r = run_json(cmd, run, timeout=1200, visible=devices)
+        results += r
+        if rc != 0 and not any(x.get("event") == "gemm" for x in r):
+            results.append({"event": "gemm", "ok": False, "rc": rc})
+    if probe_devices:
+        cmd = [binary("amd-gemm-validate"), "--shapes", PROBE_SHAPE, "--dtype", "bf16", "--iters", "3",
+               "--warmup", "1", "--no-stabilise", "--check-rows", "16"]
+        rc, r = run_json(cmd, run, timeout=120, visible=probe_devices)
+        for x in r:
+            x["probe"] = True
+        results += [x for x in r if x.get("event") in ("gemm", "start") or "error" in x]
+        if rc != 0 and not any(x.get("event") == "gemm" for x in r):
+            results.append({"event": "gemm", "probe": True, "ok": False, "rc": rc})
+    if counters and full:
         for d in (["bf16", "fp8"] if dtype == "both" else [dtype]):
-            results += collect_counters(shapes[0], run, dtype=d)
+            results += collect_counters(shapes[0], run, dtype=d, visible=devices[:1] if devices else None)
     return results
+
+
+def hip_ok(results: List[Dict]) -> bool:
+    """The pod's exit status: every check, floor, efficiency and uniformity gate of the full run;
+    on probed (tenant-held) GPUs only correctness, an out-of-memory result being no failure."""
+    for x in results:
+        ev = x.get("event")
+        if ev == "gemm" and x.get("probe"):
+            if not x.get("ok", True) and not x.get("oom"):
+                return False
+        elif ev in ("gemm", "hip-smoke", "uniformity") and not x.get("ok", True):
+            return False
+        elif ev == "aggregate" and x.get("ok") is False:
+            return False
+    return True
 
 
 # NCCL's numeric algorithm / protocol ids in its TUNING lines (NCCL_ALGO_*, NCCL_PROTO_*)
@@ -184,29 +263,45 @@ def _rccl_env(log_path: str) -> Dict[str, str]:
     return env
 
 
+RCCL_MAX_BYTES = 8 << 30      # the sweep's largest message (8 B ... 8 GiB), pod and local mode
+RCCL_STEP_TIMEOUT_S = 120.0   # the binary's hang guard: bound on one blocking step (init, one size, one check)
+
+
 def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run, ranks: Optional[str] = None,
              min_busbw: Optional[float] = None, processes: int = 0, min_bytes: int = 1024,
-             timeout: float = 1200) -> List[Dict]:
+             timeout: float = 1200, step_timeout: float = RCCL_STEP_TIMEOUT_S) -> List[Dict]:
     """The xGMI fabric proof: topology + fabric check, then a rank-count sweep in one process
     (``ranks`` "2,4,8") or, with ``processes`` N, one process per GPU joined through
-    ncclCommInitRank. RCCL's INFO log is captured and summarised (algorithm/protocol per size)."""
+    ncclCommInitRank. RCCL's INFO log is captured and summarised (algorithm/protocol per size).
+    ``step_timeout`` is the binary's own watchdog (--timeout-s, a structured timeout line naming the
+    phase); ``timeout`` bounds the whole run from here, for a binary that cannot even report."""
     if os.environ.get("RCCL_DRY_RUN") == "1":
         return _rccl_dry_run(ranks)
     base = ["--max-bytes", str(max_bytes), "--dtype", dtype, "--min-bytes", str(min_bytes)]
     if min_busbw:
         base += ["--min-busbw", str(min_busbw)]
+    if step_timeout:
+        base += ["--timeout-s", f"{step_timeout:g}"]
     tmp = tempfile.mkdtemp(prefix="amdgo-rccl-")
     try:
         if processes > 0:
             results = _run_rccl_mp(processes, base, tmp, timeout)
         else:
             cmd = [binary("amd-rccl-validate")] + base + (["--ranks", ranks] if ranks else [])
-            p = run(cmd, capture_output=True, text=True, timeout=timeout, env=_rccl_env(os.path.join(tmp, "rccl.%p.log")))
-            if p.stderr:
-                sys.stderr.write(p.stderr[-4000:])
-            results = _json_lines(p.stdout)
-            if p.returncode != 0 and not any(x.get("event") == "summary" for x in results):
-                results.append({"event": "summary", "ok": False, "rc": p.returncode})
+            try:
+                p = run(cmd, capture_output=True, text=True, timeout=timeout,
+                        env=_rccl_env(os.path.join(tmp, "rccl.%p.log")))
+                out, err, rc = p.stdout, p.stderr, p.returncode
+            except subprocess.TimeoutExpired as e:       # run() killed it
+                out, err, rc = _text(e.stdout), _text(e.stderr), None
+            if err:
+                sys.stderr.write(err[-4000:])
+            results = _json_lines(out)
+            if rc is None and not _has_timeout(results):
+                results.append(_launcher_timeout(results, timeout, rank=0))
+            if rc != 0 and not any(x.get("event") == "summary" for x in results):
+                results.append({"event": "summary", "ok": False, "rc": rc,
+                                **({"reason": _timeout_reason(results)} if _has_timeout(results) else {})})
         text = ""
         for f in sorted(glob.glob(os.path.join(tmp, "rccl.*.log"))):
             with open(f, errors="replace") as fh:
@@ -233,9 +328,34 @@ def _rccl_dry_run(ranks: Optional[str]) -> List[Dict]:
     return results
 
 
+def _text(b) -> str:
+    return b.decode(errors="replace") if isinstance(b, bytes) else (b or "")
+
+
+def _has_timeout(lines: List[Dict]) -> bool:
+    return any(x.get("event") in ("timeout", "async_error") for x in lines)
+
+
+def _timeout_reason(lines: List[Dict]) -> str:
+    t = next(x for x in lines if x.get("event") in ("timeout", "async_error"))
+    what = "timed out" if t["event"] == "timeout" else f"async error {t.get('error', '')}"
+    return f"rank {t.get('rank')} of {t.get('ranks')} {what} in {t.get('phase')} ({t.get('bytes', 0)} B)"
+
+
+def _launcher_timeout(lines: List[Dict], timeout: float, rank: int) -> Dict:
+    """A rank the launcher had to kill: the binary's watchdog never reported (stuck in the driver,
+    or an older binary). The phase is inferred from its last line."""
+    last = next((x for x in reversed(lines) if x.get("event") in ("allreduce", "start")), None)
+    phase = "init" if last is None or last.get("event") == "start" else "allreduce"
+    return {"event": "timeout", "phase": phase, "rank": rank, "ranks": (last or {}).get("ranks"),
+            "bytes": (last or {}).get("bytes", 0), "timeout_s": timeout, "killed_by": "launcher", "ok": False}
+
+
 def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict]:
     """Start N ranks of amd-rccl-validate (this process never touches the GPU); rank 0 publishes the
-    ncclUniqueId through a file, the others join. Rank 0's lines plus every rank's summary."""
+    ncclUniqueId through a file, the others join. Rank 0's lines plus every rank's summary, and a
+    structured timeout line for every rank that timed out (its own watchdog's, or the launcher's
+    when the rank had to be killed) -- the failure names the collective phase and the ranks."""
     id_file = os.path.join(tmp, "nccl.id")
     procs = []
     for r in range(n):
@@ -244,29 +364,37 @@ def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                                       env=_rccl_env(os.path.join(tmp, f"rccl.{r}.log"))))
     outs = []
-    for p in procs:
+    deadline = time.monotonic() + timeout
+    killed = set()
+    for r, p in enumerate(procs):
         try:
-            out, err = p.communicate(timeout=timeout)
+            out, err = p.communicate(timeout=max(0.1, deadline - time.monotonic()))
         except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
+            for k, q in enumerate(procs):
+                if q.poll() is None:
+                    q.kill()
+                    killed.add(k)
             out, err = p.communicate()
         if err:
             sys.stderr.write(err[-2000:])
-        outs.append((p.returncode, _json_lines(out)))
+        lines = _json_lines(out)
+        if r in killed and not _has_timeout(lines):
+            lines.append(dict(_launcher_timeout(lines, timeout, r), ranks=n))
+        outs.append((p.returncode, lines))
     results = list(outs[0][1])
     for r, (rc, lines) in enumerate(outs[1:], start=1):
-        results += [x for x in lines if x.get("event") in ("summary", "start") or "error" in x]
+        results += [x for x in lines if x.get("event") in ("summary", "start", "timeout", "async_error") or "error" in x]
+    timeouts = [x for _, lines in outs for x in lines if x.get("event") in ("timeout", "async_error")]
+    for r, (rc, lines) in enumerate(outs):
         if rc != 0 and not any(x.get("event") == "summary" for x in lines):
-            results.append({"event": "summary", "rank": r, "ok": False, "rc": rc})
-    if outs[0][0] != 0 and not any(x.get("event") == "summary" for x in outs[0][1]):
-        results.append({"event": "summary", "rank": 0, "ok": False, "rc": outs[0][0]})
+            results.append({"event": "summary", "rank": r, "ranks": n, "ok": False, "rc": rc,
+                            **({"reason": _timeout_reason(timeouts)} if timeouts else {})})
     return results
 
 
 TERMINATION_LOG_BYTES = 4000       # kubelet keeps at most 4 KiB of a termination message
-_SUMMARY_EVENTS = ("aggregate", "summary", "hip-smoke", "counters", "scaling", "fabric", "ranks_summary",
-                   "rccl-debug")
+_SUMMARY_EVENTS = ("plan", "aggregate", "uniformity", "summary", "timeout", "async_error", "hip-smoke", "counters",
+                   "scaling", "fabric", "ranks_summary", "rccl-debug")
 
 
 def termination_message(results: List[Dict], limit: int = TERMINATION_LOG_BYTES) -> str:
@@ -317,8 +445,18 @@ def main(argv=None) -> int:
     h.add_argument("--min-tflops", type=float, default=float(os.environ.get("GEMM_MIN_TFLOPS_BF16", "0") or 0),
                    help="per-GPU bf16 floor (the validator passes its model default or spec.validator.hip.env)")
     h.add_argument("--min-tflops-fp8", type=float, default=float(os.environ.get("GEMM_MIN_TFLOPS_FP8", "0") or 0))
+    h.add_argument("--min-relative", type=float, default=float(os.environ.get("GEMM_MIN_RELATIVE", "0") or 0),
+                   help="fail a GPU below this fraction of the node median (same dtype and shape)")
+    h.add_argument("--min-efficiency", type=float, default=float(os.environ.get("GEMM_MIN_EFFICIENCY", "0") or 0),
+                   help="fail a scaling step N > 1 below this efficiency")
+    h.add_argument("--devices", default=os.environ.get("GEMM_DEVICES", ""),
+                   help="HIP indices of the GPUs for the full run ('' = all, 'none' = no full run)")
+    h.add_argument("--probe-devices", default=os.environ.get("GEMM_PROBE_DEVICES", ""),
+                   help="HIP indices of tenant-held GPUs: correctness probe only")
     r = sub.add_parser("rccl")
-    r.add_argument("--max-bytes", type=int, default=int(os.environ.get("RCCL_MAX_BYTES", 1 << 30)))
+    r.add_argument("--max-bytes", type=int, default=int(os.environ.get("RCCL_MAX_BYTES", RCCL_MAX_BYTES)))
+    r.add_argument("--timeout-s", type=float, default=float(os.environ.get("RCCL_TIMEOUT_S", RCCL_STEP_TIMEOUT_S)),
+                   help="the binary's watchdog: bound on one blocking step (0 = none)")
     r.add_argument("--dtype", default=os.environ.get("RCCL_DTYPE", "float"))
     r.add_argument("--ranks", default=os.environ.get("RCCL_RANKS", "2,4,8"))
     r.add_argument("--processes", type=int, default=int(os.environ.get("RCCL_PROCESSES", "0")))
@@ -326,10 +464,14 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     if a.what == "hip":
         results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters, dtype=a.gemm_dtype,
-                          scaling=a.scaling or None, min_tflops=a.min_tflops, min_tflops_fp8=a.min_tflops_fp8)
-        ok = all(x.get("ok", True) for x in results if x.get("event") in ("gemm", "hip-smoke"))
+                          scaling=a.scaling or None, min_tflops=a.min_tflops, min_tflops_fp8=a.min_tflops_fp8,
+                          devices=_parse_devices(a.devices), probe_devices=_parse_devices(a.probe_devices),
+                          min_relative=a.min_relative, min_efficiency=a.min_efficiency,
+                          dry_run=os.environ.get("GEMM_DRY_RUN") == "1")
+        ok = hip_ok(results)
     else:
-        results = run_rccl(a.max_bytes, a.dtype, ranks=a.ranks, min_busbw=a.min_busbw, processes=a.processes)
+        results = run_rccl(a.max_bytes, a.dtype, ranks=a.ranks, min_busbw=a.min_busbw, processes=a.processes,
+                           step_timeout=a.timeout_s)
         ok = all(x.get("ok", False) for x in results if x.get("event") == "summary")
     emit(results)
     return 0 if ok else 1

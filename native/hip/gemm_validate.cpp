@@ -20,12 +20,27 @@
 // `efficiency` = aggregate / (N x the 1-GPU figure) to each aggregate line; an N above the visible
 // GPU count prints a `skipped` line instead of failing.
 //
+// --min-efficiency E fails every scaling N > 1 whose efficiency is below E: independent GEMMs on
+// separate GPUs should scale at ~1.0, so a shortfall is a GPU, power or cooling problem.
+//
+// --min-relative R compares the GPUs of this run with each other: per (dtype, shape) each GPU's best
+// TFLOP/s against the node median (upper median), one `uniformity` line each; a GPU below R x median
+// fails. Boxes differ by ~6 % in absolute terms, so absolute floors cannot be tight; a sick GPU next to
+// 7 healthy siblings stands out here.
+//
+// Memory: before allocating, each GPU's free HBM (hipMemGetInfo) is compared with what the shape needs;
+// a shortfall (or an allocation failure) is reported as `"oom":true` with need / free bytes and no
+// kernel is launched -- on a GPU a tenant holds, the validator maps that to "skipped: busy".
+//
 // Exit status 0 only if every check passed and every GPU reached its floor (--min-tflops for
-// bf16, --min-tflops-fp8 for fp8; 0 = no floor).
+// bf16, --min-tflops-fp8 for fp8; 0 = no floor) and the two gates above. The floors are fractions of
+// the dense peak, so they apply to shapes that can reach it: at least one full dispatch wave of
+// 256x256 tiles (M*N >= 256 * 256^2) and K >= 4096; smaller shapes are checked for correctness.
 //
 //   amd-gemm-validate [--shapes 8192,4096,16384x16384x1024] [--dtype bf16|fp8|both] [--iters 50]
 //                     [--warmup 5] [--devices all|0,1,...] [--scaling 1,2,4,8] [--check-rows 32]
-//                     [--min-tflops X] [--min-tflops-fp8 Y] [--stabilise-max-s 6] [--no-stabilise]
+//                     [--min-tflops X] [--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R]
+//                     [--stabilise-max-s 6] [--no-stabilise]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,9 +51,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 extern "C" {
@@ -111,7 +128,8 @@ struct Result {
   Shape s{};
   double tflops = 0, ms = 0, max_rel_err = 0, stab_spread = -1;
   int stab_dispatches = 0;
-  bool ok = false;
+  bool ok = false, oom = false;
+  size_t need_bytes = 0, free_bytes = 0;
   std::string error;
 };
 
@@ -160,6 +178,9 @@ static float bf16_to_f32(uint16_t b) {
   std::memcpy(&f, &u, 4);
   return f;
 }
+
+// Whether the per-GPU floors apply to this shape (see the header).
+static bool floor_applies(const Shape& s) { return (double)s.m * s.n >= 256.0 * 65536.0 && s.k >= 4096; }
 
 // Clock stabilisation (see the header): returns false on a launch/event error.
 static bool stabilise(const DType& dt, const Shape& s, Resources& res, const Options& o, Result& r) {
@@ -217,11 +238,28 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   CHECK(hipStreamCreateWithFlags(&res.st, hipStreamNonBlocking));
   const size_t na = (size_t)s.m * s.k, nb = (size_t)s.n * s.k, nc = (size_t)s.m * s.n;
   const int check_rows = std::max(1, std::min(o.check_rows, s.m));
-  CHECK(hipMalloc(&res.A, na * dt.esize));
-  CHECK(hipMalloc(&res.B, nb * dt.esize));
-  CHECK(hipMalloc(&res.C, nc * 2));
-  CHECK(hipMalloc(&res.ref, (size_t)check_rows * s.n * 4));
-  CHECK(hipMalloc(&res.rows, check_rows * 4));
+  // what this shape needs against what the GPU has free: a tenant may hold most of the HBM
+  r.need_bytes = na * dt.esize + nb * dt.esize + nc * 2 + (size_t)check_rows * s.n * 4 + (size_t)check_rows * 4;
+  size_t total = 0;
+  CHECK(hipMemGetInfo(&r.free_bytes, &total));
+  if (r.need_bytes > r.free_bytes) {
+    r.oom = true;
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "out of memory: the shape needs %.2f GiB, %.2f GiB of %.2f GiB free",
+                  r.need_bytes / 1073741824.0, r.free_bytes / 1073741824.0, total / 1073741824.0);
+    r.error = buf;
+    return false;
+  }
+  auto alloc = [&](void** p, size_t bytes, const char* what) {
+    const hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) return true;
+    r.oom = e == hipErrorOutOfMemory;
+    r.error = std::string(r.oom ? "out of memory: " : "") + "hipMalloc(" + what + "): " + hipGetErrorString(e);
+    return false;
+  };
+  if (!alloc(&res.A, na * dt.esize, "A") || !alloc(&res.B, nb * dt.esize, "B") || !alloc(&res.C, nc * 2, "C") ||
+      !alloc((void**)&res.ref, (size_t)check_rows * s.n * 4, "ref") || !alloc((void**)&res.rows, check_rows * 4, "rows"))
+    return false;
   if (dt.fill(res.A, na, 1000 + dev, res.st) || dt.fill(res.B, nb, 2000 + dev, res.st)) {
     r.error = "fill failed";
     return false;
@@ -286,9 +324,12 @@ struct Aggregate {
   bool ok = true;
 };
 
+// (dtype, m, n, k) -> device -> best TFLOP/s over every set it ran in (the --min-relative gate)
+static std::map<std::tuple<std::string, int, int, int>, std::map<int, double>> g_best;
+
 // One (dtype, shape) on a device set, concurrently; prints the per-GPU lines and the aggregate.
 static Aggregate run_set(const DType& dt, const Shape& s, const std::vector<int>& devs, const Options& o,
-                         double floor, int scaling_n, double single) {
+                         double floor, int scaling_n, double single, double min_eff) {
   std::vector<Result> res(devs.size());
   Rendezvous sync(devs.size());
   std::vector<std::thread> th;
@@ -300,7 +341,7 @@ static Aggregate run_set(const DType& dt, const Shape& s, const std::vector<int>
   const std::string scal = scaling_n > 0 ? ",\"gpus\":" + std::to_string(scaling_n) : std::string();
   for (size_t i = 0; i < devs.size(); ++i) {
     const auto& r = res[i];
-    const bool floor_ok = r.tflops >= floor;
+    const bool floor_ok = !floor_applies(s) || r.tflops >= floor;
     const bool ok = launched[i] && r.ok && floor_ok;
     agg.ok = agg.ok && ok;
     agg.total += r.tflops;
@@ -313,24 +354,35 @@ static Aggregate run_set(const DType& dt, const Shape& s, const std::vector<int>
     }
     for (char& c : err)
       if (c == '"' || c == '\\') c = '\'';
+    char oom[96] = "";
+    if (r.oom)
+      std::snprintf(oom, sizeof oom, ",\"oom\":true,\"need_bytes\":%zu,\"free_bytes\":%zu", r.need_bytes, r.free_bytes);
     std::printf("{\"event\":\"gemm\",\"dtype\":\"%s\",\"device\":%d%s,\"m\":%d,\"n\":%d,\"k\":%d,\"ms\":%.4f,"
                 "\"tflops\":%.1f,\"max_rel_err\":%.3e,\"stabilise_dispatches\":%d,\"stabilise_spread\":%.4f,"
-                "\"min_tflops\":%.1f,\"ok\":%s%s%s%s}\n",
+                "\"min_tflops\":%.1f,\"ok\":%s%s%s%s%s}\n",
                 dt.name, r.device, scal.c_str(), s.m, s.n, s.k, r.ms, r.tflops, r.max_rel_err, r.stab_dispatches,
-                r.stab_spread, floor, ok ? "true" : "false", err.empty() ? "" : ",\"error\":\"", err.c_str(),
+                r.stab_spread, floor_applies(s) ? floor : 0.0, ok ? "true" : "false", oom, err.empty() ? "" : ",\"error\":\"", err.c_str(),
                 err.empty() ? "" : "\"");
+    if (launched[i] && r.ok) {
+      double& best = g_best[{dt.name, s.m, s.n, s.k}][r.device];
+      best = std::max(best, r.tflops);
+    }
   }
   agg.per_gpu = agg.total / devs.size();
   std::string eff;
   if (scaling_n == 1 && agg.total > 0) single = agg.total;   // the 1-GPU run is its own reference
   if (scaling_n > 0 && single > 0) {
-    char buf[64];
-    std::snprintf(buf, sizeof buf, ",\"efficiency\":%.4f", agg.total / (scaling_n * single));
+    const double e = agg.total / (scaling_n * single);
+    const bool eff_ok = scaling_n == 1 || min_eff <= 0 || e >= min_eff;
+    char buf[96];
+    std::snprintf(buf, sizeof buf, ",\"efficiency\":%.4f,\"min_efficiency\":%.2f%s", e, min_eff,
+                  eff_ok ? "" : ",\"efficiency_ok\":false");
     eff = buf;
+    agg.ok = agg.ok && eff_ok;
   }
   std::printf("{\"event\":\"aggregate\",\"dtype\":\"%s\",\"m\":%d,\"n\":%d,\"k\":%d,\"gpus\":%zu,\"total_tflops\":%.1f,"
               "\"per_gpu_tflops\":%.1f,\"min_gpu_tflops\":%.1f,\"min_tflops\":%.1f%s%s,\"ok\":%s}\n",
-              dt.name, s.m, s.n, s.k, devs.size(), agg.total, agg.per_gpu, agg.min_gpu, floor,
+              dt.name, s.m, s.n, s.k, devs.size(), agg.total, agg.per_gpu, agg.min_gpu, floor_applies(s) ? floor : 0.0,
               scaling_n > 0 ? ",\"scaling\":true" : "", eff.c_str(), agg.ok ? "true" : "false");
   std::fflush(stdout);
   return agg;
@@ -339,7 +391,7 @@ static Aggregate run_set(const DType& dt, const Shape& s, const std::vector<int>
 int main(int argc, char** argv) {
   std::string shapes = "8192", devices = "all", dtype = "bf16", scaling;
   Options o;
-  double min_tflops = 0, min_tflops_fp8 = 0;
+  double min_tflops = 0, min_tflops_fp8 = 0, min_eff = 0, min_rel = 0;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -352,12 +404,14 @@ int main(int argc, char** argv) {
     else if (a == "--check-rows") o.check_rows = std::atoi(next().c_str());
     else if (a == "--min-tflops") min_tflops = std::atof(next().c_str());
     else if (a == "--min-tflops-fp8") min_tflops_fp8 = std::atof(next().c_str());
+    else if (a == "--min-efficiency") min_eff = std::atof(next().c_str());
+    else if (a == "--min-relative") min_rel = std::atof(next().c_str());
     else if (a == "--stabilise-max-s") o.stabilise_max_s = std::atof(next().c_str());
     else if (a == "--no-stabilise") o.stabilise = false;
     else if (a == "-h" || a == "--help") {
       std::printf("usage: amd-gemm-validate [--shapes 8192,4096,MxNxK] [--dtype bf16|fp8|both] [--iters N] "
                   "[--warmup N] [--devices all|0,1] [--scaling 1,2,4,8] [--check-rows N] [--min-tflops X] "
-                  "[--min-tflops-fp8 Y] [--stabilise-max-s S] [--no-stabilise]\n");
+                  "[--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R] [--stabilise-max-s S] [--no-stabilise]\n");
       return 0;
     } else {
       std::printf("{\"error\":\"unknown argument %s\"}\n", a.c_str());
@@ -410,7 +464,7 @@ int main(int argc, char** argv) {
     const double floor = dt == &kFp8 ? min_tflops_fp8 : min_tflops;
     for (const auto& s : shape_list) {
       if (counts.empty()) {
-        all_ok = run_set(*dt, s, devs, o, floor, 0, 0).ok && all_ok;
+        all_ok = run_set(*dt, s, devs, o, floor, 0, 0, 0).ok && all_ok;
         continue;
       }
       // the 1-GPU figure every efficiency divides by: the N=1 run when the sweep has one, else
@@ -428,11 +482,32 @@ int main(int argc, char** argv) {
           continue;
         }
         std::vector<int> sub(devs.begin(), devs.begin() + n);
-        Aggregate a = run_set(*dt, s, sub, o, floor, n, single);
+        Aggregate a = run_set(*dt, s, sub, o, floor, n, single, min_eff);
         if (n == 1) single = a.per_gpu;
         all_ok = a.ok && all_ok;
       }
     }
+  }
+  // uniformity: every GPU's best against the node's (upper) median, per dtype and shape
+  for (const auto& [key, per_dev] : g_best) {
+    if (per_dev.size() < 2) continue;
+    std::vector<double> v;
+    for (const auto& kv : per_dev) v.push_back(kv.second);
+    std::sort(v.begin(), v.end());
+    const double med = v[v.size() / 2];
+    double worst = 1e30;
+    std::string slow;
+    for (const auto& [dev, t] : per_dev) {
+      const double ratio = med > 0 ? t / med : 0;
+      worst = std::min(worst, ratio);
+      if (min_rel > 0 && ratio < min_rel) slow += (slow.empty() ? "" : ",") + std::to_string(dev);
+    }
+    const bool ok = slow.empty();
+    all_ok = all_ok && ok;
+    std::printf("{\"event\":\"uniformity\",\"dtype\":\"%s\",\"m\":%d,\"n\":%d,\"k\":%d,\"gpus\":%zu,"
+                "\"median_tflops\":%.1f,\"min_ratio\":%.4f,\"min_relative\":%.2f,\"slow_devices\":[%s],\"ok\":%s}\n",
+                std::get<0>(key).c_str(), std::get<1>(key), std::get<2>(key), std::get<3>(key), per_dev.size(), med,
+                worst, min_rel, slow.c_str(), ok ? "true" : "false");
   }
   return all_ok ? 0 : 1;
 }

@@ -20,19 +20,32 @@
 // `ok` also requires the peak bus bandwidth of the largest rank count to reach --min-busbw
 // (the validator passes spec.validator.rccl.env RCCL_MIN_BUSBW_GBPS).
 //
+// Hang guard (--timeout-s T): a watchdog thread bounds every blocking step -- communicator init, each
+// message size's all-reduces, each result check -- by T seconds and polls ncclCommGetAsyncError on the
+// live communicators every 100 ms. A faulted or missing peer otherwise blocks inside
+// ncclCommInitAll / ncclAllReduce until the pod's timeout and the failure reads "timed out". On a
+// deadline or an async error it prints one structured line
+//   {"event":"timeout"|"async_error","phase":"init|allreduce|check","ranks":N,"rank":R,"bytes":B,...}
+// aborts the communicators (ncclCommAbort, bounded) and exits 124 (timeout) / 125 (async error).
+//
 //   amd-rccl-validate [--ranks 2,4,8] [--min-bytes 8] [--max-bytes 1073741824] [--iters 20]
 //                     [--warmup 5] [--dtype float|bf16] [--min-busbw GBPS] [--topology-only]
-//                     [--sys-root /] [--mp-rank R --mp-nranks N --mp-id-file F [--device D]]
+//                     [--timeout-s T] [--sys-root /]
+//                     [--mp-rank R --mp-nranks N --mp-id-file F [--device D]]
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <set>
 #include <sstream>
 #include <string>
@@ -85,9 +98,107 @@ __global__ void check_bf16_kernel(const __bf16* p, size_t n, float expect, unsig
   if (c) atomicAdd(bad, c);
 }
 
+// --- hang guard ------------------------------------------------------------------------------
+class Watchdog {
+ public:
+  enum Phase { kIdle = 0, kInit, kAllreduce, kCheck };
+
+  void start(double timeout_s, int rank) {
+    timeout_s_ = timeout_s;
+    rank_ = rank;
+    th_ = std::thread([this] { loop(); });
+  }
+  ~Watchdog() {
+    stop_ = true;
+    if (th_.joinable()) th_.join();
+  }
+  // (Re)start the clock of one blocking step.
+  void arm(Phase p, int ranks, size_t bytes) {
+    ranks_ = ranks;
+    bytes_ = (long long)bytes;
+    phase_ = p;
+    deadline_ns_ = timeout_s_ > 0 ? now_ns() + (long long)(timeout_s_ * 1e9) : 0;
+  }
+  void disarm() {
+    deadline_ns_ = 0;
+    phase_ = kIdle;
+  }
+  void watch(const std::vector<ncclComm_t>& comms) {
+    std::lock_guard<std::mutex> lk(mu_);
+    comms_ = comms;
+  }
+  void unwatch() {
+    std::lock_guard<std::mutex> lk(mu_);
+    comms_.clear();
+  }
+
+ private:
+  static long long now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+  static const char* phase_name(int p) {
+    return p == kInit ? "init" : p == kAllreduce ? "allreduce" : p == kCheck ? "check" : "idle";
+  }
+  void loop() {
+    while (!stop_) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      std::string async;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (ncclComm_t c : comms_) {
+          ncclResult_t ae = ncclSuccess;
+          if (ncclCommGetAsyncError(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+            async = ncclGetErrorString(ae);
+            break;
+          }
+        }
+      }
+      if (!async.empty()) fail("async_error", async, 125);
+      const long long d = deadline_ns_;
+      if (d && now_ns() > d) fail("timeout", "", 124);
+    }
+  }
+  [[noreturn]] void fail(const char* event, const std::string& what, int code) {
+    for (char& ch : const_cast<std::string&>(what))
+      if (ch == '"' || ch == '\\') ch = '\'';
+    std::printf("{\"event\":\"%s\",\"phase\":\"%s\",\"ranks\":%d,\"rank\":%d,\"bytes\":%lld,\"timeout_s\":%.1f%s%s%s,"
+                "\"ok\":false}\n",
+                event, phase_name(phase_), (int)ranks_, rank_, (long long)bytes_, timeout_s_,
+                what.empty() ? "" : ",\"error\":\"", what.c_str(), what.empty() ? "" : "\"");
+    std::fflush(stdout);
+    // abort the communicators so peers blocked on this rank see the failure; bounded, since an abort
+    // can itself wait on a wedged peer
+    std::vector<ncclComm_t> comms;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      comms = comms_;
+    }
+    std::atomic<bool> done{false};
+    std::thread([comms, &done] {
+      for (ncclComm_t c : comms) ncclCommAbort(c);
+      done = true;
+    }).detach();
+    for (int i = 0; i < 100 && !done; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    _exit(code);
+  }
+
+  double timeout_s_ = 0;
+  int rank_ = 0;
+  std::atomic<bool> stop_{false};
+  std::atomic<int> phase_{kIdle}, ranks_{0};
+  std::atomic<long long> bytes_{0}, deadline_ns_{0};
+  std::mutex mu_;
+  std::vector<ncclComm_t> comms_;
+  std::thread th_;
+};
+
+Watchdog g_watchdog;
+
 struct Opts {
   std::vector<int> ranks;          // empty = all visible GPUs
   int iters = 20, warmup = 5;
+  double timeout_s = 0;
   size_t min_bytes = 8, max_bytes = (size_t)1 << 30;
   std::string dtype = "float";
   double min_busbw = 0;
@@ -194,6 +305,7 @@ int sweep(const Opts& o, const std::vector<ncclComm_t>& comms, const std::vector
       NCCLCHECK(ncclGroupEnd());
       return 0;
     };
+    g_watchdog.arm(Watchdog::kAllreduce, world, bytes);
     for (int w = 0; w < o.warmup; ++w)
       if (allreduce()) return 2;
     for (int r = 0; r < local; ++r) {
@@ -215,6 +327,7 @@ int sweep(const Opts& o, const std::vector<ncclComm_t>& comms, const std::vector
     const double t = worst_ms / o.iters * 1e-3;
     const double algbw = bytes / t / 1e9, busbw = algbw * bus_factor;
     // correctness: one fresh reduction of rank+1
+    g_watchdog.arm(Watchdog::kCheck, world, bytes);
     for (int r = 0; r < local; ++r) {
       HIPCHECK(hipSetDevice(devs[r]));
       const float v = (float)(rank_base + r + 1);
@@ -241,6 +354,7 @@ int sweep(const Opts& o, const std::vector<ncclComm_t>& comms, const std::vector
                 world, rank_base, bytes, t * 1e6, algbw, busbw, nbad, ok ? "true" : "false");
     std::fflush(stdout);
   }
+  g_watchdog.disarm();
   for (int r = 0; r < local; ++r) {
     hipSetDevice(devs[r]);
     hipFree(buf[r]);
@@ -296,7 +410,11 @@ int run_mp(const Opts& o) {
   const int dev = o.device >= 0 ? o.device : o.mp_rank % ndev;
   HIPCHECK(hipSetDevice(dev));
   ncclComm_t comm;
+  g_watchdog.start(o.timeout_s, o.mp_rank);
+  g_watchdog.arm(Watchdog::kInit, o.mp_nranks, 0);
   NCCLCHECK(ncclCommInitRank(&comm, o.mp_nranks, id, o.mp_rank));
+  g_watchdog.disarm();
+  g_watchdog.watch({comm});
   int ver = 0;
   ncclGetVersion(&ver);
   std::printf("{\"event\":\"start\",\"mode\":\"multi-process\",\"ranks\":%d,\"rank\":%d,\"device\":%d,"
@@ -305,6 +423,7 @@ int run_mp(const Opts& o) {
   std::vector<ncclComm_t> comms{comm};
   std::vector<int> devs{dev};
   const int rc = sweep(o, comms, devs, o.mp_rank, o.mp_nranks, res);
+  g_watchdog.unwatch();
   ncclCommDestroy(comm);
   if (rc) return rc;
   const bool bw_ok = res.peak_busbw >= o.min_busbw;
@@ -335,9 +454,10 @@ int main(int argc, char** argv) {
     else if (a == "--mp-nranks") o.mp_nranks = std::atoi(next().c_str());
     else if (a == "--mp-id-file") o.id_file = next();
     else if (a == "--device") o.device = std::atoi(next().c_str());
+    else if (a == "--timeout-s") o.timeout_s = std::atof(next().c_str());
     else if (a == "-h" || a == "--help") {
       std::printf("usage: amd-rccl-validate [--ranks 2,4,8] [--min-bytes B] [--max-bytes B] [--iters N] "
-                  "[--warmup N] [--dtype float|bf16] [--min-busbw GBPS] [--topology-only] [--sys-root DIR] "
+                  "[--warmup N] [--dtype float|bf16] [--min-busbw GBPS] [--topology-only] [--timeout-s T] [--sys-root DIR] "
                   "[--mp-rank R --mp-nranks N --mp-id-file F [--device D]]\n");
       return 0;
     } else {
@@ -372,7 +492,8 @@ int main(int argc, char** argv) {
   int ver = 0;
   ncclGetVersion(&ver);
   std::printf("{\"event\":\"start\",\"mode\":\"single-process\",\"visible_gpus\":%d,\"rccl_version\":%d,"
-              "\"dtype\":\"%s\"}\n", ndev, ver, o.dtype.c_str());
+              "\"dtype\":\"%s\",\"timeout_s\":%.1f}\n", ndev, ver, o.dtype.c_str(), o.timeout_s);
+  g_watchdog.start(o.timeout_s, 0);
   bool all_ok = true;
   int largest = 0;
   double largest_peak = 0;
@@ -385,9 +506,13 @@ int main(int argc, char** argv) {
     std::vector<int> devs(n);
     for (int r = 0; r < n; ++r) devs[r] = r;
     std::vector<ncclComm_t> comms(n);
+    g_watchdog.arm(Watchdog::kInit, n, 0);
     NCCLCHECK(ncclCommInitAll(comms.data(), n, devs.data()));
+    g_watchdog.disarm();
+    g_watchdog.watch(comms);
     SweepResult res;
     const int rc = sweep(o, comms, devs, 0, n, res);
+    g_watchdog.unwatch();
     for (auto c : comms) ncclCommDestroy(c);
     if (rc) return rc;
     const bool gate = n == *std::max_element(counts.begin(), counts.end()) || o.ranks.empty();

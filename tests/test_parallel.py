@@ -69,6 +69,9 @@ def test_bench_cpu_rehearsal_two_ranks():
     assert d["value"] == pytest.approx(d["per_gpu_tflops"] * 2, rel=1e-3, abs=0.02) and d["value"] > 0
     assert d["allreduce_ok"] and d["device"] == "cpu-rehearsal"
     assert d["config"]["parallelism"].startswith("dp2")
+    # each rank's own loop next to the MAX-over-ranks headline: a slow rank is visible
+    assert 0 < d["per_rank_tflops_min"] <= d["per_rank_tflops_max"] and d["slowest_rank"] in (0, 1)
+    assert d["per_rank_tflops_min"] >= d["per_gpu_tflops"] * 0.999
 
 
 def test_bench_self_launches_n_ranks_without_torchrun():

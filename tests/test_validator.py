@@ -56,7 +56,10 @@ class FakeKubelet:
 
         def finish():
             time.sleep(0.05)
-            p = self.client.get("v1", "Pod", o.name(pod), o.namespace(pod))
+            try:
+                p = self.client.get("v1", "Pod", o.name(pod), o.namespace(pod))
+            except Exception:  # noqa: BLE001 - the validator withdrew the pod first
+                return
             p["status"] = {"phase": self.phase, "initContainerStatuses": [
                 {"name": "x", "state": {"terminated": {"exitCode": 0, "message": msg}}}]}
             self.client.update_status(p)
@@ -390,7 +393,7 @@ def test_rccl_workload_cli_reads_env(monkeypatch):
     monkeypatch.setenv("RCCL_MIN_BUSBW_GBPS", "123.5")
     monkeypatch.setenv("RCCL_RANKS", "2,8")
     assert WM.main(["rccl"]) == 0
-    assert seen == {"max_bytes": 1 << 30, "dtype": "float", "ranks": "2,8", "min_busbw": 123.5, "processes": 0}
+    assert seen == {"max_bytes": 8 << 30, "dtype": "float", "ranks": "2,8", "min_busbw": 123.5, "processes": 0}
 
 
 # -- throughput floors, node shapes, busy nodes ------------------------------
@@ -405,12 +408,12 @@ def _gemm_msg(per_gpu, dtype="bf16", gpus=8):
 
 def test_gemm_floors_come_from_the_model_and_env(tmp_path, node_root):
     f = comp.gemm_floors(ctx_for(tmp_path, node_root))
-    assert f == {"bf16": round(2516.6 * 0.40, 1), "fp8": round(5033.2 * 0.40, 1)}   # MI355X dense peaks
+    assert f == {"bf16": round(2516.6 * 0.50, 1), "fp8": round(5033.2 * 0.50, 1)}   # MI355X dense peaks
     f = comp.gemm_floors(ctx_for(tmp_path, node_root, env={"GEMM_MIN_TFLOPS_BF16": "1200",
                                                            "GEMM_MIN_TFLOPS_FP8": "0"}))
     assert f == {"bf16": 1200.0, "fp8": 0.0}
     cpx = str(fakesys.make_node(tmp_path / "cpx", compute="CPX"))       # a partition has 1/8 of the CUs
-    assert comp.gemm_floors(ctx_for(tmp_path, cpx))["bf16"] == round(2516.6 * 0.40 / 8, 1)
+    assert comp.gemm_floors(ctx_for(tmp_path, cpx))["bf16"] == round(2516.6 * 0.50 / 8, 1)
     with pytest.raises(comp.ValidationError, match="not a number"):
         comp.gemm_floors(ctx_for(tmp_path, node_root, env={"GEMM_MIN_TFLOPS_BF16": "fast"}))
     assert comp.busbw_floor(ctx_for(tmp_path, node_root)) == round(153.6 * 0.25, 1)
@@ -420,11 +423,13 @@ def test_hip_below_floor_opens_no_barrier(tmp_path, node_root):
     c = FakeClient([node_obj()])
     k = FakeKubelet(c, {"amd-hip-validator": _gemm_msg(600.0)})          # a GPU at ~1/4 of its rate
     ctx = ctx_for(tmp_path, node_root, client=c)
-    with pytest.raises(comp.ValidationError, match="below the 1006.6 floor"):
+    with pytest.raises(comp.ValidationError, match="below the 1258.3 floor"):
         comp.validate_hip(ctx)
     assert not ctx.status.exists(S.HIP_READY)
     env = _pod_env(k.seen[0])
-    assert env["GEMM_MIN_TFLOPS_BF16"] == "1006.6" and env["GEMM_SCALING"] == "1,2,4,8"
+    assert env["GEMM_MIN_TFLOPS_BF16"] == "1258.3" and env["GEMM_SCALING"] == "1,2,4,8"
+    assert env["GEMM_MIN_RELATIVE"] == "0.85" and env["GEMM_MIN_EFFICIENCY"] == "0.9"
+    assert "GEMM_DEVICES" not in env and "GEMM_PROBE_DEVICES" not in env       # an idle node: every GPU
 
 
 def test_hip_records_the_scaling_sweep(tmp_path, node_root):
@@ -456,12 +461,19 @@ def test_rccl_below_floor_opens_no_barrier(tmp_path, node_root):
     assert not ctx.status.exists(S.RCCL_READY)
 
 
-def test_rccl_full_run_records_the_node_annotation(tmp_path, node_root):
+def test_rccl_full_run_keeps_the_result_on_the_node_without_writing_the_node(tmp_path, node_root):
     c = FakeClient([node_obj()])
     FakeKubelet(c, {"amd-rccl-validator": RCCL_SWEEP_MSG})
-    comp.validate_rccl(ctx_for(tmp_path, node_root, client=c))
-    ann = json.loads(c.get("v1", "Node", "n1")["metadata"]["annotations"][comp.FABRIC_ANNOTATION])
-    assert ann["ok"] and ann["peak_busbw_gbps"] == 310.0 and ann["busbw_by_ranks"]["8"] == 310.0
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    comp.validate_rccl(ctx)
+    rec = ctx.status.read(S.FABRIC_LAST_FULL)
+    assert rec["ok"] and rec["peak_busbw_gbps"] == 310.0 and rec["busbw_by_ranks"]["8"] == 310.0
+    assert not (c.get("v1", "Node", "n1")["metadata"].get("annotations") or {})   # no Node write
+    ctx.status.cleanup_ready()                      # a validator restart's preStop keeps the record
+    assert ctx.status.read(S.FABRIC_LAST_FULL)["peak_busbw_gbps"] == 310.0
+    role = open(os.path.join(os.path.dirname(comp.__file__), "..", "assets", "state-operator-validation",
+                             "0210_clusterrole.yaml")).read()
+    assert "patch" not in role and "update" not in role
 
 
 def test_rccl_time_slicing_node_asks_for_the_physical_gpus(tmp_path, node_root):
@@ -501,9 +513,131 @@ def test_busy_node_runs_topology_only_and_keeps_the_last_full_result(tmp_path, n
     assert info["fabric"]["ok"] and info["last_full"]["peak_busbw_gbps"] == 305.0
     assert not [p for p in k.seen if o.get_labels(p).get("app") == "amd-rccl-validator"]   # no collective pod
     assert ctx.status.exists(S.RCCL_READY)
-    # the GEMM numbers beside a training job measure the sharing: correctness only, no floor
+    # every GPU is held (no pod-resources socket: unattributed): no full sweep, a correctness probe on
+    # each, and an out-of-memory probe is a busy skip, not a failure
+    k.messages["amd-hip-validator"] = _probe_msg(range(8), oom={3})
     hip = comp.validate_hip(ctx)
-    assert "floor_skipped" in hip and _pod_env(k.seen[-1])["GEMM_MIN_TFLOPS_BF16"] == "0"
+    env = _pod_env(k.seen[-1])
+    assert env["GEMM_DEVICES"] == "none" and env["GEMM_PROBE_DEVICES"] == "0,1,2,3,4,5,6,7"
+    assert hip["plan"]["attribution"] == "unattributed" and hip["plan"]["full"] == []
+    assert [p["device"] for p in hip["probe"] if "skipped" in p] == [3]
+    assert ctx.status.exists(S.HIP_READY)
+
+
+def _probe_msg(devices, oom=(), bad=()):
+    lines = [{"event": "plan", "devices": [], "probe_devices": list(devices)},
+             {"event": "hip-smoke", "devices": 1, "ok": True}]
+    for d in devices:
+        r = {"event": "gemm", "probe": True, "dtype": "bf16", "device": d, "m": 1024, "n": 1024, "k": 1024,
+             "tflops": 100.0, "ok": d not in oom and d not in bad}
+        if d in oom:
+            r.update(oom=True, tflops=0.0, error="out of memory: the shape needs 0.01 GiB, 0.00 GiB of 288 GiB free")
+        if d in bad:
+            r.update(error="max_rel_err 0.5")
+        lines.append(r)
+    return "\n".join(json.dumps(x) for x in lines)
+
+
+def _tenant(name="train-0", gpus=2):
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"nodeName": "n1", "containers": [{"name": "t", "resources": {"limits": {"amd.com/gpu": str(gpus)}}}]},
+            "status": {"phase": "Running"}}
+
+
+def test_hip_plan_sweeps_only_the_gpus_no_pod_holds(tmp_path, node_root, monkeypatch):
+    """A tenant holds 2 GPUs (pod-resources: device ids of agents 2 and 5): the full sweep runs on
+    the 6 free GPUs (GEMM_DEVICES), the 2 held ones get the correctness probe."""
+    monkeypatch.setattr(comp, "_pod_device_ids", lambda ctx: {
+        "default/train-0": ["amdgpu-1000000000000020", "amdgpu-1000000000000050"],
+        "amd-gpu-operator/amd-hip-validator-n1": ["amdgpu-1000000000000000"]})
+    c = FakeClient([node_obj(), _tenant()])
+    msg = "\n".join(json.dumps(x) for x in [
+        {"event": "hip-smoke", "ok": True},
+        *[{"event": "gemm", "dtype": "bf16", "device": d, "m": 8192, "n": 8192, "k": 8192, "tflops": 1600.0 + d,
+           "ok": True} for d in (0, 1, 3, 4, 6, 7)],
+        {"event": "aggregate", "dtype": "bf16", "m": 8192, "n": 8192, "k": 8192, "gpus": 6, "total_tflops": 9621.0,
+         "per_gpu_tflops": 1603.5, "min_gpu_tflops": 1600.0, "efficiency": 0.99, "ok": True}]) + "\n" + \
+        "\n".join(_probe_msg([2, 5]).splitlines()[2:])
+    k = FakeKubelet(c, {"amd-hip-validator": msg})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    info = comp.validate_hip(ctx)
+    env = _pod_env(next(p for p in k.seen if o.get_labels(p).get("app") == "amd-hip-validator"))
+    assert env["GEMM_DEVICES"] == "0,1,3,4,6,7" and env["GEMM_PROBE_DEVICES"] == "2,5"
+    assert env["GEMM_MIN_TFLOPS_BF16"] == "1258.3"              # free GPUs keep their floor
+    assert info["plan"] == {"full": [0, 1, 3, 4, 6, 7], "probe": [2, 5], "attribution": "pod-resources",
+                            "busy_pods": ["default/train-0"]}
+    assert ctx.status.exists(S.HIP_READY)
+
+
+def test_hip_plan_holds_every_partition_of_a_held_gpu(tmp_path, monkeypatch):
+    root = str(fakesys.make_node(tmp_path / "cpx", compute="CPX"))
+    monkeypatch.setattr(comp, "_pod_device_ids", lambda ctx: {"default/train-0": ["amdgpu-1000000000000013"]})
+    ctx = ctx_for(tmp_path, root, client=FakeClient([node_obj(gpus=64), _tenant(gpus=1)]))
+    plan = comp.hip_plan(ctx, ["default/train-0"])
+    assert plan["probe"] == list(range(8, 16)) and len(plan["full"]) == 56    # GPU 1's 8 partitions
+
+
+def test_hip_probe_failure_that_is_not_oom_fails_the_node(tmp_path, node_root):
+    c = FakeClient([node_obj(), _tenant(gpus=8)])
+    k = FakeKubelet(c, {"amd-hip-validator": _probe_msg(range(8), bad={6})})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    with pytest.raises(comp.ValidationError, match="probe device 6: max_rel_err"):
+        comp.validate_hip(ctx)
+    assert not ctx.status.exists(S.HIP_READY)
+
+
+def test_hip_gpu_below_the_node_median_opens_no_barrier(tmp_path, node_root):
+    """Every GPU above the absolute floor, one at 0.8x its 7 siblings: a sick GPU, no hip-ready."""
+    per = [{"event": "gemm", "dtype": "bf16", "device": d, "m": 8192, "n": 8192, "k": 8192,
+            "tflops": 1300.0 if d == 5 else 1625.0, "ok": True} for d in range(8)]
+    msg = "\n".join(json.dumps(x) for x in [{"event": "hip-smoke", "ok": True}, *per])
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-hip-validator": msg})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    with pytest.raises(comp.ValidationError, match=r"device 5: 1300.0 TFLOP/s is 0.80x the node median 1625.0"):
+        comp.validate_hip(ctx)
+    assert not ctx.status.exists(S.HIP_READY)
+    # the same spread within 0.85 passes; GEMM_MIN_RELATIVE=0 turns the gate off
+    assert not comp._relative_outliers([dict(r, tflops=1400.0) if r["device"] == 5 else r for r in per], 0.85)
+    assert not comp._relative_outliers(per, 0.0)
+
+
+def test_hip_low_scaling_efficiency_opens_no_barrier(tmp_path, node_root):
+    msg = "\n".join(json.dumps(x) for x in [
+        {"event": "hip-smoke", "ok": True},
+        {"event": "aggregate", "dtype": "bf16", "m": 8192, "n": 8192, "k": 8192, "gpus": 1, "total_tflops": 1600.0,
+         "per_gpu_tflops": 1600.0, "min_gpu_tflops": 1600.0, "efficiency": 1.0, "ok": True},
+        {"event": "aggregate", "dtype": "bf16", "m": 8192, "n": 8192, "k": 8192, "gpus": 8, "total_tflops": 10240.0,
+         "per_gpu_tflops": 1280.0, "min_gpu_tflops": 1270.0, "efficiency": 0.8, "ok": True}])
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-hip-validator": msg})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    with pytest.raises(comp.ValidationError, match="x8: scaling efficiency 0.800 below 0.9"):
+        comp.validate_hip(ctx)
+    assert not ctx.status.exists(S.HIP_READY)
+
+
+def test_rccl_tenant_between_the_busy_check_and_the_fabric_pod_falls_back(tmp_path, node_root):
+    """The kubelet rejects the nodeName-bound fabric pod at admission (a tenant took GPUs after the
+    busy check): topology-only in seconds, not a failure after the 300 s pod timeout."""
+    c = FakeClient([node_obj()])
+    k = FakeKubelet(c, {"amd-rccl-validator": ""}, phase="Failed")
+    orig = k.on_event
+
+    def admit(ev):                        # the tenant lands as the fabric pod is created
+        if ev.type == "ADDED" and o.get_labels(ev.obj).get("app") == "amd-rccl-validator":
+            c.create(_tenant(gpus=2))
+        orig(ev)
+    k.on_event = admit
+    c.watch("v1", "Pod", admit)
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    t = time.monotonic()
+    info = comp.validate_rccl(ctx)
+    assert time.monotonic() - t < 30
+    assert info["mode"] == "topology-only" and info["busy_pods"] == ["default/train-0"]
+    # whichever the validator sees first: the admission rejection, or the tenant before the pod started
+    assert info["reason"].startswith(("fabric pod not admitted", "fabric pod withdrawn")), info["reason"]
+    assert ctx.status.exists(S.RCCL_READY)
 
 
 def test_termination_message_keeps_summaries_and_failures_first():

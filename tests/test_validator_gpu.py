@@ -170,3 +170,48 @@ def test_node_time_to_ready_both_protocols_on_the_gpu():
     assert ours["gemm_tflops_per_gpu"] and ours["gemm_tflops_per_gpu"] > 300
     assert r["agent_chain_time_to_ready_s"] < r["reference_protocol_time_to_ready_s"]
     assert ours["marks_s"]["kubelet:capacity:amd.com/gpu=1"] < ours["barriers_s"]["plugin-ready"]
+
+
+def test_gemm_validate_reports_out_of_memory_structurally():
+    """393216^3: A alone is 309 GB, more than the 288 GB of HBM. The probe checks free HBM before
+    allocating and reports a structured out-of-memory line (no kernel launched), exit 1."""
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "393216", "--iters", "1", "--warmup", "0", "--no-stabilise",
+                         timeout=120)
+    assert rc == 1, err
+    g = [x for x in lines if x.get("event") == "gemm"][0]
+    assert g["oom"] and not g["ok"] and g["error"].startswith("out of memory")
+    assert g["need_bytes"] > g["free_bytes"] > 0 and g["need_bytes"] >= 2 * 393216 ** 2 * 2
+
+
+def test_busy_gpu_oom_probe_is_a_skip_in_validate_hip(tmp_path, monkeypatch):
+    """validate_hip, local mode, the box's GPU held by a tenant pod (pod-resources mapping faked):
+    the GPU gets only the probe; its allocation failure (shape forced past HBM) is a busy skip and
+    hip-ready opens."""
+    from gpu_operator_amd import devices as D
+    from gpu_operator_amd.k8s.fake import FakeClient
+    from gpu_operator_amd.validator import components as comp
+    from gpu_operator_amd.validator import status as S
+    from gpu_operator_amd.validator import workload_main as WM
+    g0 = sorted(D.enumerate_gpus("/"), key=lambda g: g["index"])[0]
+    tenant = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "train-0", "namespace": "default"},
+              "spec": {"nodeName": "n1", "containers": [{"name": "t", "resources": {"limits": {"amd.com/gpu": "1"}}}]},
+              "status": {"phase": "Running"}}
+    did = f"amdgpu-{g0['unique_id']:016x}"
+    monkeypatch.setattr(comp, "_pod_device_ids", lambda ctx: {"default/train-0": [did]})
+    monkeypatch.setattr(WM, "PROBE_SHAPE", "393216")
+    ctx = comp.Context(status=S.StatusDir(str(tmp_path / "v")), node_name="n1", client=FakeClient([tenant]),
+                       env={"HIP_VALIDATION_MODE": "local", "GEMM_SHAPES": "4096"})
+    info = comp.validate_hip(ctx)
+    assert info["plan"]["probe"] == [g0["index"]] and g0["index"] not in info["plan"]["full"]
+    probe = [p for p in info["probe"] if p["device"] == g0["index"]][0]
+    assert probe["skipped"].startswith("busy: out of memory") and ctx.status.exists(S.HIP_READY)
+
+
+def test_rccl_watchdog_reports_a_missing_peer(tmp_path):
+    """Rank 0 of a 2-rank multi-process run whose peer never starts: ncclCommInitRank blocks in the
+    bootstrap; the watchdog prints a structured init timeout, aborts and exits 124."""
+    rc, lines, err = run("amd-rccl-validate", "--mp-rank", "0", "--mp-nranks", "2", "--mp-id-file",
+                         str(tmp_path / "id"), "--device", "0", "--timeout-s", "5", timeout=90)
+    assert rc == 124, (rc, lines, err[-2000:])
+    t = [x for x in lines if x.get("event") == "timeout"][0]
+    assert t["phase"] == "init" and t["ranks"] == 2 and t["rank"] == 0 and t["timeout_s"] == 5.0

@@ -45,9 +45,9 @@ OPERANDS = {
     "state-operator-validation": ("amd-operator-validator",
                                   [r([""], ["pods"], ["get", "list", "watch", "create", "delete"]),
                                    r(["apps"], ["daemonsets"], ["get", "list"])],
-                                  # nodes/patch: the last full fabric result (amd.com/gpu.fabric-validation)
-                                  [r([""], ["nodes"], ["get", "list", "watch", "patch"]),
-                                   r([""], ["pods"], ["get", "list"])]),
+                                  # read-only on nodes: the last full fabric result stays on the node
+                                  # (barrier dir file fabric-last-full), no Node writes
+                                  [NODES_RO, r([""], ["pods"], ["get", "list"])]),
     "state-device-plugin": ("amd-device-plugin",
                             [r([""], ["configmaps"], ["get", "list", "watch"])],
                             [NODES_RW]),
