@@ -114,6 +114,9 @@ TARGETS: List[Target] = [
            flags=["-static"], headers=["include/amdnode.h", "include/minijson.h"]),
     Target("bin/amd-node-probe", ["node/node_probe.cpp", "node/amdnode.cpp"], "cxx-exe",
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
+    # driver / toolkit / no-fabric rccl validation without a Python interpreter (validator init containers)
+    Target("bin/amd-node-validate", ["node/node_validate.cpp", "node/amdnode.cpp"], "cxx-exe",
+           flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h", "include/minijson.h"]),
 ]
 
 

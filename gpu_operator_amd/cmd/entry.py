@@ -34,7 +34,7 @@ SCRIPTS = {
 
 
 NATIVE_TOOLS = ("amd-barrier-wait", "amd-hip-smoke", "amd-gemm-validate", "amd-rccl-validate", "amd-node-probe",
-                "amd-container-runtime")
+                "amd-node-validate", "amd-container-runtime")
 
 
 def install_wrappers(bin_dir: str) -> str:

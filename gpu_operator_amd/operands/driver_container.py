@@ -23,9 +23,12 @@ kernel modules + firmware (no user-space driver libraries to expose), so:
 Reload on request: a memory-partition (NPS) change only takes effect once amdgpu reloads, and
 only this container has the module tree that loaded it (precompiled ``.ko`` files under
 ``/opt/amdgpu`` or its DKMS build). While ``init`` blocks it serves a node-local request file,
-``/run/amd/driver/reload-request`` (JSON ``{"id": ...}``, written by the partition manager):
-it unloads the modules, loads them again through the same precompiled / DKMS path, waits for
-readiness, rewrites the ``.driver-ctr`` marker and answers in ``reload-result`` with the same id.
+``/run/amd/driver/reload-request`` (JSON ``{"id", "ts", "deadline"}``, written by the partition
+manager): it unloads the modules, loads them again -- insmod of the precompiled ``.ko`` files, or
+``modprobe`` of the module DKMS built at init (a reload never rebuilds) -- within the requester's
+deadline, waits for readiness, rewrites the ``.driver-ctr`` marker and answers in ``reload-result``
+with the same id, whatever happens. A request older than this container, or past its deadline (its
+requester gave up), is answered ``stale`` and never unloads the driver.
 """
 
 from __future__ import annotations
@@ -116,6 +119,7 @@ class DriverContainer:
         self.run = run
         self.ready_timeout = ready_timeout
         self.poll = poll
+        self.started = time.time()          # reload requests written before this are stale
 
     @property
     def marker(self) -> str:
@@ -150,8 +154,15 @@ class DriverContainer:
             n += 1
         return n
 
-    def _run(self, argv: List[str], what: str) -> None:
-        p = self.run(argv, capture_output=True, text=True, timeout=1800)
+    def _run(self, argv: List[str], what: str, timeout: float = 1800.0) -> None:
+        if timeout <= 0:
+            raise DriverError(f"{what}: no time left before the reload deadline")
+        try:
+            p = self.run(argv, capture_output=True, text=True, timeout=timeout)
+        except subprocess.TimeoutExpired:
+            raise DriverError(f"{what} did not finish within {timeout:.0f}s")
+        except OSError as e:
+            raise DriverError(f"{what}: {e}")
         if p.returncode != 0:
             raise DriverError(f"{what} failed ({p.returncode}): {(p.stderr or '').strip()[-2000:]}")
 
@@ -169,17 +180,31 @@ class DriverContainer:
         self._run(["modprobe", "amdgpu"] + params, "modprobe amdgpu")
         return "dkms", ["amdgpu"]
 
-    def unload(self) -> List[str]:
+    def load_built(self, deadline: float) -> Tuple[str, List[str]]:
+        """``load`` without building: what a reload needs (init built or found the modules).
+        Every step is bounded by ``deadline`` (time.monotonic())."""
+        params = module_params(self.params_file)
+        mods = self.precompiled_modules()
+        if mods:
+            for m in mods:
+                self._run(["insmod", m] + (params if _mod_name(m) == "amdgpu" else []), f"insmod {_mod_name(m)}",
+                          deadline - time.monotonic())
+            return "precompiled", [_mod_name(m) for m in mods]
+        self._run(["modprobe", "amdgpu"] + params, "modprobe amdgpu", deadline - time.monotonic())
+        return "dkms", ["amdgpu"]
+
+    def unload(self, deadline: Optional[float] = None) -> List[str]:
         """Remove what ``load`` inserted: precompiled modules in reverse load order (amdgpu
         first), else ``modprobe -r amdgpu`` (DKMS). The GPU clients are gone by now (the partition
         manager paused them); a module still in use fails the unload."""
+        left = (lambda: deadline - time.monotonic()) if deadline is not None else (lambda: 1800.0)
         mods = [_mod_name(m) for m in self.precompiled_modules()]
         if mods:
             loaded = [m for m in reversed(mods) if os.path.isdir(os.path.join(self.sys_root, "sys/module", m))]
             for m in loaded:
-                self._run(["rmmod", m], f"rmmod {m}")
+                self._run(["rmmod", m], f"rmmod {m}", left())
             return loaded
-        self._run(["modprobe", "-r", "amdgpu"], "modprobe -r amdgpu")
+        self._run(["modprobe", "-r", "amdgpu"], "modprobe -r amdgpu", left())
         return ["amdgpu"]
 
     def _write_marker(self, info: Dict) -> None:
@@ -188,11 +213,14 @@ class DriverContainer:
             json.dump(info, f)
         os.replace(self.marker + ".tmp", self.marker)
 
-    def reload(self) -> Dict:
+    def reload(self, budget_s: Optional[float] = None) -> Dict:
+        """Unload and load again (no DKMS build), all within ``budget_s`` (the requester's deadline;
+        default ``ready_timeout``), then wait for readiness inside what is left."""
         t0 = time.monotonic()
-        removed = self.unload()
-        mode, mods = self.load()
-        why = self.wait_ready()
+        deadline = t0 + (self.ready_timeout if budget_s is None else budget_s)
+        removed = self.unload(deadline)
+        mode, mods = self.load_built(deadline)
+        why = self.wait_ready(deadline)
         info = {"kernel": self.kernel, "mode": mode, "modules": mods, "unloaded": removed,
                 "version": self.driver_version, "reload_s": round(time.monotonic() - t0, 3), "ts": time.time(),
                 "state": why}
@@ -200,8 +228,17 @@ class DriverContainer:
         log.info("amdgpu reloaded: %s", info)
         return info
 
+    def _answer(self, res: Dict) -> None:
+        res["ts"] = time.time()
+        out = os.path.join(self.driver_dir, RELOAD_RESULT)
+        with open(out + ".tmp", "w") as f:
+            json.dump(res, f)
+        os.replace(out + ".tmp", out)
+
     def serve_reloads(self, stop: threading.Event, period: float = 1.0) -> None:
-        """Answer reload requests until ``stop`` (event-driven: inotify on the driver dir)."""
+        """Answer reload requests until ``stop`` (event-driven: inotify on the driver dir). Every
+        request gets a result, also when the reload raises something unexpected; a stale request
+        (older than this container, or past the requester's deadline) never touches the driver."""
         os.makedirs(self.driver_dir, exist_ok=True)
         req = os.path.join(self.driver_dir, RELOAD_REQUEST)
         while not stop.is_set():
@@ -213,23 +250,31 @@ class DriverContainer:
                 continue
             try:
                 with open(req) as f:
-                    rid = (json.load(f) or {}).get("id", "")
+                    body = json.load(f) or {}
             except (OSError, ValueError):
-                rid = ""
+                body = {}
             try:
                 os.unlink(req)
             except FileNotFoundError:
                 pass
+            rid = body.get("id", "")
+            now = time.time()
+            ts, deadline = float(body.get("ts") or 0.0), float(body.get("deadline") or 0.0)
+            if ts < self.started or (deadline and deadline <= now):
+                why = "written before this driver container started" if ts < self.started else \
+                    "past the requester's deadline"
+                log.warning("ignoring stale reload request %s (%s)", rid, why)
+                self._answer({"id": rid, "ok": False, "stale": True, "error": f"stale request ignored: {why}"})
+                continue
             try:
-                res = {"id": rid, "ok": True, "info": self.reload()}
-            except DriverError as e:
+                res = {"id": rid, "ok": True, "info": self.reload(deadline - now if deadline else None)}
+            except Exception as e:  # noqa: BLE001 - the requester waits for an answer either way
                 log.error("reload failed: %s", e)
-                res = {"id": rid, "ok": False, "error": str(e)}
-            res["ts"] = time.time()
-            out = os.path.join(self.driver_dir, RELOAD_RESULT)
-            with open(out + ".tmp", "w") as f:
-                json.dump(res, f)
-            os.replace(out + ".tmp", out)
+                res = {"id": rid, "ok": False, "error": f"{type(e).__name__}: {e}"}
+            try:
+                self._answer(res)
+            except OSError as e:
+                log.error("could not write the reload result: %s", e)
 
     # -- readiness -----------------------------------------------------------------------------
     def ready(self) -> Tuple[bool, str]:
@@ -246,8 +291,8 @@ class DriverContainer:
             return False, f"{len(bound & agents)}/{len(bound)} GPUs enumerated by KFD"
         return True, f"{len(bound)} GPU(s), {st['kfd_gpu_nodes']} KFD agent(s)"
 
-    def wait_ready(self) -> str:
-        deadline = time.monotonic() + self.ready_timeout
+    def wait_ready(self, deadline: Optional[float] = None) -> str:
+        deadline = time.monotonic() + self.ready_timeout if deadline is None else deadline
         while True:
             ok, why = self.ready()
             if ok:

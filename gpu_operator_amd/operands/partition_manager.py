@@ -219,9 +219,32 @@ class PartitionManager:
         rid = uuid.uuid4().hex
         os.makedirs(self.driver_dir, exist_ok=True)
         req = os.path.join(self.driver_dir, RELOAD_REQUEST)
+        now = time.time()
+        # the deadline travels with the request: the driver container fits its unload / load /
+        # readiness wait into it, and ignores the request once it has passed
         with open(req + ".tmp", "w") as f:
-            json.dump({"id": rid, "node": self.node, "ts": time.time()}, f)
+            json.dump({"id": rid, "node": self.node, "ts": now, "deadline": now + self.reload_timeout}, f)
         os.replace(req + ".tmp", req)
+        try:
+            self._await_reload(rid)
+        except PartitionError:
+            self._withdraw_request(req, rid)
+            raise
+
+    @staticmethod
+    def _withdraw_request(req: str, rid: str) -> None:
+        """Remove our request if it is still unanswered: a driver container that (re)starts later
+        must not unload amdgpu for a request nobody waits for any more."""
+        try:
+            with open(req) as f:
+                if (json.load(f) or {}).get("id") != rid:
+                    return
+            os.unlink(req)
+        except (OSError, ValueError):
+            pass
+
+    def _await_reload(self, rid: str) -> None:
+        from .driver_container import RELOAD_RESULT
         res_path = os.path.join(self.driver_dir, RELOAD_RESULT)
         deadline = time.monotonic() + self.reload_timeout
         while True:

@@ -558,17 +558,27 @@ def _condition_true(values: Dict, condition: str) -> bool:
     return True
 
 
+def kube_version(version: str) -> Dict[str, str]:
+    """``.Capabilities.KubeVersion`` as Helm fills it: Version "v1.24.3", Major "1", Minor "24"; a
+    provider build ("v1.24.3+eks") reports Minor "24+", as EKS / GKE clusters do."""
+    plus = "+" in version
+    v = version.lstrip("v").split("-")[0].split("+")[0].split(".")
+    return {"Version": "v" + ".".join(v), "GitVersion": version, "Major": v[0],
+            "Minor": (v[1] if len(v) > 1 else "0") + ("+" if plus else "")}
+
+
 def render_chart(chart_dir: str, values: Optional[Dict] = None, release: str = "amd-gpu-operator",
-                 namespace: str = "amd-gpu-operator", prefix: str = "") -> Dict[str, str]:
+                 namespace: str = "amd-gpu-operator", prefix: str = "", kube: str = "v1.29.0") -> Dict[str, str]:
     """Render every template of a chart and of its enabled dependencies vendored under
     ``charts/<name>/`` (the subchart sees its own values.yaml merged with the parent's
-    ``<name>:`` section, as Helm does); returns {template path: rendered text}."""
+    ``<name>:`` section, as Helm does) for cluster version ``kube``; returns {template path:
+    rendered text}."""
     import os
     chart, base = _load_chart(chart_dir)
     vals = deep_merge(base, values or {})
     dot = {"Values": vals, "Release": {"Name": release, "Namespace": namespace, "Service": "Helm"},
            "Chart": {"Name": chart["name"], "Version": chart["version"], "AppVersion": chart.get("appVersion", "")},
-           "Capabilities": {"KubeVersion": {"Version": "v1.29.0"}}}
+           "Capabilities": {"KubeVersion": kube_version(kube)}}
     t = Template()
     tdir = os.path.join(chart_dir, "templates")
     names = sorted(os.listdir(tdir))
@@ -582,7 +592,7 @@ def render_chart(chart_dir: str, values: Optional[Dict] = None, release: str = "
         if not os.path.isdir(sub) or not _condition_true(vals, dep.get("condition", "")):
             continue
         out.update(render_chart(sub, vals.get(dep.get("alias") or dep["name"]) or {}, release, namespace,
-                                prefix=f"{prefix}charts/{dep['name']}/"))
+                                prefix=f"{prefix}charts/{dep['name']}/", kube=kube))
     return out
 
 

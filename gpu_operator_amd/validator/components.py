@@ -148,10 +148,20 @@ def validate_driver(ctx: Context) -> Dict[str, Any]:
                 raise ValidationError("timed out waiting for the driver container")
     info = retry(ctx, "driver", lambda: check_driver(ctx))
     info["mode"] = "host" if host else "container"
-    ctx.status.delete(S.DRIVER_READY)
-    ctx.status.delete(S.HOST_DRIVER_READY)
-    ctx.status.create(S.HOST_DRIVER_READY if host else S.DRIVER_READY, info)
+    name = S.HOST_DRIVER_READY if host else S.DRIVER_READY
+    ctx.status.delete(S.DRIVER_READY if host else S.HOST_DRIVER_READY)
+    _keep_first_ts(ctx, name, info)
+    ctx.status.create(name, info)
     return info
+
+
+def _keep_first_ts(ctx: Context, name: str, info: Dict[str, Any]) -> None:
+    """A re-validated barrier keeps the time the layer was first found ready (the start of node
+    time-to-ready) and records the re-check as ``revalidated_ts`` -- as amd-node-validate does."""
+    old = ctx.status.read(name)
+    if old and isinstance(old.get("ts"), (int, float)):
+        info["ts"] = old["ts"]
+        info["revalidated_ts"] = time.time()
 
 
 # ---------------------------------------------------------------------------------------------
@@ -525,7 +535,8 @@ def _run_local_hip(ctx: Context, floors: Optional[Dict[str, float]] = None,
     floors = floors or {}
     plan = plan or {"full": None, "probe": []}
     t0 = ctx.clock()
-    results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=False, run=ctx.run,
+    results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=ctx.env.get("GEMM_COUNTERS") == "1",
+                      run=ctx.run,
                       dtype=ctx.env.get("GEMM_DTYPE", "bf16"), scaling=ctx.env.get("GEMM_SCALING") or None,
                       iters=int(ctx.env.get("GEMM_ITERS", "50")),
                       min_tflops=floors.get("bf16", 0.0), min_tflops_fp8=floors.get("fp8", 0.0),

@@ -167,9 +167,13 @@ def _asset_script(state: str, fname: str) -> str:
 class Harness:
     def __init__(self, workdir: Optional[str] = None, sys_root: str = "/", dev_root: str = "/",
                  hip_mode: str = "local", gemm_shapes: str = "8192", timeout: float = 240.0,
-                 scenario: str = "host-driver"):
+                 scenario: str = "host-driver", hip_full: bool = False):
+        """``hip_full``: our validator's HIP check runs what the production pod runs (bf16 and fp8,
+        the 1/2/4/8 sweep, one rocprofv3 counter pass per dtype) instead of one bf16 shape."""
         if scenario not in ("host-driver", "driver-container"):
             raise ValueError(f"unknown scenario {scenario!r}")
+        self.hip_env = ({"GEMM_DTYPE": "both", "GEMM_SCALING": "1,2,4,8", "GEMM_COUNTERS": "1"} if hip_full
+                        else {})
         self.wd = workdir or tempfile.mkdtemp(prefix="amd-ttr-")
         self.sys_root, self.dev_root = sys_root, dev_root
         self.hip_mode, self.gemm_shapes, self.timeout, self.scenario = hip_mode, gemm_shapes, timeout, scenario
@@ -348,12 +352,17 @@ class Harness:
         """This framework's operand pods (gpu_operator_amd/assets, container workload)."""
         gate = ["amd-barrier-wait", "--dir", "/run/amd/validations", "--all", "toolkit-ready", "--timeout", "3600"]
         v = lambda comp, **e: Ctr(f"{comp}-validation", ["amd-validator"], dict({"COMPONENT": comp}, **e))  # noqa: E731
+        # as in the assets: the API-free checks are the static amd-node-validate, the rccl init
+        # container falls through to amd-validator when there is a fabric to prove
+        nv = lambda comp, **e: Ctr(f"{comp}-validation", ["amd-node-validate", comp], dict({"COMPONENT": comp}, **e))  # noqa: E731
+        rccl = Ctr("rccl-validation", ["sh", "-c", 'amd-node-validate rccl; rc=$?; [ "$rc" -eq 3 ] && exec amd-validator; '
+                                                   'exit "$rc"'], {"COMPONENT": "rccl"})
         pods = [
-            Pod("toolkit", [v("driver", WITH_WAIT="true")],
+            Pod("toolkit", [nv("driver", WITH_WAIT="true")],
                 [Ctr("amd-container-toolkit-ctr",
                      ["sh", "-c", self._map(_asset_script("state-container-toolkit", "0400_configmap.yaml"))])]),
-            Pod("validator", [v("driver", WITH_WAIT="true"), v("toolkit", WITH_WAIT="true"), v("hip"),
-                              v("plugin", WITH_WORKLOAD="false"), v("rccl")],
+            Pod("validator", [nv("driver", WITH_WAIT="true"), nv("toolkit", WITH_WAIT="true"), v("hip", **self.hip_env),
+                              v("plugin", WITH_WORKLOAD="false"), rccl],
                 [Ctr("amd-operator-validator", ["amd-validator", "--component", "ready"])], runtime_class=True),
             Pod("device-plugin", [Ctr("toolkit-validation", gate)],
                 [Ctr("amd-device-plugin", ["sh", "-c", self._map(_asset_script("state-device-plugin",
@@ -446,17 +455,26 @@ class Harness:
 
 
 def run_both(hip_mode: str = "local", gemm_shapes: str = "8192", sys_root: str = "/", dev_root: str = "/",
-             scenario: str = "host-driver", timeout: float = 240.0, keep: bool = False) -> Dict:
+             scenario: str = "host-driver", timeout: float = 240.0, keep: bool = False, full: bool = False) -> Dict:
+    """Our chain and the reference protocol in the same harness; ``full`` adds our chain once more
+    with the production HIP workload (bf16 + fp8, the scaling sweep, counters)."""
     h = Harness(sys_root=sys_root, dev_root=dev_root, hip_mode=hip_mode, gemm_shapes=gemm_shapes,
                 timeout=timeout, scenario=scenario)
     try:
         ours = h.run("ours")
         ref = h.run("reference")
+        hf = None
+        if full:
+            hf = Harness(workdir=os.path.join(h.wd, "full"), sys_root=sys_root, dev_root=dev_root, hip_mode=hip_mode,
+                         gemm_shapes=gemm_shapes, timeout=timeout, scenario=scenario, hip_full=True).run("ours")
     finally:
         if not keep:
             shutil.rmtree(h.wd, ignore_errors=True)
-    return {"agent_chain_time_to_ready_s": ours["time_to_ready_s"],
-            "reference_protocol_time_to_ready_s": ref["time_to_ready_s"], "ours": ours, "reference": ref}
+    out = {"agent_chain_time_to_ready_s": ours["time_to_ready_s"],
+           "reference_protocol_time_to_ready_s": ref["time_to_ready_s"], "ours": ours, "reference": ref}
+    if hf is not None:
+        out.update(agent_chain_full_time_to_ready_s=hf["time_to_ready_s"], ours_full=hf)
+    return out
 
 
 def main(argv=None) -> int:

@@ -1,0 +1,345 @@
+// amd-node-validate: the validator components that need no Kubernetes API, as one static binary.
+//
+//   amd-node-validate driver  [--with-wait] [--output-dir DIR] [--wait-timeout S]
+//   amd-node-validate toolkit [--with-wait] [--output-dir DIR] [--wait-timeout S]
+//   amd-node-validate rccl    [--output-dir DIR]
+//
+// The same checks and barrier payloads as validator/components.py (validate_driver,
+// validate_toolkit, the no-fabric branch of validate_rccl), without a Python interpreter on the
+// node bring-up's critical path: each of these init containers starts, checks sysfs and writes its
+// barrier in milliseconds (reference: validator/main.go:607-679 driver, :775-801 toolkit). The
+// components that talk to the API server (hip, plugin, the fabric pod) stay in `amd-validator`.
+//
+// rccl: a node with fewer than 2 physical GPUs (KFD agents grouped by PCI function) has no fabric;
+// rccl-ready is written with a skip. With 2 or more (or none enumerated, where the validator reads
+// the node's labels) it exits 3 without writing anything: the init container then execs
+// `amd-validator`, which plans and runs the fabric pod.
+//
+// Environment (the validator's names): WITH_WAIT, OUTPUT_DIR, WAIT_TIMEOUT_SECONDS,
+// SLEEP_INTERVAL_SECONDS, AMD_SYSFS_ROOT, AMD_DEV_ROOT, HOST_ROOT, DRIVER_ROOT_MODE (host |
+// container), DRIVER_VALIDATION_STRICT, AMD_MOUNTS (process-level node harnesses: container path ->
+// host path pairs, utils/mounts.py). Exit 0 ok, 1 validation failed, 2 usage, 3 not handled here.
+//
+// A barrier that already exists with the same name keeps its first `ts` (when the layer was first
+// found ready -- the start of node time-to-ready) and gets `revalidated_ts`: a validator restart
+// re-checks the driver without moving the moment it became ready.
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <dirent.h>
+#include <fstream>
+#include <set>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "amdnode.h"
+#include "minijson.h"
+
+namespace {
+
+using minijson::Value;
+
+std::string env(const char* k, const std::string& dflt = "") {
+  const char* v = std::getenv(k);
+  return v ? std::string(v) : dflt;
+}
+
+bool truthy(const std::string& v) {
+  std::string s = v;
+  std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+  return s == "1" || s == "true" || s == "yes" || s == "on";
+}
+
+bool exists(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0;
+}
+
+// utils/mounts.py: AMD_MOUNTS maps container paths to where this process finds them; unset in a
+// real container (identity).
+std::string mount_path(const std::string& p) {
+  static std::vector<std::pair<std::string, std::string>> pairs = [] {
+    std::vector<std::pair<std::string, std::string>> out;
+    const std::string raw = env("AMD_MOUNTS");
+    if (raw.empty()) return out;
+    try {
+      const Value v = minijson::parse(raw);
+      for (const auto& pr : v.a) {
+        if (pr.a.size() != 2) continue;
+        std::string c = pr.a[0].str();
+        while (c.size() > 1 && c.back() == '/') c.pop_back();
+        if (c.empty() || c[0] != '/') c = "/" + c;
+        out.emplace_back(c, pr.a[1].str());
+      }
+    } catch (const std::exception&) {
+    }
+    std::stable_sort(out.begin(), out.end(), [](const auto& a, const auto& b) { return a.first.size() > b.first.size(); });
+    return out;
+  }();
+  if (p.empty() || p[0] != '/') return p;
+  for (const auto& [c, h] : pairs) {
+    if (c == "/") return p == "/" ? h : (h.back() == '/' ? h : h + "/") + p.substr(1);
+    if (p == c) return h;
+    if (p.compare(0, c.size() + 1, c + "/") == 0) {
+      std::string base = h;
+      while (base.size() > 1 && base.back() == '/') base.pop_back();
+      return base + p.substr(c.size());
+    }
+  }
+  return p;
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+std::string num(double v) {
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "%.6f", v);
+  return buf;
+}
+
+Value strings(const std::set<std::string>& xs) {
+  Value a = Value::array();
+  for (const auto& x : xs) a.push(Value::string(x));
+  return a;
+}
+
+class ValidationError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+struct Opts {
+  std::string component, out_dir, sys_root, dev_root, host_root;
+  bool with_wait = false;
+  double wait_timeout = 3600, sleep_interval = 5;
+};
+
+// Atomic barrier write (tmp + rename, like validator/status.py), keeping an existing barrier's `ts`.
+void write_barrier(const Opts& o, const std::string& name, Value info) {
+  ::mkdir(o.out_dir.c_str(), 0755);
+  const std::string path = o.out_dir + "/" + name;
+  const double t = now_s();
+  std::string first;
+  {
+    std::ifstream f(path);
+    if (f) {
+      std::stringstream ss;
+      ss << f.rdbuf();
+      try {
+        const Value old = minijson::parse(ss.str());
+        if (const Value* ts = old.find("ts"); ts && ts->kind == Value::Number) first = ts->s;
+      } catch (const std::exception&) {
+      }
+    }
+  }
+  if (!first.empty()) {
+    info["ts"] = Value::number_text(first);
+    info["revalidated_ts"] = Value::number_text(num(t));
+  } else {
+    info["ts"] = Value::number_text(num(t));
+  }
+  info["validator"] = Value::string("native");
+  const std::string tmp = o.out_dir + "/." + name + ".tmp." + std::to_string(::getpid());
+  {
+    std::ofstream f(tmp);
+    f << minijson::dump(info);
+  }
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) throw ValidationError("cannot write barrier " + path);
+}
+
+void remove_barrier(const Opts& o, const std::string& name) { ::unlink((o.out_dir + "/" + name).c_str()); }
+
+// retry() of components.py: once, or (with-wait) until the check passes or the wait is over.
+template <typename F>
+Value retry(const Opts& o, const char* what, F check) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(o.wait_timeout);
+  double delay = 0.2;
+  for (;;) {
+    try {
+      return check();
+    } catch (const ValidationError& e) {
+      if (!o.with_wait || std::chrono::steady_clock::now() >= deadline) throw;
+      std::fprintf(stderr, "%s not ready (%s); retrying in %.1fs\n", what, e.what(), delay);
+      std::this_thread::sleep_for(std::chrono::duration<double>(delay));
+      delay = std::min(o.sleep_interval, delay * 2);
+    }
+  }
+}
+
+// --- driver (components.validate_driver) ----------------------------------------------------
+bool host_driver_installed(const Opts& o) {
+  const std::string mode = env("DRIVER_ROOT_MODE");
+  if (!mode.empty()) return mode == "host";
+  for (const char* m : {"/usr/bin/amd-smi", "/opt/rocm/bin/amd-smi", "/usr/sbin/amdgpu-install"})
+    if (exists(o.host_root + m)) return true;
+  return false;
+}
+
+Value check_driver(const Opts& o) {
+  const auto st = amdnode::driver_state(o.sys_root, o.dev_root);
+  if (!st.module_loaded) throw ValidationError("amdgpu module not loaded");
+  if (!st.live) throw ValidationError("amdgpu initstate is not live");
+  if (!st.kfd_present) throw ValidationError("/dev/kfd missing");
+  if (st.kfd_gpu_nodes == 0) throw ValidationError("KFD reports no GPU agents");
+  const auto gpus = amdnode::enumerate_gpus(o.sys_root);
+  std::set<std::string> bound, gfx, products;
+  for (const auto& g : gpus) {
+    bound.insert(g.pci_bdf);
+    gfx.insert(g.gfx_target);
+    if (!g.product_name.empty()) products.insert(g.product_name);
+  }
+  std::vector<std::string> missing;
+  for (const auto& f : amdnode::scan_pci(o.sys_root))
+    if (!f.is_virtfn && f.driver == "amdgpu" && !bound.count(f.bdf)) missing.push_back(f.bdf);
+  if (!missing.empty() && env("DRIVER_VALIDATION_STRICT", "true") == "true") {
+    std::string m;
+    for (const auto& b : missing) m += (m.empty() ? "" : ", ") + b;
+    throw ValidationError("amdgpu-bound GPUs without a KFD agent: [" + m + "]");
+  }
+  Value info = Value::object();
+  info["driver_version"] = Value::string(st.version.empty() ? "inbox" : st.version);
+  info["gpus"] = Value::number((long long)bound.size());
+  info["kfd_agents"] = Value::number(st.kfd_gpu_nodes);
+  info["gfx"] = strings(gfx);
+  info["hidden_gpus"] = Value::number((long long)missing.size());
+  info["products"] = strings(products);
+  return info;
+}
+
+Value validate_driver(const Opts& o) {
+  const bool host = host_driver_installed(o);
+  if (!host && !exists(o.out_dir + "/.driver-ctr-ready")) {
+    // the driver container's startup probe writes .driver-ctr-ready once amdgpu is live
+    if (!o.with_wait) throw ValidationError("driver container not ready (.driver-ctr-ready missing)");
+    if (amdnode::wait_files(o.out_dir, {".driver-ctr-ready"}, false, (int64_t)(o.wait_timeout * 1000)).empty())
+      throw ValidationError("timed out waiting for the driver container");
+  }
+  Value info = retry(o, "driver", [&] { return check_driver(o); });
+  info["mode"] = Value::string(host ? "host" : "container");
+  const std::string name = host ? "host-driver-ready" : "driver-ready";
+  remove_barrier(o, host ? "driver-ready" : "host-driver-ready");
+  write_barrier(o, name, info);
+  return info;
+}
+
+// --- toolkit (components.validate_toolkit) --------------------------------------------------
+Value check_toolkit(const Opts& o) {
+  if (!exists(amdnode::join(o.dev_root, "/dev/kfd"))) throw ValidationError("/dev/kfd not injected into the container");
+  std::set<std::string> render;
+  if (DIR* d = ::opendir(amdnode::join(o.dev_root, "/dev/dri").c_str())) {
+    while (dirent* e = ::readdir(d))
+      if (std::strncmp(e->d_name, "renderD", 7) == 0) render.insert(e->d_name);
+    ::closedir(d);
+  }
+  std::set<std::string> missing;
+  for (const auto& g : amdnode::enumerate_gpus(o.sys_root))
+    if (g.drm_render_minor >= 0 && !render.count("renderD" + std::to_string(g.drm_render_minor)))
+      missing.insert("renderD" + std::to_string(g.drm_render_minor));
+  if (!missing.empty()) {
+    std::string m;
+    for (const auto& x : missing) m += (m.empty() ? "'" : ", '") + x + "'";
+    throw ValidationError("render nodes not injected: [" + m + "]");
+  }
+  Value info = Value::object();
+  info["render_nodes"] = Value::number((long long)render.size());
+  info["kfd"] = Value::boolean(true);
+  return info;
+}
+
+Value validate_toolkit(const Opts& o) {
+  Value info = retry(o, "toolkit", [&] { return check_toolkit(o); });
+  write_barrier(o, "toolkit-ready", info);
+  return info;
+}
+
+// --- rccl without a fabric (components.validate_rccl, ngpu < 2) -----------------------------
+constexpr int kNotHandled = 3;
+
+Value validate_rccl(const Opts& o, int& rc) {
+  std::set<std::string> phys;
+  for (const auto& g : amdnode::enumerate_gpus(o.sys_root)) phys.insert(g.pci_bdf);
+  const int n = (int)phys.size();
+  if (n == 0 || n >= 2) {
+    rc = kNotHandled;   // a fabric to prove (or no sysfs view): amd-validator plans the pod
+    Value v = Value::object();
+    v["physical_gpus"] = Value::number(n);
+    v["handled"] = Value::boolean(false);
+    return v;
+  }
+  Value info = Value::object();
+  info["skipped"] = Value::string(std::to_string(n) + " physical GPU(s): no fabric to validate");
+  info["ok"] = Value::boolean(true);
+  write_barrier(o, "rccl-ready", info);
+  return info;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Opts o;
+  o.component = env("COMPONENT");
+  o.with_wait = truthy(env("WITH_WAIT", "false"));
+  o.out_dir = env("OUTPUT_DIR", mount_path("/run/amd/validations"));
+  o.sys_root = env("AMD_SYSFS_ROOT", "/");
+  o.dev_root = env("AMD_DEV_ROOT", "/");
+  o.host_root = env("HOST_ROOT", mount_path("/host"));
+  o.wait_timeout = std::atof(env("WAIT_TIMEOUT_SECONDS", "3600").c_str());
+  o.sleep_interval = std::atof(env("SLEEP_INTERVAL_SECONDS", "5").c_str());
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", a.c_str());
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--with-wait") o.with_wait = true;
+    else if (a == "--output-dir") o.out_dir = next();
+    else if (a == "--wait-timeout") o.wait_timeout = std::atof(next().c_str());
+    else if (a == "--sys-root") o.sys_root = next();
+    else if (a == "--dev-root") o.dev_root = next();
+    else if (a == "--host-root") o.host_root = next();
+    else if (a == "-h" || a == "--help") {
+      std::printf("usage: amd-node-validate driver|toolkit|rccl [--with-wait] [--output-dir DIR] [--wait-timeout S]\n");
+      return 0;
+    } else if (a[0] != '-') o.component = a;
+    else {
+      std::fprintf(stderr, "unknown argument %s\n", a.c_str());
+      return 2;
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = 0;
+  Value info;
+  try {
+    if (o.component == "driver") info = validate_driver(o);
+    else if (o.component == "toolkit") info = validate_toolkit(o);
+    else if (o.component == "rccl") info = validate_rccl(o, rc);
+    else {
+      std::fprintf(stderr, "amd-node-validate: component '%s' needs amd-validator\n", o.component.c_str());
+      return kNotHandled;
+    }
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "error validating %s: %s\n", o.component.c_str(), e.what());
+    return 1;
+  }
+  if (rc == kNotHandled) return rc;
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  Value line = Value::object();
+  line["component"] = Value::string(o.component);
+  line["ok"] = Value::boolean(true);
+  line["seconds"] = Value::number_text(num(dt));
+  line["info"] = info;
+  std::printf("%s\n", minijson::dump(line).c_str());
+  return 0;
+}

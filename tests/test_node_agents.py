@@ -472,6 +472,86 @@ def test_partition_driver_container_reload_timeout_fails(spx, cfg, tmp_path):
     assert m.reconcile() == "failed"
     msg = [e for e in c.events if e["reason"] == "PartitionFailed"][0]["message"]
     assert "did not answer reload request" in msg
+    # the unanswered request is withdrawn -- a driver container starting later must not
+    # unload amdgpu for it
+    assert not (tmp_path / "driver" / "reload-request").exists()
+
+
+def _driver_container(tmp_path, spx, run, **kw):
+    from gpu_operator_amd.operands import driver_container as dcm
+    return dcm.DriverContainer(sys_root=spx, dev_root=spx, image_root=str(tmp_path / "image"),
+                               host_etc=str(tmp_path / "etc"), run_dir=str(tmp_path / "run"),
+                               firmware_dir=str(tmp_path / "fw"), params_file=str(tmp_path / "none.conf"),
+                               kernel="6.8.0-45-generic", run=run, ready_timeout=3.0, **kw)
+
+
+def _serve_once(dc, timeout=5.0):
+    import threading
+    from gpu_operator_amd.operands import driver_container as dcm
+    res = os.path.join(dc.driver_dir, dcm.RELOAD_RESULT)
+    if os.path.exists(res):
+        os.unlink(res)
+    stop = threading.Event()
+    t = threading.Thread(target=dc.serve_reloads, args=(stop, 0.1), daemon=True)
+    t.start()
+    deadline = time.monotonic() + timeout
+    while not os.path.exists(res) and time.monotonic() < deadline:
+        time.sleep(0.05)
+    stop.set()
+    t.join(5)
+    return json.loads(open(res).read())
+
+
+def test_driver_container_ignores_a_stale_reload_request(spx, tmp_path):
+    """a request left from before this container started (its requester timed out, or
+    the manager restarted) is answered stale and never unloads the driver."""
+    calls = []
+    dc = _driver_container(tmp_path, spx, lambda argv, **kw: calls.append(argv))
+    os.makedirs(dc.driver_dir, exist_ok=True)
+    with open(os.path.join(dc.driver_dir, "reload-request"), "w") as f:
+        json.dump({"id": "old", "ts": dc.started - 60, "deadline": dc.started + 540}, f)
+    res = _serve_once(dc)
+    assert res["id"] == "old" and res["stale"] and not res["ok"] and calls == []
+    # ... and one whose requester's deadline has passed
+    with open(os.path.join(dc.driver_dir, "reload-request"), "w") as f:
+        json.dump({"id": "late", "ts": time.time(), "deadline": time.time() - 1}, f)
+    res = _serve_once(dc)
+    assert res["id"] == "late" and res["stale"] and calls == []
+
+
+def test_driver_container_reload_never_rebuilds_and_always_answers(spx, tmp_path):
+    """a DKMS reload is modprobe -r / modprobe (no `dkms install` under a 1800 s timeout),
+    bounded by the request's deadline; an unexpected exception still writes a result."""
+    import subprocess as sp
+    calls = []
+
+    def run(argv, timeout=None, **kw):
+        calls.append((argv, timeout))
+        return sp.CompletedProcess(argv, 0, "", "")
+    dc = _driver_container(tmp_path, spx, run, driver_version="6.12.12")
+    os.makedirs(dc.driver_dir, exist_ok=True)
+    now = time.time()
+    with open(os.path.join(dc.driver_dir, "reload-request"), "w") as f:
+        json.dump({"id": "r1", "ts": now, "deadline": now + 30}, f)
+    res = _serve_once(dc)
+    assert res["id"] == "r1" and res["ok"], res
+    assert [c[0][:2] for c in calls] == [["modprobe", "-r"], ["modprobe", "amdgpu"]]
+    assert all(c[1] <= 30 for c in calls)                      # within the requester's deadline
+
+    def boom(argv, **kw):
+        raise sp.TimeoutExpired(argv, 1)
+    dc2 = _driver_container(tmp_path, spx, boom, driver_version="6.12.12")
+    with open(os.path.join(dc2.driver_dir, "reload-request"), "w") as f:
+        json.dump({"id": "r2", "ts": time.time(), "deadline": time.time() + 30}, f)
+    res = _serve_once(dc2)
+    assert res["id"] == "r2" and not res["ok"] and "did not finish" in res["error"]
+
+
+def test_partition_entrypoint_drops_the_driver_container_reload_on_a_host_driver():
+    text = open(os.path.join(os.path.dirname(pm.__file__), "..", "assets", "state-partition-manager",
+                             "0420_configmap.yaml")).read()
+    host = text[text.index("host-driver-ready ]; then"):text.index("else")]
+    assert "unset DRIVER_RELOAD_VIA" in host
 
 
 def test_metrics_device_level_series_once_per_physical_gpu_under_cpx(tmp_path):

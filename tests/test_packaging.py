@@ -271,3 +271,21 @@ def test_operator_scc_renders_only_on_openshift():
     scc = k["SecurityContextConstraints"][0]
     assert scc["readOnlyRootFilesystem"] and not scc["allowPrivilegedContainer"] and not scc["allowHostPID"]
     assert scc["users"] == ["system:serviceaccount:amd-gpu-operator:amd-gpu-operator"]
+
+
+def test_operator_psp_renders_only_below_kubernetes_1_25():
+    """The operator pod's restricted PodSecurityPolicy (reference:
+    deployments/gpu-operator/templates/podsecuritypolicy.yaml): only with psp.enabled and on a
+    cluster older than 1.25, where policy/v1beta1 still exists."""
+    on = {"psp": {"enabled": True}}
+    k = _by_kind(gt.render_objects(CHART, on, kube="v1.24.3"))
+    psp = k["PodSecurityPolicy"][0]
+    assert psp["apiVersion"] == "policy/v1beta1" and psp["metadata"]["name"] == "amd-gpu-operator-restricted"
+    sp = psp["spec"]
+    assert not sp["privileged"] and not sp["hostPID"] and not sp["hostNetwork"] and sp["readOnlyRootFilesystem"]
+    assert sp["requiredDropCapabilities"] == ["ALL"] and "hostPath" not in sp["volumes"]
+    assert gt.kube_version("v1.24.3+eks")["Minor"] == "24+"
+    assert "PodSecurityPolicy" in _by_kind(gt.render_objects(CHART, on, kube="v1.24.3+eks"))   # "24+" minors
+    assert "PodSecurityPolicy" not in _by_kind(gt.render_objects(CHART, on, kube="v1.25.0"))
+    assert "PodSecurityPolicy" not in _by_kind(gt.render_objects(CHART, on))               # default v1.29
+    assert "PodSecurityPolicy" not in _by_kind(gt.render_objects(CHART, {}, kube="v1.24.3"))
