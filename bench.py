@@ -383,21 +383,25 @@ def _fp8_extra(ctx):
 def _time_to_ready_extra():
     """Node time-to-ready on real processes (validator/ttr.py), outside the timed region: this
     framework's operand chain vs the reference's protocol constants executed in the same
-    harness (host driver, HIP GEMM validation on this GPU)."""
+    harness (host driver, HIP GEMM validation on this GPU), plus our chain once more with the
+    production HIP workload (bf16 + fp8, the 1/2/4/8 sweep, rocprofv3 counters: what the validator's
+    HIP pod runs)."""
     try:
         from gpu_operator_amd.validator import ttr
-        r = ttr.run_both(hip_mode="local", gemm_shapes="8192", timeout=180)
+        r = ttr.run_both(hip_mode="local", gemm_shapes="8192", timeout=180, full=True)
     except Exception as e:  # noqa: BLE001 - an extra must never fail the bench
         return {"time_to_ready_error": str(e)[:300]}
     ours, ref = r["ours"], r["reference"]
     out = {"agent_chain_time_to_ready_s": r["agent_chain_time_to_ready_s"],
            "reference_protocol_time_to_ready_s": r["reference_protocol_time_to_ready_s"],
+           "agent_chain_full_time_to_ready_s": r.get("agent_chain_full_time_to_ready_s"),
            "time_to_ready_barriers_s": ours["barriers_s"],
+           "time_to_ready_full_barriers_s": (r.get("ours_full") or {}).get("barriers_s"),
            "reference_protocol_barriers_s": ref["barriers_s"]}
     if out["agent_chain_time_to_ready_s"] and out["reference_protocol_time_to_ready_s"]:
         out["time_to_ready_speedup"] = round(out["reference_protocol_time_to_ready_s"]
                                              / out["agent_chain_time_to_ready_s"], 2)
-    errs = ours["errors"] + ref["errors"]
+    errs = ours["errors"] + ref["errors"] + (r.get("ours_full") or {}).get("errors", [])
     if errs:
         out["time_to_ready_errors"] = "; ".join(errs)[:300]
     return out

@@ -1,20 +1,29 @@
-"""Kubernetes API client over HTTPS (``requests``), in-cluster or from a kubeconfig.
+"""Kubernetes API client over HTTPS, in-cluster or from a kubeconfig.
 
 Implements the :class:`~gpu_operator_amd.k8s.client.Client` protocol: discovery-based
 kind->resource mapping, CRUD, status subresource, merge patches, the pods/eviction
 subresource, events and list+watch streams with resourceVersion resume.
+
+The transport is the standard library's ``http.client`` with one keep-alive connection per
+thread (a watch stream gets its own): every node agent and validator component builds this
+client at start-up, and importing ``requests`` alone cost ~0.1 s of interpreter start per
+process on the node bring-up's critical path.
 """
 
 from __future__ import annotations
 
 import base64
+import http.client
 import json
 import logging
 import os
+import socket
+import ssl
 import tempfile
 import threading
 import time
-from typing import Any, Callable, Dict, List, Optional, Tuple
+import urllib.parse
+from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
 import yaml
 
@@ -88,16 +97,106 @@ class Config:
         return cls.from_kubeconfig()
 
 
+class Response:
+    """What the client reads back: status, body (or, streamed, the open response)."""
+
+    def __init__(self, status: int, body: bytes = b"", stream: Optional[http.client.HTTPResponse] = None,
+                 conn: Optional[http.client.HTTPConnection] = None):
+        self.status_code = status
+        self.content = body
+        self._stream, self._conn = stream, conn
+
+    @property
+    def text(self) -> str:
+        return self.content.decode("utf-8", errors="replace")
+
+    def json(self) -> Any:
+        return json.loads(self.content)
+
+    def iter_lines(self) -> Iterator[bytes]:
+        """Lines of a streamed (chunked) response as they arrive; closes the connection at the end."""
+        try:
+            while True:
+                line = self._stream.readline()
+                if not line:
+                    return
+                yield line.rstrip(b"\r\n")
+        finally:
+            self.close()
+
+    def close(self) -> None:
+        if self._conn is not None:
+            self._conn.close()
+            self._conn = None
+
+
+class _Transport:
+    """HTTP(S) to one API server: a keep-alive connection per thread, TLS from the config (CA,
+    client certificate, or no verification when the kubeconfig says insecure-skip-tls-verify)."""
+
+    def __init__(self, cfg: "Config"):
+        u = urllib.parse.urlsplit(cfg.host)
+        self.https = u.scheme == "https"
+        self.host, self.port = u.hostname or "localhost", u.port or (443 if self.https else 80)
+        self.prefix = u.path.rstrip("/")
+        self.ctx: Optional[ssl.SSLContext] = None
+        if self.https:
+            if cfg.verify:
+                self.ctx = ssl.create_default_context(cafile=cfg.ca_file) if cfg.ca_file else \
+                    ssl.create_default_context()
+            else:
+                self.ctx = ssl._create_unverified_context()   # noqa: S323 - the kubeconfig asked for it
+            if cfg.cert_file:
+                self.ctx.load_cert_chain(cfg.cert_file, cfg.key_file)
+        self._local = threading.local()
+
+    def _new(self, timeout: float) -> http.client.HTTPConnection:
+        if self.https:
+            return http.client.HTTPSConnection(self.host, self.port, timeout=timeout, context=self.ctx)
+        return http.client.HTTPConnection(self.host, self.port, timeout=timeout)
+
+    def request(self, method: str, path: str, body: Optional[bytes], headers: Dict[str, str], timeout: float,
+                stream: bool = False) -> Response:
+        path = self.prefix + path
+        if stream:                                   # a watch: its own connection, closed after
+            conn = self._new(timeout)
+            conn.request(method, path, body=body, headers=headers)
+            r = conn.getresponse()
+            if r.status >= 400:
+                data = r.read()
+                conn.close()
+                return Response(r.status, data)
+            return Response(r.status, stream=r, conn=conn)
+        for attempt in (0, 1):
+            conn = getattr(self._local, "conn", None)
+            fresh = conn is None
+            if fresh:
+                conn = self._local.conn = self._new(timeout)
+            conn.timeout = timeout
+            if conn.sock is not None:
+                conn.sock.settimeout(timeout)
+            try:
+                conn.request(method, path, body=body, headers=headers)
+                r = conn.getresponse()
+                data = r.read()
+                if r.will_close:
+                    conn.close()
+                    self._local.conn = None
+                return Response(r.status, data)
+            except (http.client.HTTPException, ConnectionError, BrokenPipeError, socket.timeout, OSError):
+                conn.close()
+                self._local.conn = None
+                # a kept-alive connection the server closed: retry once on a new one
+                if fresh or attempt == 1:
+                    raise
+        raise RuntimeError("unreachable")
+
+
 class RestClient:
     def __init__(self, config: Optional[Config] = None, timeout: float = 30.0):
-        import requests
-
         self.cfg = config or Config.auto()
         self.timeout = timeout
-        self.session = requests.Session()
-        if self.cfg.cert_file:
-            self.session.cert = (self.cfg.cert_file, self.cfg.key_file)
-        self.session.verify = self.cfg.ca_file if (self.cfg.verify and self.cfg.ca_file) else self.cfg.verify
+        self._http = _Transport(self.cfg)
         self._resources: Dict[str, Dict[str, Tuple[str, bool]]] = {}
         self._lock = threading.Lock()
 
@@ -110,12 +209,14 @@ class RestClient:
         return h
 
     def _request(self, method: str, path: str, body: Any = None, params: Optional[Dict[str, Any]] = None,
-                 content_type: str = "application/json", stream: bool = False, timeout=None):
-        url = self.cfg.host + path
-        data = json.dumps(body) if body is not None else None
-        r = self.session.request(method, url, data=data, params=params, stream=stream,
-                                 headers=self._headers(content_type),
-                                 timeout=timeout if timeout is not None else self.timeout)
+                 content_type: str = "application/json", stream: bool = False, timeout=None) -> Response:
+        if params:
+            path += "?" + urllib.parse.urlencode(params)
+        data = json.dumps(body).encode() if body is not None else None
+        to = timeout if timeout is not None else self.timeout
+        if isinstance(to, tuple):                     # (connect, read): one socket timeout, the read one
+            to = to[-1]
+        r = self._http.request(method, path, data, self._headers(content_type), to, stream=stream)
         if r.status_code >= 400:
             try:
                 st = r.json()
@@ -269,9 +370,8 @@ class RestClient:
                                       params={"watch": "1", "resourceVersion": rv,
                                               "allowWatchBookmarks": "true", "timeoutSeconds": "300", **sel},
                                       stream=True, timeout=(10, 330))
-                    # chunk_size=None: yield each chunk as it arrives (the API server sends one
-                    # event per chunk); a fixed size would hold small events back
-                    for line in r.iter_lines(chunk_size=None):
+                    # one JSON event per line, read as each arrives
+                    for line in r.iter_lines():
                         if stop.is_set():
                             break
                         if not line:

@@ -175,11 +175,9 @@ def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
                           amd_visible_devices=os.environ.get("AMD_VISIBLE_DEVICES"))
         return results
     full = devices is None or len(devices) > 0
-    smoke_on = devices if full else (probe_devices or [])[:1]
-    rc, r = run_json([binary("amd-hip-smoke")], run, visible=smoke_on if smoke_on else None)
-    results += r or [{"event": "hip-smoke", "ok": False, "rc": rc}]
+    # hip-smoke runs inside the first GEMM process (--smoke: one HIP runtime start, not two)
     if full:
-        cmd = [binary("amd-gemm-validate"), "--shapes", ",".join(shapes), "--iters", str(iters)]
+        cmd = [binary("amd-gemm-validate"), "--smoke", "--shapes", ",".join(shapes), "--iters", str(iters)]
         if dtype != "bf16":
             cmd += ["--dtype", dtype]
         if scaling:
@@ -193,16 +191,17 @@ def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
         if min_efficiency:
             cmd += ["--min-efficiency", f"{min_efficiency:g}"]
         rc, r = run_json(cmd, run, timeout=1200, visible=devices)
-        results += r
+        results += r or [{"event": "hip-smoke", "ok": False, "rc": rc}]
         if rc != 0 and not any(x.get("event") == "gemm" for x in r):
             results.append({"event": "gemm", "ok": False, "rc": rc})
     if probe_devices:
         cmd = [binary("amd-gemm-validate"), "--shapes", PROBE_SHAPE, "--dtype", "bf16", "--iters", "3",
-               "--warmup", "1", "--no-stabilise", "--check-rows", "16"]
+               "--warmup", "1", "--no-stabilise", "--check-rows", "16"] + ([] if full else ["--smoke"])
         rc, r = run_json(cmd, run, timeout=120, visible=probe_devices)
         for x in r:
-            x["probe"] = True
-        results += [x for x in r if x.get("event") in ("gemm", "start") or "error" in x]
+            if x.get("event") != "hip-smoke":
+                x["probe"] = True
+        results += [x for x in r if x.get("event") in ("gemm", "start", "hip-smoke") or "error" in x]
         if rc != 0 and not any(x.get("event") == "gemm" for x in r):
             results.append({"event": "gemm", "probe": True, "ok": False, "rc": rc})
     if counters and full:

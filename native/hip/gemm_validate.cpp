@@ -40,7 +40,11 @@
 //   amd-gemm-validate [--shapes 8192,4096,16384x16384x1024] [--dtype bf16|fp8|both] [--iters 50]
 //                     [--warmup 5] [--devices all|0,1,...] [--scaling 1,2,4,8] [--check-rows 32]
 //                     [--min-tflops X] [--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R]
-//                     [--stabilise-max-s 6] [--no-stabilise]
+//                     [--stabilise-max-s 6] [--no-stabilise] [--smoke]
+//
+// --smoke first runs hip-smoke (smoke.hip: the vectorAdd analogue, every element checked on the
+// host) on each selected GPU in this process and prints its `hip-smoke` line -- one HIP runtime
+// start for both checks on the validator's critical path instead of two processes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -67,6 +71,36 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
 int amdgo_gemm_fp8_ref_rows(const void* A, const void* Bt, const int* rows, int nrows, float* out, int N,
                             int K, void* stream);
 int amdgo_fill_uniform_fp8(void* p, size_t n, uint32_t seed, void* stream);
+int amdgo_vector_add_f32(const float* a, const float* b, float* c, size_t n, void* stream);
+}
+
+// hip-smoke on each device (the amd-hip-smoke binary's check, in this process): fp32 C = A + B over
+// 50,000 elements, every element verified on the host.
+static bool smoke(const std::vector<int>& devs) {
+  constexpr size_t n = 50000;
+  std::vector<float> a(n), b(n), c(n);
+  for (size_t i = 0; i < n; ++i) {
+    a[i] = (float)(i % 1000) / 7.0f;
+    b[i] = (float)((i * 7) % 1000) / 13.0f;
+  }
+  int failures = 0;
+  for (int d : devs) {
+    float *da = nullptr, *db = nullptr, *dc = nullptr;
+    bool ok = hipSetDevice(d) == hipSuccess && hipMalloc(&da, n * 4) == hipSuccess &&
+              hipMalloc(&db, n * 4) == hipSuccess && hipMalloc(&dc, n * 4) == hipSuccess &&
+              hipMemcpy(da, a.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(db, b.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+              amdgo_vector_add_f32(da, db, dc, n, nullptr) == 0 &&
+              hipMemcpy(c.data(), dc, n * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    for (size_t i = 0; ok && i < n; ++i) ok = c[i] == a[i] + b[i];
+    for (float* p : {da, db, dc})
+      if (p) (void)hipFree(p);
+    failures += !ok;
+  }
+  std::printf("{\"event\":\"hip-smoke\",\"devices\":%zu,\"elements\":%zu,\"ok\":%s}\n", devs.size(), n,
+              failures ? "false" : "true");
+  std::fflush(stdout);
+  return failures == 0;
 }
 
 // One operand precision: element size plus its GEMM, reference and fill entry points.
@@ -392,6 +426,7 @@ int main(int argc, char** argv) {
   std::string shapes = "8192", devices = "all", dtype = "bf16", scaling;
   Options o;
   double min_tflops = 0, min_tflops_fp8 = 0, min_eff = 0, min_rel = 0;
+  bool run_smoke = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -408,10 +443,12 @@ int main(int argc, char** argv) {
     else if (a == "--min-relative") min_rel = std::atof(next().c_str());
     else if (a == "--stabilise-max-s") o.stabilise_max_s = std::atof(next().c_str());
     else if (a == "--no-stabilise") o.stabilise = false;
+    else if (a == "--smoke") run_smoke = true;
     else if (a == "-h" || a == "--help") {
       std::printf("usage: amd-gemm-validate [--shapes 8192,4096,MxNxK] [--dtype bf16|fp8|both] [--iters N] "
                   "[--warmup N] [--devices all|0,1] [--scaling 1,2,4,8] [--check-rows N] [--min-tflops X] "
-                  "[--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R] [--stabilise-max-s S] [--no-stabilise]\n");
+                  "[--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R] [--stabilise-max-s S] [--no-stabilise] "
+                  "[--smoke]\n");
       return 0;
     } else {
       std::printf("{\"error\":\"unknown argument %s\"}\n", a.c_str());
@@ -459,6 +496,7 @@ int main(int argc, char** argv) {
               devs.size(), ndev, prop.gcnArchName, prop.multiProcessorCount, (size_t)prop.sharedMemPerBlock,
               o.iters, o.stabilise ? "true" : "false");
   bool all_ok = true;
+  if (run_smoke) all_ok = smoke(devs);
   const std::vector<int> counts = parse_ints(scaling);
   for (const DType* dt : dtypes) {
     const double floor = dt == &kFp8 ? min_tflops_fp8 : min_tflops;

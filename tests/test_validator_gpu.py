@@ -215,3 +215,10 @@ def test_rccl_watchdog_reports_a_missing_peer(tmp_path):
     assert rc == 124, (rc, lines, err[-2000:])
     t = [x for x in lines if x.get("event") == "timeout"][0]
     assert t["phase"] == "init" and t["ranks"] == 2 and t["rank"] == 0 and t["timeout_s"] == 5.0
+
+
+def test_gemm_validate_runs_hip_smoke_in_process():
+    rc, lines, err = run("amd-gemm-validate", "--smoke", "--shapes", "4096", "--iters", "5", "--no-stabilise")
+    assert rc == 0, err
+    sm = [x for x in lines if x.get("event") == "hip-smoke"]
+    assert len(sm) == 1 and sm[0]["ok"] and sm[0]["devices"] >= 1 and sm[0]["elements"] == 50000

@@ -31,7 +31,7 @@ class FakeRun:
 def _gemm_lines(cmd, vis):
     n = len(vis.split(",")) if vis else 8
     shape = int(cmd[cmd.index("--shapes") + 1])
-    out = []
+    out = [{"event": "hip-smoke", "devices": n, "ok": True}] if "--smoke" in cmd else []
     for d in range(n):
         r = {"event": "gemm", "dtype": "bf16", "device": d, "m": shape, "n": shape, "k": shape, "tflops": 1600.0,
              "ok": True}
@@ -59,7 +59,9 @@ def test_full_sweep_on_free_gpus_probe_on_held_ones(fake_bins):
     assert full[full.index("--min-relative") + 1] == "0.85" and full[full.index("--min-efficiency") + 1] == "0.9"
     probe = calls[("amd-gemm-validate", "2,5")]
     assert probe[probe.index("--shapes") + 1] == "1024" and "--no-stabilise" in probe and "--scaling" not in probe
-    assert ("amd-hip-smoke", "0,1,3,4,6,7") in calls
+    assert "--smoke" in full and "--smoke" not in probe          # hip-smoke inside the full run's process
+    assert [c[0] for c in fake_bins.calls] == ["amd-gemm-validate", "amd-gemm-validate"]
+    assert [r for r in res if r.get("event") == "hip-smoke"][0]["ok"]
     full_devs = sorted(r["device"] for r in res if r.get("event") == "gemm" and not r.get("probe"))
     assert full_devs == [0, 1, 3, 4, 6, 7]                      # mapped back from the child's 0..5
     assert next(r for r in res if r.get("event") == "uniformity")["slow_devices"] == [0]
@@ -72,8 +74,8 @@ def test_full_sweep_on_free_gpus_probe_on_held_ones(fake_bins):
 
 def test_every_gpu_held_runs_the_probe_only(fake_bins):
     res = WM.run_hip(["8192"], run=fake_bins, devices=[], probe_devices=[0, 1], counters=True)
-    assert [c[0] for c in fake_bins.calls] == ["amd-hip-smoke", "amd-gemm-validate"]
-    assert fake_bins.calls[0][2] == "0"                          # smoke on the first held GPU
+    assert [c[0] for c in fake_bins.calls] == ["amd-gemm-validate"]   # no counters, no full run
+    assert "--smoke" in fake_bins.calls[0][1] and fake_bins.calls[0][2] == "0,1"
     assert all(r.get("probe") for r in res if r.get("event") == "gemm")
     assert WM.hip_ok(res) and res[0] == {"event": "plan", "devices": [], "probe_devices": [0, 1]}
 
