@@ -355,14 +355,15 @@ class Harness:
         # as in the assets: the API-free checks are the static amd-node-validate, the rccl init
         # container falls through to amd-validator when there is a fabric to prove
         nv = lambda comp, **e: Ctr(f"{comp}-validation", ["amd-node-validate", comp], dict({"COMPONENT": comp}, **e))  # noqa: E731
-        rccl = Ctr("rccl-validation", ["sh", "-c", 'amd-node-validate rccl; rc=$?; [ "$rc" -eq 3 ] && exec amd-validator; '
-                                                   'exit "$rc"'], {"COMPONENT": "rccl"})
+        fast = lambda comp, **e: Ctr(f"{comp}-validation", ["sh", "-c", f'amd-node-validate {comp}; rc=$?; '  # noqa: E731
+                                                             '[ "$rc" -eq 3 ] && exec amd-validator; exit "$rc"'],
+                                     dict({"COMPONENT": comp}, **e))
         pods = [
             Pod("toolkit", [nv("driver", WITH_WAIT="true")],
                 [Ctr("amd-container-toolkit-ctr",
                      ["sh", "-c", self._map(_asset_script("state-container-toolkit", "0400_configmap.yaml"))])]),
             Pod("validator", [nv("driver", WITH_WAIT="true"), nv("toolkit", WITH_WAIT="true"), v("hip", **self.hip_env),
-                              v("plugin", WITH_WORKLOAD="false"), rccl],
+                              fast("plugin", WITH_WORKLOAD="false"), fast("rccl")],
                 [Ctr("amd-operator-validator", ["amd-validator", "--component", "ready"])], runtime_class=True),
             Pod("device-plugin", [Ctr("toolkit-validation", gate)],
                 [Ctr("amd-device-plugin", ["sh", "-c", self._map(_asset_script("state-device-plugin",

@@ -3,12 +3,21 @@
 //   amd-node-validate driver  [--with-wait] [--output-dir DIR] [--wait-timeout S]
 //   amd-node-validate toolkit [--with-wait] [--output-dir DIR] [--wait-timeout S]
 //   amd-node-validate rccl    [--output-dir DIR]
+//   amd-node-validate plugin  [--output-dir DIR]
 //
 // The same checks and barrier payloads as validator/components.py (validate_driver,
 // validate_toolkit, the no-fabric branch of validate_rccl), without a Python interpreter on the
 // node bring-up's critical path: each of these init containers starts, checks sysfs and writes its
 // barrier in milliseconds (reference: validator/main.go:607-679 driver, :775-801 toolkit). The
 // components that talk to the API server (hip, plugin, the fabric pod) stay in `amd-validator`.
+//
+// plugin (WITH_WORKLOAD=false, the DaemonSet's setting): polls this Node (GET /api/v1/nodes/NODE_NAME
+// every 100 ms, bounded by 150 s like the validator's event-driven wait) until its capacity
+// advertises amd.com/gpu (or, PARTITION_STRATEGY=mixed, amd.com/partition-*), then writes
+// plugin-ready. The API server is reached in-cluster (service-account token and CA, TLS through
+// OpenSSL with host-name verification) or through a single-cluster KUBECONFIG with a token or no
+// credentials. Anything else -- a workload pod to spawn, client certificates, the reference's poll
+// mode, an unreachable API -- exits 3 and `amd-validator` does it.
 //
 // rccl: a node with fewer than 2 physical GPUs (KFD agents grouped by PCI function) has no fabric;
 // rccl-ready is written with a skip. With 2 or more (or none enumerated, where the validator reads
@@ -23,7 +32,16 @@
 // A barrier that already exists with the same name keeps its first `ts` (when the layer was first
 // found ready -- the start of node time-to-ready) and gets `revalidated_ts`: a validator restart
 // re-checks the driver without moving the moment it became ready.
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <openssl/err.h>
+#include <openssl/pem.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+#include <poll.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -261,8 +279,275 @@ Value validate_toolkit(const Opts& o) {
   return info;
 }
 
-// --- rccl without a fabric (components.validate_rccl, ngpu < 2) -----------------------------
 constexpr int kNotHandled = 3;
+
+// Exit 3: a case only the Python validator handles (see the header).
+class NotHandled : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+// --- a minimal Kubernetes API GET (plugin) --------------------------------------------------
+struct Api {
+  std::string host, prefix, token, ca_file, ca_pem;
+  int port = 443;
+  bool tls = true, verify = true;
+};
+
+std::string slurp(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+std::string trim(std::string s) {
+  const auto b = s.find_first_not_of(" \t\r\n\"'");
+  const auto e = s.find_last_not_of(" \t\r\n\"'");
+  return b == std::string::npos ? "" : s.substr(b, e - b + 1);
+}
+
+void parse_url(const std::string& url, Api& a) {
+  std::string rest = url;
+  if (rest.rfind("https://", 0) == 0) {
+    a.tls = true;
+    rest = rest.substr(8);
+  } else if (rest.rfind("http://", 0) == 0) {
+    a.tls = false;
+    rest = rest.substr(7);
+  } else {
+    throw NotHandled("API server URL " + url);
+  }
+  const auto slash = rest.find('/');
+  std::string hostport = rest.substr(0, slash);
+  a.prefix = slash == std::string::npos ? "" : rest.substr(slash);
+  while (!a.prefix.empty() && a.prefix.back() == '/') a.prefix.pop_back();
+  a.port = a.tls ? 443 : 80;
+  if (!hostport.empty() && hostport[0] == '[') {              // [v6]:port
+    const auto rb = hostport.find(']');
+    a.host = hostport.substr(1, rb - 1);
+    if (rb + 1 < hostport.size() && hostport[rb + 1] == ':') a.port = std::atoi(hostport.c_str() + rb + 2);
+  } else {
+    const auto colon = hostport.rfind(':');
+    a.host = colon == std::string::npos ? hostport : hostport.substr(0, colon);
+    if (colon != std::string::npos) a.port = std::atoi(hostport.c_str() + colon + 1);
+  }
+}
+
+std::string b64decode(const std::string& in) {
+  static const std::string chars = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string out;
+  int val = 0, bits = -8;
+  for (char c : in) {
+    const auto p = chars.find(c);
+    if (p == std::string::npos) continue;
+    val = (val << 6) + (int)p;
+    bits += 6;
+    if (bits >= 0) {
+      out.push_back((char)((val >> bits) & 0xFF));
+      bits -= 8;
+    }
+  }
+  return out;
+}
+
+// In-cluster (service account) or a one-cluster, token-or-anonymous KUBECONFIG; else NotHandled.
+Api api_config() {
+  Api a;
+  const std::string sa = mount_path("/var/run/secrets/kubernetes.io/serviceaccount");
+  const std::string host = env("KUBERNETES_SERVICE_HOST");
+  if (!host.empty() && exists(sa + "/token")) {
+    a.host = host;
+    a.port = std::atoi(env("KUBERNETES_SERVICE_PORT", "443").c_str());
+    a.tls = true;
+    a.token = trim(slurp(sa + "/token"));
+    a.ca_file = sa + "/ca.crt";
+    return a;
+  }
+  const std::string kc = env("KUBECONFIG");
+  if (kc.empty() || !exists(kc)) throw NotHandled("no in-cluster service account and no KUBECONFIG");
+  std::istringstream in(slurp(kc));
+  std::string line, server;
+  int clusters = 0, users = 0;
+  while (std::getline(in, line)) {
+    const std::string t = trim(line.substr(0, line.find('#') == std::string::npos ? line.size() : line.find('#')));
+    auto value = [&](const char* key) -> const char* {
+      const std::string k = std::string(key) + ":";
+      const auto p = t.find(k);
+      return (p == 0 || (p == 2 && t.rfind("- ", 0) == 0)) ? t.c_str() + p + k.size() : nullptr;
+    };
+    if (const char* v = value("server")) { server = trim(v); ++clusters; }
+    else if (const char* v = value("token")) a.token = trim(v);
+    else if (const char* v = value("certificate-authority")) a.ca_file = trim(v);
+    else if (const char* v = value("certificate-authority-data")) a.ca_pem = b64decode(trim(v));
+    else if (const char* v = value("insecure-skip-tls-verify")) a.verify = trim(v) != "true";
+    else if (value("client-certificate") || value("client-certificate-data") || value("client-key") ||
+             value("client-key-data") || value("exec") || value("auth-provider"))
+      throw NotHandled("kubeconfig client credentials");
+    else if (value("user")) ++users;
+  }
+  if (clusters != 1) throw NotHandled("kubeconfig with " + std::to_string(clusters) + " clusters");
+  parse_url(server, a);
+  return a;
+}
+
+// One HTTP/1.1 GET (Connection: close); returns the status, fills body. Transport problems are
+// NotHandled: the Python validator then retries and reports them properly.
+int http_get(const Api& a, const std::string& path, std::string& body, double timeout_s = 10.0) {
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(a.host.c_str(), std::to_string(a.port).c_str(), &hints, &res) != 0 || !res)
+    throw NotHandled("cannot resolve " + a.host);
+  int fd = -1;
+  for (addrinfo* r = res; r && fd < 0; r = r->ai_next) {
+    fd = ::socket(r->ai_family, r->ai_socktype, r->ai_protocol);
+    if (fd < 0) continue;
+    timeval tv{(time_t)timeout_s, 0};
+    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    if (::connect(fd, r->ai_addr, r->ai_addrlen) != 0) {
+      ::close(fd);
+      fd = -1;
+    }
+  }
+  freeaddrinfo(res);
+  if (fd < 0) throw NotHandled("cannot connect to " + a.host + ":" + std::to_string(a.port));
+  SSL_CTX* ctx = nullptr;
+  SSL* ssl = nullptr;
+  auto cleanup = [&] {
+    if (ssl) SSL_free(ssl);
+    if (ctx) SSL_CTX_free(ctx);
+    ::close(fd);
+  };
+  if (a.tls) {
+    ctx = SSL_CTX_new(TLS_client_method());
+    if (a.verify) {
+      SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+      bool loaded = false;
+      if (!a.ca_pem.empty()) {
+        BIO* bio = BIO_new_mem_buf(a.ca_pem.data(), (int)a.ca_pem.size());
+        while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
+          loaded = X509_STORE_add_cert(SSL_CTX_get_cert_store(ctx), x) == 1 || loaded;
+          X509_free(x);
+        }
+        BIO_free(bio);
+      } else if (!a.ca_file.empty()) {
+        loaded = SSL_CTX_load_verify_locations(ctx, a.ca_file.c_str(), nullptr) == 1;
+      } else {
+        loaded = SSL_CTX_set_default_verify_paths(ctx) == 1;
+      }
+      if (!loaded) {
+        cleanup();
+        throw NotHandled("cannot load the API server CA");
+      }
+    }
+    ssl = SSL_new(ctx);
+    SSL_set_fd(ssl, fd);
+    SSL_set_tlsext_host_name(ssl, a.host.c_str());
+    if (a.verify) {
+      // in-cluster the API server is an IP (KUBERNETES_SERVICE_HOST): match it against the
+      // certificate's IP SANs, a name against its DNS SANs
+      in6_addr ip6;
+      in_addr ip4;
+      if (inet_pton(AF_INET, a.host.c_str(), &ip4) == 1 || inet_pton(AF_INET6, a.host.c_str(), &ip6) == 1)
+        X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl), a.host.c_str());
+      else
+        SSL_set1_host(ssl, a.host.c_str());
+    }
+    if (SSL_connect(ssl) != 1) {
+      cleanup();
+      throw NotHandled("TLS handshake with the API server failed");
+    }
+  }
+  std::string req = "GET " + a.prefix + path + " HTTP/1.1\r\nHost: " + a.host + "\r\nAccept: application/json\r\n" +
+                    (a.token.empty() ? "" : "Authorization: Bearer " + a.token + "\r\n") +
+                    "User-Agent: amd-node-validate\r\nConnection: close\r\n\r\n";
+  auto wr = [&](const char* p, size_t n) { return ssl ? SSL_write(ssl, p, (int)n) : (int)::send(fd, p, n, 0); };
+  auto rd = [&](char* p, size_t n) { return ssl ? SSL_read(ssl, p, (int)n) : (int)::recv(fd, p, n, 0); };
+  for (size_t off = 0; off < req.size();) {
+    const int n = wr(req.data() + off, req.size() - off);
+    if (n <= 0) {
+      cleanup();
+      throw NotHandled("write to the API server failed");
+    }
+    off += (size_t)n;
+  }
+  std::string raw;
+  char buf[16384];
+  for (;;) {
+    const int n = rd(buf, sizeof buf);
+    if (n <= 0) break;
+    raw.append(buf, (size_t)n);
+  }
+  cleanup();
+  const auto hdr_end = raw.find("\r\n\r\n");
+  if (raw.rfind("HTTP/1.", 0) != 0 || hdr_end == std::string::npos) throw NotHandled("malformed API response");
+  const int status = std::atoi(raw.c_str() + raw.find(' ') + 1);
+  std::string headers = raw.substr(0, hdr_end);
+  std::transform(headers.begin(), headers.end(), headers.begin(), ::tolower);
+  body = raw.substr(hdr_end + 4);
+  if (headers.find("transfer-encoding: chunked") != std::string::npos) {
+    std::string out;
+    size_t p = 0;
+    for (;;) {
+      const auto eol = body.find("\r\n", p);
+      if (eol == std::string::npos) break;
+      const size_t n = std::strtoul(body.substr(p, eol - p).c_str(), nullptr, 16);
+      if (n == 0) break;
+      out.append(body, eol + 2, n);
+      p = eol + 2 + n + 2;
+    }
+    body.swap(out);
+  }
+  return status;
+}
+
+// --- plugin (components.validate_plugin, WITH_WORKLOAD=false) -------------------------------
+Value validate_plugin(const Opts& o) {
+  if (truthy(env("WITH_WORKLOAD", "true"))) throw NotHandled("plugin validation with a workload pod");
+  if (env("VALIDATOR_WAIT_MODE") == "poll") throw NotHandled("the reference's poll mode");
+  const std::string node = env("NODE_NAME");
+  if (node.empty()) throw NotHandled("NODE_NAME unset");
+  const bool mixed = env("PARTITION_STRATEGY", env("MIG_STRATEGY", "single")) == "mixed";
+  const Api api = api_config();
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(150);
+  for (;;) {
+    std::string body;
+    const int status = http_get(api, "/api/v1/nodes/" + node, body);
+    if (status != 200) throw NotHandled("GET node " + node + ": HTTP " + std::to_string(status));
+    Value res = Value::object();
+    long long devices = 0;
+    try {
+      const Value n = minijson::parse(body);
+      const Value* st = n.find("status");
+      const Value* cap = st ? st->find("capacity") : nullptr;
+      if (cap && cap->is_object()) {
+        for (const auto& [k, v] : cap->o) {
+          if (k != "amd.com/gpu" && !(mixed && k.rfind("amd.com/partition-", 0) == 0)) continue;
+          const long long c = v.is_string() ? std::atoll(v.s.c_str()) : v.integer();
+          if (c > 0) {
+            res[k] = Value::number(c);
+            devices += c;
+          }
+        }
+      }
+    } catch (const std::exception& e) {
+      throw NotHandled(std::string("node JSON: ") + e.what());
+    }
+    if (devices > 0) {
+      Value info = Value::object();
+      info["resources"] = res;
+      info["devices"] = Value::number(devices);
+      write_barrier(o, "plugin-ready", info);
+      return info;
+    }
+    if (std::chrono::steady_clock::now() >= deadline)
+      throw ValidationError("no amd.com/gpu resources on node " + node + " after 150s");
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  }
+}
+
+// --- rccl without a fabric (components.validate_rccl, ngpu < 2) -----------------------------
 
 Value validate_rccl(const Opts& o, int& rc) {
   std::set<std::string> phys;
@@ -310,7 +595,7 @@ int main(int argc, char** argv) {
     else if (a == "--dev-root") o.dev_root = next();
     else if (a == "--host-root") o.host_root = next();
     else if (a == "-h" || a == "--help") {
-      std::printf("usage: amd-node-validate driver|toolkit|rccl [--with-wait] [--output-dir DIR] [--wait-timeout S]\n");
+      std::printf("usage: amd-node-validate driver|toolkit|plugin|rccl [--with-wait] [--output-dir DIR] [--wait-timeout S]\n");
       return 0;
     } else if (a[0] != '-') o.component = a;
     else {
@@ -325,10 +610,14 @@ int main(int argc, char** argv) {
     if (o.component == "driver") info = validate_driver(o);
     else if (o.component == "toolkit") info = validate_toolkit(o);
     else if (o.component == "rccl") info = validate_rccl(o, rc);
+    else if (o.component == "plugin") info = validate_plugin(o);
     else {
       std::fprintf(stderr, "amd-node-validate: component '%s' needs amd-validator\n", o.component.c_str());
       return kNotHandled;
     }
+  } catch (const NotHandled& e) {
+    std::fprintf(stderr, "amd-node-validate %s: handing over to amd-validator (%s)\n", o.component.c_str(), e.what());
+    return kNotHandled;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "error validating %s: %s\n", o.component.c_str(), e.what());
     return 1;

@@ -121,3 +121,73 @@ def test_mount_table_maps_the_default_paths(tmp_path, node):
     p = subprocess.run([BIN, "driver"], capture_output=True, text=True, timeout=30, env=e)
     assert p.returncode == 0, p.stderr
     assert os.path.exists(tmp_path / "v" / "host-driver-ready")
+
+
+def _api(tmp_path, node_caps, tls=False):
+    """The fake API server (HTTP, or HTTPS with a self-signed certificate for 127.0.0.1) holding one
+    Node; returns (server, kubeconfig path)."""
+    import ssl
+    from gpu_operator_amd.k8s.apiserver import FakeAPIServer
+    from gpu_operator_amd.k8s.fake import FakeClient
+    node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": "n1"},
+            "status": {"capacity": dict(node_caps), "allocatable": dict(node_caps)}}
+    backing = FakeClient([node])
+    srv = FakeAPIServer(backing)
+    url = srv.url
+    ca = ""
+    if tls:
+        key, crt = tmp_path / "key.pem", tmp_path / "crt.pem"
+        subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-days", "1", "-subj", "/CN=api",
+                        "-addext", "subjectAltName=IP:127.0.0.1", "-keyout", str(key), "-out", str(crt)],
+                       check=True, capture_output=True, timeout=60)
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.load_cert_chain(str(crt), str(key))
+        srv.httpd.socket = ctx.wrap_socket(srv.httpd.socket, server_side=True)
+        url = url.replace("http://", "https://")
+        ca = f"    certificate-authority: {crt}\n"
+    srv.start()
+    kc = tmp_path / "kubeconfig"
+    kc.write_text(f"apiVersion: v1\nkind: Config\ncurrent-context: t\nclusters:\n- cluster:\n    server: {url}\n{ca}"
+                  "  name: t\ncontexts:\n- context:\n    cluster: t\n    user: t\n  name: t\nusers:\n- name: t\n"
+                  "  user:\n    token: abc\n")
+    return srv, backing, str(kc)
+
+
+@pytest.mark.parametrize("tls", [False, True])
+def test_plugin_reads_node_capacity_over_the_api(tmp_path, node, tls):
+    srv, backing, kc = _api(tmp_path, {}, tls=tls)
+    try:
+        def advertise():
+            time.sleep(0.5)                      # the device plugin registers after the check starts
+            backing.patch("v1", "Node", "n1", {"status": {"capacity": {"amd.com/gpu": "8", "cpu": "96"}}})
+        import threading
+        threading.Thread(target=advertise, daemon=True).start()
+        env = {"KUBECONFIG": kc, "NODE_NAME": "n1", "WITH_WORKLOAD": "false"}
+        t = time.monotonic()
+        rc, out, err = native("plugin", node, tmp_path / "n", env)
+        assert rc == 0, err
+        assert 0.4 < time.monotonic() - t < 10
+        assert barriers(tmp_path / "n")["plugin-ready"] == {"resources": {"amd.com/gpu": 8}, "devices": 8}
+        # the same barrier as the Python validator's
+        from gpu_operator_amd.k8s.rest import Config, RestClient
+        cl = RestClient(Config.from_kubeconfig(kc))
+        ctx = comp.Context(status=S.StatusDir(str(tmp_path / "p")), node_name="n1", client=cl, env={})
+        comp.validate_plugin(ctx)
+        assert barriers(tmp_path / "p") == barriers(tmp_path / "n")
+    finally:
+        srv.stop()
+
+
+def test_plugin_hands_over_what_it_does_not_handle(tmp_path, node):
+    srv, backing, kc = _api(tmp_path, {"amd.com/gpu": "8", "amd.com/partition-cpx": "8"})
+    try:
+        base = {"KUBECONFIG": kc, "NODE_NAME": "n1", "WITH_WORKLOAD": "false"}
+        assert native("plugin", node, tmp_path / "a", dict(base, WITH_WORKLOAD="true"))[0] == 3
+        assert native("plugin", node, tmp_path / "b", dict(base, VALIDATOR_WAIT_MODE="poll"))[0] == 3
+        assert native("plugin", node, tmp_path / "c", dict(base, NODE_NAME=""))[0] == 3
+        assert native("plugin", node, tmp_path / "d", dict(base, KUBECONFIG=str(tmp_path / "none")))[0] == 3
+        rc, _, _ = native("plugin", node, tmp_path / "e", dict(base, PARTITION_STRATEGY="mixed"))
+        assert rc == 0 and barriers(tmp_path / "e")["plugin-ready"]["devices"] == 16
+        assert not any(os.listdir(tmp_path / d) for d in "abcd" if os.path.isdir(tmp_path / d))
+    finally:
+        srv.stop()
