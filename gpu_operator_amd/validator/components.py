@@ -693,10 +693,12 @@ def summarize_rccl(results: List[Dict[str, Any]]) -> Dict[str, Any]:
 
 
 def _run_rccl_local(ctx: Context, ngpu: int, floor: float) -> List[Dict[str, Any]]:
-    from .workload_main import run_rccl
+    from .workload_main import RCCL_MAX_BYTES, RCCL_STEP_TIMEOUT_S, run_rccl
     ranks = ctx.env.get("RCCL_RANKS") or ",".join(str(n) for n in (2, 4, 8) if n <= ngpu) or str(ngpu)
-    return run_rccl(int(ctx.env.get("RCCL_MAX_BYTES", 1 << 26)), ctx.env.get("RCCL_DTYPE", "bf16"), ranks=ranks,
-                    min_busbw=floor or None)
+    # the same sweep (up to 8 GiB) and hang guard as the fabric pod's
+    return run_rccl(int(ctx.env.get("RCCL_MAX_BYTES", RCCL_MAX_BYTES)), ctx.env.get("RCCL_DTYPE", "bf16"), ranks=ranks,
+                    min_busbw=floor or None,
+                    step_timeout=float(ctx.env.get("RCCL_TIMEOUT_S", RCCL_STEP_TIMEOUT_S)))
 
 
 def run_topology_check(ctx: Context) -> Dict[str, Any]:

