@@ -25,7 +25,6 @@ import time
 import urllib.parse
 from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
-import yaml
 
 from . import errors
 from . import objects as o
@@ -66,6 +65,7 @@ class Config:
 
     @classmethod
     def from_kubeconfig(cls, path: Optional[str] = None, context: Optional[str] = None) -> "Config":
+        import yaml            # in-cluster agents never parse a kubeconfig
         path = path or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
         with open(path) as f:
             kc = yaml.safe_load(f)

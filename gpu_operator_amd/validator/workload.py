@@ -20,7 +20,6 @@ import threading
 import time
 from typing import Any, Callable, Dict, List, Optional
 
-import yaml
 
 from ..k8s import errors
 from ..k8s import objects as o
@@ -34,6 +33,7 @@ def load_pod_spec(name: str) -> Dict[str, Any]:
     for d in MANIFEST_DIRS:
         p = os.path.join(d, name)
         if os.path.exists(p):
+            import yaml        # only here: the validator's other components never parse YAML
             with open(p) as f:
                 return yaml.safe_load(f)
     raise FileNotFoundError(f"validation pod manifest {name} not found in {MANIFEST_DIRS}")
