@@ -70,6 +70,7 @@ ASSETS = os.path.join(REPO, "gpu_operator_amd", "assets")
 NATIVE_BIN = os.path.join(REPO, "gpu_operator_amd", "_native", "bin")
 
 KUBELET_SYNC_S = 1.0                              # harness kubelet: sandbox-creation retry period
+CONTAINER_POLL_S = 0.005                          # harness kubelet: container-exit detection granularity
 CRASHLOOP_BACKOFF_S = [10.0, 20.0, 40.0, 80.0, 160.0, 300.0]   # kubelet container restart back-off
 NODE = "ttr-node"
 NAMESPACE = "amd-gpu-operator"
@@ -306,8 +307,10 @@ class Harness:
                 attempt = 0
                 while True:
                     p = self._spawn(pod, c)
+                    # the exit of an init container is seen within CONTAINER_POLL_S (measurement
+                    # granularity, the same for both protocols)
                     while p.poll() is None:
-                        if self._stop.wait(0.02):
+                        if self._stop.wait(CONTAINER_POLL_S):
                             return
                     if p.returncode == 0:
                         break
