@@ -117,7 +117,7 @@ TARGETS: List[Target] = [
     # driver / toolkit / no-fabric rccl validation without a Python interpreter (validator init containers)
     # (plugin: a TLS GET of its Node -- OpenSSL linked in statically, no runtime dependency on the image's)
     Target("bin/amd-node-validate", ["node/node_validate.cpp", "node/amdnode.cpp"], "cxx-exe",
-           flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h", "include/minijson.h"],
+           flags=["-static-libstdc++", "-static-libgcc", "-s"], headers=["include/amdnode.h", "include/minijson.h"],
            libs=["-Wl,-Bstatic", "-lssl", "-lcrypto", "-Wl,-Bdynamic", "-ldl", "-lpthread"]),
 ]
 

@@ -16,6 +16,11 @@
 //   197 / 198 / 265 / 266 = ZC (EPI 8, src C = 0 first K-tile): bf16 v50 / v51, fp8 v20 / v21 forms
 //   200 / 267 / 268 = WG512 epilogue (EPI 10: workgroup-shared staging, 2 x 512-byte rows per store): bf16 v50, fp8 v20 / v21
 //   199 = direct epilogue (EPI 9: EF layout, stores from the accumulators, no LDS staging)
+//   215 / 216 / 217 = LEAN epilogue (EPI 15: chunk-swizzled staging, saddr stores): 197 / 198 / VP G4_ZC;
+//   218 / 219 = VP + PA G4_ZC with LEAN / STAGED_ZC, 222 = 218 on the square raster; 223 / 224 = VP
+//   G4_ZC square raster with LEAN / STAGED_ZC (224 = production v54);
+//   fp8 269 / 270 = 265 / 266 with it; 271 = VP + PA p_zc square raster (262 + ZC), 272 = 271 + LEAN,
+//   273 = VP + PA p_zc linear raster + LEAN
 //   211-214 = 197 with store cache policy sc1 nt / sc0 sc1 / sc0 sc1 nt / sc0 nt
 //   196 / 264 = deferred C stores (EPI 7): bf16 g4 serpentine (v50 + DS), fp8 p linear (v20 + DS); K >= 8 K-tiles
 //   163 / 164 = knock-outs: production epilogue storing only the first quarter / half of C; 233 = fp8 quarter
@@ -270,6 +275,47 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
                          s, a, b, c, M, N, K);
       break;
     }
+    case 215: case 217: {   // LEAN epilogue (EPI 15): 197 / the VP G4_ZC form (DM 1) with it
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      if (v == 215)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, W4AP_EPI_LEAN>), dim3(g), dim3(W4_THREADS), 0,
+                           s, a, b, c, M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN, 1>), dim3(g), dim3(W4_THREADS),
+                           0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 218: case 219: {   // VP + PA (DM 2) G4_ZC, serpentine K, linear raster: LEAN / STAGED_ZC epilogue
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      if (v == 218)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN, 2>), dim3(g), dim3(W4_THREADS),
+                           0, s, a, b, c, M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 2>), dim3(g),
+                           dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 222:     // VP + PA G4_ZC + LEAN on the square raster
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN, 2>), dim3(256), dim3(W4_THREADS), 0,
+                         s, a, b, c, M, N, K);
+      break;
+    case 223: case 224:     // VP (DM 1) G4_ZC on the square raster: LEAN / STAGED_ZC (= production v54)
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      if (v == 223)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN, 1>), dim3(256), dim3(W4_THREADS),
+                           0, s, a, b, c, M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC, 1>), dim3(256),
+                           dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 216:     // LEAN epilogue on the square raster (198 + EPI 15)
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, true, W4AP_EPI_LEAN>), dim3(256), dim3(W4_THREADS), 0,
+                         s, a, b, c, M, N, K);
+      break;
     case 198:     // ZC on the square raster (v51 + ZC)
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(W4_THREADS), 0,
@@ -393,6 +439,31 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     case 266:     // ZC square raster (v21 + ZC)
       if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 271:     // VP + PA form of p_zc (ZC, EPI 8) on the square raster, serpentine K (262 + ZC)
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC, 2>), dim3(256), dim3(F8_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
+    case 272:     // 271 with the LEAN epilogue (EPI 15, PA row map)
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN, 2>), dim3(256), dim3(F8_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
+    case 273:     // VP + PA p_zc, linear raster and K, LEAN epilogue
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, false, false, W4AP_EPI_LEAN, 2>), dim3(g), dim3(F8_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
+    case 269:     // LEAN epilogue (EPI 15) for v20 (p_zc, linear K)
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, false, false, W4AP_EPI_LEAN>), dim3(g), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 270:     // LEAN epilogue for v21 (square raster)
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_LEAN>), dim3(256), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 267:     // WG512 epilogue (EPI 10) for v20 (p_zc, linear K)

@@ -131,13 +131,19 @@ constexpr int W4AP_EPI_WG512 = 10;      // ZC; the workgroup stages 512-byte C r
                                         // the shared 32 KiB, 2 barriers per pass: one store = 2 full rows
 constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile starts accumulators with src C = 0,
                                         // so the epilogue only reads them (generated *_zc schedules)
+constexpr int W4AP_EPI_LEAN = 15;       // ZC, staged through 16-byte-chunk-swizzled LDS rows (a 16-byte read needs
+                                        // no lane-dependent half swap) and stored with global saddr stores: one
+                                        // per-lane 32-bit offset for the whole tile, the row step in an SGPR base.
+                                        // Removes the ~320 per-tile VALU ops (v_cndmask, 64-bit address math)
+                                        // that the STAGED_ZC store loop compiles to
 
 // What the staged epilogue does for an EPI value. The tools-only lab library specialises this for its
 // knock-out forms (native/hip/gemm_bf16_asm_lab.hip); the production forms are the primary template.
 template <int EPI>
 struct W4apEpi {
   static constexpr bool run = true;                         // run the staged epilogue at all
-  static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC || EPI == W4AP_EPI_WG512;   // K-loop zeroes (src C = 0)
+  static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC || EPI == W4AP_EPI_WG512 ||
+                             EPI == W4AP_EPI_LEAN;                                  // K-loop zeroes (src C = 0)
   template <int S>                                          // pass S's 16-byte C store
   static __device__ __forceinline__ void store(__bf16* dst, uint4 v) {
     if constexpr (EPI == W4AP_EPI_STAGED) *reinterpret_cast<uint4*>(dst) = v;
@@ -352,6 +358,68 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
 #pragma unroll
         for (int e = 0; e < 8; ++e) b[e] = (__bf16)x[e];
         store_c16(cw + (size_t)(16 * m) * N + 32 * p, __builtin_bit_cast(uint4, b));
+      });
+    } else if constexpr (EPI == W4AP_EPI_LEAN) {
+      // 4 passes of 32 C rows x 128 columns through this wave's 8 KiB. Lane (r, j) of accumulator m*8+n
+      // holds row 16m + r, columns 16n + 4j .. +3: the 8-byte half j & 1 of 16-byte chunk 2n + (j >> 1).
+      // Chunk c of staged row r sits at c ^ (r & 15): a ds_write_b64 half-wave covers 16 rows x one chunk
+      // pair = every bank once, and a row read back is a permutation of the row's 16 chunks (no conflicts).
+      const int lr = lane & 15, lj = lane >> 4;
+      const uint32_t vst = DM == 2 ? (uint32_t)lj * 64u * (uint32_t)N + (uint32_t)lr * 16u    // PA: rows 32 apart
+                                   : (uint32_t)lj * 2u * (uint32_t)N + (uint32_t)lr * 16u;
+      const uint64_t cb = (uint64_t)(uintptr_t)(C + (size_t)tm * W4AP_TILE * N + tn * W4AP_TILE + wc * 128);
+      const uint64_t cbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cb >> 32)) << 32) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cb);
+      const uint64_t rowb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)N * 2u);
+      // the wave-uniform part of a store's C row, walked by one SGPR pointer (laundered so the compiler
+      // cannot fold every store's row into a hoisted 64-bit constant: 32 of them spill the SGPR file).
+      // DM 0/1: row 128 wr + 32 s + 4 k, +4 rows a store. DM 2 maps LDS slot wr*128 + s*32 + r to panel
+      // row 32 (slot & 7) + (slot >> 3) = 32 lj + [128 (k & 1) + 16 wr + 4 s + (k >> 1)]: even k at the
+      // pointer, odd k 128 rows on, +1 row a pair
+      uint64_t cp = cbase + (uint64_t)(DM == 2 ? 16 * wr : 128 * wr) * rowb;
+      const uint64_t cstep = DM == 2 ? rowb : 4 * rowb;
+      const uint64_t codd = 128 * rowb;
+      static_for<0, 4>([&](auto S) {
+        constexpr int s = decltype(S)::value;
+        static_for<0, 16>([&](auto I) {
+          constexpr int u = decltype(I)::value;
+          constexpr int mm = u >> 3, n = u & 7;
+          constexpr int i = (2 * s + mm) * 8 + n;
+          float x0, x1, x2, x3;
+          asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                       "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                       : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                       : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+          bf16x4 v;
+          v[0] = (__bf16)x0;
+          v[1] = (__bf16)x1;
+          v[2] = (__bf16)x2;
+          v[3] = (__bf16)x3;
+          const int c = 2 * n + (lj >> 1);
+          *reinterpret_cast<bf16x4*>(stg + (mm * 16 + lr) * 256 + ((c ^ lr) << 4) + ((lj & 1) << 3)) = v;
+        });
+        asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
+        if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA landed
+        const uint32_t vs = vst;           // (a generic lambda does not capture a name used only in asm operands)
+        // all 8 row reads in flight before the first store (the stores' memory clobber orders them)
+        w4a_u32x4 rows[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = k * 4 + lj;
+          rows[k] = *reinterpret_cast<const w4a_u32x4*>(stg + r * 256 + ((lr ^ (r & 15)) << 4));
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t base = (DM == 2 && (k & 1)) ? cp + codd : cp;
+          // s_nop: a VALU write of a > 8-byte store's data VGPRs needs one wait state after the store,
+          // which the compiler cannot see inside the asm
+          asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 0" :: "v"(vs), "v"(rows[k]), "s"(base) : "memory");
+          if (DM != 2 || (k & 1)) {
+            cp += cstep;
+            asm volatile("" : "+s"(cp));
+          }
+        }
+        asm volatile("" ::: "memory");
       });
     } else if constexpr (!W4apEpi<EPI>::run) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -322,7 +322,7 @@ def test_production_asm_headers_carry_only_shipped_schedules():
     prod = [open(os.path.join(hip, h)).read() for h in ("gemm_bf16_asm_loop.h", "gemm_fp8_asm_loop.h")]
     assert sum(p.count("\n") for p in prod) < 10000
     asm_defs = sorted(re.findall(r"^#define (\w+_ASM_\w+) \\", "\n".join(prod), re.M))
-    assert asm_defs == ["F8AP_ASM_P_ZC", "W4AP_ASM_G4_ZC", "W4AP_ASM_G6D6_ZC", "W4VP_ASM_G4_ZC"]
+    assert asm_defs == ["F8AP_ASM_P_ZC", "F8VP_ASM_P_ZC", "W4AP_ASM_G4_ZC", "W4AP_ASM_G6D6_ZC", "W4VP_ASM_G4_ZC"]
     for f in os.listdir(hip):
         text = open(os.path.join(hip, f), errors="replace").read()
         if "_asm_loop_lab.h\"" in text and not f.endswith("_lab.h"):

@@ -535,7 +535,7 @@ EF = ["p", "s1d3", "p_nt"]
 # (%[koff], %[nkoff] for the next tile) used as the soffset: one SALU add per K-tile instead of a VALU
 # add, no per-piece row-block SGPRs, and A and B pieces may use different row maps -- DM = 2 reads each
 # A-panel DMA instruction's 8 rows 32 apart (PA: K not a power of two, see gemm_bf16.hip v47).
-VP = ["p", "s1d3"]
+VP = ["p", "s1d3", "p_zc"]   # p_zc: the ZC first K-tile (src C = 0) in VP form
 
 
 def to_vp(lines: List[str]) -> List[str]:
@@ -620,7 +620,7 @@ def render() -> str:
         parts.append(f"#define F8VP_SC_{n.upper()} {i}")
     parts.append("")
     for name in VP:
-        lines = to_vp(kloop_persistent(SCHEDULES[name]))
+        lines = to_vp(ap_lines(name))
         parts.append(f"#define F8VP_ASM_{name.upper()} \\")
         for ln in lines:
             parts.append(f'  "{ln}\\n\\t" \\')
@@ -638,8 +638,8 @@ def render() -> str:
     return "\n".join(parts)
 
 
-# The schedule gemm_fp8.hip dispatches: v20 / v21 F8AP p_zc.
-SHIPPED = {"F8AP": ["p_zc"]}
+# The schedules gemm_fp8.hip dispatches: v20 / v21 F8AP p_zc, v22 / v23 F8VP p_zc (VP + PA DMA form).
+SHIPPED = {"F8AP": ["p_zc"], "F8VP": ["p_zc"]}
 
 
 def ap_lines(name: str) -> List[str]:
@@ -656,17 +656,19 @@ def render_production() -> str:
              "// at the SC index it has in the lab header gemm_fp8_asm_loop_lab.h, which carries every",
              "// schedule and, when included first, masks this one.",
              "#pragma once", f"#ifndef {LAB_GUARD}", ""]
-    for fam in ("F8EF", "F8DS", "F8VP"):
+    for fam in ("F8EF", "F8DS"):
         parts.append(f"#define {fam}_LOOP_SELECT(SC) {lab_only}")
-    sel = [f"if constexpr (SC == {PERSISTENT.index(n)}) W4AP_LOOP(F8AP_ASM_{n.upper()});" for n in SHIPPED["F8AP"]]
-    parts.append("#define F8AP_LOOP_SELECT(SC) \\")
-    parts.append("  " + " else \\\n  ".join(sel + [lab_only]))
-    for n in SHIPPED["F8AP"]:
-        parts.append(f"#define F8AP_SC_{n.upper()} {PERSISTENT.index(n)}")
-    parts.append("")
-    for n in SHIPPED["F8AP"]:
-        parts.append(f"#define F8AP_ASM_{n.upper()} \\")
-        parts += [f'  "{ln}\\n\\t" \\' for ln in ap_lines(n)] + ['  ""', ""]
+    for fam, names, macro, lines_of in (("F8AP", PERSISTENT, "W4AP_LOOP", ap_lines),
+                                        ("F8VP", VP, "W4VP_LOOP", lambda n: to_vp(ap_lines(n)))):
+        sel = [f"if constexpr (SC == {names.index(n)}) {macro}({fam}_ASM_{n.upper()});" for n in SHIPPED[fam]]
+        parts.append(f"#define {fam}_LOOP_SELECT(SC) \\")
+        parts.append("  " + " else \\\n  ".join(sel + [lab_only]))
+        for n in SHIPPED[fam]:
+            parts.append(f"#define {fam}_SC_{n.upper()} {names.index(n)}")
+        parts.append("")
+        for n in SHIPPED[fam]:
+            parts.append(f"#define {fam}_ASM_{n.upper()} \\")
+            parts += [f'  "{ln}\\n\\t" \\' for ln in lines_of(n)] + ['  ""', ""]
     parts.append(f"#endif  // {LAB_GUARD}")
     return "\n".join(parts) + "\n"
 
