@@ -134,9 +134,11 @@ class FakeKubelet:
                 stream = K.device_plugin_stub(ch)["ListAndWatch"](K.DP["Empty"]())
                 for resp in stream:
                     n = sum(1 for d in resp.devices if d.health == K.HEALTHY)
+                    # marked as the PATCH goes out: a validator polling the Node can see the new
+                    # capacity before this thread gets the response back
+                    self.on_event(f"kubelet:capacity:{resource}={n}")
                     self.client.patch("v1", "Node", self.node, {"status": {"capacity": {resource: str(n)},
                                                                            "allocatable": {resource: str(n)}}})
-                    self.on_event(f"kubelet:capacity:{resource}={n}")
                     if self._stop.is_set():
                         stream.cancel()
                         break

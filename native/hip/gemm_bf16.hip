@@ -29,7 +29,9 @@
 //   47 / 48 = v44 / v45 with permuted A-panel DMA rows (PA), the default for other K not a power of two.
 //   50 / 51 / 52 = the asm pipeline: w4ap (gemm_bf16_kernels.h) with the g4 schedule, g4 on the square
 //        raster, the g6d6 schedule (tools/gen_bf16_asm_loop.py generates gemm_bf16_asm_loop.h).
-//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 = that kernel pinned (no automatic switch; still falls back to a kernel
+//   55 / 56 (round 4) = v53 / v54 with the A-panel pieces reading rows 32 apart (PA, DM 2) and the LEAN
+//        epilogue (EPI 15: chunk-swizzled staging, saddr C stores; gemm_w4ap.h).
+//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
 // Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
 // add per K-tile, loop-invariant soffsets; 17 fewer SALU per K-tile, +0.6-0.8 % at 8192^3 and
@@ -104,10 +106,11 @@ static int resolve_variant(int M, int N, int K, hipStream_t s) {
   if (v == 25 && persistent_grid(nwg, s) < NXCD) v = 44;
   // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups; its square raster
   // (v51) needs exactly 256 workgroups over 16x16 super-tiles
-  if ((v == 50 || v == 51 || v == 52 || v == 53 || v == 54) &&
+  if ((v == 50 || v == 51 || v == 52 || v == 53 || v == 54 || v == 55 || v == 56) &&
       (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg, s) < NXCD))
     v = 44;
   if (v == 54 && (!sq || cus != 256)) v = 53;
+  if (v == 56 && (!sq || cus != 256)) v = 55;
   if (v == 51 && (!sq || cus != 256)) v = 50;
   if ((v == 44 || v == 45) && cus != 256) v = 42;       // serpentine K assumes 32 co-resident WGs / XCD
   // K not a power of two: A-panel DMA instructions read rows 32 apart (PA, v47 / v48). At a 24 KiB
@@ -126,7 +129,7 @@ extern "C" {
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
   if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50 &&
-      v != 51 && v != 52 && v != 53 && v != 54)
+      v != 51 && v != 52 && v != 53 && v != 54 && v != 55 && v != 56)
     return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
@@ -185,6 +188,14 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
       break;
     case 54:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC, 1>), dim3(256), dim3(W4_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
+    case 55:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN, 2>), dim3(persistent_grid(nwg, s)),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    case 56:
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN, 2>), dim3(256), dim3(W4_THREADS),
                          0, s, a, b, c, M, N, K);
       break;
     case 52:

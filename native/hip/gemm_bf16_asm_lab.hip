@@ -18,7 +18,8 @@
 //   199 = direct epilogue (EPI 9: EF layout, stores from the accumulators, no LDS staging)
 //   215 / 216 / 217 = LEAN epilogue (EPI 15: chunk-swizzled staging, saddr stores): 197 / 198 / VP G4_ZC;
 //   218 / 219 = VP + PA G4_ZC with LEAN / STAGED_ZC, 222 = 218 on the square raster; 223 / 224 = VP
-//   G4_ZC square raster with LEAN / STAGED_ZC (224 = production v54);
+//   G4_ZC square raster with LEAN / STAGED_ZC (224 = production v54); 225 / 226 / 227 = LEAN_PIPE (EPI 16,
+//   pipelined half-passes): 197 / 218 / 222 with it; fp8 274 = 272 with it, 275 = 265 with it;
 //   fp8 269 / 270 = 265 / 266 with it; 271 = VP + PA p_zc square raster (262 + ZC), 272 = 271 + LEAN,
 //   273 = VP + PA p_zc linear raster + LEAN
 //   211-214 = 197 with store cache policy sc1 nt / sc0 sc1 / sc0 sc1 nt / sc0 nt
@@ -311,6 +312,22 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
         hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC, 1>), dim3(256),
                            dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
+    case 225: case 226: {   // LEAN_PIPE epilogue (EPI 16): 197 with it / VP + PA G4_ZC with it, linear raster
+      const int g = ((nwg < device_cu_count() ? nwg : device_cu_count()) / NXCD) * NXCD;
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      if (v == 225)
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, false, W4AP_EPI_LEAN_PIPE>), dim3(g), dim3(W4_THREADS),
+                           0, s, a, b, c, M, N, K);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN_PIPE, 2>), dim3(g),
+                           dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      break;
+    }
+    case 227:     // VP + PA G4_ZC + LEAN_PIPE on the square raster
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN_PIPE, 2>), dim3(256), dim3(W4_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
     case 216:     // LEAN epilogue on the square raster (198 + EPI 15)
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, true, W4AP_EPI_LEAN>), dim3(256), dim3(W4_THREADS), 0,
@@ -455,6 +472,16 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
       if (g < NXCD) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, false, false, W4AP_EPI_LEAN, 2>), dim3(g), dim3(F8_THREADS),
                          0, s, a, b, c, M, N, K);
+      break;
+    case 274:     // 272 with the LEAN_PIPE epilogue (EPI 16)
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN_PIPE, 2>), dim3(256), dim3(F8_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
+    case 275:     // v20 (p_zc, linear) with the LEAN_PIPE epilogue
+      if (g < NXCD) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, false, false, W4AP_EPI_LEAN_PIPE>), dim3(g), dim3(F8_THREADS), 0,
+                         s, a, b, c, M, N, K);
       break;
     case 269:     // LEAN epilogue (EPI 15) for v20 (p_zc, linear K)
       if (g < NXCD) return (int)hipErrorInvalidValue;

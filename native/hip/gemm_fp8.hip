@@ -20,7 +20,12 @@
 //       Both start each tile's accumulators with src C = 0 (the p_zc schedule, EPI 8; 8192^2x2048 +3.9 %). Against hipBLASLt fp8 on MI355X (profiles/r3_s2/): 8192^3 1.005-1.021x (q16p
 //       0.974-0.981x), 4096^3 1.04x, 16384^3 1.03x (v21), 16384^2x2048 1.05x (v21), 16384^2x1024
 //       1.09x (v21), 16384x8192x8192 1.00x.
-//   10 / 15 / 16 / 17 / 18 / 20 / 21 = that kernel pinned (no automatic switch; falls back when the
+//   22 / 23 (round 4): v21 / v20 in the VP DMA form with the A-panel pieces reading rows 32 apart (PA,
+//       DM 2; the p_zc schedule, gen_fp8_asm_loop.py VP) and the LEAN epilogue (EPI 15: chunk-swizzled
+//       staging, saddr C stores, gemm_w4ap.h). v22 replaces v21 as the default on the square raster:
+//       16384^2x1024 1.19x hipBLASLt (v21 1.13x), 12288^3 1.02x (v21 1.00x), 8192^2x2048 1.10x (1.08x),
+//       16384^3 1.035x (1.031x), 8192^3 1.035x (1.023x); profiles/r4_lean/. v23 is pinned-only.
+//   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 = that kernel pinned (no automatic switch; falls back when the
 //       shape or the device cannot run it).
 // q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
 // (profiles/r2_fp8_q16/): 8192^3 +5.3 %, 16384^3 +3.1 %, 4096^3 +4.1 %, 16384x8192x8192 +2.2 %.
@@ -44,7 +49,7 @@ static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
   int v = g_fp8_variant;
   const bool ap_ok = cus == 256 && K % (2 * F8_BK) == 0 && K >= 4 * F8_BK && pgrid >= NXCD;
   if (v == 0 && ap_ok) {
-    v = (sq && nwg >= 2 * cus) ? 21 : 20;
+    v = (sq && nwg >= 2 * cus) ? 22 : 20;
   } else if (v == 0) {
     v = sq ? 16 : 15;
     // Short K (<= 12 K-tiles) with several tiles per CU: the persistent block-scaled kernel hides
@@ -54,8 +59,8 @@ static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
     if (K <= 12 * F8_BK && nwg >= 2 * cus) v = 10;
     else if (K <= 64 * F8_BK && nwg >= 4 * cus) v = 18;
   }
-  if ((v == 20 || v == 21) && !ap_ok) v = sq ? 16 : 15;
-  if (v == 21 && !sq) v = 20;
+  if ((v == 20 || v == 21 || v == 22 || v == 23) && !ap_ok) v = sq ? 16 : 15;
+  if ((v == 21 || v == 22) && !sq) v = v == 22 ? 23 : 20;
   if (v == 16 && !sq) v = 15;
   if ((v == 10 || v == 18) && pgrid < NXCD) v = 15;
   if ((v == 15 || v == 16) && cus != 256) v = 17;   // serpentine K assumes 32 co-resident tiles per XCD
@@ -66,7 +71,7 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
-  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21)
+  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21 && v != 22 && v != 23)
     return (int)hipErrorInvalidValue;
   g_fp8_variant = v;
   return 0;
@@ -99,6 +104,14 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
     case 21:
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
+      break;
+    case 22:
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN, 2>), dim3(256), dim3(F8_THREADS), 0, s,
+                         a, b, c, M, N, K);
+      break;
+    case 23:
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, false, false, W4AP_EPI_LEAN, 2>), dim3(pgrid), dim3(F8_THREADS),
+                         0, s, a, b, c, M, N, K);
       break;
     case 15:
       hipLaunchKernelGGL(Q16(32, false), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);

@@ -136,14 +136,15 @@ constexpr int W4AP_EPI_LEAN = 15;       // ZC, staged through 16-byte-chunk-swiz
                                         // per-lane 32-bit offset for the whole tile, the row step in an SGPR base.
                                         // Removes the ~320 per-tile VALU ops (v_cndmask, 64-bit address math)
                                         // that the STAGED_ZC store loop compiles to
+constexpr int W4AP_EPI_LEAN_PIPE = 16;  // LEAN in 8 software-pipelined half-passes (double-buffered staging)
 
 // What the staged epilogue does for an EPI value. The tools-only lab library specialises this for its
 // knock-out forms (native/hip/gemm_bf16_asm_lab.hip); the production forms are the primary template.
 template <int EPI>
 struct W4apEpi {
   static constexpr bool run = true;                         // run the staged epilogue at all
-  static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC || EPI == W4AP_EPI_WG512 ||
-                             EPI == W4AP_EPI_LEAN;                                  // K-loop zeroes (src C = 0)
+  static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC || EPI == W4AP_EPI_WG512 || EPI == W4AP_EPI_LEAN ||
+                             EPI == W4AP_EPI_LEAN_PIPE;                             // K-loop zeroes (src C = 0)
   template <int S>                                          // pass S's 16-byte C store
   static __device__ __forceinline__ void store(__bf16* dst, uint4 v) {
     if constexpr (EPI == W4AP_EPI_STAGED) *reinterpret_cast<uint4*>(dst) = v;
@@ -421,6 +422,83 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         }
         asm volatile("" ::: "memory");
       });
+    } else if constexpr (EPI == W4AP_EPI_LEAN_PIPE) {
+      // LEAN in 8 half-passes of 16 rows (one accumulator row block each) through two 4 KiB halves of
+      // the wave's staging, software-pipelined: half-pass h + 1's accumulator reads, cvts and LDS writes
+      // run while half-pass h's row reads land, then h's 4 stores go out (order W0 R0 | W1 R1 S0 | W2 R2
+      // S1 | ...): the LDS round trip and the store issue hide under VALU work instead of stalling it.
+      const int lr = lane & 15, lj = lane >> 4;
+      const uint32_t vst = DM == 2 ? (uint32_t)lj * 64u * (uint32_t)N + (uint32_t)lr * 16u
+                                   : (uint32_t)lj * 2u * (uint32_t)N + (uint32_t)lr * 16u;
+      const uint64_t cb = (uint64_t)(uintptr_t)(C + (size_t)tm * W4AP_TILE * N + tn * W4AP_TILE + wc * 128);
+      const uint64_t cbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cb >> 32)) << 32) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cb);
+      const uint64_t rowb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)N * 2u);
+      // DM 0/1: half-pass h, read k (row 4k + lj of the block) is tile row 128 wr + 16 h + 4 k: +4 rows a
+      // store. DM 2: LDS slot wr*128 + 16 h + 4 k + lj -> panel row 32 lj + [128 (k & 1) + 16 wr + 2 h +
+      // (k >> 1)]: the pointer walks 16 wr + 2 h, read k adds 128 (k & 1) + (k >> 1) rows
+      uint64_t cp = cbase + (uint64_t)(DM == 2 ? 16 * wr : 128 * wr) * rowb;
+      const uint64_t c1 = rowb, c128 = 128 * rowb, c129 = 129 * rowb, c4 = 4 * rowb, c2 = 2 * rowb;
+      auto stage = [&](auto H) {
+        constexpr int h = decltype(H)::value;
+        char* const buf = stg + (h & 1) * 4096;
+        static_for<0, 8>([&](auto I) {
+          constexpr int n = decltype(I)::value;
+          constexpr int i = h * 8 + n;
+          float x0, x1, x2, x3;
+          asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                       "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                       : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                       : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+          bf16x4 v;
+          v[0] = (__bf16)x0;
+          v[1] = (__bf16)x1;
+          v[2] = (__bf16)x2;
+          v[3] = (__bf16)x3;
+          const int c = 2 * n + (lj >> 1);
+          *reinterpret_cast<bf16x4*>(buf + lr * 256 + ((c ^ lr) << 4) + ((lj & 1) << 3)) = v;
+        });
+      };
+      auto load = [&](auto H, w4a_u32x4* rows) {
+        constexpr int h = decltype(H)::value;
+        const char* const buf = stg + (h & 1) * 4096;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = k * 4 + lj;
+          rows[k] = *reinterpret_cast<const w4a_u32x4*>(buf + r * 256 + ((lr ^ r) << 4));
+        }
+      };
+      auto store = [&](const w4a_u32x4* rows) {
+        const uint32_t vs = vst;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint64_t base = cp;
+          if (DM == 2) base = cp + (k == 0 ? 0 : k == 1 ? c128 : k == 2 ? c1 : c129);
+          // s_nop: the store's data VGPRs may be rewritten by the next VALU (one wait state)
+          asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 0" :: "v"(vs), "v"(rows[k]), "s"(base) : "memory");
+          if (DM != 2) {
+            cp += c4;
+            asm volatile("" : "+s"(cp));
+          }
+        }
+        if (DM == 2) {
+          cp += c2;
+          asm volatile("" : "+s"(cp));
+        }
+      };
+      w4a_u32x4 ra[4], rb[4];
+      stage(std::integral_constant<int, 0>{});
+      load(std::integral_constant<int, 0>{}, ra);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA landed (before any C store)
+      static_for<0, 8>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        if constexpr (h + 1 < 8) {
+          stage(std::integral_constant<int, h + 1>{});
+          load(std::integral_constant<int, h + 1>{}, (h & 1) ? ra : rb);
+        }
+        store((h & 1) ? rb : ra);
+      });
+      asm volatile("" ::: "memory");
     } else if constexpr (!W4apEpi<EPI>::run) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {

@@ -205,11 +205,11 @@ def _audit_asm_pipeline(body, st):
 
 
 def test_w4ap_production_pipeline(asm):
-    """Production v50 / v51 / v52 / v53 / v54: the persistent asm K pipeline (main schedule, its
-    square-raster form, the long-K schedule, the VP DMA form for K not a power of two, linear and
-    square raster)."""
+    """Production v50 / v51 / v52 / v53 / v54 / v55 / v56: the persistent asm K pipeline (main schedule,
+    its square-raster form, the long-K schedule, the VP DMA form, linear and square raster, and the
+    VP + PA form with the LEAN epilogue, linear and square raster)."""
     kernels = _kernels(asm, "gemm_bf16_256x256_w4apI")
-    assert len(kernels) == 5
+    assert len(kernels) == 7
     for body, st in kernels:
         # the zc schedules (every production form) peel the first K-tile pair (src C = 0): 8 bodies
         assert _audit_asm_pipeline(body, st) == 8 * 128

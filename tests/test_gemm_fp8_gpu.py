@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[0, 10, 15, 16, 17, 18, 20, 21])   # the production set (gemm.FP8_VARIANTS)
+@pytest.fixture(params=[0, 10, 15, 16, 17, 18, 20, 21, 22, 23])   # the production set (gemm.FP8_VARIANTS)
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
@@ -117,11 +117,11 @@ def test_fill_uniform_fp8_range_and_determinism(cuda_device):
     assert torch.unique(t1.view(torch.uint8)).numel() > 100
 
 
-@pytest.mark.parametrize("variant", [16, 21])
+@pytest.mark.parametrize("variant", [16, 21, 22])
 def test_fp8_square_raster_covers_every_tile(cuda_device, variant):
-    """The square cross-XCD raster (q16 v16, persistent asm q16ap v21) over 12288x12288x8192 (48x48
-    tiles, 9 dispatch waves, snaking super-rows); one checked row per tile row covers every output
-    tile."""
+    """The square cross-XCD raster (q16 v16, persistent asm q16ap v21, its VP + PA + LEAN form v22) over
+    12288x12288x8192 (48x48 tiles, 9 dispatch waves, snaking super-rows); one checked row per tile row
+    covers every output tile (and, for v22, every residue of the PA row map)."""
     import torch
     from gpu_operator_amd.ops import gemm as G
 
@@ -149,16 +149,17 @@ def test_fp8_production_variant_set_is_closed(cuda_device):
     import torch
     from gpu_operator_amd.ops import gemm as G
 
-    for bad in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 19, 22, 28, 40, 99):
+    for bad in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 19, 24, 28, 40, 99):
         with pytest.raises(ValueError):
             G.set_fp8_variant(bad)
     assert G.get_fp8_variant() == 0
     cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
     if cus == 256:       # MI355X: the persistent asm pipeline
-        assert G.resolve_fp8_variant(8192, 8192, 8192) == 21
+        assert G.resolve_fp8_variant(8192, 8192, 8192) == 22
         assert G.resolve_fp8_variant(8192, 8192 + 256, 8192) == 20     # not 16x16-tile multiples
-        assert G.resolve_fp8_variant(16384, 16384, 16384) == 21
-        assert G.resolve_fp8_variant(16384, 16384, 1024) == 21
+        assert G.resolve_fp8_variant(16384, 16384, 16384) == 22
+        assert G.resolve_fp8_variant(16384, 16384, 1024) == 22
+        assert G.resolve_fp8_variant(12288, 12288, 12288) == 22
         assert G.resolve_fp8_variant(4096, 4096, 4096) == 20
         assert G.resolve_fp8_variant(4096 + 256, 4096, 4096) == 20
         assert G.resolve_fp8_variant(8192, 8192, 8192 + 128) in (16, 18)   # odd K-tile count

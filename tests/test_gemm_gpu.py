@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -179,11 +179,15 @@ def test_asm_pipeline_is_bitwise_v44(cuda_device, m, n, k):
         G.set_variant(53)            # the same pipeline in the VP DMA form: same MFMA order
         assert G.resolve_variant(m, n, k) == 53
         c53 = G.gemm_bf16(a, bt)
+        G.set_variant(55)            # VP + PA rows + LEAN epilogue: permuted staging, same sums
+        assert G.resolve_variant(m, n, k) == 55
+        c55 = G.gemm_bf16(a, bt)
     finally:
         G.set_variant(old)
     torch.cuda.synchronize()
     assert torch.equal(c44, c50)
     assert torch.equal(c44, c53)
+    assert torch.equal(c44, c55)
 
 
 @pytest.mark.parametrize("m,n,k", [(4096, 8192, 256), (8192, 8192, 1024), (4096, 4096, 2048)])
@@ -210,9 +214,12 @@ def test_asm_square_raster_is_bitwise_v45(cuda_device, m, n, k):
         c50 = G.gemm_bf16(a, bt)
         G.set_variant(54)            # v51 in the VP DMA form
         c54 = G.gemm_bf16(a, bt)
+        G.set_variant(56)            # v54 with PA rows and the LEAN epilogue
+        c56 = G.gemm_bf16(a, bt)
     finally:
         G.set_variant(old)
     torch.cuda.synchronize()
     assert torch.equal(c45, c51)
     assert torch.equal(c45, c54)
+    assert torch.equal(c45, c56)
     assert torch.equal(c50, c52)      # same pipeline, different instruction placement
