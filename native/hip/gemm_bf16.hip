@@ -21,7 +21,8 @@
 // and knock-out timings live in the tools-only gemm_bf16_lab.hip.
 //   0  = automatic (default): on the 256-CU MI355X with a power-of-two K >= 256, the persistent asm
 //        K pipeline -- v50, v51 (square raster: >= 8 dispatch waves, K >= 8192, 16x16-tile
-//        multiples), v52 (one or two dispatch waves, K >= 32768); otherwise v44, v25 for K <= 4096
+//        multiples), v52 (one or two dispatch waves, K >= 32768), v56 (16x16-tile multiples with K <= 2048
+//        or one dispatch wave), v55 (other one-wave grids); otherwise v44, v25 for K <= 4096
 //        with >= 2 tiles per CU, v45 for >= 8 dispatch waves with K >= 8192 on 16x16-tile
 //        multiples; v42 / v18 on devices without 256 CUs.
 //   53 / 54 = the asm pipeline (g4) in the VP DMA form (gemm_w4ap.h DM 1), linear / square raster: the
@@ -30,7 +31,8 @@
 //   50 / 51 / 52 = the asm pipeline: w4ap (gemm_bf16_kernels.h) with the g4 schedule, g4 on the square
 //        raster, the g6d6 schedule (tools/gen_bf16_asm_loop.py generates gemm_bf16_asm_loop.h).
 //   55 / 56 (round 4) = v53 / v54 with the A-panel pieces reading rows 32 apart (PA, DM 2) and the LEAN
-//        epilogue (EPI 15: chunk-swizzled staging, saddr C stores; gemm_w4ap.h).
+//        epilogue (EPI 15: chunk-swizzled staging, saddr C stores; v56 pipelines it over 8 half-passes, EPI
+//        16; gemm_w4ap.h): the power-of-two-K default for short K or one dispatch wave.
 //   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
 // Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
@@ -89,6 +91,12 @@ static int resolve_variant(int M, int N, int K, hipStream_t s) {
     v = 50;
     if (sq && nwg >= 8 * cus && K >= 128 * BK) v = 51;
     else if (nwg <= 2 * cus && K >= 512 * BK) v = 52;
+    // Round 4 (profiles/r4_lean/, r4_prod/): on 16x16-tile multiples with short K (<= 2048) or one
+    // dispatch wave, v56 (VP + PA DMA, pipelined LEAN epilogue, square raster): 16384^2x1024 1440 TF/s =
+    // 1.08x hipBLASLt (v50 1.06x), 8192^2x1024 1.09x (1.02x), 8192^2x2048 1.05x (1.03x), 4096^2x2048
+    // 1.03x (1.00x); other one-wave grids v55 (VP + PA, LEAN, linear raster).
+    else if (sq && (K <= 32 * BK || nwg <= cus)) v = 56;
+    else if (nwg <= cus) v = 55;
   } else if (v == 0) {
     v = 44;
     // Short K (K-loop of <= 64 K-tiles) with several tiles per CU: the persistent v25 hides each
@@ -195,7 +203,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 56:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN, 2>), dim3(256), dim3(W4_THREADS),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN_PIPE, 2>), dim3(256), dim3(W4_THREADS),
                          0, s, a, b, c, M, N, K);
       break;
     case 52:

@@ -112,6 +112,25 @@ def test_vp_square_raster_covers_every_tile(cuda_device):
     torch.testing.assert_close(c[rows].float(), ref, atol=0.15, rtol=1e-2)
 
 
+def test_short_k_square_raster_covers_every_tile(cuda_device):
+    """12288x12288x2048 (48x48 tiles, 9 dispatch waves, short K) takes v56 -- VP + PA DMA rows, the
+    pipelined LEAN epilogue, square raster -- under the default variant; one checked row per tile row
+    (at varying residues of the PA row map) covers every output tile."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    m = n = 12288
+    k = 2048
+    if torch.cuda.get_device_properties(cuda_device).multi_processor_count == 256:
+        assert G.resolve_variant(m, n, k) == 56
+    a = G.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=cuda_device), 15)
+    bt = G.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=cuda_device), 16)
+    c = G.gemm_bf16(a, bt)
+    rows = torch.tensor([tm * 256 + (tm * 43) % 256 for tm in range(m // 256)], device=cuda_device)
+    ref = a[rows].float() @ bt.float().t()
+    torch.testing.assert_close(c[rows].float(), ref, atol=0.15, rtol=1e-2)
+
+
 def test_default_dispatch_square_raster_covers_every_tile(cuda_device):
     """12288x12288x8192 (48x48 tiles, 9 dispatch waves) takes the square cross-XCD raster (v51)
     under the default variant; one checked row per tile row covers every output tile."""
@@ -134,19 +153,20 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
     assert G.get_variant() == 0
 
 
-@pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 50), (16384, 16384, 1024, 50), (8192, 8192, 4096, 50),
+@pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 50), (16384, 16384, 1024, 56), (8192, 8192, 4096, 50),
+                                        (8192, 8192, 2048, 56), (4096, 8192, 1024, 56), (4096, 4096, 2048, 56), (2048, 4096, 512, 55),
                                         (12288, 12288, 12288, 54), (8192, 8192, 12288, 53), (8192, 8192, 8256, 47),
                                         (12288, 12288, 8256, 48),
                                         (12288, 12288, 8192, 51), (16384, 16384, 16384, 51),
-                                        (4096, 4096, 16384, 50), (4096, 8192, 8192, 50), (4096, 4096, 32768, 52),
-                                        (4096, 4096, 4096, 50),
+                                        (4096, 4096, 16384, 56), (4096, 8192, 8192, 50), (4096, 4096, 32768, 52),
+                                        (4096, 4096, 4096, 56),
                                         (8192, 8192, 128, 25), (256, 256, 64, 0), (300, 256, 256, 0)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""
@@ -154,7 +174,7 @@ def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     from gpu_operator_amd.ops import gemm as G
 
     if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
-        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42, 53: 42, 54: 42}.get(want, want)
+        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42, 53: 42, 54: 42, 55: 42, 56: 42}.get(want, want)
     assert G.get_variant() == 0
     assert G.resolve_variant(m, n, k) == want
 
