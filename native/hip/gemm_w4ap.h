@@ -489,13 +489,15 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       w4a_u32x4 ra[4], rb[4];
       stage(std::integral_constant<int, 0>{});
       load(std::integral_constant<int, 0>{}, ra);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA landed (before any C store)
       static_for<0, 8>([&](auto H) {
         constexpr int h = decltype(H)::value;
         if constexpr (h + 1 < 8) {
           stage(std::integral_constant<int, h + 1>{});
           load(std::integral_constant<int, h + 1>{}, (h & 1) ? ra : rb);
         }
+        // the next tile's DMA landed before any C store (its K-loop's landing waits count only its own
+        // pieces); waiting here, not before half-pass 1, gives the DMA two half-passes of cover
+        if constexpr (h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         store((h & 1) ? rb : ra);
       });
       asm volatile("" ::: "memory");

@@ -35,6 +35,7 @@ def main():
     G.fill_uniform_(A, 1)
     G.fill_uniform_(Bt, 2)
     run = runner(G, a.variant, "bf16")
+    run.select()
     for _ in range(a.iters):
         if a.blas:
             torch.matmul(A, Bt.t(), out=C)
@@ -55,6 +56,7 @@ def main_fp8(a):
     C = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
     one = torch.ones((), dtype=torch.float32, device=dev)
     run = runner(G, a.variant, "fp8")
+    run.select()
     for _ in range(a.iters):
         if a.blas:
             C = torch._scaled_mm(A, Bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)

@@ -2,7 +2,9 @@
 """GEMM shape sweep: hand-written MFMA kernel vs hipBLASLt (torch.matmul) on the same random data.
 
 Shapes follow SURVEY.md §7.5: M=N=K in {1024, 4096, 8192, 16384} plus skinny 16384x16384x1024.
-Interleaves the two implementations in one process (methodology rule: A/B in one process).
+Interleaves the two implementations in one process (methodology rule: A/B in one process); every
+timed block follows ~0.1 s of back-to-back calls (the MI355X clock ramps over the first ~25 GEMMs)
+and spans >= 0.05 s, so 1024^3 and 4096^3 are timed over hundreds of launches, not 20.
 Prints one JSON line per shape. ``--variants`` takes production numbers (``p0`` = automatic
 dispatch of the shipped library, ``p44`` = pinned) or lab numbers (plain integers: the tools-only
 experiment library, tools/gemm_lab.py; build it with ``python -m gpu_operator_amd._build --lab``).
@@ -27,17 +29,42 @@ def time_fn(fn, iters, torch):
     return start.elapsed_time(end) / iters / 1e3
 
 
+class _Pinned:
+    """A callable (A, Bt, C) for a production ('p<v>') or lab ('<v>') variant. ``select()`` pins a
+    production variant once before a timed block, so the timed launches carry no variant switch."""
+
+    def __init__(self, G, spec: str, dtype: str):
+        self.G, self.dtype = G, dtype
+        if spec.startswith("p"):
+            self.v, self.lab = int(spec[1:]), None
+        else:
+            import gemm_lab
+            self.v, self.lab = int(spec), gemm_lab
+
+    def select(self):
+        if self.lab is None:
+            (self.G.set_variant if self.dtype == "bf16" else self.G.set_fp8_variant)(self.v)
+
+    def __call__(self, A, Bt, C):
+        if self.lab is not None:
+            f = self.lab.gemm_bf16 if self.dtype == "bf16" else self.lab.gemm_fp8
+            return f(self.v, A, Bt, C)
+        return (self.G.gemm_bf16 if self.dtype == "bf16" else self.G.gemm_fp8)(A, Bt, C)
+
+
 def runner(G, spec: str, dtype: str):
-    """A callable (A, Bt, C) for a production ('p<v>') or lab ('<v>') variant."""
-    if spec.startswith("p"):
-        v = int(spec[1:])
-        if dtype == "bf16":
-            return lambda A, Bt, C: (G.set_variant(v), G.gemm_bf16(A, Bt, C))
-        return lambda A, Bt, C: (G.set_fp8_variant(v), G.gemm_fp8(A, Bt, C))
-    import gemm_lab
-    v = int(spec)
-    return (lambda A, Bt, C: gemm_lab.gemm_bf16(v, A, Bt, C)) if dtype == "bf16" else \
-        (lambda A, Bt, C: gemm_lab.gemm_fp8(v, A, Bt, C))
+    return _Pinned(G, spec, dtype)
+
+
+def timed(fn, a, torch, select=None):
+    """Seconds per call: the clock ramped (~0.1 s of back-to-back calls first), then a block of at
+    least ``a.iters`` calls and ~0.05 s, so a short kernel is timed over many launches."""
+    if select:
+        select()
+    t = time_fn(fn, 5, torch)
+    n = max(3, int(0.1 / max(t, 1e-6)))
+    time_fn(fn, min(n, 5000), torch)
+    return time_fn(fn, max(a.iters, min(5000, int(0.05 / max(t, 1e-6)))), torch)
 
 
 def main():
@@ -70,18 +97,15 @@ def main():
         checks = {}
         for v in variants:
             C.zero_()
+            run[v].select()
             run[v](A, Bt, C)
             checks[v] = G.verify(A, Bt, C, nrows=16)
         ours = {v: [] for v in variants}
         blas = []
         for _ in range(a.rounds):
             for v in variants:
-                for _ in range(3):
-                    run[v](A, Bt, C)
-                ours[v].append(time_fn(lambda: run[v](A, Bt, C), a.iters, torch))
-            for _ in range(3):
-                torch.matmul(A, Bt.t())
-            blas.append(time_fn(lambda: torch.matmul(A, Bt.t(), out=C), a.iters, torch))
+                ours[v].append(timed(lambda: run[v](A, Bt, C), a, torch, run[v].select))
+            blas.append(timed(lambda: torch.matmul(A, Bt.t(), out=C), a, torch))
         t_b = min(blas)
         rec = {"m": m, "n": n, "k": k, "hipblaslt_tflops": round(G.tflops(m, n, k, t_b), 1)}
         for v in variants:
@@ -120,19 +144,16 @@ def sweep_fp8(a):
         checks = {}
         for v in variants:
             C.zero_()
+            run[v].select()
             run[v](A, Bt, C)
             checks[v] = G.verify(A, Bt, C, nrows=16)
         ours = {v: [] for v in variants}
         tb = []
         for _ in range(a.rounds):
             for v in variants:
-                for _ in range(3):
-                    run[v](A, Bt, C)
-                ours[v].append(time_fn(lambda: run[v](A, Bt, C), a.iters, torch))
+                ours[v].append(timed(lambda: run[v](A, Bt, C), a, torch, run[v].select))
             if blas_ok:
-                for _ in range(3):
-                    blas()
-                tb.append(time_fn(blas, a.iters, torch))
+                tb.append(timed(blas, a, torch))
         rec = {"dtype": "fp8_e4m3fn", "m": m, "n": n, "k": k,
                "hipblaslt_tflops": round(G.tflops(m, n, k, min(tb)), 1) if tb else None}
         for v in variants:
