@@ -87,6 +87,22 @@ typedef uint32_t w4a_u32x4 __attribute__((ext_vector_type(4)));
                  [m0b0] "s"(m0b0), [m0b1] "s"(m0b1), [flags] "s"(flags)                                          \
                : "memory", "scc", W4A_VCLOBBERS, W4_AGPR_CLOBBERS)
 
+// LEAN staging layout (EPI 15 / 16): 8-byte half h of 16-byte chunk c of a staged 256-byte C row r
+// sits at chunk c ^ ((r & 15) >> 1), half h ^ (r & 1). A ds_write_b64 lane group (16 lanes = 16 rows,
+// one chunk half; banks mod 32) lands on 16 distinct 8-byte slots of 128 bytes -- every bank once --
+// and each half-wave of a ds_read_b64 (2 rows x 16 chunks, one half each; banks mod 64) covers all 64
+// banks once, so neither side conflicts and a 16-byte row piece comes back as two 8-byte reads in
+// order (no lane-dependent swap). MI355X_MICROARCH.md, LDS banking table.
+__device__ __forceinline__ uint32_t lean_off(int r, int c, int h) {
+  return (uint32_t)(r * 256 + ((c ^ ((r & 15) >> 1)) << 4) + ((h ^ (r & 1)) << 3));
+}
+typedef uint32_t w4a_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ w4a_u32x4 lean_read(const char* stg, int r, int c) {
+  const w4a_u32x2 lo = *reinterpret_cast<const w4a_u32x2*>(stg + lean_off(r, c, 0));
+  const w4a_u32x2 hi = *reinterpret_cast<const w4a_u32x2*>(stg + lean_off(r, c, 1));
+  return w4a_u32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
 constexpr int W4AP_TILE = 256;                     // output tile edge
 constexpr int W4AP_ROW = 128;                      // bytes per staged K-row (one K-tile)
 constexpr int W4AP_PANEL = W4AP_TILE * W4AP_ROW;   // 32 KiB per operand per K-tile
@@ -131,8 +147,8 @@ constexpr int W4AP_EPI_WG512 = 10;      // ZC; the workgroup stages 512-byte C r
                                         // the shared 32 KiB, 2 barriers per pass: one store = 2 full rows
 constexpr int W4AP_EPI_STAGED_ZC = 8;   // staged nt; the K-loop's first K-tile starts accumulators with src C = 0,
                                         // so the epilogue only reads them (generated *_zc schedules)
-constexpr int W4AP_EPI_LEAN = 15;       // ZC, staged through 16-byte-chunk-swizzled LDS rows (a 16-byte read needs
-                                        // no lane-dependent half swap) and stored with global saddr stores: one
+constexpr int W4AP_EPI_LEAN = 15;       // ZC, staged through conflict-free swizzled LDS rows read back in 8-byte
+                                        // halves (lean_off: no lane-dependent half swap) and stored with global saddr stores: one
                                         // per-lane 32-bit offset for the whole tile, the row step in an SGPR base.
                                         // Removes the ~320 per-tile VALU ops (v_cndmask, 64-bit address math)
                                         // that the STAGED_ZC store loop compiles to
@@ -363,8 +379,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     } else if constexpr (EPI == W4AP_EPI_LEAN) {
       // 4 passes of 32 C rows x 128 columns through this wave's 8 KiB. Lane (r, j) of accumulator m*8+n
       // holds row 16m + r, columns 16n + 4j .. +3: the 8-byte half j & 1 of 16-byte chunk 2n + (j >> 1).
-      // Chunk c of staged row r sits at c ^ (r & 15): a ds_write_b64 half-wave covers 16 rows x one chunk
-      // pair = every bank once, and a row read back is a permutation of the row's 16 chunks (no conflicts).
+      // Staged through lean_off (bank-conflict free on both sides, no half swap on the way back).
       const int lr = lane & 15, lj = lane >> 4;
       const uint32_t vst = DM == 2 ? (uint32_t)lj * 64u * (uint32_t)N + (uint32_t)lr * 16u    // PA: rows 32 apart
                                    : (uint32_t)lj * 2u * (uint32_t)N + (uint32_t)lr * 16u;
@@ -397,7 +412,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
           v[2] = (__bf16)x2;
           v[3] = (__bf16)x3;
           const int c = 2 * n + (lj >> 1);
-          *reinterpret_cast<bf16x4*>(stg + (mm * 16 + lr) * 256 + ((c ^ lr) << 4) + ((lj & 1) << 3)) = v;
+          *reinterpret_cast<bf16x4*>(stg + lean_off(mm * 16 + lr, c, lj & 1)) = v;
         });
         asm volatile("" ::: "memory");     // a wave's LDS ops execute in order: no wait, no barrier
         if constexpr (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA landed
@@ -407,7 +422,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int r = k * 4 + lj;
-          rows[k] = *reinterpret_cast<const w4a_u32x4*>(stg + r * 256 + ((lr ^ (r & 15)) << 4));
+          rows[k] = lean_read(stg, r, lr);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -456,7 +471,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
           v[2] = (__bf16)x2;
           v[3] = (__bf16)x3;
           const int c = 2 * n + (lj >> 1);
-          *reinterpret_cast<bf16x4*>(buf + lr * 256 + ((c ^ lr) << 4) + ((lj & 1) << 3)) = v;
+          *reinterpret_cast<bf16x4*>(buf + lean_off(lr, c, lj & 1)) = v;
         });
       };
       auto load = [&](auto H, w4a_u32x4* rows) {
@@ -465,7 +480,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int r = k * 4 + lj;
-          rows[k] = *reinterpret_cast<const w4a_u32x4*>(buf + r * 256 + ((lr ^ r) << 4));
+          rows[k] = lean_read(buf, r, lr);
         }
       };
       auto store = [&](const w4a_u32x4* rows) {
