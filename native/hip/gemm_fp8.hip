@@ -22,7 +22,8 @@
 //       1.09x (v21), 16384x8192x8192 1.00x.
 //   22 / 23 (round 4): v21 / v20 in the VP DMA form with the A-panel pieces reading rows 32 apart (PA,
 //       DM 2; the p_zc schedule, gen_fp8_asm_loop.py VP) and the LEAN epilogue (EPI 15: chunk-swizzled
-//       staging, saddr C stores, gemm_w4ap.h). v22 replaces v21 as the default on the square raster:
+//       staging, saddr C stores, gemm_w4ap.h). v22 replaces v21 as the default on the square raster
+//       when both sides have >= 32 tiles (v21 stays ahead with a 16-tile side at short K):
 //       16384^2x1024 1.19x hipBLASLt (v21 1.13x), 12288^3 1.02x (v21 1.00x), 8192^2x2048 1.10x (1.08x),
 //       16384^3 1.035x (1.031x), 8192^3 1.035x (1.023x); profiles/r4_lean/. v23 is pinned-only.
 //   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 = that kernel pinned (no automatic switch; falls back when the
@@ -49,7 +50,9 @@ static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
   int v = g_fp8_variant;
   const bool ap_ok = cus == 256 && K % (2 * F8_BK) == 0 && K >= 4 * F8_BK && pgrid >= NXCD;
   if (v == 0 && ap_ok) {
-    v = (sq && nwg >= 2 * cus) ? 22 : 20;
+    // v22 needs >= 32 tiles on both sides: with a 16-tile side (4096) and short K it measured 3-6 %
+    // behind v21 (12288x4096x1024 2129 vs 2253 TF/s, 8192x4096x1024 1958 vs 2072; profiles/r4_sweep/rules2_fp8.jsonl)
+    v = (sq && nwg >= 2 * cus) ? ((M / F8_BM >= 32 && N / F8_BN >= 32) ? 22 : 21) : 20;
   } else if (v == 0) {
     v = sq ? 16 : 15;
     // Short K (<= 12 K-tiles) with several tiles per CU: the persistent block-scaled kernel hides
