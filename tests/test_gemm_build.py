@@ -177,7 +177,10 @@ def _audit_asm_pipeline(body, st):
     assert st["NumVgprs"] <= 256, st
     _no_compiler_agpr_access(body)
     mfma = len(re.findall(r"v_mfma_f32_16x16x32_bf16", body))
-    reads = body.count("ds_read_b128")
+    # 16-byte reads: fragment reads, and the staged epilogue's C rows (the LEAN forms read those as
+    # 8-byte halves, which hipcc may pair into ds_read2st64_b64)
+    reads = (body.count("ds_read_b128") + len(re.findall(r"\bds_read_b64\b", body)) // 2 +
+             len(re.findall(r"\bds_read2(?:st64)?_b64\b", body)))
     dma = len(re.findall(r"buffer_load_dwordx4 .* lds", body))
     # every K-tile in the asm block is 128 MFMAs fed by 32 fragment reads and 16 LDS-DMA pieces;
     # the persistent form adds the epilogue reads of the next tile's prologue
