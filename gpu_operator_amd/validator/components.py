@@ -531,12 +531,13 @@ def _gate_value(ctx: Context, key: str, default: float) -> float:
 def _run_local_hip(ctx: Context, floors: Optional[Dict[str, float]] = None,
                    plan: Optional[Dict[str, Any]] = None) -> List[Dict[str, Any]]:
     """The HIP workload in this process's container (HIP_VALIDATION_MODE=local)."""
-    from .workload_main import run_hip
+    from .workload_main import run_hip, stream_run
     floors = floors or {}
     plan = plan or {"full": None, "probe": []}
     t0 = ctx.clock()
     results = run_hip(ctx.env.get("GEMM_SHAPES", "8192").split(","), counters=ctx.env.get("GEMM_COUNTERS") == "1",
-                      run=ctx.run,
+                      # the real binaries: return at their last result line, not at their exit
+                      run=stream_run if ctx.run is subprocess.run else ctx.run,
                       dtype=ctx.env.get("GEMM_DTYPE", "bf16"), scaling=ctx.env.get("GEMM_SCALING") or None,
                       iters=int(ctx.env.get("GEMM_ITERS", "50")),
                       min_tflops=floors.get("bf16", 0.0), min_tflops_fp8=floors.get("fp8", 0.0),

@@ -75,6 +75,57 @@ def _json_lines(text: str) -> List[Dict]:
     return out
 
 
+def stream_run(cmd: List[str], capture_output: bool = True, text: bool = True, timeout: Optional[float] = None,
+               env: Optional[Dict[str, str]] = None) -> subprocess.CompletedProcess:
+    """subprocess.run for a workload binary whose output ends with ``{"event":"done","ok":..}``
+    (amd-gemm-validate): returns as soon as that line arrives, with the status it states, and leaves
+    the process's exit -- the HIP runtime's and the kernel driver's teardown of its GPU state, about
+    0.1 s after the last line on MI355X (tools/hipinit_probe.sh) -- to a reaper thread, so the HIP
+    barrier does not wait for it. Without the line (a crash, another binary) it is subprocess.run."""
+    import queue
+    import threading
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    lines: "queue.Queue[Optional[str]]" = queue.Queue()
+    err: List[str] = []
+
+    def pump_out():
+        for ln in p.stdout:
+            lines.put(ln)
+        lines.put(None)
+
+    def pump_err():
+        for ln in p.stderr:
+            err.append(ln)
+
+    pumps = [threading.Thread(target=f, daemon=True) for f in (pump_out, pump_err)]
+    for t in pumps:
+        t.start()
+    deadline = None if timeout is None else time.monotonic() + timeout
+    out: List[str] = []
+    while True:
+        try:
+            ln = lines.get(timeout=None if deadline is None else max(0.0, deadline - time.monotonic()))
+        except queue.Empty:
+            p.kill()
+            p.wait()
+            raise subprocess.TimeoutExpired(cmd, timeout, "".join(out), "".join(err))
+        if ln is None:
+            break
+        out.append(ln)
+        if '"done"' in ln:
+            try:
+                d = json.loads(ln)
+            except ValueError:
+                continue
+            if isinstance(d, dict) and d.get("event") == "done":
+                threading.Thread(target=p.wait, daemon=True).start()      # reap the exiting child
+                return subprocess.CompletedProcess(cmd, 0 if d.get("ok") else 1, "".join(out), "".join(err))
+    rc = p.wait(timeout=None if deadline is None else max(1.0, deadline - time.monotonic()))
+    pumps[1].join(5.0)                           # the rest of stderr (its pipe closed at exit)
+    return subprocess.CompletedProcess(cmd, rc, "".join(out), "".join(err))
+
+
 def run_json(cmd: List[str], run: Callable = subprocess.run, timeout: float = 600,
              visible: Optional[List[int]] = None) -> (int, List[Dict]):
     """Run a workload binary and parse its JSON lines. ``visible``: HIP_VISIBLE_DEVICES for the
@@ -86,7 +137,7 @@ def run_json(cmd: List[str], run: Callable = subprocess.run, timeout: float = 60
     p = run(cmd, capture_output=True, text=True, timeout=timeout, **kw)
     if p.stderr:
         sys.stderr.write(p.stderr[-4000:])
-    lines = _json_lines(p.stdout)
+    lines = [x for x in _json_lines(p.stdout) if x.get("event") != "done"]
     if visible is not None:
         for x in lines:
             if isinstance(x.get("device"), int) and 0 <= x["device"] < len(visible):
@@ -157,7 +208,7 @@ def _parse_devices(spec: Optional[str]) -> Optional[List[int]]:
 
 
 def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
-            run: Callable = subprocess.run, dtype: str = "bf16", scaling: Optional[str] = None,
+            run: Callable = stream_run, dtype: str = "bf16", scaling: Optional[str] = None,
             min_tflops: float = 0.0, min_tflops_fp8: float = 0.0, devices: Optional[List[int]] = None,
             probe_devices: Optional[List[int]] = None, min_relative: float = 0.0,
             min_efficiency: float = 0.0, dry_run: bool = False) -> List[Dict]:
@@ -206,7 +257,9 @@ def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
             results.append({"event": "gemm", "probe": True, "ok": False, "rc": rc})
     if counters and full:
         for d in (["bf16", "fp8"] if dtype == "both" else [dtype]):
-            results += collect_counters(shapes[0], run, dtype=d, visible=devices[:1] if devices else None)
+            # the profiler writes its counters from the child's exit path: wait for it (subprocess.run)
+            results += collect_counters(shapes[0], subprocess.run if run is stream_run else run, dtype=d,
+                                        visible=devices[:1] if devices else None)
     return results
 
 

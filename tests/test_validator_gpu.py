@@ -34,6 +34,7 @@ def test_gemm_validate_binary_checks_and_reports_tflops():
     assert all(g["stabilise_dispatches"] >= 50 for g in gemms)
     agg = [x for x in lines if x["event"] == "aggregate" and x["m"] == 8192][0]
     assert agg["per_gpu_tflops"] > 1200           # MI355X bf16, random operands, steady clock
+    assert lines[-1] == {"event": "done", "ok": True}     # where the validator stops reading
 
 
 def test_gemm_validate_scaling_sweep_on_one_gpu():

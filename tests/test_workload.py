@@ -143,3 +143,34 @@ def test_rccl_binary_passes_its_watchdog_deadline(monkeypatch):
     WM.run_rccl(8 << 30, "bf16", run=run, ranks="2,4,8")
     cmd = seen[0]
     assert cmd[cmd.index("--timeout-s") + 1] == "120" and cmd[cmd.index("--max-bytes") + 1] == str(8 << 30)
+
+
+def _script(tmp_path, name, body):
+    p = tmp_path / name
+    p.write_text("#!/bin/sh\n" + body)
+    p.chmod(p.stat().st_mode | stat.S_IEXEC)
+    return str(p)
+
+
+def test_stream_run_returns_at_the_done_line(tmp_path):
+    """amd-gemm-validate's last line is {"event":"done"}: the HIP step returns there and does not wait
+    for the process's exit (its GPU teardown), which a reaper thread collects later."""
+    fake = _script(tmp_path, "gemm", 'echo \'{"event":"gemm","ok":true}\'\necho \'{"event":"done","ok":true}\'\n'
+                                     'sleep 3\n')
+    t = time.monotonic()
+    rc, lines = WM.run_json([fake], WM.stream_run, timeout=30)
+    assert time.monotonic() - t < 2.0
+    assert rc == 0 and lines == [{"event": "gemm", "ok": True}]          # the done line is consumed
+    bad = _script(tmp_path, "bad", 'echo \'{"event":"gemm","ok":false}\'\necho \'{"event":"done","ok":false}\'\n')
+    assert WM.run_json([bad], WM.stream_run, timeout=30)[0] == 1
+
+
+def test_stream_run_without_done_line_waits_and_times_out(tmp_path):
+    crash = _script(tmp_path, "crash", 'echo \'{"event":"gemm","ok":true}\'\necho boom >&2\nexit 7\n')
+    p = WM.stream_run([crash], timeout=30)
+    assert p.returncode == 7 and "boom" in p.stderr
+    hang = _script(tmp_path, "hang", 'echo \'{"event":"start"}\'\nsleep 30\n')
+    t = time.monotonic()
+    with pytest.raises(subprocess.TimeoutExpired):
+        WM.stream_run([hang], timeout=1.0)
+    assert time.monotonic() - t < 5.0
