@@ -31,8 +31,10 @@
 //   50 / 51 / 52 = the asm pipeline: w4ap (gemm_bf16_kernels.h) with the g4 schedule, g4 on the square
 //        raster, the g6d6 schedule (tools/gen_bf16_asm_loop.py generates gemm_bf16_asm_loop.h).
 //   55 / 56 (round 4) = v53 / v54 with the A-panel pieces reading rows 32 apart (PA, DM 2) and the LEAN
-//        epilogue (EPI 15: chunk-swizzled staging, saddr C stores; v56 pipelines it over 8 half-passes, EPI
-//        16; gemm_w4ap.h): the power-of-two-K default for short K or one dispatch wave.
+//        epilogue (EPI 15: conflict-free staging, saddr C stores; v56 pipelines it over 8 half-passes and
+//        interleaves each half-pass's stores into the next one's staging, EPI 17 LEAN_ILV: 16384^2x1024
+//        +2.2 %, 8192^2x2048 +1.2 % over the plain pipeline, profiles/r4_sweep/lab_ilv_*.jsonl;
+//        gemm_w4ap.h): the power-of-two-K default for short K or one dispatch wave.
 //   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 = that kernel pinned (no automatic switch; still falls back to a kernel
 //        that can run the shape or the device).
 // Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
@@ -203,7 +205,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 56:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN_PIPE, 2>), dim3(256), dim3(W4_THREADS),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN_ILV, 2>), dim3(256), dim3(W4_THREADS),
                          0, s, a, b, c, M, N, K);
       break;
     case 52:

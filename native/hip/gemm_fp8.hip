@@ -21,7 +21,8 @@
 //       0.974-0.981x), 4096^3 1.04x, 16384^3 1.03x (v21), 16384^2x2048 1.05x (v21), 16384^2x1024
 //       1.09x (v21), 16384x8192x8192 1.00x.
 //   22 / 23 (round 4): v21 / v20 in the VP DMA form with the A-panel pieces reading rows 32 apart (PA,
-//       DM 2; the p_zc schedule, gen_fp8_asm_loop.py VP) and the LEAN epilogue (EPI 15: chunk-swizzled
+//       DM 2; the p_zc schedule, gen_fp8_asm_loop.py VP) and the LEAN epilogue (v22: its pipelined,
+//       store-interleaved form EPI 17, +0.4-0.5 % over EPI 15/16; v23: EPI 15 -- conflict-free
 //       staging, saddr C stores, gemm_w4ap.h). v22 replaces v21 as the default on the square raster
 //       when both sides have >= 32 tiles (v21 stays ahead with a 16-tile side at short K):
 //       16384^2x1024 1.19x hipBLASLt (v21 1.13x), 12288^3 1.02x (v21 1.00x), 8192^2x2048 1.10x (1.08x),
@@ -109,7 +110,7 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
                          a, b, c, M, N, K);
       break;
     case 22:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN, 2>), dim3(256), dim3(F8_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN_ILV, 2>), dim3(256), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 23:

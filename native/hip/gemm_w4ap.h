@@ -153,6 +153,7 @@ constexpr int W4AP_EPI_LEAN = 15;       // ZC, staged through conflict-free swiz
                                         // Removes the ~320 per-tile VALU ops (v_cndmask, 64-bit address math)
                                         // that the STAGED_ZC store loop compiles to
 constexpr int W4AP_EPI_LEAN_PIPE = 16;  // LEAN in 8 software-pipelined half-passes (double-buffered staging)
+constexpr int W4AP_EPI_LEAN_ILV = 17;   // LEAN_PIPE with each half-pass's stores interleaved into the next staging
 
 // What the staged epilogue does for an EPI value. The tools-only lab library specialises this for its
 // knock-out forms (native/hip/gemm_bf16_asm_lab.hip); the production forms are the primary template.
@@ -160,7 +161,7 @@ template <int EPI>
 struct W4apEpi {
   static constexpr bool run = true;                         // run the staged epilogue at all
   static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC || EPI == W4AP_EPI_WG512 || EPI == W4AP_EPI_LEAN ||
-                             EPI == W4AP_EPI_LEAN_PIPE;                             // K-loop zeroes (src C = 0)
+                             EPI == W4AP_EPI_LEAN_PIPE || EPI == W4AP_EPI_LEAN_ILV;  // K-loop zeroes (src C = 0)
   template <int S>                                          // pass S's 16-byte C store
   static __device__ __forceinline__ void store(__bf16* dst, uint4 v) {
     if constexpr (EPI == W4AP_EPI_STAGED) *reinterpret_cast<uint4*>(dst) = v;
@@ -437,7 +438,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         }
         asm volatile("" ::: "memory");
       });
-    } else if constexpr (EPI == W4AP_EPI_LEAN_PIPE) {
+    } else if constexpr (EPI == W4AP_EPI_LEAN_PIPE || EPI == W4AP_EPI_LEAN_ILV) {
       // LEAN in 8 half-passes of 16 rows (one accumulator row block each) through two 4 KiB halves of
       // the wave's staging, software-pipelined: half-pass h + 1's accumulator reads, cvts and LDS writes
       // run while half-pass h's row reads land, then h's 4 stores go out (order W0 R0 | W1 R1 S0 | W2 R2
@@ -454,7 +455,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       // (k >> 1)]: the pointer walks 16 wr + 2 h, read k adds 128 (k & 1) + (k >> 1) rows
       uint64_t cp = cbase + (uint64_t)(DM == 2 ? 16 * wr : 128 * wr) * rowb;
       const uint64_t c1 = rowb, c128 = 128 * rowb, c129 = 129 * rowb, c4 = 4 * rowb, c2 = 2 * rowb;
-      auto stage = [&](auto H) {
+      auto stage = [&](auto H, auto&& after) {
         constexpr int h = decltype(H)::value;
         char* const buf = stg + (h & 1) * 4096;
         static_for<0, 8>([&](auto I) {
@@ -472,8 +473,10 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
           v[3] = (__bf16)x3;
           const int c = 2 * n + (lj >> 1);
           *reinterpret_cast<bf16x4*>(buf + lean_off(lr, c, lj & 1)) = v;
+          after(I);
         });
       };
+      auto nothing = [](auto) {};
       auto load = [&](auto H, w4a_u32x4* rows) {
         constexpr int h = decltype(H)::value;
         const char* const buf = stg + (h & 1) * 4096;
@@ -483,37 +486,45 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
           rows[k] = lean_read(buf, r, lr);
         }
       };
-      auto store = [&](const w4a_u32x4* rows) {
+      auto store_one = [&](const w4a_u32x4* rows, int k) {
         const uint32_t vs = vst;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          uint64_t base = cp;
-          if (DM == 2) base = cp + (k == 0 ? 0 : k == 1 ? c128 : k == 2 ? c1 : c129);
-          // s_nop: the store's data VGPRs may be rewritten by the next VALU (one wait state)
-          asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 0" :: "v"(vs), "v"(rows[k]), "s"(base) : "memory");
-          if (DM != 2) {
-            cp += c4;
-            asm volatile("" : "+s"(cp));
-          }
-        }
-        if (DM == 2) {
-          cp += c2;
+        uint64_t base = cp;
+        if (DM == 2) base = cp + (k == 0 ? 0 : k == 1 ? c128 : k == 2 ? c1 : c129);
+        // s_nop: the store's data VGPRs may be rewritten by the next VALU (one wait state)
+        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 0" :: "v"(vs), "v"(rows[k]), "s"(base) : "memory");
+        if (DM != 2 || k == 3) {
+          cp += DM == 2 ? c2 : c4;
           asm volatile("" : "+s"(cp));
         }
       };
+      auto store = [&](const w4a_u32x4* rows) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) store_one(rows, k);
+      };
       w4a_u32x4 ra[4], rb[4];
-      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 0>{}, nothing);
       load(std::integral_constant<int, 0>{}, ra);
       static_for<0, 8>([&](auto H) {
         constexpr int h = decltype(H)::value;
-        if constexpr (h + 1 < 8) {
-          stage(std::integral_constant<int, h + 1>{});
+        const w4a_u32x4* const cur = (h & 1) ? rb : ra;
+        if constexpr (EPI == W4AP_EPI_LEAN_ILV && h + 1 < 8) {
+          // ILV: half-pass h's 4 stores ride between half-pass h + 1's accumulator stagings (one after
+          // every second ds_write), so no store burst stalls the VALU stream
+          if constexpr (h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          stage(std::integral_constant<int, h + 1>{}, [&](auto I) {
+            if constexpr (decltype(I)::value & 1) store_one(cur, decltype(I)::value >> 1);
+          });
           load(std::integral_constant<int, h + 1>{}, (h & 1) ? ra : rb);
+        } else {
+          if constexpr (h + 1 < 8) {
+            stage(std::integral_constant<int, h + 1>{}, nothing);
+            load(std::integral_constant<int, h + 1>{}, (h & 1) ? ra : rb);
+          }
+          // the next tile's DMA landed before any C store (its K-loop's landing waits count only its
+          // own pieces); waiting here, not before half-pass 1, gives the DMA two half-passes of cover
+          if constexpr (h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          store(cur);
         }
-        // the next tile's DMA landed before any C store (its K-loop's landing waits count only its own
-        // pieces); waiting here, not before half-pass 1, gives the DMA two half-passes of cover
-        if constexpr (h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        store((h & 1) ? rb : ra);
       });
       asm volatile("" ::: "memory");
     } else if constexpr (!W4apEpi<EPI>::run) {
