@@ -20,7 +20,8 @@
 //   218 / 219 = VP + PA G4_ZC with LEAN / STAGED_ZC, 222 = 218 on the square raster; 223 / 224 = VP
 //   G4_ZC square raster with LEAN / STAGED_ZC (224 = production v54); 225 / 226 / 227 = LEAN_PIPE (EPI 16,
 //   pipelined half-passes): 197 / 218 / 222 with it; fp8 274 = 272 with it, 275 = 265 with it; 228 / 229 /
-//   fp8 276 = LEAN_ILV (EPI 17, stores interleaved into the next staging): 227 / 225 / 274 with it;
+//   fp8 276 = LEAN_ILV (EPI 17, stores interleaved into the next staging): 227 / 225 / 274 with it; 238 /
+//   fp8 277 = 228 / 276 with LEAN_ILVB (EPI 18, burst accumulator reads);
 //   fp8 269 / 270 = 265 / 266 with it; 271 = VP + PA p_zc square raster (262 + ZC), 272 = 271 + LEAN,
 //   273 = VP + PA p_zc linear raster + LEAN
 //   211-214 = 197 with store cache policy sc1 nt / sc0 sc1 / sc0 sc1 nt / sc0 nt
@@ -341,6 +342,11 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
                          s, a, b, c, M, N, K);
       break;
     }
+    case 238:     // 228 with LEAN_ILVB (EPI 18: a half-pass's accumulators read in one burst)
+      if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN_ILVB, 2>), dim3(256), dim3(W4_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
     case 216:     // LEAN epilogue on the square raster (198 + EPI 15)
       if ((M / BM) % 16 || (N / BN) % 16 || device_cu_count() != 256) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_G4_ZC, true, true, W4AP_EPI_LEAN>), dim3(256), dim3(W4_THREADS), 0,
@@ -499,6 +505,11 @@ int amdgo_asmlab_gemm_fp8(int v, const void* A, const void* Bt, void* C, int M, 
     case 276:     // 274 with LEAN_ILV (EPI 17)
       if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN_ILV, 2>), dim3(256), dim3(F8_THREADS),
+                         0, s, a, b, c, M, N, K);
+      break;
+    case 277:     // 276 with LEAN_ILVB (EPI 18)
+      if (g < NXCD || !sq) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN_ILVB, 2>), dim3(256), dim3(F8_THREADS),
                          0, s, a, b, c, M, N, K);
       break;
     case 269:     // LEAN epilogue (EPI 15) for v20 (p_zc, linear K)

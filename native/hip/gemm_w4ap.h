@@ -154,6 +154,7 @@ constexpr int W4AP_EPI_LEAN = 15;       // ZC, staged through conflict-free swiz
                                         // that the STAGED_ZC store loop compiles to
 constexpr int W4AP_EPI_LEAN_PIPE = 16;  // LEAN in 8 software-pipelined half-passes (double-buffered staging)
 constexpr int W4AP_EPI_LEAN_ILV = 17;   // LEAN_PIPE with each half-pass's stores interleaved into the next staging
+constexpr int W4AP_EPI_LEAN_ILVB = 18;  // LEAN_ILV reading a half-pass's accumulators in one burst (lab)
 
 // What the staged epilogue does for an EPI value. The tools-only lab library specialises this for its
 // knock-out forms (native/hip/gemm_bf16_asm_lab.hip); the production forms are the primary template.
@@ -161,7 +162,8 @@ template <int EPI>
 struct W4apEpi {
   static constexpr bool run = true;                         // run the staged epilogue at all
   static constexpr bool zc = EPI == W4AP_EPI_STAGED_ZC || EPI == W4AP_EPI_WG512 || EPI == W4AP_EPI_LEAN ||
-                             EPI == W4AP_EPI_LEAN_PIPE || EPI == W4AP_EPI_LEAN_ILV;  // K-loop zeroes (src C = 0)
+                             EPI == W4AP_EPI_LEAN_PIPE || EPI == W4AP_EPI_LEAN_ILV ||
+                             EPI == W4AP_EPI_LEAN_ILVB;                            // K-loop zeroes (src C = 0)
   template <int S>                                          // pass S's 16-byte C store
   static __device__ __forceinline__ void store(__bf16* dst, uint4 v) {
     if constexpr (EPI == W4AP_EPI_STAGED) *reinterpret_cast<uint4*>(dst) = v;
@@ -438,7 +440,8 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
         }
         asm volatile("" ::: "memory");
       });
-    } else if constexpr (EPI == W4AP_EPI_LEAN_PIPE || EPI == W4AP_EPI_LEAN_ILV) {
+    } else if constexpr (EPI == W4AP_EPI_LEAN_PIPE || EPI == W4AP_EPI_LEAN_ILV || EPI == W4AP_EPI_LEAN_ILVB) {
+      constexpr bool ILV = EPI != W4AP_EPI_LEAN_PIPE;
       // LEAN in 8 half-passes of 16 rows (one accumulator row block each) through two 4 KiB halves of
       // the wave's staging, software-pipelined: half-pass h + 1's accumulator reads, cvts and LDS writes
       // run while half-pass h's row reads land, then h's 4 stores go out (order W0 R0 | W1 R1 S0 | W2 R2
@@ -458,6 +461,36 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       auto stage = [&](auto H, auto&& after) {
         constexpr int h = decltype(H)::value;
         char* const buf = stg + (h & 1) * 4096;
+        if constexpr (EPI == W4AP_EPI_LEAN_ILVB) {
+          // ILVB: the half-pass's 32 accumulator registers in one read burst, then the cvts and LDS
+          // writes -- no accvgpr-read -> VALU wait state per accumulator
+          float x[32];
+          static_for<0, 8>([&](auto I) {
+            constexpr int i = h * 8 + decltype(I)::value;
+            constexpr int q = 4 * decltype(I)::value;
+            float a0, a1, a2, a3;        // (asm operands cannot name the enclosing lambda's array)
+            asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                         "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                         : "=v"(a0), "=v"(a1), "=v"(a2), "=v"(a3)
+                         : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+            x[q] = a0;
+            x[q + 1] = a1;
+            x[q + 2] = a2;
+            x[q + 3] = a3;
+          });
+          static_for<0, 8>([&](auto I) {
+            constexpr int n = decltype(I)::value;
+            bf16x4 v;
+            v[0] = (__bf16)x[4 * n];
+            v[1] = (__bf16)x[4 * n + 1];
+            v[2] = (__bf16)x[4 * n + 2];
+            v[3] = (__bf16)x[4 * n + 3];
+            const int c = 2 * n + (lj >> 1);
+            *reinterpret_cast<bf16x4*>(buf + lean_off(lr, c, lj & 1)) = v;
+            after(I);
+          });
+          return;
+        }
         static_for<0, 8>([&](auto I) {
           constexpr int n = decltype(I)::value;
           constexpr int i = h * 8 + n;
@@ -507,7 +540,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       static_for<0, 8>([&](auto H) {
         constexpr int h = decltype(H)::value;
         const w4a_u32x4* const cur = (h & 1) ? rb : ra;
-        if constexpr (EPI == W4AP_EPI_LEAN_ILV && h + 1 < 8) {
+        if constexpr (ILV && h + 1 < 8) {
           // ILV: half-pass h's 4 stores ride between half-pass h + 1's accumulator stagings (one after
           // every second ds_write), so no store burst stalls the VALU stream
           if constexpr (h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
