@@ -562,6 +562,17 @@ def _local_workload(ctx: Context, mode: str) -> Dict[str, Any]:
     return info
 
 
+_CORRECTNESS_MARKS = ("check failed", "max_rel_err", "hip-smoke", "probe device", "error", "oom", "out of memory")
+_THROUGHPUT_MARKS = ("TFLOP/s", "floor", "efficiency", "median", "slow devices")
+
+
+def _throughput_only(bad: List[str]) -> bool:
+    """Every gate failure is a throughput gate (floor, node median, scaling efficiency, uniformity);
+    none is a wrong result, a failed smoke test or a probe failure."""
+    return bool(bad) and all(any(m in b for m in _THROUGHPUT_MARKS) and not any(m in b for m in _CORRECTNESS_MARKS)
+                             for b in bad)
+
+
 def validate_hip(ctx: Context) -> Dict[str, Any]:
     """hip-smoke + the MFMA GEMM probe (bf16 and fp8, 1/2/4/8-GPU sweep), gated on correctness, on
     per-GPU throughput floors (models/ defaults, spec.validator.hip.env overrides), on the node
@@ -580,24 +591,36 @@ def validate_hip(ctx: Context) -> Dict[str, Any]:
     floors = gemm_floors(ctx, gpus)
     busy = gpu_pods_on_node(ctx)
     plan = hip_plan(ctx, busy, gpus)
-    if mode == "local":
-        results = _run_local_hip(ctx, floors, plan)
-    else:
-        env = _hip_env(ctx, floors, plan)
-        if dry:
-            env["GEMM_DRY_RUN"] = "1"
-        res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                                 env, timeout=ctx.pod_timeout)
-        results = res["results"]
-    info = summarize_gemm(results)
-    info["floors_tflops"] = floors
-    info["plan"] = {"full": "all" if plan["full"] is None else plan["full"], "probe": plan["probe"],
-                    "attribution": plan["attribution"], **({"busy_pods": busy[:16]} if busy else {})}
-    if busy:
-        info["busy"] = f"{len(busy)} GPU pod(s) on the node hold {len(plan['held_bdfs'])} GPU(s) " \
-                       f"({plan['attribution']}): full sweep on {len(plan['full'])} free, probe on {len(plan['probe'])}"
-    bad = gate_gemm(info, floors, busy, min_relative=_gate_value(ctx, "GEMM_MIN_RELATIVE", GEMM_MIN_RELATIVE),
-                    min_efficiency=_gate_value(ctx, "GEMM_MIN_EFFICIENCY", GEMM_MIN_EFFICIENCY))
+
+    def measure():
+        if mode == "local":
+            results = _run_local_hip(ctx, floors, plan)
+        else:
+            env = _hip_env(ctx, floors, plan)
+            if dry:
+                env["GEMM_DRY_RUN"] = "1"
+            res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                                     env, timeout=ctx.pod_timeout)
+            results = res["results"]
+        info = summarize_gemm(results)
+        info["floors_tflops"] = floors
+        info["plan"] = {"full": "all" if plan["full"] is None else plan["full"], "probe": plan["probe"],
+                        "attribution": plan["attribution"], **({"busy_pods": busy[:16]} if busy else {})}
+        if busy:
+            info["busy"] = f"{len(busy)} GPU pod(s) on the node hold {len(plan['held_bdfs'])} GPU(s) " \
+                           f"({plan['attribution']}): full sweep on {len(plan['full'])} free, probe on {len(plan['probe'])}"
+        bad = gate_gemm(info, floors, busy, min_relative=_gate_value(ctx, "GEMM_MIN_RELATIVE", GEMM_MIN_RELATIVE),
+                        min_efficiency=_gate_value(ctx, "GEMM_MIN_EFFICIENCY", GEMM_MIN_EFFICIENCY))
+        return info, bad
+
+    info, bad = measure()
+    if bad and _throughput_only(bad) and ctx.env.get("GEMM_REMEASURE", "1") != "0":
+        # a throughput gate alone (every result correct): measure once more before failing the node,
+        # so a transient clock or power event costs seconds, not a crash-loop back-off
+        log.warning("HIP validation: %s -- measuring once more", bad[:4])
+        first = bad
+        info, bad = measure()
+        info["remeasured"] = {"first_failure": first[:8]}
     if bad:
         raise ValidationError(f"HIP validation failed: {bad[:8]}")
     ctx.status.create(S.HIP_READY, info)

@@ -26,7 +26,8 @@
 //       staging, saddr C stores, gemm_w4ap.h). v22 replaces v21 as the default on the square raster
 //       when both sides have >= 32 tiles (v21 stays ahead with a 16-tile side at short K):
 //       16384^2x1024 1.19x hipBLASLt (v21 1.13x), 12288^3 1.02x (v21 1.00x), 8192^2x2048 1.10x (1.08x),
-//       16384^3 1.035x (1.031x), 8192^3 1.035x (1.023x); profiles/r4_lean/. v23 is pinned-only.
+//       16384^3 1.035x (1.031x), 8192^3 1.035x (1.023x); profiles/r4_lean/. One dispatch wave: v22 (v23 off the
+//       16x16-tile multiples).
 //   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 = that kernel pinned (no automatic switch; falls back when the
 //       shape or the device cannot run it).
 // q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
@@ -51,9 +52,15 @@ static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
   int v = g_fp8_variant;
   const bool ap_ok = cus == 256 && K % (2 * F8_BK) == 0 && K >= 4 * F8_BK && pgrid >= NXCD;
   if (v == 0 && ap_ok) {
-    // v22 needs >= 32 tiles on both sides: with a 16-tile side (4096) and short K it measured 3-6 %
-    // behind v21 (12288x4096x1024 2129 vs 2253 TF/s, 8192x4096x1024 1958 vs 2072; profiles/r4_sweep/rules2_fp8.jsonl)
-    v = (sq && nwg >= 2 * cus) ? ((M / F8_BM >= 32 && N / F8_BN >= 32) ? 22 : 21) : 20;
+    // v22 on multi-wave square grids needs >= 32 tiles on both sides or K >= 4096: with a 16-tile side
+    // and short K it measured 3-6 % behind v21 (12288x4096x1024 2129 vs 2253 TF/s, 8192x4096x1024 1958
+    // vs 2072; profiles/r4_sweep/rules2_fp8.jsonl). One dispatch wave: v22, or v23 off the 16x16-tile
+    // multiples (4096^3 2996 vs v20 2957, 4096^2x8192 +1.3 %, 2048x4096x4096 1.010x vs 0.997x;
+    // profiles/r4_sweep/onewave_fp8.jsonl).
+    const bool wide = M / F8_BM >= 32 && N / F8_BN >= 32;
+    if (nwg <= cus) v = sq ? 22 : 23;
+    else if (sq && nwg >= 2 * cus) v = (wide || K >= 4096) ? 22 : 21;
+    else v = 20;
   } else if (v == 0) {
     v = sq ? 16 : 15;
     // Short K (<= 12 K-tiles) with several tiles per CU: the persistent block-scaled kernel hides

@@ -161,7 +161,9 @@ def test_fp8_production_variant_set_is_closed(cuda_device):
         assert G.resolve_fp8_variant(16384, 16384, 1024) == 22
         assert G.resolve_fp8_variant(12288, 12288, 12288) == 22
         assert G.resolve_fp8_variant(12288, 4096, 1024) == 21            # a 16-tile side keeps v21
-        assert G.resolve_fp8_variant(4096, 4096, 4096) == 20
+        assert G.resolve_fp8_variant(4096, 4096, 4096) == 22                # one dispatch wave
+        assert G.resolve_fp8_variant(2048, 4096, 4096) == 23                # one wave, not 16x16-tile multiples
+        assert G.resolve_fp8_variant(4096, 8192, 4096) == 22                # a 16-tile side, K >= 4096
         assert G.resolve_fp8_variant(4096 + 256, 4096, 4096) == 20
         assert G.resolve_fp8_variant(8192, 8192, 8192 + 128) in (16, 18)   # odd K-tile count
     assert G.resolve_fp8_variant(300, 256, 256) == 0

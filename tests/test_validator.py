@@ -53,6 +53,8 @@ class FakeKubelet:
         self.seen.append(pod)
         app = o.get_labels(pod).get("app")
         msg = self.messages.get(app, "")
+        if isinstance(msg, list):               # one message per pod, the last one repeats
+            msg = msg.pop(0) if len(msg) > 1 else msg[0]
 
         def finish():
             time.sleep(0.05)
@@ -430,6 +432,26 @@ def test_hip_below_floor_opens_no_barrier(tmp_path, node_root):
     assert env["GEMM_MIN_TFLOPS_BF16"] == "1258.3" and env["GEMM_SCALING"] == "1,2,4,8"
     assert env["GEMM_MIN_RELATIVE"] == "0.85" and env["GEMM_MIN_EFFICIENCY"] == "0.9"
     assert "GEMM_DEVICES" not in env and "GEMM_PROBE_DEVICES" not in env       # an idle node: every GPU
+
+
+def test_hip_throughput_failure_is_measured_once_more(tmp_path, node_root):
+    """A throughput gate alone (every result correct) re-measures once before failing the node: a
+    transient costs one more run, not a crash-loop back-off. A persistent one still fails."""
+    c = FakeClient([node_obj()])
+    k = FakeKubelet(c, {"amd-hip-validator": [_gemm_msg(600.0), _gemm_msg(1500.0)]})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    info = comp.validate_hip(ctx)
+    assert ctx.status.exists(S.HIP_READY) and len(k.seen) == 2
+    assert "below the 1258.3 floor" in info["remeasured"]["first_failure"][0]
+    # a wrong result is never re-measured
+    bad = _gemm_msg(1500.0).replace('"tflops": 1500.0, "ok": true', '"tflops": 1500.0, "ok": false')
+    c2 = FakeClient([node_obj()])
+    k2 = FakeKubelet(c2, {"amd-hip-validator": bad})
+    with pytest.raises(comp.ValidationError, match="check failed"):
+        comp.validate_hip(ctx_for(tmp_path / "b", node_root, client=c2))
+    assert len(k2.seen) == 1
+    assert comp._throughput_only(["gemm bf16 device 0: below floor: 329.1 < 1258.3 TFLOP/s"])
+    assert not comp._throughput_only(["gemm bf16 device 0: check failed", "gemm bf16 device 1: below floor: 1 < 2 TFLOP/s"])
 
 
 def test_hip_records_the_scaling_sweep(tmp_path, node_root):
