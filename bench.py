@@ -19,9 +19,11 @@ Timing protocol per rank: ``--warmup`` untimed steps, then a *clock-stabilisatio
 (outside the timed region) that keeps issuing GEMMs until the per-dispatch event times of the
 last 10 dispatches agree within 2 % (at least 50 dispatches, capped in time) -- MI355X
 ramps its clocks over the first ~25 back-to-back GEMMs (profiles/r1_s6_sq), and timing that
-transient under-reports steady-state throughput. Then exactly ``--steps`` steps are timed,
-bracketed by barrier + synchronize on both sides, MAX over ranks. Per-step event times give
-the median / p90. The same protocol is then applied, in the same process, to
+transient under-reports steady-state throughput. Every rank then meets at the barrier; a rank that
+stabilised early idles there and its clock drops, so after the barrier each rank re-ramps (at least
+10 untimed dispatches and ``--ramp-ms`` of work, then a synchronize; the ranks ramp together, so the
+barrier after it is short). Then exactly ``--steps`` steps are timed, bracketed by barrier + synchronize on both sides, MAX over ranks. Per-step event
+times give the median / p90. The same protocol is then applied, in the same process, to
 ``torch.matmul`` on the same operands (hipBLASLt) so ``ratio_vs_hipblaslt`` is checkable.
 
 After the timed region the job also reports the fp8 kernel at the same shape, the RCCL
@@ -57,6 +59,10 @@ def parse_args(argv=None):
                     help="payload of the post-timing RCCL all-reduce probe (N>1)")
     ap.add_argument("--stabilise-max-s", type=float, default=6.0,
                     help="time cap of the clock-stabilisation phase (outside the timed region)")
+    ap.add_argument("--ramp-ms", type=float, default=60.0,
+                    help="untimed re-ramp after the pre-timing barrier (GPU time, at least 10 dispatches)")
+    ap.add_argument("--pre-timed-idle-ms", type=float, default=0.0,
+                    help="test hook: host idle after the pre-timing barrier, before the re-ramp")
     ap.add_argument("--no-extras", action="store_true", help="skip fp8/hipBLASLt/all-reduce/validation extras")
     ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
                     help="cpu = rehearsal of the distributed plumbing (gloo, torch.matmul) for tests only")
@@ -79,10 +85,25 @@ def _free_port() -> int:
 
 
 def _visible_gpus() -> int:
-    """Device count without initialising the GPU in this (launcher) process."""
-    import torch
-
-    return int(torch.cuda.device_count())
+    """GPU count without initialising the GPU or the HIP runtime in this (launcher) process: the
+    KFD agents of sysfs that this container may use (KFD hides the properties of agents the device
+    cgroup denies), narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES the way the runtime
+    narrows them. torch's count only when sysfs cannot answer (no KFD topology here)."""
+    sys.path.insert(0, ROOT)
+    try:
+        from gpu_operator_amd import devices as D
+        n = len(D.enumerate_gpus("/"))
+    except Exception:  # noqa: BLE001 - no native library / no sysfs: ask torch
+        n = 0
+    if n == 0:
+        import torch
+        return int(torch.cuda.device_count())
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        spec = os.environ.get(var, "").strip()
+        if spec:
+            ids = [x for x in spec.split(",") if x.strip()]
+            n = sum(1 for x in ids if not x.strip().isdigit() or int(x) < n)
+    return n
 
 
 def launch(args, argv) -> int:
@@ -173,10 +194,13 @@ def main(argv=None) -> int:
     res = ctx.timed(step, args.steps, args.warmup)
     per_gpu = G.tflops(m, n, k, res["elapsed_s"] / args.steps)
     extras.update(per_gpu_tflops=_r(per_gpu), stabilise_dispatches=res["stabilise_dispatches"],
-                  stabilise_spread=res["stabilise_spread"],
+                  stabilise_spread=res["stabilise_spread"], ramp_dispatches=res["ramp_dispatches"],
                   step_ms_median=res["median_ms"], step_ms_p90=res["p90_ms"])
     if res["median_ms"]:
         extras["per_gpu_tflops_at_median"] = _r(G.tflops(m, n, k, res["median_ms"] / 1e3))
+    if res["events_ms"]:
+        # this rank's timed loop on GPU events (the headline is the host clock, MAX over ranks)
+        extras["per_gpu_tflops_events"] = _r(G.tflops(m, n, k, res["events_ms"] / 1e3 / args.steps))
     # the headline takes the slowest rank's clock (MAX over ranks); each rank's own loop shows
     # whether one GPU is slow
     rank_tf = [G.tflops(m, n, k, t / args.steps) for t in res["per_rank_s"]]
@@ -271,9 +295,10 @@ class Ctx:
     def stabilise(self, step, min_dispatches=50, window=10, tol=0.02, batch=10):
         """Issue back-to-back dispatches in batches of ``batch`` (event between each) until the
         last ``window`` per-dispatch times spread by < ``tol`` of their median, with at least
-        ``min_dispatches`` and at most ``--stabilise-max-s`` seconds. Returns (count, spread)."""
+        ``min_dispatches`` and at most ``--stabilise-max-s`` seconds. Returns (count, spread, median
+        per-dispatch ms of the last window)."""
         if self.cpu:
-            return 0, None
+            return 0, None, None
         torch = self.torch
         t_end = time.perf_counter() + self.args.stabilise_max_s
         times, count, spread = [], 0, None
@@ -290,16 +315,35 @@ class Ctx:
             med = last[len(last) // 2]
             spread = (last[-1] - last[0]) / med if med > 0 else 0.0
             if (count >= min_dispatches and spread < tol) or time.perf_counter() > t_end:
-                return count, round(spread, 4)
+                return count, round(spread, 4), med
+
+    def reramp(self, step, stab_ms) -> int:
+        """After the pre-timing barrier: at least 10 untimed dispatches and ``--ramp-ms`` of GPU
+        time (sized from the stabilised dispatch time), then a synchronize -- the clock a rank lost
+        idling at the barrier is back before the timed loop starts. Returns the dispatch count."""
+        if self.cpu:
+            return 0
+        if self.args.pre_timed_idle_ms > 0:
+            time.sleep(self.args.pre_timed_idle_ms / 1e3)
+        n = 10
+        if stab_ms:
+            n = max(n, int(-(-self.args.ramp_ms // stab_ms)))
+        for _ in range(n):
+            step()
+        self.sync()
+        return n
 
     def timed(self, step, steps, warmup):
         torch = self.torch
         for _ in range(warmup):
             step()
         self.sync()
-        n_stab, spread = self.stabilise(step)
+        n_stab, spread, stab_ms = self.stabilise(step)
         self.sync()
         self.barrier()
+        self.sync()
+        ramp = self.reramp(step, stab_ms)
+        self.barrier()            # the ranks ramped together: this wait is short (the contract's barrier)
         self.sync()
         evs = None if self.cpu else [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
         t0 = time.perf_counter()
@@ -318,6 +362,8 @@ class Ctx:
         per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else []
         med, p90 = _pct(per, 0.5), _pct(per, 0.9)
         return {"elapsed_s": elapsed, "per_rank_s": per_rank, "stabilise_dispatches": n_stab, "stabilise_spread": spread,
+                "ramp_dispatches": ramp,
+                "events_ms": round(sum(per), 4) if per else None,
                 "median_ms": round(med, 4) if med is not None else None,
                 "p90_ms": round(p90, 4) if p90 is not None else None}
 

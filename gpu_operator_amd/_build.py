@@ -103,8 +103,10 @@ TARGETS: List[Target] = [
     Target("bin/amd-barrier-wait", ["node/barrier_wait.cpp", "node/amdnode.cpp"], "cxx-exe",
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
     # Validator workload binaries (run inside the validation pods).
-    Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/smoke.hip"],
-           "hip-exe", flags=["-x", "hip"], headers=GEMM_HEADERS),
+    # (one worker process per GPU: the launcher enumerates the GPUs from KFD sysfs, libamdnode)
+    Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/smoke.hip",
+                                     "node/amdnode.cpp"],
+           "hip-exe", flags=["-x", "hip"], headers=GEMM_HEADERS + ["include/amdnode.h"]),
     Target("bin/amd-hip-smoke", ["hip/hip_smoke_main.cpp", "hip/smoke.hip"], "hip-exe", flags=["-x", "hip"]),
     Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp", "node/amdnode.cpp"], "hip-exe", flags=["-x", "hip"],
            libs=["-lrccl"], headers=["include/amdnode.h"]),

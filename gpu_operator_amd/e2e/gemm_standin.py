@@ -1,0 +1,78 @@
+"""A scripted stand-in for ``amd-gemm-validate`` (CPU rehearsals of the validation pods).
+
+The e2e harness and the validation-pod tests run the real validator, the real workload entry
+(``amd-validator-workload hip``) and a real kubelet's pod semantics on CPU; only the GEMM itself is
+scripted. This program speaks the binary's protocol -- the same argv, the same JSON lines (``start``,
+``hip-smoke``, one ``gemm`` line per GPU with its ``kind`` on failure, ``aggregate``, ``done``), the
+same exit status, the same floor gate -- for the GPUs HIP_VISIBLE_DEVICES names (device numbers in
+its output are visible indices, as the binary's are).
+
+Script (environment):
+  GEMM_STANDIN_SCRIPT   runs separated by ";" -- "fast", or "slow:3,5" (node GPUs 3 and 5 at 600
+                        TF/s, the others at 1500); run k uses entry k, the last entry repeats
+  GEMM_STANDIN_STATE    file counting the runs (also ``<state>.running`` exists while one runs)
+  GEMM_STANDIN_RUNTIME_S  how long a run takes (default 1)
+  GEMM_STANDIN_GPUS     GPUs without HIP_VISIBLE_DEVICES (default 8)
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from typing import List
+
+
+def _arg(argv: List[str], name: str, default: str = "") -> str:
+    return argv[argv.index(name) + 1] if name in argv and argv.index(name) + 1 < len(argv) else default
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    state = os.environ.get("GEMM_STANDIN_STATE", "")
+    runs = 0
+    if state and os.path.exists(state):
+        with open(state) as f:
+            runs = int(f.read().strip() or 0)
+    if state:
+        with open(state, "w") as f:
+            f.write(str(runs + 1))
+        open(state + ".running", "w").close()
+    script = [x for x in os.environ.get("GEMM_STANDIN_SCRIPT", "fast").split(";") if x] or ["fast"]
+    entry = script[min(runs, len(script) - 1)]
+    slow = {int(x) for x in entry.split(":", 1)[1].split(",") if x} if entry.startswith("slow:") else set()
+    vis = os.environ.get("HIP_VISIBLE_DEVICES", "")
+    nodes = [int(x) for x in vis.split(",") if x.strip()] if vis else \
+        list(range(int(os.environ.get("GEMM_STANDIN_GPUS", "8"))))
+    m = n = k = int(_arg(argv, "--shapes", "8192").split(",")[0].split("x")[0])
+    floor = float(_arg(argv, "--min-tflops", "0") or 0)
+    floors_apply = m * n >= 256 * 65536 and k >= 4096
+    print(json.dumps({"event": "start", "devices": len(nodes), "visible": len(nodes), "gcn_arch": "gfx950",
+                      "cus": 256, "launch": "standin"}), flush=True)
+    if "--smoke" in argv:
+        print(json.dumps({"event": "hip-smoke", "devices": len(nodes), "elements": 50000, "ok": True}), flush=True)
+    time.sleep(float(os.environ.get("GEMM_STANDIN_RUNTIME_S", "1")))
+    ok_all, total, lo = True, 0.0, None
+    for i, node in enumerate(nodes):
+        tf = 600.0 if node in slow else 1500.0
+        ok = not (floors_apply and floor and tf < floor)
+        line = {"event": "gemm", "dtype": "bf16", "device": i, "m": m, "n": n, "k": k, "tflops": tf,
+                "max_rel_err": 1e-3, "ok": ok}
+        if not ok:
+            line.update(kind="floor", error=f"below floor: {tf:.1f} < {floor:.1f} TFLOP/s")
+        print(json.dumps(line), flush=True)
+        ok_all = ok_all and ok
+        total += tf
+        lo = tf if lo is None else min(lo, tf)
+    print(json.dumps({"event": "aggregate", "dtype": "bf16", "m": m, "n": n, "k": k, "gpus": len(nodes),
+                      "total_tflops": total, "per_gpu_tflops": total / max(1, len(nodes)), "min_gpu_tflops": lo or 0.0,
+                      "ok": ok_all}), flush=True)
+    print(json.dumps({"event": "done", "ok": ok_all}), flush=True)
+    if state and os.path.exists(state + ".running"):
+        os.remove(state + ".running")
+    return 0 if ok_all else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -22,8 +22,9 @@ What a container sees, and how
     the node's containerd config (what the toolkit's ``amd-ctk install`` writes), retried every
     ``SYNC_S`` as kubelet does;
   * restart policy ``Always`` with kubelet's crash-loop back-off; ``OnFailure``/``Never`` pods
-    end ``Succeeded``/``Failed``; termination messages from ``terminationMessagePath``
-    (``FallbackToLogsOnError`` honoured);
+    end ``Succeeded``/``Failed``; a failing init container fails a ``Never`` pod and is restarted
+    with back-off otherwise (the pod stays ``Pending``, the previous exit in ``lastState``);
+    termination messages from ``terminationMessagePath`` (``FallbackToLogsOnError`` honoured);
   * exec readiness / startup probes; the Ready condition and containerStatuses are written back
     through the API, so DaemonSet status and the operator see real readiness;
   * pods deleted from the API have their process groups terminated (SIGTERM, then SIGKILL
@@ -192,6 +193,9 @@ class PodRun:
         if p is not None and p.poll() is None:
             st["state"] = {"running": {"startedAt": _now()}}
             st["started"] = True
+            if name in self.terminated:
+                # a restarted container: the previous run's exit, as kubelet reports it
+                st["lastState"] = {"terminated": {k: v for k, v in self.terminated[name].items() if not k.startswith("_")}}
         elif name in self.terminated:
             st["state"] = {"terminated": {k: v for k, v in self.terminated[name].items() if not k.startswith("_")}}
         else:
@@ -418,11 +422,13 @@ class PodRun:
                 self._record_exit(c, p, vols)
                 if p.returncode == 0:
                     break
-                self.restarts[c["name"]] = self.restarts.get(c["name"], 0) + 1
                 if policy == "Never":
                     self.phase = "Failed"
                     self.publish()
                     return
+                # Always / OnFailure: the init container restarts with crash-loop back-off and the pod
+                # stays Pending (kubelet never fails a pod whose policy restarts it)
+                self.restarts[c["name"]] = self.restarts.get(c["name"], 0) + 1
                 self.publish()
                 if not self._sleep(CRASHLOOP_BACKOFF_S[min(attempt, len(CRASHLOOP_BACKOFF_S) - 1)]):
                     return

@@ -37,7 +37,29 @@ WORKLOAD_CONFIG_LABEL = "amd.com/gpu.workload.config"
 
 
 class ValidationError(Exception):
-    pass
+    """A component's check failed. ``failures``: the structured gate failures behind it (GateFailure),
+    when the check was a gate."""
+
+    def __init__(self, msg: str, failures: Optional[List["GateFailure"]] = None):
+        super().__init__(msg)
+        self.failures = list(failures or [])
+
+
+@dataclass(frozen=True)
+class GateFailure:
+    """One reason a measurement must not open a barrier. ``kind`` says what failed, so what to do
+    about it never depends on the wording of ``text``: ``correctness`` (a wrong result, a failed
+    launch, smoke test or probe, a lost worker), ``oom`` (the shape did not fit the free HBM),
+    ``floor`` (below the per-GPU TFLOP/s floor), ``relative`` (below the node median), ``efficiency``
+    (a scaling step below the gate), ``uniformity`` (the workload's own node-median gate)."""
+    kind: str
+    text: str
+
+    def __str__(self) -> str:
+        return self.text
+
+
+THROUGHPUT_KINDS = frozenset({"floor", "relative", "efficiency", "uniformity"})
 
 
 @dataclass
@@ -361,7 +383,7 @@ def _env_float(ctx: Context, key: str) -> Optional[float]:
 def gemm_floors(ctx: Context, gpus: Optional[List[Dict[str, Any]]] = None) -> Dict[str, float]:
     """Per-GPU TFLOP/s floors of the GEMM probe, by dtype. ``GEMM_MIN_TFLOPS_BF16`` /
     ``GEMM_MIN_TFLOPS_FP8`` (spec.validator.hip.env) win when set (0 = no floor); otherwise
-    ``GEMM_FLOOR_FRACTION`` (default 0.40) of the node model's dense peak, scaled to the CUs of
+    ``GEMM_FLOOR_FRACTION`` (default GEMM_FLOOR_FRACTION, 0.50) of the node model's dense peak, scaled to the CUs of
     one HIP device (a CPX partition has 1/8 of the GPU). Unknown model: no floor."""
     gpus = gpus if gpus is not None else _gpus(ctx)
     model = node_model(ctx, gpus)
@@ -441,14 +463,15 @@ def floor_applies(m: int, n: int, k: int) -> bool:
     return (m or 0) * (n or 0) >= 256 * 256 * 256 and (k or 0) >= 4096
 
 
-def _relative_outliers(per: List[Dict[str, Any]], frac: float) -> List[str]:
+def _relative_outliers(per: List[Dict[str, Any]], frac: float, disturbed: frozenset = frozenset()) -> List[str]:
     """GPUs whose best TFLOP/s is below ``frac`` x the node's (upper) median at the same dtype and
-    shape: a 40 %-slow GPU passes any absolute floor loose enough for every box, not this."""
+    shape: a 40 %-slow GPU passes any absolute floor loose enough for every box, not this. Disturbed
+    GPUs (a tenant arrived during the sweep) are neither judged nor part of the median."""
     if not frac:
         return []
     best: Dict[tuple, Dict[Any, float]] = {}
     for r in per:
-        if not r.get("ok") or not r.get("tflops"):
+        if not r.get("ok") or not r.get("tflops") or r.get("device") in disturbed:
             continue
         key = (_dtype_key(r.get("dtype", "bf16")), r.get("m"), r.get("n"), r.get("k"))
         d = best.setdefault(key, {})
@@ -465,43 +488,82 @@ def _relative_outliers(per: List[Dict[str, Any]], frac: float) -> List[str]:
     return bad
 
 
+def _line_kind(r: Dict[str, Any]) -> str:
+    """The kind of a failing workload line: the workload's own ``kind`` field; a line without one (an
+    older workload image) is a correctness failure unless it says out-of-memory structurally."""
+    k = r.get("kind")
+    if k in THROUGHPUT_KINDS or k in ("correctness", "oom"):
+        return k
+    return "oom" if r.get("oom") else "correctness"
+
+
+def _set_devices(info: Dict[str, Any]) -> Dict[tuple, set]:
+    """(dtype, m, n, k, gpus) -> the devices whose per-GPU lines belong to that set."""
+    out: Dict[tuple, set] = {}
+    for r in info["gemm"]:
+        out.setdefault((r.get("dtype"), r.get("m"), r.get("n"), r.get("k"), r.get("gpus")), set()).add(r.get("device"))
+    return out
+
+
 def gate_gemm(info: Dict[str, Any], floors: Dict[str, float], busy: List[str] = (),
-              min_relative: float = GEMM_MIN_RELATIVE, min_efficiency: float = GEMM_MIN_EFFICIENCY) -> List[str]:
+              min_relative: float = GEMM_MIN_RELATIVE, min_efficiency: float = GEMM_MIN_EFFICIENCY,
+              disturbed: frozenset = frozenset()) -> List[GateFailure]:
     """Why a GEMM result must not open hip-ready: failed checks, any GPU of the full run below its
     dtype's floor, below ``min_relative`` x the node median, or a scaling step below
     ``min_efficiency``; on probed (tenant-held) GPUs a failed correctness check -- an allocation
     failure there is a busy skip. Also checked in the pod (--min-tflops, --min-relative,
     --min-efficiency); done here again so an older workload image cannot pass a slow GPU. The full
-    run only ever covers GPUs no pod holds (hip_plan), so the floors apply to all of it."""
-    bad = [f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('error', 'check failed')}"
-           for r in info["gemm"] if not r.get("ok")]
-    bad += [f"probe device {p['device']}: {p.get('error', 'check failed')}" for p in info.get("probe", [])
-            if not p["ok"] and "skipped" not in p]
-    bad += [f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: not ok" for r in info["aggregate"]
-            if r.get("ok") is False and not bad and r.get("efficiency_ok") is not False]
+    run only ever covers GPUs no pod holds (hip_plan), so the floors apply to all of it -- except on
+    ``disturbed`` GPUs (a tenant was given them while the sweep ran): their throughput measured the
+    sharing, so only their correctness counts, and no set that ran on one is gated on throughput."""
+    disturbed = frozenset(disturbed)
+    sets = _set_devices(info)
+
+    def touched(r: Dict[str, Any]) -> bool:
+        devs = sets.get((r.get("dtype"), r.get("m"), r.get("n"), r.get("k"), r.get("gpus") if r.get("scaling") else None))
+        return bool(disturbed) and (devs is None or bool(devs & disturbed))
+
+    bad: List[GateFailure] = []
+    for r in info["gemm"]:
+        if r.get("ok"):
+            continue
+        kind = _line_kind(r)
+        if kind in THROUGHPUT_KINDS and r.get("device") in disturbed:
+            continue
+        bad.append(GateFailure(kind, f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: "
+                                     f"{r.get('error', 'check failed')}"))
+    bad += [GateFailure("correctness", f"probe device {p['device']}: {p.get('error', 'check failed')}")
+            for p in info.get("probe", []) if not p["ok"] and "skipped" not in p]
+    bad += [GateFailure("correctness", f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: not ok")
+            for r in info["aggregate"]
+            if r.get("ok") is False and not bad and r.get("efficiency_ok") is not False and not touched(r)]
     if info.get("smoke_ok") is False:
-        bad.append("hip-smoke failed")
+        bad.append(GateFailure("correctness", "hip-smoke failed"))
     for r in info["gemm"]:
         floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0)
-        if not floor_applies(r.get("m"), r.get("n"), r.get("k")):
+        if not floor_applies(r.get("m"), r.get("n"), r.get("k")) or r.get("device") in disturbed:
             continue
         if r.get("ok") and floor and r.get("tflops", 0.0) < floor:
-            bad.append(f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: {r.get('tflops')} TFLOP/s "
-                       f"below the {floor} floor")
+            bad.append(GateFailure("floor", f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: "
+                                            f"{r.get('tflops')} TFLOP/s below the {floor} floor"))
     for r in info["aggregate"]:          # the slowest GPU of each set (per-GPU lines may be cut)
+        if touched(r):
+            continue
         floor = floors.get(_dtype_key(r.get("dtype", "bf16")), 0.0) if floor_applies(r.get("m"), r.get("n"), r.get("k")) else 0.0
         slow = r.get("min_gpu_tflops", r.get("per_gpu_tflops", 0.0))
         if floor and slow < floor and not bad:
-            bad.append(f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: slowest GPU {slow} TFLOP/s "
-                       f"below the {floor} floor")
+            bad.append(GateFailure("floor", f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: slowest GPU "
+                                            f"{slow} TFLOP/s below the {floor} floor"))
         eff = r.get("efficiency")
-        if min_efficiency and eff is not None and (r.get("gpus") or 1) > 1 and eff < min_efficiency:
-            bad.append(f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: scaling efficiency {eff:.3f} "
-                       f"below {min_efficiency:g}")
-    bad += _relative_outliers(info["gemm"], min_relative)
-    bad += [f"uniformity {u.get('dtype')} {u.get('m')}x{u.get('n')}x{u.get('k')}: slow devices "
-            f"{u.get('slow_devices')} (min ratio {u.get('min_ratio')})" for u in info.get("uniformity", [])
-            if u.get("ok") is False]
+        if min_efficiency and eff is not None and (r.get("gpus") or 1) > 1 and eff < min_efficiency and \
+                r.get("efficiency_gated", True) is not False:
+            bad.append(GateFailure("efficiency", f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: scaling "
+                                                 f"efficiency {eff:.3f} below {min_efficiency:g}"))
+    bad += [GateFailure("relative", b) for b in _relative_outliers(info["gemm"], min_relative, disturbed)]
+    if not disturbed:         # the workload's median counted the disturbed GPUs: the check above replaces it
+        bad += [GateFailure("uniformity", f"uniformity {u.get('dtype')} {u.get('m')}x{u.get('n')}x{u.get('k')}: "
+                                          f"slow devices {u.get('slow_devices')} (min ratio {u.get('min_ratio')})")
+                for u in info.get("uniformity", []) if u.get("ok") is False]
     return list(dict.fromkeys(bad))
 
 
@@ -562,23 +624,41 @@ def _local_workload(ctx: Context, mode: str) -> Dict[str, Any]:
     return info
 
 
-_CORRECTNESS_MARKS = ("check failed", "max_rel_err", "hip-smoke", "probe device", "error", "oom", "out of memory")
-_THROUGHPUT_MARKS = ("TFLOP/s", "floor", "efficiency", "median", "slow devices")
-
-
-def _throughput_only(bad: List[str]) -> bool:
+def throughput_only(bad: List[GateFailure]) -> bool:
     """Every gate failure is a throughput gate (floor, node median, scaling efficiency, uniformity);
-    none is a wrong result, a failed smoke test or a probe failure."""
-    return bool(bad) and all(any(m in b for m in _THROUGHPUT_MARKS) and not any(m in b for m in _CORRECTNESS_MARKS)
-                             for b in bad)
+    none is a wrong result, a failed smoke test, a probe failure or an allocation failure."""
+    return bool(bad) and all(b.kind in THROUGHPUT_KINDS for b in bad)
+
+
+def disturbed_gpus(ctx: Context, plan: Dict[str, Any], gpus: List[Dict[str, Any]]) -> Dict[str, Any]:
+    """GPUs of the full sweep that a tenant holds now (the HIP pod is privileged and requests no GPU
+    resource, so the device plugin kept advertising them while it ran): ``devices`` (HIP indices),
+    ``pods`` and ``attribution``. Without a device mapping for a running GPU pod every GPU of the
+    sweep counts as disturbed (held_gpus never guesses a tenant's GPU is free). Reference: the plugin
+    workload asks the scheduler for its GPU (validator/main.go:978-983), so it cannot share one."""
+    now = gpu_pods_on_node(ctx)
+    if not now:
+        return {"devices": [], "pods": [], "attribution": "none"}
+    held = held_gpus(ctx, now, gpus)
+    hb = set(held["held_bdfs"])
+    full = None if plan["full"] is None else set(plan["full"])
+    devs = sorted(g["index"] for g in gpus if g["pci_bdf"] in hb and (full is None or g["index"] in full))
+    if not gpus and held["attribution"] == "unattributed":
+        devs = ["all"]
+    return {"devices": devs, "pods": now[:16], "attribution": held["attribution"]}
 
 
 def validate_hip(ctx: Context) -> Dict[str, Any]:
     """hip-smoke + the MFMA GEMM probe (bf16 and fp8, 1/2/4/8-GPU sweep), gated on correctness, on
     per-GPU throughput floors (models/ defaults, spec.validator.hip.env overrides), on the node
     median and on scaling efficiency. Tenant-safe: GPUs that running pods hold (kubelet
-    pod-resources) get a correctness-only probe, never the full sweep (hip_plan). The reference
-    gates on vectorAdd's exit code alone (validator/main.go:1176-1211)."""
+    pod-resources) get a correctness-only probe, never the full sweep (hip_plan); GPUs a tenant was
+    given while the sweep ran are re-checked after it and reported ``disturbed``, their throughput
+    out of every gate. The pod fails fast: a failing workload ends the pod at once (restartPolicy
+    Never, wait_for_pod), its result lines come back with the failure, and the failure is a
+    ValidationError naming each gate. A throughput-only failure (every result correct) is measured
+    once more, with a fresh plan. The reference gates on vectorAdd's exit code alone
+    (validator/main.go:1176-1211)."""
     mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
     # GEMM_VALIDATION_MODE=dry-run (CPU rehearsals with a kubelet): the pod is planned, scheduled
     # and run, the GEMMs are not; HIP_VALIDATION_MODE=skip without it: nothing is spawned
@@ -589,19 +669,33 @@ def validate_hip(ctx: Context) -> Dict[str, Any]:
         return info
     gpus = _gpus(ctx)
     floors = gemm_floors(ctx, gpus)
-    busy = gpu_pods_on_node(ctx)
-    plan = hip_plan(ctx, busy, gpus)
+    min_rel = _gate_value(ctx, "GEMM_MIN_RELATIVE", GEMM_MIN_RELATIVE)
+    min_eff = _gate_value(ctx, "GEMM_MIN_EFFICIENCY", GEMM_MIN_EFFICIENCY)
 
     def measure():
+        # the plan is taken right before each run: a re-measure never runs on a GPU a tenant now holds
+        busy = gpu_pods_on_node(ctx)
+        plan = hip_plan(ctx, busy, gpus)
+        failed: Optional[W.PodFailed] = None
         if mode == "local":
             results = _run_local_hip(ctx, floors, plan)
         else:
             env = _hip_env(ctx, floors, plan)
             if dry:
                 env["GEMM_DRY_RUN"] = "1"
-            res = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                                     env, timeout=ctx.pod_timeout)
-            results = res["results"]
+            try:
+                results = W.run_workload_pod(ctx.client, "hip-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                                             env, timeout=ctx.pod_timeout)["results"]
+            except W.PodFailed as e:
+                if not e.results:
+                    raise ValidationError(f"HIP validation pod failed with no result: {e}"[:1000],
+                                          [GateFailure("correctness", str(e)[:400])])
+                failed, results = e, e.results
+            except TimeoutError as e:
+                raise ValidationError(f"HIP validation pod did not finish within {ctx.pod_timeout:.0f}s: {e}",
+                                      [GateFailure("correctness", f"timeout after {ctx.pod_timeout:.0f}s")])
+            except RuntimeError as e:          # the pod was deleted under the validator
+                raise ValidationError(f"HIP validation pod: {e}", [GateFailure("correctness", str(e))])
         info = summarize_gemm(results)
         info["floors_tflops"] = floors
         info["plan"] = {"full": "all" if plan["full"] is None else plan["full"], "probe": plan["probe"],
@@ -609,20 +703,33 @@ def validate_hip(ctx: Context) -> Dict[str, Any]:
         if busy:
             info["busy"] = f"{len(busy)} GPU pod(s) on the node hold {len(plan['held_bdfs'])} GPU(s) " \
                            f"({plan['attribution']}): full sweep on {len(plan['full'])} free, probe on {len(plan['probe'])}"
-        bad = gate_gemm(info, floors, busy, min_relative=_gate_value(ctx, "GEMM_MIN_RELATIVE", GEMM_MIN_RELATIVE),
-                        min_efficiency=_gate_value(ctx, "GEMM_MIN_EFFICIENCY", GEMM_MIN_EFFICIENCY))
+        dist = disturbed_gpus(ctx, plan, gpus) if mode != "local" or ctx.client is not None else {"devices": []}
+        # a tenant that held its GPUs before the run is in the plan already (probe only): only the
+        # sweep's own GPUs can be disturbed
+        devs = frozenset(d for d in dist["devices"] if d != "all")
+        if "all" in dist["devices"]:
+            devs = frozenset(r.get("device") for r in info["gemm"])
+        if devs:
+            info["disturbed"] = {**dist, "devices": sorted(devs, key=str)}
+        bad = gate_gemm(info, floors, busy, min_relative=min_rel, min_efficiency=min_eff, disturbed=devs)
+        if failed is not None:
+            info["pod_failed"] = {"exit_code": failed.exit_code, "reason": failed.reason}
+            if not bad and not devs:
+                # the workload failed a gate this validator cannot see in its lines: never pass it
+                bad = [GateFailure("correctness", f"workload exited {failed.exit_code} with no failing result line")]
         return info, bad
 
     info, bad = measure()
-    if bad and _throughput_only(bad) and ctx.env.get("GEMM_REMEASURE", "1") != "0":
-        # a throughput gate alone (every result correct): measure once more before failing the node,
-        # so a transient clock or power event costs seconds, not a crash-loop back-off
-        log.warning("HIP validation: %s -- measuring once more", bad[:4])
+    if throughput_only(bad) and ctx.env.get("GEMM_REMEASURE", "1") != "0":
+        # a throughput gate alone (every result correct): measure once more -- one more pod in pod
+        # mode -- before failing the node, so a transient clock or power event costs one run
+        log.warning("HIP validation: %s -- measuring once more", [str(b) for b in bad[:4]])
         first = bad
         info, bad = measure()
-        info["remeasured"] = {"first_failure": first[:8]}
+        info["remeasured"] = {"first_failure": [str(b) for b in first[:8]],
+                              "first_kinds": sorted({b.kind for b in first})}
     if bad:
-        raise ValidationError(f"HIP validation failed: {bad[:8]}")
+        raise ValidationError(f"HIP validation failed: {[str(b) for b in bad[:8]]}", bad)
     ctx.status.create(S.HIP_READY, info)
     return info
 
@@ -692,8 +799,14 @@ def validate_plugin(ctx: Context) -> Dict[str, Any]:
         else:
             # prefer a partition resource (like the reference prefers MIG), else one whole GPU
             name = next((k for k in sorted(res) if k.startswith(PARTITION_RESOURCE_PREFIX)), GPU_RESOURCE)
-            out = W.run_workload_pod(ctx.client, "plugin-workload-validation.yaml", ctx.namespace, ctx.node_name,
-                                     _validator_env(ctx), timeout=ctx.pod_timeout, gpu_limit={name: 1})
+            try:
+                out = W.run_workload_pod(ctx.client, "plugin-workload-validation.yaml", ctx.namespace, ctx.node_name,
+                                         _validator_env(ctx), timeout=ctx.pod_timeout, gpu_limit={name: 1})
+            except W.PodFailed as e:
+                raise ValidationError(f"plugin workload failed on its {name}: {e}"[:1000],
+                                      [GateFailure("correctness", f"plugin workload exit {e.exit_code}")])
+            except (TimeoutError, RuntimeError) as e:
+                raise ValidationError(f"plugin workload pod: {e}", [GateFailure("correctness", str(e))])
             info["workload"] = summarize_gemm(out["results"])
     ctx.status.create(S.PLUGIN_READY, info)
     return info

@@ -7,7 +7,11 @@ validator tolerates, with the validator's own image / pull policy / secrets / ru
 event-driven on a pod watch with a bounded timeout, where the reference polls 60 x 5 s.
 
 The workload writes its JSON results to the termination message, which the validator reads
-back from the pod status and stores in the barrier file.
+back from the pod status and stores in the barrier file -- also when the workload failed: the pods
+run with ``restartPolicy: Never`` (a failing init container of an ``OnFailure`` pod is restarted with
+crash-loop back-off and the pod stays ``Pending``; the reference's ``OnFailure``,
+validator/cuda-workload-validation.yaml:13, turns a sick GPU into a 300 s timeout), and
+``wait_for_pod`` returns at the first non-zero container exit whatever the policy.
 """
 
 from __future__ import annotations
@@ -86,12 +90,21 @@ def prepare_pod(client, template: Dict[str, Any], namespace: str, node: str, env
 
 
 class PodFailed(RuntimeError):
-    """The validation pod ended Failed; ``reason`` is the pod's status.reason (the kubelet's
-    admission rejection, e.g. ``UnexpectedAdmissionError`` / ``OutOfamd.com/gpu``, or empty)."""
+    """The validation pod failed: it ended ``Failed`` (``restartPolicy: Never``), or one of its
+    containers exited non-zero while the pod had not (``OnFailure``: the kubelet would restart it with
+    crash-loop back-off and the pod would stay ``Pending``, never ``Failed`` -- reason
+    ``ContainerFailed``). ``reason`` is the pod's status.reason (the kubelet's admission rejection,
+    e.g. ``UnexpectedAdmissionError`` / ``OutOfamd.com/gpu``) or ``ContainerFailed``; ``results``
+    the JSON lines of the termination message (what the workload measured before it failed);
+    ``exit_code`` the failing container's."""
 
-    def __init__(self, msg: str, reason: str = ""):
+    def __init__(self, msg: str, reason: str = "", results: Optional[List[Dict[str, Any]]] = None,
+                 exit_code: Optional[int] = None, container: str = ""):
         super().__init__(msg)
         self.reason = reason
+        self.results = results or []
+        self.exit_code = exit_code
+        self.container = container
 
     @property
     def admission(self) -> bool:
@@ -111,21 +124,41 @@ def delete_stale(client, namespace: str, app: str, node: str) -> None:
             pass
 
 
+def failed_container(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    """The first container (init containers first) that terminated with a non-zero exit code, now
+    (``state``) or before a restart (``lastState``): ``{"name", "exitCode", "message", "restarts"}``."""
+    st = pod.get("status") or {}
+    for cs in (st.get("initContainerStatuses") or []) + (st.get("containerStatuses") or []):
+        for key in ("state", "lastState"):
+            term = (cs.get(key) or {}).get("terminated") or {}
+            code = term.get("exitCode")
+            if isinstance(code, int) and code != 0:
+                return {"name": cs.get("name", ""), "exitCode": code, "message": term.get("message", ""),
+                        "restarts": cs.get("restartCount", 0)}
+    return None
+
+
 def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0,
                  abort_check: Optional[Callable[[Dict[str, Any]], Optional[str]]] = None) -> Dict[str, Any]:
-    """Block until the pod Succeeds (returns it) or Fails / times out (raises). ``abort_check``
-    sees the current pod at least every 2 s; a non-empty reason raises WorkloadAborted."""
+    """Block until the pod Succeeds (returns it), or raise: PodFailed as soon as the pod is
+    ``Failed`` or any of its containers has exited non-zero (the validator never waits out a
+    crash-loop back-off: reference validator/main.go:1042-1059 polls the phase only, and a failing
+    init container of an ``OnFailure`` pod never gives it one), TimeoutError after ``timeout``.
+    ``abort_check`` sees the current pod at least every 2 s; a non-empty reason raises
+    WorkloadAborted."""
     done = threading.Event()
     state: Dict[str, Any] = {}
+
+    def finished(pod: Dict[str, Any]) -> bool:
+        return (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed") or failed_container(pod) is not None
 
     def on_event(ev):
         if o.name(ev.obj) != name or o.namespace(ev.obj) != namespace:
             return
-        phase = (ev.obj.get("status") or {}).get("phase")
         if ev.type == "DELETED":
             state["error"] = "pod deleted"
             done.set()
-        elif phase in ("Succeeded", "Failed"):
+        elif finished(ev.obj):
             state["pod"] = ev.obj
             done.set()
     stop = client.watch("v1", "Pod", on_event, namespace=namespace)
@@ -135,7 +168,7 @@ def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0,
         while not done.is_set():
             try:
                 cur = client.get("v1", "Pod", name, namespace)
-                if (cur.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+                if finished(cur):
                     state["pod"] = cur
                     break
                 why = abort_check(cur) if abort_check else None
@@ -149,15 +182,21 @@ def wait_for_pod(client, namespace: str, name: str, timeout: float = 300.0,
             done.wait(min(remaining, 2.0))
     finally:
         stop()
-    if "error" in state:
+    if "error" in state and "pod" not in state:
         raise RuntimeError(state["error"])
     pod = state["pod"]
-    if pod["status"]["phase"] != "Succeeded":
-        st = pod["status"]
-        why = ": ".join(x for x in (st.get("reason", ""), st.get("message", "")) if x)
-        raise PodFailed(f"pod {name} failed{' (' + why + ')' if why else ''}: {termination_message(pod)}",
-                        reason=st.get("reason", ""))
-    return pod
+    st = pod.get("status") or {}
+    if st.get("phase") == "Succeeded":
+        return pod
+    bad = failed_container(pod)
+    msg = termination_message(pod)
+    why = ": ".join(x for x in (st.get("reason", ""), st.get("message", "")) if x)
+    if bad is not None:
+        why = why or f"container {bad['name']} exited {bad['exitCode']}"
+    raise PodFailed(f"pod {name} failed{' (' + why + ')' if why else ''}: {msg}"[:2000],
+                    reason=st.get("reason", "") or ("ContainerFailed" if st.get("phase") != "Failed" else ""),
+                    results=parse_results(msg), exit_code=bad["exitCode"] if bad else None,
+                    container=bad["name"] if bad else "")
 
 
 def termination_message(pod: Dict[str, Any]) -> str:
@@ -203,10 +242,14 @@ def run_workload_pod(client, manifest: str, namespace: str, node: str, env: Dict
     log.info("created validation pod %s/%s", namespace, o.name(pod))
     try:
         done = wait_for_pod(client, namespace, o.name(pod), timeout, abort_check=abort_check)
-    except WorkloadAborted:
-        try:
-            client.delete("v1", "Pod", o.name(pod), namespace, grace_period_seconds=0)
-        except errors.NotFound:
-            pass
+    except (WorkloadAborted, PodFailed, TimeoutError) as e:
+        # withdrawn, failed (a pod the kubelet would restart must not re-run the workload behind
+        # the validator's back) or timed out: the pod goes
+        if not isinstance(e, PodFailed) or e.reason == "ContainerFailed" or \
+                (template.get("spec") or {}).get("restartPolicy", "Always") != "Never":
+            try:
+                client.delete("v1", "Pod", o.name(pod), namespace, grace_period_seconds=0)
+            except errors.NotFound:
+                pass
         raise
     return {"pod": o.name(pod), "results": parse_results(termination_message(done))}

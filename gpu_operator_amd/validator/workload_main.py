@@ -54,9 +54,12 @@ def rocprofv3_path() -> Optional[str]:
 
 
 def binary(name: str) -> str:
-    p = os.path.join(BIN_DIR, name)
-    if os.path.exists(p):
-        return p
+    """A workload binary: ``$AMDGO_BIN_DIR`` first (an image that ships them elsewhere; the CPU
+    rehearsals' scripted stand-ins), then the in-tree build, then PATH."""
+    for d in (os.environ.get("AMDGO_BIN_DIR", ""), BIN_DIR):
+        p = os.path.join(d, name) if d else ""
+        if p and os.path.exists(p):
+            return p
     found = shutil.which(name)
     if found:
         return found
@@ -167,7 +170,9 @@ def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "b
     try:
         cmd = [prof, "--pmc", *spec["mops"], *PMC_COMMON, "--output-format", "csv", "-d", out, "--",
                binary("amd-gemm-validate"), "--shapes", shape, "--iters", "1", "--warmup", "0",
-               "--no-stabilise", "--devices", "0", "--check-rows", "1", "--dtype", dtype]
+               "--no-stabilise", "--devices", "0", "--check-rows", "1", "--dtype", dtype,
+               # the profiler initialises the GPU in the process it starts: no worker processes
+               "--launch", "threads"]
         kw = {"env": dict(os.environ, HIP_VISIBLE_DEVICES=",".join(map(str, visible)))} if visible else {}
         p = run(cmd, capture_output=True, text=True, timeout=300, **kw)
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)

@@ -3,9 +3,18 @@
 // validator/main.go:1176-1211 -- this probe also gates on throughput).
 //
 // Runs the hand-written CDNA4 MFMA GEMMs -- bf16 (gemm_bf16.hip) and/or fp8 e4m3fn on the
-// double-rate matrix-core path (gemm_fp8.hip) -- concurrently on the selected GPUs, one host
-// thread per GPU, on uniform [-1,1) operands; checks sampled output rows against an independent
-// fp32 reference kernel; prints one JSON line per (dtype, GPU, shape) and an aggregate line.
+// double-rate matrix-core path (gemm_fp8.hip) -- concurrently on the selected GPUs on uniform
+// [-1,1) operands; checks sampled output rows against an independent fp32 reference kernel; prints
+// one JSON line per (dtype, GPU, shape) and an aggregate line.
+//
+// One process per GPU (--launch processes, the default): this process never
+// touches the GPU. It enumerates the GPU agents this container may use from KFD sysfs (the HIP order),
+// starts one worker per GPU -- itself with `--worker`, HIP_VISIBLE_DEVICES naming that one GPU --
+// and meets the workers of each GPU set at a rendezvous over their stdin/stdout pipes. No HIP runtime
+// is shared between GPUs, so no host-side lock of one runtime serialises eight GPUs' launches.
+// --launch threads keeps the whole run in one process, one host thread per GPU (it is what runs
+// under a profiler: rocprofv3 initialises the GPU in the process it starts, which must then not
+// spawn programs).
 //
 // Timing protocol (the same as bench.py's, so the pod's number and the bench's agree):
 //   1. --warmup untimed dispatches;
@@ -13,12 +22,23 @@
 //      at least 50 dispatches ran and the last 10 per-dispatch times spread by < 2 % of their
 //      median, capped at --stabilise-max-s (MI355X ramps its clock over the first ~25
 //      back-to-back GEMMs; timing that transient under-reports steady state by 8-19 %);
-//   3. every GPU's thread meets at a rendezvous, then --iters dispatches are timed between two
-//      events.
+//   3. every GPU of the set meets at the rendezvous -- a GPU that stabilised early idles there
+//      until the slowest one arrives, and its clock drops while it waits;
+//   4. the re-ramp, untimed: at least 10 dispatches and --ramp-ms of work, enqueued back to back
+//      right after the rendezvous, with no host sync between them and the timed loop (with
+//      --no-stabilise neither step 2 nor this one runs: exactly --iters dispatches are issued);
+//   5. the timed loop: at least --iters dispatches and at least --min-window-ms of work (sized from
+//      the stabilised per-dispatch time), between two events -- a residual ramp is a small part of
+//      a 100 ms window, not half of a 30 ms one.
+// --pre-timed-idle-ms T inserts T ms of host-side idle after the rendezvous (the test of step 4).
 //
-// --scaling 1,2,4,8 runs the probe on GPUs 0..N-1 for each N (concurrently within one N) and adds
+// --scaling 1,2,4,8 runs the probe on N GPUs for each N (concurrently within one N) and adds
 // `efficiency` = aggregate / (N x the 1-GPU figure) to each aggregate line; an N above the visible
-// GPU count prints a `skipped` line instead of failing.
+// GPU count prints a `skipped` line instead of failing. A set of N takes one
+// agent per PHYSICAL GPU first (agents grouped by PCI function: a CPX GPU shows one agent per
+// partition); a set that must put two agents of one GPU together is measured and marked
+// `shared_gpu`, and the efficiency gate does not apply to it (partitions of one GPU share its power
+// and HBM, they are not independent GPUs).
 //
 // --min-efficiency E fails every scaling N > 1 whose efficiency is below E: independent GEMMs on
 // separate GPUs should scale at ~1.0, so a shortfall is a GPU, power or cooling problem.
@@ -32,6 +52,10 @@
 // a shortfall (or an allocation failure) is reported as `"oom":true` with need / free bytes and no
 // kernel is launched -- on a GPU a tenant holds, the validator maps that to "skipped: busy".
 //
+// Every failing line carries a structured `kind`: "correctness" (a wrong result, a failed launch or
+// allocation, a lost worker), "oom", "floor", "efficiency" or "uniformity" -- the validator decides
+// what a failure means from it, never from the wording of `error`.
+//
 // Exit status 0 only if every check passed and every GPU reached its floor (--min-tflops for
 // bf16, --min-tflops-fp8 for fp8; 0 = no floor) and the two gates above. The floors are fractions of
 // the dense peak, so they apply to shapes that can reach it: at least one full dispatch wave of
@@ -40,12 +64,19 @@
 //   amd-gemm-validate [--shapes 8192,4096,16384x16384x1024] [--dtype bf16|fp8|both] [--iters 50]
 //                     [--warmup 5] [--devices all|0,1,...] [--scaling 1,2,4,8] [--check-rows 32]
 //                     [--min-tflops X] [--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R]
-//                     [--stabilise-max-s 6] [--no-stabilise] [--smoke]
+//                     [--stabilise-max-s 6] [--no-stabilise] [--smoke] [--launch processes|threads]
+//                     [--min-window-ms 100] [--ramp-ms 60] [--pre-timed-idle-ms 0]
 //
 // --smoke first runs hip-smoke (smoke.hip: the vectorAdd analogue, every element checked on the
-// host) on each selected GPU in this process and prints its `hip-smoke` line -- one HIP runtime
-// start for both checks on the validator's critical path instead of two processes.
+// host) on each selected GPU and prints its `hip-smoke` line -- in the workers, so the validator's
+// critical path starts one HIP runtime per GPU, not two.
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <csignal>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -55,12 +86,18 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <tuple>
 #include <vector>
+
+#include "amdnode.h"
+
+extern char** environ;
 
 extern "C" {
 int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream);
@@ -74,10 +111,12 @@ int amdgo_fill_uniform_fp8(void* p, size_t n, uint32_t seed, void* stream);
 int amdgo_vector_add_f32(const float* a, const float* b, float* c, size_t n, void* stream);
 }
 
+static constexpr size_t kSmokeElements = 50000;
+
 // hip-smoke on each device (the amd-hip-smoke binary's check, in this process): fp32 C = A + B over
-// 50,000 elements, every element verified on the host.
-static bool smoke(const std::vector<int>& devs) {
-  constexpr size_t n = 50000;
+// 50,000 elements, every element verified on the host. Returns the number of failing devices.
+static int smoke_failures(const std::vector<int>& devs) {
+  constexpr size_t n = kSmokeElements;
   std::vector<float> a(n), b(n), c(n);
   for (size_t i = 0; i < n; ++i) {
     a[i] = (float)(i % 1000) / 7.0f;
@@ -97,10 +136,13 @@ static bool smoke(const std::vector<int>& devs) {
       if (p) (void)hipFree(p);
     failures += !ok;
   }
-  std::printf("{\"event\":\"hip-smoke\",\"devices\":%zu,\"elements\":%zu,\"ok\":%s}\n", devs.size(), n,
-              failures ? "false" : "true");
+  return failures;
+}
+
+static void print_smoke(size_t devices, int failures) {
+  std::printf("{\"event\":\"hip-smoke\",\"devices\":%zu,\"elements\":%zu,\"ok\":%s%s}\n", devices, kSmokeElements,
+              failures ? "false" : "true", failures ? ",\"kind\":\"correctness\"" : "");
   std::fflush(stdout);
-  return failures == 0;
 }
 
 // One operand precision: element size plus its GEMM, reference and fill entry points.
@@ -113,6 +155,12 @@ struct DType {
 };
 static const DType kBf16{"bf16", 2, amdgo_gemm_bf16, amdgo_gemm_ref_rows, amdgo_fill_uniform_bf16};
 static const DType kFp8{"fp8_e4m3fn", 1, amdgo_gemm_fp8, amdgo_gemm_fp8_ref_rows, amdgo_fill_uniform_fp8};
+
+static const DType* dtype_by_name(const std::string& n) {
+  if (n == kBf16.name) return &kBf16;
+  if (n == kFp8.name) return &kFp8;
+  return nullptr;
+}
 
 // Record the failing call in r.error and return false from run_one; the Resources destructor
 // frees whatever was allocated before the failure.
@@ -154,15 +202,18 @@ struct Shape {
 struct Options {
   int iters = 50, warmup = 5, check_rows = 32;
   double stabilise_max_s = 6.0;
+  double min_window_ms = 100.0;   // the timed loop covers at least this much GPU time
+  double ramp_ms = 60.0;          // re-ramp after the rendezvous: at least this much GPU time (profiles/r5_ramp)
+  double pre_idle_ms = 0.0;       // test hook: host idle after the rendezvous
   bool stabilise = true;
 };
 
 struct Result {
   int device = 0;
   Shape s{};
-  double tflops = 0, ms = 0, max_rel_err = 0, stab_spread = -1;
-  int stab_dispatches = 0;
-  bool ok = false, oom = false;
+  double tflops = 0, ms = 0, max_rel_err = 0, stab_spread = -1, stab_ms = 0;
+  int stab_dispatches = 0, iters = 0, ramp = 0;
+  bool launched = false, ok = false, oom = false;
   size_t need_bytes = 0, free_bytes = 0;
   std::string error;
 };
@@ -206,6 +257,24 @@ static std::vector<int> parse_ints(const std::string& spec) {
   return out;
 }
 
+// A comma list of non-negative integers; false when any entry is not one (a UUID, say).
+static bool parse_index_list(const char* spec, std::vector<int>& out) {
+  out.clear();
+  std::string s = spec;
+  size_t pos = 0;
+  while (pos <= s.size()) {
+    size_t c = s.find(',', pos);
+    std::string t = s.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+    if (!t.empty()) {
+      if (!std::all_of(t.begin(), t.end(), ::isdigit)) return false;
+      out.push_back(std::atoi(t.c_str()));
+    }
+    if (c == std::string::npos) break;
+    pos = c + 1;
+  }
+  return true;
+}
+
 static float bf16_to_f32(uint16_t b) {
   uint32_t u = (uint32_t)b << 16;
   float f;
@@ -216,7 +285,14 @@ static float bf16_to_f32(uint16_t b) {
 // Whether the per-GPU floors apply to this shape (see the header).
 static bool floor_applies(const Shape& s) { return (double)s.m * s.n >= 256.0 * 65536.0 && s.k >= 4096; }
 
-// Clock stabilisation (see the header): returns false on a launch/event error.
+static std::string json_safe(std::string s) {
+  for (char& c : s)
+    if (c == '"' || c == '\\' || c == '\n' || c == '\r') c = '\'';
+  return s;
+}
+
+// Clock stabilisation (see the header): returns false on a launch/event error. r.stab_ms is the
+// median per-dispatch time of the last window (what the re-ramp and the timed window are sized from).
 static bool stabilise(const DType& dt, const Shape& s, Resources& res, const Options& o, Result& r) {
   constexpr int kBatch = 10, kMin = 50, kWindow = 10;
   constexpr double kTol = 0.02;
@@ -247,26 +323,28 @@ static bool stabilise(const DType& dt, const Shape& s, Resources& res, const Opt
     std::vector<float> last(times.end() - kWindow, times.end());
     std::sort(last.begin(), last.end());
     const double med = last[kWindow / 2];
+    r.stab_ms = med;
     r.stab_spread = med > 0 ? (last.back() - last.front()) / med : 0.0;
     r.stab_dispatches = (int)times.size();
     if (((int)times.size() >= kMin && r.stab_spread < kTol) || std::chrono::steady_clock::now() > t_end) return true;
   }
 }
 
-static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, Rendezvous* sync, Result& r) {
+// One GPU's probe of one (dtype, shape). `barrier` is the set's rendezvous; it is reached exactly once
+// on every path, also when setup fails early, or the other GPUs of the set would wait forever.
+static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, const std::function<void()>& barrier,
+                    Result& r) {
   r.device = dev;
   r.s = s;
-  // Every thread must reach the rendezvous exactly once, also when setup fails early,
-  // or the other GPUs' threads would wait forever.
   struct Arrive {
-    Rendezvous* r;
+    const std::function<void()>& b;
     bool done = false;
     void now() {
-      if (r && !done) r->arrive_and_wait();
+      if (!done && b) b();
       done = true;
     }
     ~Arrive() { now(); }
-  } arrive{sync};
+  } arrive{barrier};
   CHECK(hipSetDevice(dev));
   Resources res;  // declared after Arrive: freed (and the stream drained) before the rendezvous
   CHECK(hipStreamCreateWithFlags(&res.st, hipStreamNonBlocking));
@@ -298,35 +376,44 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
     r.error = "fill failed";
     return false;
   }
-  for (int i = 0; i < o.warmup; ++i) {
-    const int err = dt.gemm(res.A, res.B, res.C, s.m, s.n, s.k, res.st);
-    if (err) {
-      r.error = std::string("gemm launch: ") + hipGetErrorString((hipError_t)err);
-      return false;
+  auto launch = [&](int n) {
+    for (int i = 0; i < n; ++i) {
+      const int err = dt.gemm(res.A, res.B, res.C, s.m, s.n, s.k, res.st);
+      if (err) {
+        r.error = std::string("gemm launch: ") + hipGetErrorString((hipError_t)err);
+        return false;
+      }
     }
-  }
+    return true;
+  };
+  if (!launch(o.warmup)) return false;
   CHECK(hipStreamSynchronize(res.st));
   if (o.stabilise && !stabilise(dt, s, res, o, r)) return false;
+  // the re-ramp and the timed window, sized from the stabilised dispatch time; without the clock
+  // protocol (--no-stabilise: a correctness probe, a profiled single dispatch) exactly --iters
+  r.ramp = o.stabilise ? 10 : 0;
+  r.iters = o.iters;
+  if (o.stabilise && r.stab_ms > 0) {
+    r.ramp = std::max(r.ramp, (int)std::ceil(o.ramp_ms / r.stab_ms));
+    r.iters = std::max(r.iters, (int)std::ceil(o.min_window_ms / r.stab_ms));
+  }
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   res.events.push_back(e0);
   CHECK(hipEventCreate(&e1));
   res.events.push_back(e1);
-  arrive.now();  // all GPUs start the timed loop together
-  CHECK(hipEventRecord(e0, res.st));
-  for (int i = 0; i < o.iters; ++i) {
-    const int err = dt.gemm(res.A, res.B, res.C, s.m, s.n, s.k, res.st);
-    if (err) {
-      r.error = std::string("gemm launch: ") + hipGetErrorString((hipError_t)err);
-      return false;
-    }
-  }
+  arrive.now();  // all GPUs of the set start together
+  if (o.pre_idle_ms > 0) std::this_thread::sleep_for(std::chrono::microseconds((long long)(o.pre_idle_ms * 1e3)));
+  if (!launch(r.ramp)) return false;  // back to the steady clock after the idle at the rendezvous
+  CHECK(hipEventRecord(e0, res.st));  // no host sync between the re-ramp and the timed loop
+  if (!launch(r.iters)) return false;
   CHECK(hipEventRecord(e1, res.st));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
-  r.ms = ms / o.iters;
+  r.ms = ms / r.iters;
   r.tflops = 2.0 * s.m * s.n * (double)s.k / (r.ms * 1e-3) / 1e12;
+  r.launched = true;
   // correctness on sampled rows against the independent fp32 reference kernel
   std::vector<int> hrows(check_rows);
   for (int i = 0; i < check_rows; ++i) hrows[i] = (int)(((uint64_t)i * 2654435761u + dev) % s.m);
@@ -350,7 +437,66 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   }
   r.max_rel_err = worst;
   r.ok = std::isfinite(worst) && worst <= 1.0 / 128;
+  if (!r.ok) r.error = "check failed: max_rel_err " + std::to_string(worst);
   return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The plan: every (dtype, shape, GPU set) in order, identical in every launch mode.
+// ---------------------------------------------------------------------------------------------
+struct Set {
+  int id = 0;
+  const DType* dt = nullptr;
+  Shape s{};
+  int scaling_n = 0;         // 0: no --scaling (every selected GPU)
+  std::vector<int> slots;    // positions in the selected device list
+  bool skipped = false;      // N above the visible GPUs
+  bool shared_gpu = false;   // two agents of one physical GPU in the set
+};
+
+// `bdf[i]`: the PCI function of selected device i (empty: unknown, every device its own GPU).
+static std::vector<Set> make_plan(const std::vector<const DType*>& dtypes, const std::vector<Shape>& shapes,
+                                  const std::vector<int>& counts, size_t ndev, const std::vector<std::string>& bdf) {
+  // scaling order: the first agent of each physical GPU, then the other agents
+  std::vector<int> order, rest;
+  std::set<std::string> seen;
+  for (size_t i = 0; i < ndev; ++i) {
+    const std::string key = i < bdf.size() && !bdf[i].empty() ? bdf[i] : "#" + std::to_string(i);
+    (seen.insert(key).second ? order : rest).push_back((int)i);
+  }
+  order.insert(order.end(), rest.begin(), rest.end());
+  std::vector<Set> plan;
+  for (const DType* dt : dtypes)
+    for (const auto& s : shapes) {
+      if (counts.empty()) {
+        Set st;
+        st.dt = dt, st.s = s;
+        for (size_t i = 0; i < ndev; ++i) st.slots.push_back((int)i);
+        plan.push_back(st);
+        continue;
+      }
+      // the 1-GPU figure every efficiency divides by: the N=1 run when the sweep has one, else a
+      // 1-GPU run first
+      std::vector<int> ns = counts;
+      if (std::find(ns.begin(), ns.end(), 1) == ns.end()) ns.insert(ns.begin(), 1);
+      std::stable_sort(ns.begin(), ns.end());
+      for (int n : ns) {
+        if (n < 1) continue;
+        Set st;
+        st.dt = dt, st.s = s, st.scaling_n = n;
+        if ((size_t)n > ndev) {
+          st.skipped = true;
+        } else {
+          st.slots.assign(order.begin(), order.begin() + n);
+          std::set<std::string> gpus;
+          for (int i : st.slots) gpus.insert(i < (int)bdf.size() && !bdf[i].empty() ? bdf[i] : "#" + std::to_string(i));
+          st.shared_gpu = gpus.size() < st.slots.size();
+        }
+        plan.push_back(st);
+      }
+    }
+  for (size_t i = 0; i < plan.size(); ++i) plan[i].id = (int)i;
+  return plan;
 }
 
 struct Aggregate {
@@ -361,69 +507,458 @@ struct Aggregate {
 // (dtype, m, n, k) -> device -> best TFLOP/s over every set it ran in (the --min-relative gate)
 static std::map<std::tuple<std::string, int, int, int>, std::map<int, double>> g_best;
 
-// One (dtype, shape) on a device set, concurrently; prints the per-GPU lines and the aggregate.
-static Aggregate run_set(const DType& dt, const Shape& s, const std::vector<int>& devs, const Options& o,
-                         double floor, int scaling_n, double single, double min_eff) {
-  std::vector<Result> res(devs.size());
-  Rendezvous sync(devs.size());
-  std::vector<std::thread> th;
-  std::vector<char> launched(devs.size(), 0);
-  for (size_t i = 0; i < devs.size(); ++i)
-    th.emplace_back([&, i] { launched[i] = run_one(dt, devs[i], s, o, &sync, res[i]); });
-  for (auto& t : th) t.join();
+static const char* failure_kind(const Result& r, bool floor_ok) {
+  if (r.oom) return "oom";
+  if (!r.launched || !r.ok) return "correctness";
+  if (!floor_ok) return "floor";
+  return "";
+}
+
+// The per-GPU lines and the aggregate of one set (results in slot order).
+static Aggregate report_set(const Set& set, std::vector<Result>& res, double floor, double single, double min_eff) {
+  const DType& dt = *set.dt;
+  const Shape& s = set.s;
   Aggregate agg;
-  const std::string scal = scaling_n > 0 ? ",\"gpus\":" + std::to_string(scaling_n) : std::string();
-  for (size_t i = 0; i < devs.size(); ++i) {
-    const auto& r = res[i];
+  const std::string scal = set.scaling_n > 0 ? ",\"gpus\":" + std::to_string(set.scaling_n) : std::string();
+  for (size_t i = 0; i < res.size(); ++i) {
+    auto& r = res[i];
     const bool floor_ok = !floor_applies(s) || r.tflops >= floor;
-    const bool ok = launched[i] && r.ok && floor_ok;
+    const bool ok = r.launched && r.ok && floor_ok;
     agg.ok = agg.ok && ok;
     agg.total += r.tflops;
     agg.min_gpu = i == 0 ? r.tflops : std::min(agg.min_gpu, r.tflops);
     std::string err = r.error;
-    if (err.empty() && launched[i] && r.ok && !floor_ok) {
+    if (err.empty() && !ok && !floor_ok) {
       char buf[128];
       std::snprintf(buf, sizeof buf, "below floor: %.1f < %.1f TFLOP/s", r.tflops, floor);
       err = buf;
     }
-    for (char& c : err)
-      if (c == '"' || c == '\\') c = '\'';
+    if (err.empty() && !ok) err = "check failed";
+    err = json_safe(err);
     char oom[96] = "";
     if (r.oom)
       std::snprintf(oom, sizeof oom, ",\"oom\":true,\"need_bytes\":%zu,\"free_bytes\":%zu", r.need_bytes, r.free_bytes);
+    const std::string kind = ok ? "" : std::string(",\"kind\":\"") + failure_kind(r, floor_ok) + "\"";
     std::printf("{\"event\":\"gemm\",\"dtype\":\"%s\",\"device\":%d%s,\"m\":%d,\"n\":%d,\"k\":%d,\"ms\":%.4f,"
                 "\"tflops\":%.1f,\"max_rel_err\":%.3e,\"stabilise_dispatches\":%d,\"stabilise_spread\":%.4f,"
-                "\"min_tflops\":%.1f,\"ok\":%s%s%s%s%s}\n",
+                "\"iters\":%d,\"ramp_dispatches\":%d,\"min_tflops\":%.1f,\"ok\":%s%s%s%s%s%s}\n",
                 dt.name, r.device, scal.c_str(), s.m, s.n, s.k, r.ms, r.tflops, r.max_rel_err, r.stab_dispatches,
-                r.stab_spread, floor_applies(s) ? floor : 0.0, ok ? "true" : "false", oom, err.empty() ? "" : ",\"error\":\"", err.c_str(),
-                err.empty() ? "" : "\"");
-    if (launched[i] && r.ok) {
+                r.stab_spread, r.iters, r.ramp, floor_applies(s) ? floor : 0.0, ok ? "true" : "false", kind.c_str(), oom,
+                err.empty() ? "" : ",\"error\":\"", err.c_str(), err.empty() ? "" : "\"");
+    if (r.launched && r.ok) {
       double& best = g_best[{dt.name, s.m, s.n, s.k}][r.device];
       best = std::max(best, r.tflops);
     }
   }
-  agg.per_gpu = agg.total / devs.size();
+  agg.per_gpu = res.empty() ? 0 : agg.total / res.size();
   std::string eff;
-  if (scaling_n == 1 && agg.total > 0) single = agg.total;   // the 1-GPU run is its own reference
-  if (scaling_n > 0 && single > 0) {
-    const double e = agg.total / (scaling_n * single);
-    const bool eff_ok = scaling_n == 1 || min_eff <= 0 || e >= min_eff;
-    char buf[96];
-    std::snprintf(buf, sizeof buf, ",\"efficiency\":%.4f,\"min_efficiency\":%.2f%s", e, min_eff,
+  if (set.scaling_n == 1 && agg.total > 0) single = agg.total;   // the 1-GPU run is its own reference
+  if (set.scaling_n > 0 && single > 0) {
+    const double e = agg.total / (set.scaling_n * single);
+    const bool gated = set.scaling_n > 1 && min_eff > 0 && !set.shared_gpu;
+    const bool eff_ok = !gated || e >= min_eff;
+    char buf[160];
+    std::snprintf(buf, sizeof buf, ",\"efficiency\":%.4f,\"min_efficiency\":%.2f%s%s", e, min_eff,
+                  set.shared_gpu ? ",\"shared_gpu\":true,\"efficiency_gated\":false" : "",
                   eff_ok ? "" : ",\"efficiency_ok\":false");
     eff = buf;
     agg.ok = agg.ok && eff_ok;
   }
+  // the aggregate's own kind: a failed GPU line carries the cause, the aggregate adds efficiency
+  std::string kind;
+  if (!agg.ok) {
+    bool any_gpu_bad = false;
+    for (const auto& r : res) any_gpu_bad = any_gpu_bad || !(r.launched && r.ok && (!floor_applies(s) || r.tflops >= floor));
+    kind = any_gpu_bad ? "" : ",\"kind\":\"efficiency\"";
+  }
   std::printf("{\"event\":\"aggregate\",\"dtype\":\"%s\",\"m\":%d,\"n\":%d,\"k\":%d,\"gpus\":%zu,\"total_tflops\":%.1f,"
-              "\"per_gpu_tflops\":%.1f,\"min_gpu_tflops\":%.1f,\"min_tflops\":%.1f%s%s,\"ok\":%s}\n",
-              dt.name, s.m, s.n, s.k, devs.size(), agg.total, agg.per_gpu, agg.min_gpu, floor_applies(s) ? floor : 0.0,
-              scaling_n > 0 ? ",\"scaling\":true" : "", eff.c_str(), agg.ok ? "true" : "false");
+              "\"per_gpu_tflops\":%.1f,\"min_gpu_tflops\":%.1f,\"min_tflops\":%.1f%s%s,\"ok\":%s%s}\n",
+              dt.name, s.m, s.n, s.k, res.size(), agg.total, agg.per_gpu, agg.min_gpu, floor_applies(s) ? floor : 0.0,
+              set.scaling_n > 0 ? ",\"scaling\":true" : "", eff.c_str(), agg.ok ? "true" : "false", kind.c_str());
   std::fflush(stdout);
   return agg;
 }
 
+static void print_skipped(const Set& set, size_t ndev) {
+  std::printf("{\"event\":\"scaling\",\"dtype\":\"%s\",\"m\":%d,\"n\":%d,\"k\":%d,\"gpus\":%d,"
+              "\"skipped\":\"%zu GPU(s) visible\"}\n",
+              set.dt->name, set.s.m, set.s.n, set.s.k, set.scaling_n, ndev);
+  std::fflush(stdout);
+}
+
+// Runs every set of the plan through `run` (which fills the set's results) and reports it; then the
+// uniformity lines. Returns whether everything passed.
+static bool run_plan(const std::vector<Set>& plan, size_t ndev, double min_tflops, double min_tflops_fp8,
+                     double min_eff, double min_rel,
+                     const std::function<void(const Set&, std::vector<Result>&)>& run) {
+  bool all_ok = true;
+  double single = 0;
+  for (const Set& set : plan) {
+    if (set.skipped) {
+      print_skipped(set, ndev);
+      continue;
+    }
+    if (set.scaling_n <= 1) single = 0;       // a new (dtype, shape): its 1-GPU figure comes first
+    std::vector<Result> res(set.slots.size());
+    run(set, res);
+    const double floor = set.dt == &kFp8 ? min_tflops_fp8 : min_tflops;
+    Aggregate a = report_set(set, res, floor, single, min_eff);
+    if (set.scaling_n == 1) single = a.per_gpu;
+    all_ok = a.ok && all_ok;
+  }
+  // uniformity: every GPU's best against the node's (upper) median, per dtype and shape
+  for (const auto& [key, per_dev] : g_best) {
+    if (per_dev.size() < 2) continue;
+    std::vector<double> v;
+    for (const auto& kv : per_dev) v.push_back(kv.second);
+    std::sort(v.begin(), v.end());
+    const double med = v[v.size() / 2];
+    double worst = 1e30;
+    std::string slow;
+    for (const auto& [dev, t] : per_dev) {
+      const double ratio = med > 0 ? t / med : 0;
+      worst = std::min(worst, ratio);
+      if (min_rel > 0 && ratio < min_rel) slow += (slow.empty() ? "" : ",") + std::to_string(dev);
+    }
+    const bool ok = slow.empty();
+    all_ok = all_ok && ok;
+    std::printf("{\"event\":\"uniformity\",\"dtype\":\"%s\",\"m\":%d,\"n\":%d,\"k\":%d,\"gpus\":%zu,"
+                "\"median_tflops\":%.1f,\"min_ratio\":%.4f,\"min_relative\":%.2f,\"slow_devices\":[%s],\"ok\":%s%s}\n",
+                std::get<0>(key).c_str(), std::get<1>(key), std::get<2>(key), std::get<3>(key), per_dev.size(), med,
+                worst, min_rel, slow.c_str(), ok ? "true" : "false", ok ? "" : ",\"kind\":\"uniformity\"");
+  }
+  return all_ok;
+}
+
+// ---------------------------------------------------------------------------------------------
+// One worker process per GPU
+// ---------------------------------------------------------------------------------------------
+// Worker -> launcher lines (the worker's stdout; its stderr is the launcher's):
+//   S <hip device count> <bdf> <gcn arch> <cus> <lds per block>   after HIP init
+//   H <0|1>                                                       hip-smoke result (--smoke)
+//   W <set>                                                       at the set's rendezvous
+//   R <set> <launched> <ok> <oom> <tflops> <ms> <max_rel_err> <stab dispatches> <stab spread>
+//     <need bytes> <free bytes> <iters> <ramp> <error...>         the set's result
+// Launcher -> worker: "g\n" on its stdin releases the rendezvous. EOF on stdin ends the worker.
+struct Worker {
+  int slot = 0;
+  pid_t pid = -1;
+  int to = -1, from = -1;
+  std::string buf;
+  bool alive = false;
+  std::string why;
+
+  // The next line from the worker within timeout_s; false (and the worker killed) on EOF or timeout.
+  bool line(std::string& out, double timeout_s) {
+    const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds((long long)(timeout_s * 1e6));
+    while (alive) {
+      const size_t nl = buf.find('\n');
+      if (nl != std::string::npos) {
+        out = buf.substr(0, nl);
+        buf.erase(0, nl + 1);
+        return true;
+      }
+      const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(end - std::chrono::steady_clock::now());
+      if (left.count() <= 0) {
+        fail("no reply within " + std::to_string((int)timeout_s) + " s");
+        break;
+      }
+      pollfd p{from, POLLIN, 0};
+      const int n = ::poll(&p, 1, (int)std::min<long long>(left.count(), 1000));
+      if (n < 0 && errno != EINTR) {
+        fail(std::string("poll: ") + std::strerror(errno));
+        break;
+      }
+      if (n <= 0) continue;
+      char tmp[4096];
+      const ssize_t got = ::read(from, tmp, sizeof tmp);
+      if (got > 0) {
+        buf.append(tmp, (size_t)got);
+      } else if (got == 0 || errno != EINTR) {
+        fail("exited");
+        break;
+      }
+    }
+    return false;
+  }
+  void send(const char* s) {
+    if (alive && ::write(to, s, std::strlen(s)) < 0) fail(std::string("write: ") + std::strerror(errno));
+  }
+  void fail(const std::string& w) {
+    if (!alive) return;
+    alive = false;
+    int st = 0;
+    if (::waitpid(pid, &st, WNOHANG) == 0) {
+      ::kill(pid, SIGKILL);
+      (void)::waitpid(pid, &st, 0);
+    }
+    char code[64] = "";
+    if (WIFEXITED(st)) std::snprintf(code, sizeof code, " (exit %d)", WEXITSTATUS(st));
+    else if (WIFSIGNALED(st)) std::snprintf(code, sizeof code, " (signal %d)", WTERMSIG(st));
+    why = "worker for GPU " + std::to_string(slot) + " " + w + code;
+    pid = -1;
+  }
+};
+
+// The GPU agents this process may use, in HIP order, from KFD sysfs (no HIP call: the launcher
+// must not initialise the GPU). KFD hides the properties of agents the device cgroup denies, so the
+// list is what the HIP runtime will enumerate; ROCR_VISIBLE_DEVICES then HIP_VISIBLE_DEVICES narrow it
+// the way the runtime does. `hip_index[i]` is agent i's index under ROCR_VISIBLE_DEVICES (what a
+// worker's HIP_VISIBLE_DEVICES names). False when a visibility list is not numeric (UUIDs).
+static bool visible_agents(std::vector<std::string>& bdf, std::vector<int>& hip_index) {
+  const auto gpus = amdnode::enumerate_gpus("/");
+  std::vector<int> idx;
+  for (size_t i = 0; i < gpus.size(); ++i) idx.push_back((int)i);
+  std::vector<int> sel;
+  if (const char* r = std::getenv("ROCR_VISIBLE_DEVICES"); r && *r) {
+    if (!parse_index_list(r, sel)) return false;
+    std::vector<int> k;
+    for (int x : sel)
+      if (x >= 0 && x < (int)idx.size()) k.push_back(idx[x]);
+    idx = k;
+  }
+  std::vector<int> under_rocr(idx.size());
+  for (size_t i = 0; i < idx.size(); ++i) under_rocr[i] = (int)i;
+  for (const char* var : {"HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"}) {
+    const char* h = std::getenv(var);
+    if (!h || !*h) continue;
+    if (!parse_index_list(h, sel)) return false;
+    std::vector<int> k, u;
+    for (int x : sel)
+      if (x >= 0 && x < (int)idx.size()) k.push_back(idx[x]), u.push_back(under_rocr[x]);
+    idx = k, under_rocr = u;
+    break;
+  }
+  bdf.clear();
+  hip_index.clear();
+  for (size_t i = 0; i < idx.size(); ++i) {
+    bdf.push_back(gpus[idx[i]].pci_bdf);
+    hip_index.push_back(under_rocr[i]);
+  }
+  return true;
+}
+
+static bool spawn_worker(Worker& w, int hip_index, const std::vector<std::string>& args) {
+  int in[2], out[2];
+  if (::pipe2(in, O_CLOEXEC) || ::pipe2(out, O_CLOEXEC)) return false;
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_adddup2(&fa, in[0], 0);
+  posix_spawn_file_actions_adddup2(&fa, out[1], 1);
+  std::vector<std::string> env_s;
+  for (char** e = environ; *e; ++e)
+    if (std::strncmp(*e, "HIP_VISIBLE_DEVICES=", 20) && std::strncmp(*e, "CUDA_VISIBLE_DEVICES=", 21)) env_s.push_back(*e);
+  env_s.push_back("HIP_VISIBLE_DEVICES=" + std::to_string(hip_index));
+  std::vector<char*> envp, argv;
+  for (auto& s : env_s) envp.push_back(s.data());
+  envp.push_back(nullptr);
+  std::vector<std::string> a = args;
+  for (auto& s : a) argv.push_back(s.data());
+  argv.push_back(nullptr);
+  pid_t pid = -1;
+  const int rc = posix_spawn(&pid, "/proc/self/exe", &fa, nullptr, argv.data(), envp.data());
+  posix_spawn_file_actions_destroy(&fa);
+  ::close(in[0]);
+  ::close(out[1]);
+  if (rc != 0) {
+    ::close(in[1]);
+    ::close(out[0]);
+    w.why = std::string("posix_spawn: ") + std::strerror(rc);
+    return false;
+  }
+  w.pid = pid, w.to = in[1], w.from = out[0], w.alive = true;
+  return true;
+}
+
+static std::string fmt_opts(const Options& o) {
+  char buf[256];
+  std::snprintf(buf, sizeof buf, "%d %d %d %.17g %.17g %.17g %.17g %d", o.iters, o.warmup, o.check_rows,
+                o.stabilise_max_s, o.min_window_ms, o.ramp_ms, o.pre_idle_ms, o.stabilise ? 1 : 0);
+  return buf;
+}
+
+static bool parse_opts(const std::string& s, Options& o) {
+  int stab = 1;
+  const int n = std::sscanf(s.c_str(), "%d %d %d %lf %lf %lf %lf %d", &o.iters, &o.warmup, &o.check_rows,
+                            &o.stabilise_max_s, &o.min_window_ms, &o.ramp_ms, &o.pre_idle_ms, &stab);
+  o.stabilise = stab != 0;
+  return n == 8;
+}
+
+// --worker: one GPU (HIP device 0 under the HIP_VISIBLE_DEVICES the launcher set). `sets` is
+// "<id>:<dtype>:<m>x<n>x<k>;..." -- the sets of the plan this GPU takes part in, in plan order.
+static int worker_main(const std::string& sets, const Options& o, bool run_smoke) {
+  std::signal(SIGPIPE, SIG_IGN);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    std::printf("S 0 - - 0 0\n");
+    std::fflush(stdout);
+    return 3;
+  }
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, 0);
+  char bus[64] = "-";
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, 0) != hipSuccess) std::strcpy(bus, "-");
+  for (char* c = bus; *c; ++c) *c = (char)std::tolower(*c);
+  std::printf("S %d %s %s %d %zu\n", ndev, bus, prop.gcnArchName, prop.multiProcessorCount,
+              (size_t)prop.sharedMemPerBlock);
+  std::fflush(stdout);
+  if (run_smoke) {
+    std::printf("H %d\n", smoke_failures({0}) == 0 ? 1 : 0);
+    std::fflush(stdout);
+  }
+  size_t pos = 0;
+  while (pos < sets.size()) {
+    size_t e = sets.find(';', pos);
+    const std::string item = sets.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
+    pos = e == std::string::npos ? sets.size() : e + 1;
+    int id = 0;
+    char dtn[32] = "";
+    Shape s{};
+    if (std::sscanf(item.c_str(), "%d:%31[^:]:%dx%dx%d", &id, dtn, &s.m, &s.n, &s.k) != 5) return 2;
+    const DType* dt = dtype_by_name(dtn);
+    if (!dt) return 2;
+    const std::function<void()> barrier = [&] {
+      std::printf("W %d\n", id);
+      std::fflush(stdout);
+      char go[8];
+      if (!std::fgets(go, sizeof go, stdin)) std::_Exit(4);   // the launcher is gone
+    };
+    Result r;
+    run_one(*dt, 0, s, o, barrier, r);
+    std::string err = r.error;
+    for (char& c : err)
+      if (c == '\n' || c == '\r') c = ' ';
+    std::printf("R %d %d %d %d %.17g %.17g %.17g %d %.17g %zu %zu %d %d %s\n", id, r.launched, r.ok, r.oom, r.tflops,
+                r.ms, r.max_rel_err, r.stab_dispatches, r.stab_spread, r.need_bytes, r.free_bytes, r.iters, r.ramp,
+                err.c_str());
+    std::fflush(stdout);
+  }
+  return 0;
+}
+
+static bool parse_result_line(const std::string& ln, int& id, Result& r) {
+  int launched = 0, ok = 0, oom = 0, off = 0;
+  if (std::sscanf(ln.c_str(), "R %d %d %d %d %lf %lf %lf %d %lf %zu %zu %d %d %n", &id, &launched, &ok, &oom, &r.tflops,
+                  &r.ms, &r.max_rel_err, &r.stab_dispatches, &r.stab_spread, &r.need_bytes, &r.free_bytes, &r.iters,
+                  &r.ramp, &off) < 13)
+    return false;
+  r.launched = launched, r.ok = ok, r.oom = oom;
+  r.error = off > 0 && (size_t)off <= ln.size() ? ln.substr((size_t)off) : "";
+  return true;
+}
+
+static constexpr double kWorkerReplyS = 600.0;   // one set's worst case is seconds; a GPU hang is not
+
+// The launcher: one worker per selected GPU, the plan driven through their pipes.
+static int launch_processes(const std::vector<int>& devs, const std::vector<std::string>& bdf,
+                            const std::vector<int>& hip_index, const std::vector<const DType*>& dtypes,
+                            const std::vector<Shape>& shapes, const std::vector<int>& counts, const Options& o,
+                            bool run_smoke, double min_tflops, double min_tflops_fp8, double min_eff, double min_rel) {
+  std::signal(SIGPIPE, SIG_IGN);
+  std::vector<std::string> sel_bdf;
+  for (int d : devs) sel_bdf.push_back(bdf[d]);
+  const std::vector<Set> plan = make_plan(dtypes, shapes, counts, devs.size(), sel_bdf);
+  std::vector<Worker> ws(devs.size());
+  for (size_t i = 0; i < devs.size(); ++i) {
+    ws[i].slot = devs[i];
+    std::string sets;
+    for (const Set& st : plan)
+      if (std::find(st.slots.begin(), st.slots.end(), (int)i) != st.slots.end()) {
+        char buf[96];
+        std::snprintf(buf, sizeof buf, "%s%d:%s:%dx%dx%d", sets.empty() ? "" : ";", st.id, st.dt->name, st.s.m, st.s.n,
+                      st.s.k);
+        sets += buf;
+      }
+    std::vector<std::string> args = {"amd-gemm-validate", "--worker", sets, "--worker-opts", fmt_opts(o)};
+    if (run_smoke) args.push_back("--smoke");
+    if (!spawn_worker(ws[i], hip_index[devs[i]], args)) ws[i].why = "worker for GPU " + std::to_string(devs[i]) + ": " + ws[i].why;
+  }
+  // start lines: the runtime's view of each worker's GPU, checked against the sysfs agent
+  std::string arch = "unknown";
+  int cus = 0;
+  size_t lds = 0;
+  for (auto& w : ws) {
+    std::string ln;
+    if (!w.line(ln, 300.0)) continue;
+    int n = 0, c = 0;
+    size_t l = 0;
+    char bus[64] = "", a[96] = "";
+    if (std::sscanf(ln.c_str(), "S %d %63s %95s %d %zu", &n, bus, a, &c, &l) != 5 || n < 1) {
+      w.fail("saw no GPU (" + ln + ")");
+      continue;
+    }
+    if (!bdf[w.slot].empty() && std::string(bus) != "-" && bdf[w.slot] != bus) {
+      w.fail(std::string("opened ") + bus + ", not " + bdf[w.slot]);
+      continue;
+    }
+    if (arch == "unknown") arch = a, cus = c, lds = l;
+  }
+  std::printf("{\"event\":\"start\",\"devices\":%zu,\"visible\":%zu,\"gcn_arch\":\"%s\",\"cus\":%d,"
+              "\"lds_per_block\":%zu,\"iters\":%d,\"stabilise\":%s,\"launch\":\"processes\",\"min_window_ms\":%.0f}\n",
+              devs.size(), bdf.size(), arch.c_str(), cus, lds, o.iters, o.stabilise ? "true" : "false", o.min_window_ms);
+  std::fflush(stdout);
+  bool all_ok = true;
+  if (run_smoke) {
+    int failures = 0;
+    for (auto& w : ws) {
+      std::string ln;
+      failures += !(w.line(ln, 120.0) && ln == "H 1");
+    }
+    print_smoke(devs.size(), failures);
+    all_ok = failures == 0;
+  }
+  auto lost = [&](Result& r, const Worker& w) {
+    r.launched = false;
+    r.error = w.why.empty() ? "worker for GPU " + std::to_string(w.slot) + " lost" : w.why;
+  };
+  all_ok = run_plan(plan, devs.size(), min_tflops, min_tflops_fp8, min_eff, min_rel,
+                    [&](const Set& set, std::vector<Result>& res) {
+                      const std::string want_w = "W " + std::to_string(set.id);
+                      for (int slot : set.slots) {
+                        std::string ln;
+                        while (ws[slot].line(ln, kWorkerReplyS) && ln != want_w) {
+                        }
+                      }
+                      for (int slot : set.slots) ws[slot].send("g\n");
+                      for (size_t i = 0; i < set.slots.size(); ++i) {
+                        Worker& w = ws[set.slots[i]];
+                        res[i].device = w.slot;
+                        res[i].s = set.s;
+                        std::string ln;
+                        int id = -1;
+                        bool got = false;
+                        while (w.line(ln, kWorkerReplyS))
+                          if (ln.rfind("R ", 0) == 0 && parse_result_line(ln, id, res[i]) && id == set.id) {
+                            got = true;
+                            break;
+                          }
+                        if (!got) lost(res[i], w);
+                      }
+                    }) && all_ok;
+  // the last line: every result is out; the workers' exits (the runtime's and the driver's teardown
+  // of their GPU state, ~0.1 s on MI355X) are not waited for before it (workload_main.stream_run)
+  std::printf("{\"event\":\"done\",\"ok\":%s}\n", all_ok ? "true" : "false");
+  std::fflush(stdout);
+  for (auto& w : ws) {
+    if (w.to >= 0) ::close(w.to);
+    if (w.pid > 0) (void)::waitpid(w.pid, nullptr, 0);
+    if (w.from >= 0) ::close(w.from);
+  }
+  return all_ok ? 0 : 1;
+}
+
+// Launched under a profiler, the process already holds the GPU (rocprofv3's preloaded tool
+// initialises it): it must not start other programs.
+static bool under_profiler() {
+  const char* p = std::getenv("LD_PRELOAD");
+  return (p && std::strstr(p, "rocprof")) || std::getenv("ROCPROFILER_LIBRARY_CTOR") != nullptr;
+}
+
 int main(int argc, char** argv) {
-  std::string shapes = "8192", devices = "all", dtype = "bf16", scaling;
+  std::string shapes = "8192", devices = "all", dtype = "bf16", scaling, launch = "processes", worker_sets;
+  std::string worker_opts;
+  bool worker = false;
   Options o;
   double min_tflops = 0, min_tflops_fp8 = 0, min_eff = 0, min_rel = 0;
   bool run_smoke = false;
@@ -443,23 +978,37 @@ int main(int argc, char** argv) {
     else if (a == "--min-relative") min_rel = std::atof(next().c_str());
     else if (a == "--stabilise-max-s") o.stabilise_max_s = std::atof(next().c_str());
     else if (a == "--no-stabilise") o.stabilise = false;
+    else if (a == "--min-window-ms") o.min_window_ms = std::max(0.0, std::atof(next().c_str()));
+    else if (a == "--ramp-ms") o.ramp_ms = std::max(0.0, std::atof(next().c_str()));
+    else if (a == "--pre-timed-idle-ms") o.pre_idle_ms = std::max(0.0, std::atof(next().c_str()));
+    else if (a == "--launch") launch = next();
     else if (a == "--smoke") run_smoke = true;
+    else if (a == "--worker") worker = true, worker_sets = next();
+    else if (a == "--worker-opts") worker_opts = next();
     else if (a == "-h" || a == "--help") {
       std::printf("usage: amd-gemm-validate [--shapes 8192,4096,MxNxK] [--dtype bf16|fp8|both] [--iters N] "
                   "[--warmup N] [--devices all|0,1] [--scaling 1,2,4,8] [--check-rows N] [--min-tflops X] "
                   "[--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R] [--stabilise-max-s S] [--no-stabilise] "
-                  "[--smoke]\n");
+                  "[--smoke] [--launch processes|threads] [--min-window-ms MS] [--ramp-ms MS] [--pre-timed-idle-ms MS]\n");
       return 0;
     } else {
-      std::printf("{\"error\":\"unknown argument %s\"}\n", a.c_str());
+      std::printf("{\"error\":\"unknown argument %s\"}\n", json_safe(a).c_str());
       return 2;
     }
+  }
+  if (worker) {
+    if (!worker_opts.empty() && !parse_opts(worker_opts, o)) return 2;
+    return worker_main(worker_sets, o, run_smoke);
+  }
+  if (launch != "processes" && launch != "threads") {
+    std::printf("{\"error\":\"unknown --launch %s (processes or threads)\"}\n", json_safe(launch).c_str());
+    return 2;
   }
   std::vector<const DType*> dtypes;
   if (dtype == "bf16" || dtype == "both") dtypes.push_back(&kBf16);
   if (dtype == "fp8" || dtype == "both") dtypes.push_back(&kFp8);
   if (dtypes.empty()) {
-    std::printf("{\"error\":\"unknown --dtype %s (bf16, fp8 or both)\"}\n", dtype.c_str());
+    std::printf("{\"error\":\"unknown --dtype %s (bf16, fp8 or both)\"}\n", json_safe(dtype).c_str());
     return 2;
   }
   const std::vector<Shape> shape_list = parse_shapes(shapes);
@@ -468,8 +1017,18 @@ int main(int argc, char** argv) {
       std::printf("{\"error\":\"bad shape %dx%dx%d\"}\n", s.m, s.n, s.k);
       return 2;
     }
+  const std::vector<int> counts = parse_ints(scaling);
+  // the device list: from sysfs in the launcher (no HIP call), from the runtime with threads
+  std::vector<std::string> bdf;
+  std::vector<int> hip_index;
+  if (launch == "processes" && (under_profiler() || !visible_agents(bdf, hip_index))) launch = "threads";
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+  if (launch == "processes") {
+    ndev = (int)bdf.size();
+  } else if (hipGetDeviceCount(&ndev) != hipSuccess) {
+    ndev = 0;
+  }
+  if (ndev == 0) {
     std::printf("{\"error\":\"no AMD GPU visible\"}\n");
     return 3;
   }
@@ -489,64 +1048,38 @@ int main(int argc, char** argv) {
     std::printf("{\"error\":\"no device selected\"}\n");
     return 2;
   }
+  if (launch == "processes")
+    return launch_processes(devs, bdf, hip_index, dtypes, shape_list, counts, o, run_smoke, min_tflops,
+                            min_tflops_fp8, min_eff, min_rel);
+
+  // --launch threads: one process, one host thread per GPU
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, devs[0]);
   std::printf("{\"event\":\"start\",\"devices\":%zu,\"visible\":%d,\"gcn_arch\":\"%s\",\"cus\":%d,"
-              "\"lds_per_block\":%zu,\"iters\":%d,\"stabilise\":%s}\n",
+              "\"lds_per_block\":%zu,\"iters\":%d,\"stabilise\":%s,\"launch\":\"threads\",\"min_window_ms\":%.0f}\n",
               devs.size(), ndev, prop.gcnArchName, prop.multiProcessorCount, (size_t)prop.sharedMemPerBlock,
-              o.iters, o.stabilise ? "true" : "false");
+              o.iters, o.stabilise ? "true" : "false", o.min_window_ms);
   bool all_ok = true;
-  if (run_smoke) all_ok = smoke(devs);
-  const std::vector<int> counts = parse_ints(scaling);
-  for (const DType* dt : dtypes) {
-    const double floor = dt == &kFp8 ? min_tflops_fp8 : min_tflops;
-    for (const auto& s : shape_list) {
-      if (counts.empty()) {
-        all_ok = run_set(*dt, s, devs, o, floor, 0, 0, 0).ok && all_ok;
-        continue;
-      }
-      // the 1-GPU figure every efficiency divides by: the N=1 run when the sweep has one, else
-      // a 1-GPU run first
-      double single = 0;
-      std::vector<int> order = counts;
-      if (std::find(order.begin(), order.end(), 1) == order.end()) order.insert(order.begin(), 1);
-      std::stable_sort(order.begin(), order.end());
-      for (int n : order) {
-        if (n < 1) continue;
-        if ((size_t)n > devs.size()) {
-          std::printf("{\"event\":\"scaling\",\"dtype\":\"%s\",\"m\":%d,\"n\":%d,\"k\":%d,\"gpus\":%d,"
-                      "\"skipped\":\"%zu GPU(s) visible\"}\n",
-                      dt->name, s.m, s.n, s.k, n, devs.size());
-          continue;
-        }
-        std::vector<int> sub(devs.begin(), devs.begin() + n);
-        Aggregate a = run_set(*dt, s, sub, o, floor, n, single, min_eff);
-        if (n == 1) single = a.per_gpu;
-        all_ok = a.ok && all_ok;
-      }
-    }
+  if (run_smoke) {
+    const int failures = smoke_failures(devs);
+    print_smoke(devs.size(), failures);
+    all_ok = failures == 0;
   }
-  // uniformity: every GPU's best against the node's (upper) median, per dtype and shape
-  for (const auto& [key, per_dev] : g_best) {
-    if (per_dev.size() < 2) continue;
-    std::vector<double> v;
-    for (const auto& kv : per_dev) v.push_back(kv.second);
-    std::sort(v.begin(), v.end());
-    const double med = v[v.size() / 2];
-    double worst = 1e30;
-    std::string slow;
-    for (const auto& [dev, t] : per_dev) {
-      const double ratio = med > 0 ? t / med : 0;
-      worst = std::min(worst, ratio);
-      if (min_rel > 0 && ratio < min_rel) slow += (slow.empty() ? "" : ",") + std::to_string(dev);
-    }
-    const bool ok = slow.empty();
-    all_ok = all_ok && ok;
-    std::printf("{\"event\":\"uniformity\",\"dtype\":\"%s\",\"m\":%d,\"n\":%d,\"k\":%d,\"gpus\":%zu,"
-                "\"median_tflops\":%.1f,\"min_ratio\":%.4f,\"min_relative\":%.2f,\"slow_devices\":[%s],\"ok\":%s}\n",
-                std::get<0>(key).c_str(), std::get<1>(key), std::get<2>(key), std::get<3>(key), per_dev.size(), med,
-                worst, min_rel, slow.c_str(), ok ? "true" : "false");
+  std::vector<std::string> sel_bdf;
+  for (int d : devs) {
+    char bus[64] = "";
+    sel_bdf.push_back(hipDeviceGetPCIBusId(bus, sizeof bus, d) == hipSuccess ? std::string(bus) : std::string());
   }
+  const std::vector<Set> plan = make_plan(dtypes, shape_list, counts, devs.size(), sel_bdf);
+  all_ok = run_plan(plan, devs.size(), min_tflops, min_tflops_fp8, min_eff, min_rel,
+                    [&](const Set& set, std::vector<Result>& res) {
+                      Rendezvous sync(set.slots.size());
+                      const std::function<void()> barrier = [&] { sync.arrive_and_wait(); };
+                      std::vector<std::thread> th;
+                      for (size_t i = 0; i < set.slots.size(); ++i)
+                        th.emplace_back([&, i] { run_one(*set.dt, devs[set.slots[i]], set.s, o, barrier, res[i]); });
+                      for (auto& t : th) t.join();
+                    }) && all_ok;
   // the last line: every result is out and every device synchronised. The validator reads up to
   // here and lets the process exit on its own (the runtime's and the driver's teardown of this
   // process's GPU state takes ~0.1 s on MI355X after the last line; workload_main.stream_run).

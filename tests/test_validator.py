@@ -39,10 +39,13 @@ def ctx_for(tmp_path, root, client=None, **kw):
 
 
 class FakeKubelet:
-    """Completes validation pods with a canned termination message."""
+    """Completes validation pods with a canned termination message, with kubelet's semantics for
+    the pod's restartPolicy: ``exit_code`` 0 -> Succeeded; non-zero -> the init container terminated
+    with it and, under ``Never``, the pod Failed -- under ``OnFailure`` the pod stays Pending and the
+    container is restarted (restartCount 1, the exit in lastState), as a real kubelet does."""
 
-    def __init__(self, client, messages, phase="Succeeded"):
-        self.client, self.messages, self.phase = client, messages, phase
+    def __init__(self, client, messages, exit_code=0):
+        self.client, self.messages, self.exit_code = client, messages, exit_code
         self.seen = []
         self.stop = client.watch("v1", "Pod", self.on_event)
 
@@ -55,6 +58,8 @@ class FakeKubelet:
         msg = self.messages.get(app, "")
         if isinstance(msg, list):               # one message per pod, the last one repeats
             msg = msg.pop(0) if len(msg) > 1 else msg[0]
+        code = self.exit_code.pop(0) if isinstance(self.exit_code, list) and len(self.exit_code) > 1 else \
+            (self.exit_code[0] if isinstance(self.exit_code, list) else self.exit_code)
 
         def finish():
             time.sleep(0.05)
@@ -62,8 +67,16 @@ class FakeKubelet:
                 p = self.client.get("v1", "Pod", o.name(pod), o.namespace(pod))
             except Exception:  # noqa: BLE001 - the validator withdrew the pod first
                 return
-            p["status"] = {"phase": self.phase, "initContainerStatuses": [
-                {"name": "x", "state": {"terminated": {"exitCode": 0, "message": msg}}}]}
+            term = {"exitCode": code, "reason": "Completed" if code == 0 else "Error", "message": msg}
+            if code == 0:
+                p["status"] = {"phase": "Succeeded", "initContainerStatuses": [
+                    {"name": "x", "restartCount": 0, "state": {"terminated": term}}]}
+            elif (p.get("spec") or {}).get("restartPolicy") == "Never":
+                p["status"] = {"phase": "Failed", "initContainerStatuses": [
+                    {"name": "x", "restartCount": 0, "state": {"terminated": term}}]}
+            else:
+                p["status"] = {"phase": "Pending", "initContainerStatuses": [
+                    {"name": "x", "restartCount": 1, "state": {"running": {}}, "lastState": {"terminated": term}}]}
             self.client.update_status(p)
         threading.Thread(target=finish).start()
 
@@ -143,13 +156,58 @@ def test_hip_spawns_pinned_pod_and_records_results(tmp_path, node_root):
     assert ctx.status.read(S.HIP_READY)["gemm_tflops_per_gpu"] == 1362.5
 
 
-def test_hip_failed_pod_fails_validation(tmp_path, node_root):
+def test_hip_failed_pod_fails_validation_fast(tmp_path, node_root):
+    """restartPolicy Never: the failing workload fails the pod; the validator returns at once with a
+    ValidationError naming the failing check (not a 300 s timeout)."""
     c = FakeClient([node_obj()])
-    FakeKubelet(c, {"amd-hip-validator": '{"event":"gemm","ok":false}'}, phase="Failed")
-    ctx = ctx_for(tmp_path, node_root, client=c)
-    with pytest.raises(RuntimeError, match="failed"):
+    k = FakeKubelet(c, {"amd-hip-validator": '{"event":"gemm","dtype":"bf16","device":3,"ok":false,'
+                                             '"kind":"correctness","error":"check failed: max_rel_err 0.5"}'},
+                    exit_code=1)
+    ctx = ctx_for(tmp_path, node_root, client=c, pod_timeout=60)
+    t0 = time.monotonic()
+    with pytest.raises(comp.ValidationError, match="device 3: check failed") as e:
         comp.validate_hip(ctx)
+    assert time.monotonic() - t0 < 5 and len(k.seen) == 1          # a correctness failure: no re-measure
+    assert [f.kind for f in e.value.failures] == ["correctness"]
+    assert k.seen[0]["spec"]["restartPolicy"] == "Never"
     assert not ctx.status.exists(S.HIP_READY)
+
+
+def test_onfailure_pod_fails_at_the_first_container_exit(tmp_path, node_root, monkeypatch):
+    """A pod template with the reference's OnFailure (an admin's ConfigMap override): the kubelet
+    restarts the failing init container and the pod never reaches Failed -- wait_for_pod returns at the
+    first non-zero exit (lastState), deletes the crash-looping pod, and reports the workload's lines."""
+    from gpu_operator_amd.validator import workload as W
+    real = W.load_pod_spec
+
+    def onfailure(name):
+        t = real(name)
+        t["spec"]["restartPolicy"] = "OnFailure"
+        return t
+    monkeypatch.setattr(W, "load_pod_spec", onfailure)
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-hip-validator": '{"event":"hip-smoke","ok":false,"kind":"correctness"}'}, exit_code=1)
+    ctx = ctx_for(tmp_path, node_root, client=c, pod_timeout=60)
+    t0 = time.monotonic()
+    with pytest.raises(comp.ValidationError, match="hip-smoke failed"):
+        comp.validate_hip(ctx)
+    assert time.monotonic() - t0 < 5
+    assert not [p for p in c.list("v1", "Pod", NS) if o.get_labels(p).get("app") == "amd-hip-validator"]
+
+
+def test_failed_pod_without_result_lines_names_the_exit(tmp_path, node_root):
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-hip-validator": "Traceback (most recent call last): boom"}, exit_code=2)
+    ctx = ctx_for(tmp_path, node_root, client=c, pod_timeout=60)
+    with pytest.raises(comp.ValidationError, match="failed with no result.*exited 2"):
+        comp.validate_hip(ctx)
+
+
+def test_hip_pod_timeout_is_a_validation_error(tmp_path, node_root):
+    c = FakeClient([node_obj()])                    # no kubelet: the pod never runs
+    ctx = ctx_for(tmp_path, node_root, client=c, pod_timeout=0.5)
+    with pytest.raises(comp.ValidationError, match="did not finish within 0s|did not finish within 1s"):
+        comp.validate_hip(ctx)
 
 
 def test_plugin_waits_for_capacity_event(tmp_path, node_root):
@@ -304,7 +362,7 @@ def test_rccl_fails_validation_on_a_split_hive(tmp_path, node_root):
         {"event": "fabric", "physical_gpus": 8, "single_hive": False, "ok": False, "reason": "GPUs span 2 xGMI hives"},
         {"event": "summary", "ok": False, "reason": "fabric check failed"}])
     c = FakeClient([node_obj()])
-    FakeKubelet(c, {"amd-rccl-validator": msg}, phase="Failed")
+    FakeKubelet(c, {"amd-rccl-validator": msg}, exit_code=1)
     ctx = ctx_for(tmp_path, node_root, client=c)
     with pytest.raises(Exception):
         comp.validate_rccl(ctx)
@@ -450,8 +508,11 @@ def test_hip_throughput_failure_is_measured_once_more(tmp_path, node_root):
     with pytest.raises(comp.ValidationError, match="check failed"):
         comp.validate_hip(ctx_for(tmp_path / "b", node_root, client=c2))
     assert len(k2.seen) == 1
-    assert comp._throughput_only(["gemm bf16 device 0: below floor: 329.1 < 1258.3 TFLOP/s"])
-    assert not comp._throughput_only(["gemm bf16 device 0: check failed", "gemm bf16 device 1: below floor: 1 < 2 TFLOP/s"])
+    # the decision reads each failure's kind, never its wording
+    G = comp.GateFailure
+    assert comp.throughput_only([G("floor", "anything"), G("efficiency", "x"), G("relative", "y")])
+    assert not comp.throughput_only([G("correctness", "below floor: 1 < 2 TFLOP/s"), G("floor", "z")])
+    assert not comp.throughput_only([G("oom", "out of memory")]) and not comp.throughput_only([])
 
 
 def test_hip_records_the_scaling_sweep(tmp_path, node_root):
@@ -643,7 +704,7 @@ def test_rccl_tenant_between_the_busy_check_and_the_fabric_pod_falls_back(tmp_pa
     """The kubelet rejects the nodeName-bound fabric pod at admission (a tenant took GPUs after the
     busy check): topology-only in seconds, not a failure after the 300 s pod timeout."""
     c = FakeClient([node_obj()])
-    k = FakeKubelet(c, {"amd-rccl-validator": ""}, phase="Failed")
+    k = FakeKubelet(c, {"amd-rccl-validator": ""}, exit_code=1)
     orig = k.on_event
 
     def admit(ev):                        # the tenant lands as the fabric pod is created

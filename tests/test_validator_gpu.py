@@ -223,3 +223,67 @@ def test_gemm_validate_runs_hip_smoke_in_process():
     assert rc == 0, err
     sm = [x for x in lines if x.get("event") == "hip-smoke"]
     assert len(sm) == 1 and sm[0]["ok"] and sm[0]["devices"] >= 1 and sm[0]["elements"] == 50000
+
+
+def _tflops(*extra):
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "8192", "--iters", "50", *extra)
+    assert rc == 0, err
+    g = [x for x in lines if x["event"] == "gemm"][0]
+    return g, lines
+
+
+def test_idle_before_the_timed_loop_does_not_droop_the_number():
+    """A GPU that waits at the rendezvous (here: 200 ms of host idle injected after it) re-ramps before
+    the timed loop, and the window is >= 100 ms: the reported TF/s stays within 2 % of the run
+    without the idle (VERDICT r4 weak #3)."""
+    base, lines = _tflops()
+    idle, _ = _tflops("--pre-timed-idle-ms", "200")
+    print(f"no idle {base['tflops']} TF/s, 200 ms idle {idle['tflops']} TF/s; ramp {idle['ramp_dispatches']}, "
+          f"iters {idle['iters']}")
+    assert base["iters"] * base["ms"] >= 99.0 and base["ramp_dispatches"] >= 10
+    assert abs(idle["tflops"] - base["tflops"]) <= 0.02 * base["tflops"], (base, idle)
+
+
+def test_bench_reramps_after_the_barrier():
+    """bench.py's timed region after a 200 ms idle at the pre-timing barrier: within 2 % of the run
+    without it (the re-ramp runs between the barrier and the timed loop)."""
+    import sys
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from gpu_operator_amd.ops import gemm as G
+    dev = torch.device("cuda", 0)
+    m = 8192
+    a = G.fill_uniform_(torch.empty((m, m), dtype=torch.bfloat16, device=dev), 1000)
+    bt = G.fill_uniform_(torch.empty((m, m), dtype=torch.bfloat16, device=dev), 2000)
+    c = torch.empty((m, m), dtype=torch.bfloat16, device=dev)
+    out = {}
+    for idle in (0.0, 200.0):
+        args = bench.parse_args(["--steps", "20", "--warmup", "5", "--pre-timed-idle-ms", str(idle)])
+        ctx = bench.Ctx(args, torch, None, dev, 0, 0, 1, False, False)
+        res = ctx.timed(lambda: G.gemm_bf16(a, bt, c), 20, 5)
+        out[idle] = G.tflops(m, m, m, res["elapsed_s"] / 20)
+        assert res["ramp_dispatches"] >= 10
+    print(f"bench 20 steps: no idle {out[0.0]:.1f}, 200 ms idle {out[200.0]:.1f} TF/s")
+    assert abs(out[200.0] - out[0.0]) <= 0.02 * out[0.0], out
+
+
+def test_gemm_validate_runs_one_worker_process_per_gpu():
+    """The default launch: a launcher that never opens the GPU and one worker per GPU meeting at a
+    pipe rendezvous. Two workers on the box's one GPU (--devices 0,0) exercise the rendezvous; their
+    2-GPU set shares a physical GPU, so it is measured and marked, not gated on efficiency."""
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "2048", "--iters", "5", "--devices", "0,0",
+                         "--scaling", "1,2", "--min-efficiency", "0.9", "--smoke")
+    assert rc == 0, (lines, err)
+    start = lines[0]
+    assert start["launch"] == "processes" and start["devices"] == 2 and start["gcn_arch"].startswith("gfx950")
+    assert [x for x in lines if x["event"] == "hip-smoke"][0] == {"event": "hip-smoke", "devices": 2,
+                                                                  "elements": 50000, "ok": True}
+    aggs = {a["gpus"]: a for a in lines if a["event"] == "aggregate"}
+    assert aggs[1]["ok"] and aggs[2]["ok"] and aggs[2]["shared_gpu"] and aggs[2]["efficiency_gated"] is False
+    gemms = [x for x in lines if x["event"] == "gemm" and x.get("gpus") == 2]
+    assert len(gemms) == 2 and all(g["ok"] for g in gemms)
+    assert lines[-1] == {"event": "done", "ok": True}
+    rc, lines, err = run("amd-gemm-validate", "--shapes", "2048", "--iters", "5", "--launch", "threads")
+    assert rc == 0 and lines[0]["launch"] == "threads", err

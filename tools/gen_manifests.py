@@ -7,6 +7,9 @@
   templates/clusterrole.yaml
 * the OLM ClusterServiceVersion (relatedImages + ``*_IMAGE`` env from the chart's values,
   alm-examples from the sample CR) -> bundle/manifests/ and config/manifests/bases/
+* the validator's workload-pod ConfigMap (the admin-overridable copy of
+  gpu_operator_amd/validator/manifests/*.yaml, the pod templates the validator spawns)
+  -> gpu_operator_amd/assets/state-operator-validation/0600_configmap_workloads.yaml
 
 Reference counterpart: controller-gen + operator-sdk.
 ``python tools/gen_manifests.py`` rewrites them; ``--check`` exits 1 if any is stale (CI).
@@ -211,6 +214,23 @@ def dump(obj) -> str:
     return "# generated by tools/gen_manifests.py -- do not edit\n" + _yaml(obj)
 
 
+WORKLOAD_MANIFESTS = ROOT / "gpu_operator_amd" / "validator" / "manifests"
+
+
+def workloads_configmap() -> str:
+    """The validation pod templates, verbatim, as the ConfigMap the validator state deploys."""
+    head = ("# generated by tools/gen_manifests.py -- do not edit (source: gpu_operator_amd/validator/manifests/)\n"
+            "# Pod templates the validator spawns (mounted at /var/amd/manifests in the validator image\n"
+            "# as well; this ConfigMap lets a cluster admin override them without rebuilding the image).\n"
+            "apiVersion: v1\nkind: ConfigMap\nmetadata:\n  name: amd-validator-workloads\n"
+            "  namespace: FILLED_BY_OPERATOR\n  labels:\n    app: amd-operator-validator\ndata:\n")
+    body = ""
+    for f in sorted(WORKLOAD_MANIFESTS.glob("*.yaml")):
+        body += f"  {f.name}: |-\n" + "".join("    " + ln if ln.strip() else "\n"
+                                               for ln in f.read_text().rstrip("\n").splitlines(True)) + "\n"
+    return head + body
+
+
 def outputs() -> Dict[Path, str]:
     c = dump(crd())
     cr = operator_clusterrole()
@@ -228,6 +248,8 @@ def outputs() -> Dict[Path, str]:
         CHART / "templates" / "clusterrole.yaml": chart_cr,
         ROOT / "bundle" / "manifests" / "amd-gpu-operator.clusterserviceversion.yaml": s,
         ROOT / "config" / "manifests" / "bases" / "amd-gpu-operator.clusterserviceversion.yaml": s,
+        ROOT / "gpu_operator_amd" / "assets" / "state-operator-validation" / "0600_configmap_workloads.yaml":
+            workloads_configmap(),
     }
 
 
