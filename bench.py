@@ -440,6 +440,12 @@ def _time_to_ready_extra():
     ours, ref = r["ours"], r["reference"]
     out = {"agent_chain_time_to_ready_s": r["agent_chain_time_to_ready_s"],
            "reference_protocol_time_to_ready_s": r["reference_protocol_time_to_ready_s"],
+           # the harness's simulated waits on the validator's path (sandbox retry tick, crash-loop
+           # back-off) apart from the measured rest: processes, API calls, barriers, GPU work
+           "time_to_ready_measured_s": r.get("agent_chain_time_to_ready_measured_s"),
+           "time_to_ready_modelled_s": r.get("agent_chain_time_to_ready_modelled_s"),
+           "reference_protocol_time_to_ready_measured_s": r.get("reference_protocol_time_to_ready_measured_s"),
+           "reference_protocol_time_to_ready_modelled_s": r.get("reference_protocol_time_to_ready_modelled_s"),
            "agent_chain_full_time_to_ready_s": r.get("agent_chain_full_time_to_ready_s"),
            "time_to_ready_barriers_s": ours["barriers_s"],
            "time_to_ready_full_barriers_s": (r.get("ours_full") or {}).get("barriers_s"),

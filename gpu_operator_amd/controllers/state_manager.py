@@ -267,18 +267,29 @@ class StateManager:
         if self.spec.driver.use_precompiled():
             self._dtk_enabled = False
         elif self.dtk_requested:
+            broken = False
             try:
                 ist = self.client.get("image.openshift.io/v1", "ImageStream", "driver-toolkit", "openshift")
                 for tag in (ist.get("spec") or {}).get("tags") or []:
+                    name = tag.get("name") or ""
+                    if not name:
+                        # a nameless tag: the ImageStream an OpenShift upgrade left broken (RHBZ#2015024;
+                        # reference controllers/object_controls.go:3301-3319) -- flagged, never indexed
+                        broken = True
+                        continue
                     frm = (tag.get("from") or {}).get("name")
-                    if frm:
-                        self.dtk_images[tag["name"]] = frm
+                    if name == "latest" or not frm:
+                        continue
+                    self.dtk_images[name] = frm
                 has_is = True
             except (errors.NotFound, errors.NoKindMatch):
                 has_is = False
+            if broken:
+                log.warning("the driver-toolkit ImageStream has a tag without a name (RHBZ#2015024): it is broken")
             self._dtk_enabled = has_is and bool(self.rhcos_versions)
             if self.metrics:
                 self.metrics.dtk_imagestream_missing.set(0 if has_is else 1)
+                self.metrics.dtk_imagestream_broken.set(1 if broken else 0)
                 self.metrics.dtk_nfd_too_old.set(1 if self.has_gpu_nodes and not self.rhcos_versions else 0)
                 missing = [v for v in self.rhcos_versions if v not in self.dtk_images]
                 self.metrics.dtk_rhcos_tags_missing.set(1 if missing else 0)

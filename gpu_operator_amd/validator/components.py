@@ -448,6 +448,13 @@ def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
                 "total_tflops": r["total_tflops"], "per_gpu_tflops": r["per_gpu_tflops"],
                 **({"efficiency": r["efficiency"]} if "efficiency" in r else {})}
         out["tflops_by_dtype_gpus"] = by
+    # every GPU's best TFLOP/s per (dtype, shape): the workload's compact lines, else the per-GPU ones
+    lines = [r for r in results if r.get("event") == "gpu_tflops"]
+    if not lines and per:
+        from .workload_main import gpu_tflops_lines
+        lines = gpu_tflops_lines(per)
+    if lines:
+        out["gpu_tflops"] = [{k: r[k] for k in ("dtype", "m", "n", "k", "tflops")} for r in lines]
     sc = [r for r in results if r.get("event") == "scaling"]
     if sc:
         out["scaling_skipped"] = sorted({r["gpus"] for r in sc if r.get("skipped")})

@@ -58,6 +58,9 @@ class NodeMetrics:
         self.gemm_tflops = Gauge(p + "validator_gemm_tflops",
                                  "validator MFMA GEMM throughput on `gpus` GPUs at once (scope node = aggregate, "
                                  "per_gpu = mean per GPU)", node + ["scope", "dtype", "gpus"], registry=r)
+        self.gemm_gpu_tflops = Gauge(p + "validator_gemm_gpu_tflops",
+                                     "validator MFMA GEMM throughput of one GPU (its best over the sweep's sets)",
+                                     node + ["gpu", "dtype", "m", "n", "k"], registry=r)
         self.gemm_eff = Gauge(p + "validator_gemm_scaling_efficiency",
                               "aggregate GEMM TFLOP/s on `gpus` GPUs / (gpus x the 1-GPU figure)",
                               node + ["dtype", "gpus"], registry=r)
@@ -92,6 +95,10 @@ class NodeMetrics:
             g = str(hip.get("gpus") or "")
             self.gemm_tflops.labels(n, "node", "bf16", g).set(hip["gemm_tflops_total"])
             self.gemm_tflops.labels(n, "per_gpu", "bf16", g).set(hip.get("gemm_tflops_per_gpu", 0))
+        for line in hip.get("gpu_tflops") or []:      # one series per GPU: a GPU failing the median shows
+            for gpu, v in (line.get("tflops") or {}).items():
+                self.gemm_gpu_tflops.labels(n, str(gpu), comp._dtype_key(line.get("dtype", "bf16")), str(line.get("m")),
+                                            str(line.get("n")), str(line.get("k"))).set(v)
         rc = sd.read(S.RCCL_READY) or {}
         if rc.get("peak_busbw_gbps") is not None:
             self.busbw.labels(n, str(rc.get("ranks"))).set(rc["peak_busbw_gbps"])

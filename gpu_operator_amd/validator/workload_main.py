@@ -260,12 +260,29 @@ def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
         results += [x for x in r if x.get("event") in ("gemm", "start", "hip-smoke") or "error" in x]
         if rc != 0 and not any(x.get("event") == "gemm" for x in r):
             results.append({"event": "gemm", "probe": True, "ok": False, "rc": rc})
+    results += gpu_tflops_lines(results)
     if counters and full:
         for d in (["bf16", "fp8"] if dtype == "both" else [dtype]):
             # the profiler writes its counters from the child's exit path: wait for it (subprocess.run)
             results += collect_counters(shapes[0], subprocess.run if run is stream_run else run, dtype=d,
                                         visible=devices[:1] if devices else None)
     return results
+
+
+def gpu_tflops_lines(results: List[Dict]) -> List[Dict]:
+    """One compact ``gpu_tflops`` line per (dtype, shape): every GPU's best TFLOP/s over the sets it
+    ran in (node HIP indices). A summary line: it survives the 4 KiB termination message that the
+    per-GPU lines of a 2-dtype x 1/2/4/8 sweep (30 lines) do not, so the validator can export one
+    series per GPU (validator_gemm_gpu_tflops)."""
+    best: Dict[tuple, Dict[str, float]] = {}
+    for r in results:
+        if r.get("event") != "gemm" or r.get("probe") or not r.get("ok") or not r.get("tflops"):
+            continue
+        d = best.setdefault((r.get("dtype", "bf16"), r.get("m"), r.get("n"), r.get("k")), {})
+        dev = str(r.get("device"))
+        d[dev] = max(d.get(dev, 0.0), float(r["tflops"]))
+    return [{"event": "gpu_tflops", "dtype": dt, "m": m, "n": n, "k": k, "tflops": dict(sorted(v.items()))}
+            for (dt, m, n, k), v in sorted(best.items(), key=lambda kv: str(kv[0]))]
 
 
 def hip_ok(results: List[Dict]) -> bool:
@@ -451,7 +468,7 @@ def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict
 
 TERMINATION_LOG_BYTES = 4000       # kubelet keeps at most 4 KiB of a termination message
 _SUMMARY_EVENTS = ("plan", "aggregate", "uniformity", "summary", "timeout", "async_error", "hip-smoke", "counters",
-                   "scaling", "fabric", "ranks_summary", "rccl-debug")
+                   "scaling", "fabric", "ranks_summary", "rccl-debug", "gpu_tflops")
 
 
 def termination_message(results: List[Dict], limit: int = TERMINATION_LOG_BYTES) -> str:
@@ -514,7 +531,8 @@ def main(argv=None) -> int:
     r.add_argument("--max-bytes", type=int, default=int(os.environ.get("RCCL_MAX_BYTES", RCCL_MAX_BYTES)))
     r.add_argument("--timeout-s", type=float, default=float(os.environ.get("RCCL_TIMEOUT_S", RCCL_STEP_TIMEOUT_S)),
                    help="the binary's watchdog: bound on one blocking step (0 = none)")
-    r.add_argument("--dtype", default=os.environ.get("RCCL_DTYPE", "float"))
+    r.add_argument("--dtype", default=os.environ.get("RCCL_DTYPE", "bf16"),
+                   help="all-reduce element type (bf16, the validator's local mode default too)")
     r.add_argument("--ranks", default=os.environ.get("RCCL_RANKS", "2,4,8"))
     r.add_argument("--processes", type=int, default=int(os.environ.get("RCCL_PROCESSES", "0")))
     r.add_argument("--min-busbw", type=float, default=float(os.environ.get("RCCL_MIN_BUSBW_GBPS", "0") or 0))

@@ -568,3 +568,54 @@ def test_ocp_proxy_without_trusted_ca_sets_env_only():
     drv = container(ds, "amdgpu-driver-ctr")
     assert env(drv)["HTTPS_PROXY"] == "http://proxy.corp:3128"
     assert C.TRUSTED_CA_CONFIGMAP not in {m["name"] for m in drv.get("volumeMounts", [])}
+
+
+# ------------------------------------------------------------------------------ OpenShift driver toolkit
+def test_broken_driver_toolkit_imagestream_is_flagged_not_fatal():
+    """A nameless tag in openshift/driver-toolkit (the broken ImageStream of RHBZ#2015024; reference
+    controllers/object_controls.go:3301-3319): the reconcile completes, the nameless and `latest` tags
+    are skipped, the RHCOS tag is used, and amd_gpu_operator_openshift_driver_toolkit_imagestream_broken
+    is 1. A healthy ImageStream sets it back to 0."""
+    node = gpu_node("a", os_id="rhcos", os_ver="4.16",
+                    extra_labels={C.NFD_OSTREE_LABEL: "416.94.202406172220-0"})
+    c = cluster([node])
+    c.create({"apiVersion": "config.openshift.io/v1", "kind": "ClusterVersion", "metadata": {"name": "version"},
+              "status": {"desired": {"version": "4.16.3"}}})
+    ist = {"apiVersion": "image.openshift.io/v1", "kind": "ImageStream",
+           "metadata": {"name": "driver-toolkit", "namespace": "openshift"},
+           "spec": {"tags": [{"from": {"kind": "DockerImage", "name": "quay.io/openshift/dtk@sha256:aaaa"}},
+                             {"name": "latest", "from": {"kind": "DockerImage", "name": "quay.io/openshift/dtk@sha256:bbbb"}},
+                             {"name": "416.94.202406172220-0",
+                              "from": {"kind": "DockerImage", "name": "quay.io/openshift/dtk@sha256:cccc"}}]}}
+    c.create(ist)
+    rec = reconcile_once(c)
+    m = rec.metrics
+    assert m.dtk_imagestream_broken._value.get() == 1
+    assert m.dtk_imagestream_missing._value.get() == 0 and m.dtk_rhcos_tags_missing._value.get() == 0
+    assert rec.sm.dtk_images == {"416.94.202406172220-0": "quay.io/openshift/dtk@sha256:cccc"}
+    assert m.dtk_enabled._value.get() == 1
+    ist = c.get("image.openshift.io/v1", "ImageStream", "driver-toolkit", "openshift")
+    ist["spec"]["tags"] = ist["spec"]["tags"][1:]
+    c.update(ist)
+    rec.reconcile(("", "cluster-policy"))
+    assert rec.metrics.dtk_imagestream_broken._value.get() == 0
+
+
+def test_openshift_dtk_alerts_ship_on_openshift_only():
+    """The four driver-toolkit alerts (reference 0400_prometheus_rule_openshift.yaml:45-103), each on a
+    gauge the operator sets."""
+    from gpu_operator_amd.controllers import resource_manager as RM
+    ocp = RM.load_state("state-operator-metrics", openshift=True)
+    plain = RM.load_state("state-operator-metrics", openshift=False)
+    rules = [o_ for o_ in ocp.objects if o_["kind"] == "PrometheusRule"]
+    names = {r["alert"]: r["expr"] for pr in rules for g in pr["spec"]["groups"] for r in g["rules"]}
+    dtk = {k: v for k, v in names.items() if "DriverToolkit" in k}
+    assert sorted(dtk) == ["AMDGPUOperatorDriverToolkitImageStreamBroken", "AMDGPUOperatorDriverToolkitImageStreamMissing",
+                           "AMDGPUOperatorDriverToolkitImageTagsMissing", "AMDGPUOperatorDriverToolkitNfdTooOld"]
+    from gpu_operator_amd.controllers.operator_metrics import OperatorMetrics
+    from prometheus_client import generate_latest
+    exported = generate_latest(OperatorMetrics().registry).decode()
+    for expr in dtk.values():
+        for metric in [w for w in expr.replace("\n", " ").split() if w.startswith("amd_gpu_operator_")]:
+            assert metric in exported, metric
+    assert not [x for x in plain.objects if "dtk" in (x.get("metadata") or {}).get("name", "")]

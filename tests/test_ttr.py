@@ -43,6 +43,11 @@ def test_our_protocol_brings_the_node_up_on_real_processes(node):
     assert "node:labelled" in m and "exporter:first-scrape" in m
     assert r["restarts"] == {} and r["processes"] >= 12
     assert r["time_to_ready_s"] < 15
+    # the harness's simulated waits are reported apart from the measurement:
+    # the validator pod's sandbox retry after the runtime handler existed is at most one sync tick
+    assert 0.0 <= r["time_to_ready_modelled_s"] <= ttr.KUBELET_SYNC_S + 0.2
+    assert r["time_to_ready_modelled_s"] == r["modelled_waits_s"].get("validator", {}).get("sandbox_retry_s", 0.0)
+    assert abs(r["time_to_ready_measured_s"] + r["time_to_ready_modelled_s"] - r["time_to_ready_s"]) < 1e-3
 
 
 def test_reference_protocol_executes_its_constants(node):

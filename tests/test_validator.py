@@ -281,6 +281,10 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
     sd.create(S.DRIVER_READY, {"ts": t + 0.5})
     sd.create(S.TOOLKIT_READY, {"ts": t + 3.0})
     sd.create(S.HIP_READY, {"ts": t + 9.0, "gemm_tflops_total": 10900.0, "gemm_tflops_per_gpu": 1362.5,
+                            "gpu_tflops": [{"dtype": "bf16", "m": 8192, "n": 8192, "k": 8192,
+                                            "tflops": {str(i): 1650.0 + i for i in range(8)}},
+                                           {"dtype": "fp8_e4m3fn", "m": 8192, "n": 8192, "k": 8192,
+                                            "tflops": {"0": 3300.0}}],
                             "tflops_by_dtype_gpus": {
                                 "bf16": {"1": {"total_tflops": 1400.0, "per_gpu_tflops": 1400.0, "efficiency": 1.0},
                                          "8": {"total_tflops": 10900.0, "per_gpu_tflops": 1362.5,
@@ -304,6 +308,13 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
     assert 'amd_gpu_operator_amd_pci_devices_total{node="n1"} 8.0' in text
     assert 'amd_gpu_operator_validator_allreduce_busbw_gbps{node="n1",ranks="8"} 310.0' in text
     assert 'amd_gpu_operator_validator_allreduce_busbw_gbps{node="n1",ranks="2"} 141.0' in text
+    # one series per GPU (SURVEY §5.5 {gpu,dtype,m,n,k}): a GPU failing the node-median gate is visible
+    per_gpu = [ln for ln in text.splitlines() if ln.startswith("amd_gpu_operator_validator_gemm_gpu_tflops{")
+               and 'dtype="bf16"' in ln]
+    assert len(per_gpu) == 8
+    assert ('amd_gpu_operator_validator_gemm_gpu_tflops{dtype="bf16",gpu="3",k="8192",m="8192",n="8192",node="n1"} '
+            '1653.0') in text
+    assert 'amd_gpu_operator_validator_gemm_gpu_tflops{dtype="fp8",gpu="0",k="8192",m="8192",n="8192",node="n1"} 3300.0' in text
 
 
 def test_cli_driver_component(tmp_path, node_root, capsys):
@@ -453,7 +464,8 @@ def test_rccl_workload_cli_reads_env(monkeypatch):
     monkeypatch.setenv("RCCL_MIN_BUSBW_GBPS", "123.5")
     monkeypatch.setenv("RCCL_RANKS", "2,8")
     assert WM.main(["rccl"]) == 0
-    assert seen == {"max_bytes": 8 << 30, "dtype": "float", "ranks": "2,8", "min_busbw": 123.5, "processes": 0}
+    # bf16 in the pod, as in local mode
+    assert seen == {"max_bytes": 8 << 30, "dtype": "bf16", "ranks": "2,8", "min_busbw": 123.5, "processes": 0}
 
 
 # -- throughput floors, node shapes, busy nodes ------------------------------
