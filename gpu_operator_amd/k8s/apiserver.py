@@ -63,6 +63,8 @@ class FakeAPIServer:
         self.url = f"http://127.0.0.1:{self.port}"
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
         self.requests: List[Tuple[str, str]] = []
+        self.connections = 0                       # TCP connections accepted (a client's churn shows here)
+        self.authorization: List[str] = []        # the Authorization header of every request
 
     def start(self) -> "FakeAPIServer":
         self.thread.start()
@@ -163,6 +165,10 @@ class FakeAPIServer:
             def log_message(self, *a):
                 pass
 
+            def setup(self):
+                srv.connections += 1
+                super().setup()
+
             def _send(self, code: int, body) -> None:
                 data = json.dumps(body).encode()
                 self.send_response(code)
@@ -183,6 +189,7 @@ class FakeAPIServer:
                 u = urlparse(self.path)
                 q = {k: v[-1] for k, v in parse_qs(u.query).items()}
                 srv.requests.append((verb, u.path))
+                srv.authorization.append(self.headers.get("Authorization", ""))
                 try:
                     if u.path == "/version":
                         return self._send(200, {"gitVersion": srv.version, "major": "1",

@@ -130,6 +130,10 @@ class Response:
             self._conn = None
 
 
+_IDEMPOTENT = frozenset({"GET", "HEAD", "PUT", "DELETE", "OPTIONS"})
+_KEEPALIVE_TRUST_S = 5.0    # a kept-alive connection idle longer than this is not reused for POST/PATCH
+
+
 class _Transport:
     """HTTP(S) to one API server: a keep-alive connection per thread, TLS from the config (CA,
     client certificate, or no verification when the kubeconfig says insecure-skip-tls-verify)."""
@@ -167,8 +171,15 @@ class _Transport:
                 conn.close()
                 return Response(r.status, data)
             return Response(r.status, stream=r, conn=conn)
+        idempotent = method in _IDEMPOTENT
         for attempt in (0, 1):
             conn = getattr(self._local, "conn", None)
+            if conn is not None and not idempotent and \
+                    time.monotonic() - getattr(self._local, "last", 0.0) > _KEEPALIVE_TRUST_S:
+                # a POST/PATCH is never sent twice: rather than risk it on a connection the server may
+                # have closed while idle, open a fresh one
+                conn.close()
+                conn = self._local.conn = None
             fresh = conn is None
             if fresh:
                 conn = self._local.conn = self._new(timeout)
@@ -179,15 +190,20 @@ class _Transport:
                 conn.request(method, path, body=body, headers=headers)
                 r = conn.getresponse()
                 data = r.read()
+                self._local.last = time.monotonic()
                 if r.will_close:
                     conn.close()
                     self._local.conn = None
                 return Response(r.status, data)
-            except (http.client.HTTPException, ConnectionError, BrokenPipeError, socket.timeout, OSError):
+            except (http.client.HTTPException, OSError) as e:
                 conn.close()
                 self._local.conn = None
-                # a kept-alive connection the server closed: retry once on a new one
-                if fresh or attempt == 1:
+                # retry once, on a new connection, only what a server that closed an idle kept-alive
+                # connection produces (no response byte ever came back) -- never a timeout (the request
+                # may have been applied), never a non-idempotent request
+                stale = isinstance(e, (http.client.RemoteDisconnected, ConnectionResetError, BrokenPipeError,
+                                       ConnectionAbortedError)) and not isinstance(e, socket.timeout)
+                if fresh or attempt == 1 or not stale or not idempotent:
                     raise
         raise RuntimeError("unreachable")
 

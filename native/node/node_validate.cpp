@@ -11,13 +11,15 @@
 // barrier in milliseconds (reference: validator/main.go:607-679 driver, :775-801 toolkit). The
 // components that talk to the API server (hip, plugin, the fabric pod) stay in `amd-validator`.
 //
-// plugin (WITH_WORKLOAD=false, the DaemonSet's setting): polls this Node (GET /api/v1/nodes/NODE_NAME
-// every 100 ms, bounded by 150 s like the validator's event-driven wait) until its capacity
-// advertises amd.com/gpu (or, PARTITION_STRATEGY=mixed, amd.com/partition-*), then writes
-// plugin-ready. The API server is reached in-cluster (service-account token and CA, TLS through
-// OpenSSL with host-name verification) or through a single-cluster KUBECONFIG with a token or no
-// credentials. Anything else -- a workload pod to spawn, client certificates, the reference's poll
-// mode, an unreachable API -- exits 3 and `amd-validator` does it.
+// plugin (WITH_WORKLOAD=false, the DaemonSet's setting): GETs this Node, then watches it (one watch,
+// fieldSelector=metadata.name, on the same kept-alive connection), bounded by 150 s like the
+// validator's event-driven wait, until its capacity advertises amd.com/gpu (or,
+// PARTITION_STRATEGY=mixed, amd.com/partition-*), then writes plugin-ready -- one connection and one
+// TLS handshake per node, not a request every 100 ms. The API server is reached in-cluster
+// (service-account token and CA, TLS through OpenSSL with host-name verification) or through the
+// current context of a KUBECONFIG whose user has a token or no credentials. Anything else -- a
+// workload pod to spawn, client certificates, the reference's poll mode, an unreachable API -- exits 3
+// and `amd-validator` does it.
 //
 // rccl: a node with fewer than 2 physical GPUs (KFD agents grouped by PCI function) has no fabric;
 // rccl-ready is written with a skip. With 2 or more (or none enumerated, where the validator reads
@@ -51,6 +53,8 @@
 #include <cstring>
 #include <dirent.h>
 #include <fstream>
+#include <map>
+#include <memory>
 #include <set>
 #include <sstream>
 #include <string>
@@ -351,7 +355,54 @@ std::string b64decode(const std::string& in) {
   return out;
 }
 
-// In-cluster (service account) or a one-cluster, token-or-anonymous KUBECONFIG; else NotHandled.
+// A KUBECONFIG, block-style YAML only: its `clusters`, `contexts` and `users` lists as name -> fields
+// (a list item's nested keys flattened: cluster.server -> server, user.token -> token) and
+// `current-context`. Flow style or anything else this reader cannot follow is NotHandled.
+struct KubeConfig {
+  std::vector<std::map<std::string, std::string>> clusters, contexts, users;
+  std::string current;
+};
+
+KubeConfig parse_kubeconfig(const std::string& text) {
+  KubeConfig kc;
+  std::istringstream in(text);
+  std::string line;
+  std::vector<std::map<std::string, std::string>>* section = nullptr;
+  while (std::getline(in, line)) {
+    const auto hash = line.find(" #");
+    if (hash != std::string::npos) line = line.substr(0, hash);
+    if (!line.empty() && line[0] == '#') continue;
+    const size_t indent = line.find_first_not_of(' ');
+    if (indent == std::string::npos) continue;
+    std::string t = line.substr(indent);
+    while (!t.empty() && (t.back() == '\r' || t.back() == ' ')) t.pop_back();
+    if (t.empty()) continue;
+    if (t.find('{') != std::string::npos || t.find('[') == 0) throw NotHandled("kubeconfig in YAML flow style");
+    const auto colon = t.find(':');
+    if (indent == 0 && t.rfind("- ", 0) != 0 && t != "-") {    // a top-level key (list items may sit at 0)
+      const std::string key = t.substr(0, colon);
+      section = key == "clusters" ? &kc.clusters : key == "contexts" ? &kc.contexts : key == "users" ? &kc.users : nullptr;
+      if (key == "current-context" && colon != std::string::npos) kc.current = trim(t.substr(colon + 1));
+      continue;
+    }
+    if (!section) continue;
+    if (t.rfind("- ", 0) == 0 || t == "-") {
+      section->emplace_back();
+      t = t.size() > 2 ? trim(t.substr(2)) : "";
+      if (t.empty()) continue;
+    }
+    if (section->empty()) throw NotHandled("kubeconfig list without items");
+    const auto c = t.find(':');
+    if (c == std::string::npos) continue;
+    const std::string key = t.substr(0, c), value = trim(t.substr(c + 1));
+    if (!value.empty()) section->back()[key] = value;
+    else if (key != "cluster" && key != "user" && key != "context") section->back()[key] = "";
+  }
+  return kc;
+}
+
+// In-cluster (service account), or the current context of a KUBECONFIG whose user authenticates
+// with a token or not at all; else NotHandled.
 Api api_config() {
   Api a;
   const std::string sa = mount_path("/var/run/secrets/kubernetes.io/serviceaccount");
@@ -364,186 +415,343 @@ Api api_config() {
     a.ca_file = sa + "/ca.crt";
     return a;
   }
-  const std::string kc = env("KUBECONFIG");
-  if (kc.empty() || !exists(kc)) throw NotHandled("no in-cluster service account and no KUBECONFIG");
-  std::istringstream in(slurp(kc));
-  std::string line, server;
-  int clusters = 0, users = 0;
-  while (std::getline(in, line)) {
-    const std::string t = trim(line.substr(0, line.find('#') == std::string::npos ? line.size() : line.find('#')));
-    auto value = [&](const char* key) -> const char* {
-      const std::string k = std::string(key) + ":";
-      const auto p = t.find(k);
-      return (p == 0 || (p == 2 && t.rfind("- ", 0) == 0)) ? t.c_str() + p + k.size() : nullptr;
-    };
-    if (const char* v = value("server")) { server = trim(v); ++clusters; }
-    else if (const char* v = value("token")) a.token = trim(v);
-    else if (const char* v = value("certificate-authority")) a.ca_file = trim(v);
-    else if (const char* v = value("certificate-authority-data")) a.ca_pem = b64decode(trim(v));
-    else if (const char* v = value("insecure-skip-tls-verify")) a.verify = trim(v) != "true";
-    else if (value("client-certificate") || value("client-certificate-data") || value("client-key") ||
-             value("client-key-data") || value("exec") || value("auth-provider"))
-      throw NotHandled("kubeconfig client credentials");
-    else if (value("user")) ++users;
+  const std::string path = env("KUBECONFIG");
+  if (path.empty() || !exists(path)) throw NotHandled("no in-cluster service account and no KUBECONFIG");
+  const KubeConfig kc = parse_kubeconfig(slurp(path));
+  auto by_name = [](const std::vector<std::map<std::string, std::string>>& v, const std::string& name,
+                    const char* what) -> const std::map<std::string, std::string>* {
+    const std::map<std::string, std::string>* hit = nullptr;
+    for (const auto& m : v) {
+      const auto n = m.find("name");
+      if (n != m.end() && n->second == name) {
+        if (hit) throw NotHandled(std::string("kubeconfig: two ") + what + " named " + name);
+        hit = &m;
+      }
+    }
+    return hit;
+  };
+  // the context: current-context, or the only one; none at all: the only cluster and user
+  const std::map<std::string, std::string>* ctx = nullptr;
+  if (!kc.current.empty()) {
+    ctx = by_name(kc.contexts, kc.current, "contexts");
+    if (!ctx) throw NotHandled("kubeconfig: current-context " + kc.current + " not found");
+  } else if (kc.contexts.size() == 1) {
+    ctx = &kc.contexts[0];
+  } else if (!kc.contexts.empty()) {
+    throw NotHandled("kubeconfig: several contexts and no current-context");
   }
-  if (clusters != 1) throw NotHandled("kubeconfig with " + std::to_string(clusters) + " clusters");
-  parse_url(server, a);
+  const std::map<std::string, std::string>* cluster = nullptr;
+  const std::map<std::string, std::string>* user = nullptr;
+  if (ctx) {
+    const auto cn = ctx->find("cluster");
+    if (cn == ctx->end()) throw NotHandled("kubeconfig: context without a cluster");
+    cluster = by_name(kc.clusters, cn->second, "clusters");
+    const auto un = ctx->find("user");
+    if (un != ctx->end()) {
+      user = by_name(kc.users, un->second, "users");
+      if (!user) throw NotHandled("kubeconfig: user " + un->second + " not found");
+    }
+  } else {
+    if (kc.clusters.size() != 1 || kc.users.size() > 1) throw NotHandled("kubeconfig without a context to select by");
+    cluster = &kc.clusters[0];
+    user = kc.users.empty() ? nullptr : &kc.users[0];
+  }
+  if (!cluster || !cluster->count("server")) throw NotHandled("kubeconfig: the context's cluster has no server");
+  auto get = [](const std::map<std::string, std::string>* m, const char* k) {
+    if (!m) return std::string();
+    const auto it = m->find(k);
+    return it == m->end() ? std::string() : it->second;
+  };
+  if (user)
+    for (const char* k : {"client-certificate", "client-certificate-data", "client-key", "client-key-data", "exec",
+                          "auth-provider", "tokenFile", "username", "password"})
+      if (user->count(k)) throw NotHandled(std::string("kubeconfig user credentials: ") + k);
+  a.token = get(user, "token");
+  a.ca_file = get(cluster, "certificate-authority");
+  const std::string ca_data = get(cluster, "certificate-authority-data");
+  if (!ca_data.empty()) a.ca_pem = b64decode(ca_data);
+  a.verify = get(cluster, "insecure-skip-tls-verify") != "true";
+  parse_url(get(cluster, "server"), a);
   return a;
 }
 
-// One HTTP/1.1 GET (Connection: close); returns the status, fills body. Transport problems are
-// NotHandled: the Python validator then retries and reports them properly.
-int http_get(const Api& a, const std::string& path, std::string& body, double timeout_s = 10.0) {
-  addrinfo hints{}, *res = nullptr;
-  hints.ai_socktype = SOCK_STREAM;
-  if (getaddrinfo(a.host.c_str(), std::to_string(a.port).c_str(), &hints, &res) != 0 || !res)
-    throw NotHandled("cannot resolve " + a.host);
-  int fd = -1;
-  for (addrinfo* r = res; r && fd < 0; r = r->ai_next) {
-    fd = ::socket(r->ai_family, r->ai_socktype, r->ai_protocol);
-    if (fd < 0) continue;
-    timeval tv{(time_t)timeout_s, 0};
-    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
-    ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
-    if (::connect(fd, r->ai_addr, r->ai_addrlen) != 0) {
-      ::close(fd);
-      fd = -1;
+// One connection to the API server (TLS through OpenSSL with host-name verification), buffered,
+// kept alive across requests. Transport problems are NotHandled: the Python validator then retries
+// and reports them properly.
+class Conn {
+ public:
+  Conn(const Api& a, double timeout_s) : a_(a) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(a.host.c_str(), std::to_string(a.port).c_str(), &hints, &res) != 0 || !res)
+      throw NotHandled("cannot resolve " + a.host);
+    for (addrinfo* r = res; r && fd_ < 0; r = r->ai_next) {
+      fd_ = ::socket(r->ai_family, r->ai_socktype, r->ai_protocol);
+      if (fd_ < 0) continue;
+      set_timeout(timeout_s);
+      if (::connect(fd_, r->ai_addr, r->ai_addrlen) != 0) {
+        ::close(fd_);
+        fd_ = -1;
+      }
     }
+    freeaddrinfo(res);
+    if (fd_ < 0) throw NotHandled("cannot connect to " + a.host + ":" + std::to_string(a.port));
+    if (a.tls) handshake();
   }
-  freeaddrinfo(res);
-  if (fd < 0) throw NotHandled("cannot connect to " + a.host + ":" + std::to_string(a.port));
-  SSL_CTX* ctx = nullptr;
-  SSL* ssl = nullptr;
-  auto cleanup = [&] {
-    if (ssl) SSL_free(ssl);
-    if (ctx) SSL_CTX_free(ctx);
-    ::close(fd);
-  };
-  if (a.tls) {
-    ctx = SSL_CTX_new(TLS_client_method());
-    if (a.verify) {
-      SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+  ~Conn() {
+    if (ssl_) SSL_free(ssl_);
+    if (ctx_) SSL_CTX_free(ctx_);
+    if (fd_ >= 0) ::close(fd_);
+  }
+  Conn(const Conn&) = delete;
+  Conn& operator=(const Conn&) = delete;
+
+  void set_timeout(double s) {
+    timeval tv{(time_t)s, (suseconds_t)((s - (double)(time_t)s) * 1e6)};
+    ::setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    ::setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+  }
+
+  // Sends a GET; returns the status and reads the response head (chunked / length / close).
+  int get(const std::string& path) {
+    const std::string req = "GET " + a_.prefix + path + " HTTP/1.1\r\nHost: " + a_.host +
+                            "\r\nAccept: application/json\r\n" +
+                            (a_.token.empty() ? "" : "Authorization: Bearer " + a_.token + "\r\n") +
+                            "User-Agent: amd-node-validate\r\nConnection: keep-alive\r\n\r\n";
+    for (size_t off = 0; off < req.size();) {
+      const int n = ssl_ ? SSL_write(ssl_, req.data() + off, (int)(req.size() - off))
+                         : (int)::send(fd_, req.data() + off, req.size() - off, MSG_NOSIGNAL);
+      if (n <= 0) throw NotHandled("write to the API server failed");
+      off += (size_t)n;
+    }
+    std::string status_line;
+    if (!line(status_line) || status_line.rfind("HTTP/1.", 0) != 0) throw NotHandled("malformed API response");
+    const int status = std::atoi(status_line.c_str() + status_line.find(' ') + 1);
+    chunked_ = false, close_ = false, length_ = -1;
+    for (std::string h; line(h) && !h.empty();) {
+      std::transform(h.begin(), h.end(), h.begin(), ::tolower);
+      if (h.rfind("transfer-encoding:", 0) == 0 && h.find("chunked") != std::string::npos) chunked_ = true;
+      else if (h.rfind("content-length:", 0) == 0) length_ = std::atol(h.c_str() + 15);
+      else if (h.rfind("connection:", 0) == 0 && h.find("close") != std::string::npos) close_ = true;
+    }
+    return status;
+  }
+
+  // The whole body of the last response (length-delimited, chunked, or up to the close).
+  std::string body() {
+    std::string out;
+    if (chunked_) {
+      for (std::string piece; chunk(piece);) out += piece;
+    } else if (length_ >= 0) {
+      if (!exact((size_t)length_, out)) throw NotHandled("short API response");
+    } else {
+      while (fill()) {
+      }
+      out.swap(buf_);
+      close_ = true;
+    }
+    return out;
+  }
+
+  // The next chunk of a chunked body; false at its end (or when the stream breaks).
+  bool chunk(std::string& out) {
+    std::string size_line;
+    if (!line(size_line)) return false;
+    const size_t n = std::strtoul(size_line.c_str(), nullptr, 16);
+    if (n == 0) {
+      std::string trailer;
+      while (line(trailer) && !trailer.empty()) {
+      }
+      return false;
+    }
+    out.clear();
+    std::string crlf;
+    return exact(n, out) && line(crlf);
+  }
+
+  bool reusable() const { return !close_; }
+
+ private:
+  void handshake() {
+    ctx_ = SSL_CTX_new(TLS_client_method());
+    if (a_.verify) {
+      SSL_CTX_set_verify(ctx_, SSL_VERIFY_PEER, nullptr);
       bool loaded = false;
-      if (!a.ca_pem.empty()) {
-        BIO* bio = BIO_new_mem_buf(a.ca_pem.data(), (int)a.ca_pem.size());
+      if (!a_.ca_pem.empty()) {
+        BIO* bio = BIO_new_mem_buf(a_.ca_pem.data(), (int)a_.ca_pem.size());
         while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
-          loaded = X509_STORE_add_cert(SSL_CTX_get_cert_store(ctx), x) == 1 || loaded;
+          loaded = X509_STORE_add_cert(SSL_CTX_get_cert_store(ctx_), x) == 1 || loaded;
           X509_free(x);
         }
         BIO_free(bio);
-      } else if (!a.ca_file.empty()) {
-        loaded = SSL_CTX_load_verify_locations(ctx, a.ca_file.c_str(), nullptr) == 1;
+      } else if (!a_.ca_file.empty()) {
+        loaded = SSL_CTX_load_verify_locations(ctx_, a_.ca_file.c_str(), nullptr) == 1;
       } else {
-        loaded = SSL_CTX_set_default_verify_paths(ctx) == 1;
+        loaded = SSL_CTX_set_default_verify_paths(ctx_) == 1;
       }
-      if (!loaded) {
-        cleanup();
-        throw NotHandled("cannot load the API server CA");
-      }
+      if (!loaded) throw NotHandled("cannot load the API server CA");
     }
-    ssl = SSL_new(ctx);
-    SSL_set_fd(ssl, fd);
-    SSL_set_tlsext_host_name(ssl, a.host.c_str());
-    if (a.verify) {
+    ssl_ = SSL_new(ctx_);
+    SSL_set_fd(ssl_, fd_);
+    SSL_set_tlsext_host_name(ssl_, a_.host.c_str());
+    if (a_.verify) {
       // in-cluster the API server is an IP (KUBERNETES_SERVICE_HOST): match it against the
       // certificate's IP SANs, a name against its DNS SANs
       in6_addr ip6;
       in_addr ip4;
-      if (inet_pton(AF_INET, a.host.c_str(), &ip4) == 1 || inet_pton(AF_INET6, a.host.c_str(), &ip6) == 1)
-        X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl), a.host.c_str());
+      if (inet_pton(AF_INET, a_.host.c_str(), &ip4) == 1 || inet_pton(AF_INET6, a_.host.c_str(), &ip6) == 1)
+        X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl_), a_.host.c_str());
       else
-        SSL_set1_host(ssl, a.host.c_str());
+        SSL_set1_host(ssl_, a_.host.c_str());
     }
-    if (SSL_connect(ssl) != 1) {
-      cleanup();
-      throw NotHandled("TLS handshake with the API server failed");
-    }
+    if (SSL_connect(ssl_) != 1) throw NotHandled("TLS handshake with the API server failed");
   }
-  std::string req = "GET " + a.prefix + path + " HTTP/1.1\r\nHost: " + a.host + "\r\nAccept: application/json\r\n" +
-                    (a.token.empty() ? "" : "Authorization: Bearer " + a.token + "\r\n") +
-                    "User-Agent: amd-node-validate\r\nConnection: close\r\n\r\n";
-  auto wr = [&](const char* p, size_t n) { return ssl ? SSL_write(ssl, p, (int)n) : (int)::send(fd, p, n, 0); };
-  auto rd = [&](char* p, size_t n) { return ssl ? SSL_read(ssl, p, (int)n) : (int)::recv(fd, p, n, 0); };
-  for (size_t off = 0; off < req.size();) {
-    const int n = wr(req.data() + off, req.size() - off);
-    if (n <= 0) {
-      cleanup();
-      throw NotHandled("write to the API server failed");
-    }
-    off += (size_t)n;
+  bool fill() {
+    char tmp[16384];
+    const int n = ssl_ ? SSL_read(ssl_, tmp, sizeof tmp) : (int)::recv(fd_, tmp, sizeof tmp, 0);
+    if (n <= 0) return false;
+    buf_.append(tmp, (size_t)n);
+    return true;
   }
-  std::string raw;
-  char buf[16384];
-  for (;;) {
-    const int n = rd(buf, sizeof buf);
-    if (n <= 0) break;
-    raw.append(buf, (size_t)n);
-  }
-  cleanup();
-  const auto hdr_end = raw.find("\r\n\r\n");
-  if (raw.rfind("HTTP/1.", 0) != 0 || hdr_end == std::string::npos) throw NotHandled("malformed API response");
-  const int status = std::atoi(raw.c_str() + raw.find(' ') + 1);
-  std::string headers = raw.substr(0, hdr_end);
-  std::transform(headers.begin(), headers.end(), headers.begin(), ::tolower);
-  body = raw.substr(hdr_end + 4);
-  if (headers.find("transfer-encoding: chunked") != std::string::npos) {
-    std::string out;
-    size_t p = 0;
+  bool line(std::string& out) {
     for (;;) {
-      const auto eol = body.find("\r\n", p);
-      if (eol == std::string::npos) break;
-      const size_t n = std::strtoul(body.substr(p, eol - p).c_str(), nullptr, 16);
-      if (n == 0) break;
-      out.append(body, eol + 2, n);
-      p = eol + 2 + n + 2;
+      const auto eol = buf_.find("\r\n");
+      if (eol != std::string::npos) {
+        out = buf_.substr(0, eol);
+        buf_.erase(0, eol + 2);
+        return true;
+      }
+      if (!fill()) return false;
     }
-    body.swap(out);
   }
-  return status;
-}
+  bool exact(size_t n, std::string& out) {
+    while (buf_.size() < n)
+      if (!fill()) return false;
+    out.append(buf_, 0, n);
+    buf_.erase(0, n);
+    return true;
+  }
+
+  const Api a_;
+  int fd_ = -1;
+  SSL_CTX* ctx_ = nullptr;
+  SSL* ssl_ = nullptr;
+  std::string buf_;
+  bool chunked_ = false, close_ = false;
+  long length_ = -1;
+};
 
 // --- plugin (components.validate_plugin, WITH_WORKLOAD=false) -------------------------------
+// GPU resources in a Node object's capacity (amd.com/gpu; amd.com/partition-* under mixed).
+long long gpu_capacity(const Value& n, bool mixed, Value& res) {
+  long long devices = 0;
+  const Value* st = n.find("status");
+  const Value* cap = st ? st->find("capacity") : nullptr;
+  if (cap && cap->is_object()) {
+    for (const auto& [k, v] : cap->o) {
+      if (k != "amd.com/gpu" && !(mixed && k.rfind("amd.com/partition-", 0) == 0)) continue;
+      const long long c = v.is_string() ? std::atoll(v.s.c_str()) : v.integer();
+      if (c > 0) {
+        res[k] = Value::number(c);
+        devices += c;
+      }
+    }
+  }
+  return devices;
+}
+
+// One GET of the Node, then one watch of it (fieldSelector=metadata.name) on the same kept-alive
+// connection, from the resourceVersion of that GET: the device plugin's registration arrives as a
+// watch event, with no polling and no connection per check. A watch the server ends (its
+// timeoutSeconds, an ERROR event such as 410 Gone) is re-established from a fresh GET, at most once per
+// second; a server without watches is polled every 5 s, the reference's period
+// (validator/main.go:1102-1122), over the same connection.
 Value validate_plugin(const Opts& o) {
   if (truthy(env("WITH_WORKLOAD", "true"))) throw NotHandled("plugin validation with a workload pod");
   if (env("VALIDATOR_WAIT_MODE") == "poll") throw NotHandled("the reference's poll mode");
   const std::string node = env("NODE_NAME");
   if (node.empty()) throw NotHandled("NODE_NAME unset");
+  for (char c : node)
+    if (!std::isalnum((unsigned char)c) && c != '-' && c != '.') throw NotHandled("node name " + node);
   const bool mixed = env("PARTITION_STRATEGY", env("MIG_STRATEGY", "single")) == "mixed";
+  const double budget = std::atof(env("RESOURCE_TIMEOUT_SECONDS", "150").c_str());
   const Api api = api_config();
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(150);
+  using clock = std::chrono::steady_clock;
+  const auto deadline = clock::now() + std::chrono::milliseconds((long long)(budget * 1e3));
+  auto left_s = [&] { return std::chrono::duration<double>(deadline - clock::now()).count(); };
+  auto found = [&](const Value& res, long long devices) {
+    Value info = Value::object();
+    info["resources"] = res;
+    info["devices"] = Value::number(devices);
+    write_barrier(o, "plugin-ready", info);
+    return info;
+  };
+  std::unique_ptr<Conn> conn;
+  bool watches = true;
+  auto last_list = clock::now() - std::chrono::seconds(10);
   for (;;) {
-    std::string body;
-    const int status = http_get(api, "/api/v1/nodes/" + node, body);
+    if (left_s() <= 0) throw ValidationError("no amd.com/gpu resources on node " + node + " after " +
+                                             std::to_string((int)budget) + "s");
+    if (!conn || !conn->reusable()) conn.reset(new Conn(api, 10.0));
+    // the Node now (and the resourceVersion to watch from)
+    const auto gap = std::chrono::duration<double>(clock::now() - last_list).count();
+    const double pause = watches ? 1.0 - gap : 5.0 - gap;
+    if (pause > 0) std::this_thread::sleep_for(std::chrono::milliseconds((long long)(std::min(pause, left_s()) * 1e3)));
+    last_list = clock::now();
+    conn->set_timeout(10.0);
+    const int status = conn->get("/api/v1/nodes/" + node);
+    const std::string body = conn->body();
     if (status != 200) throw NotHandled("GET node " + node + ": HTTP " + std::to_string(status));
-    Value res = Value::object();
-    long long devices = 0;
+    std::string rv;
     try {
       const Value n = minijson::parse(body);
-      const Value* st = n.find("status");
-      const Value* cap = st ? st->find("capacity") : nullptr;
-      if (cap && cap->is_object()) {
-        for (const auto& [k, v] : cap->o) {
-          if (k != "amd.com/gpu" && !(mixed && k.rfind("amd.com/partition-", 0) == 0)) continue;
-          const long long c = v.is_string() ? std::atoll(v.s.c_str()) : v.integer();
-          if (c > 0) {
-            res[k] = Value::number(c);
-            devices += c;
-          }
-        }
-      }
+      Value res = Value::object();
+      if (const long long d = gpu_capacity(n, mixed, res)) return found(res, d);
+      const Value* md = n.find("metadata");
+      const Value* r = md ? md->find("resourceVersion") : nullptr;
+      rv = r ? r->s : "";         // string or number text
+    } catch (const NotHandled&) {
+      throw;
     } catch (const std::exception& e) {
       throw NotHandled(std::string("node JSON: ") + e.what());
     }
-    if (devices > 0) {
-      Value info = Value::object();
-      info["resources"] = res;
-      info["devices"] = Value::number(devices);
-      write_barrier(o, "plugin-ready", info);
-      return info;
+    if (!watches) continue;
+    if (!conn->reusable()) conn.reset(new Conn(api, 10.0));
+    const int wait_s = std::max(1, (int)std::min(left_s(), 300.0));
+    conn->set_timeout(wait_s + 10.0);
+    const int ws = conn->get("/api/v1/nodes?fieldSelector=metadata.name%3D" + node + "&watch=1&timeoutSeconds=" +
+                             std::to_string(wait_s) + (rv.empty() ? "" : "&resourceVersion=" + rv));
+    if (ws != 200) {
+      (void)conn->body();
+      watches = false;      // no watches here: poll at the reference's period
+      continue;
     }
-    if (std::chrono::steady_clock::now() >= deadline)
-      throw ValidationError("no amd.com/gpu resources on node " + node + " after 150s");
-    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    // watch events: one JSON object per line, lines split across chunks in any way
+    std::string pending, piece;
+    bool restart = false;
+    while (!restart && conn->chunk(piece)) {
+      pending += piece;
+      for (size_t eol; (eol = pending.find('\n')) != std::string::npos;) {
+        const std::string ev = pending.substr(0, eol);
+        pending.erase(0, eol + 1);
+        if (ev.find_first_not_of(" \r\t") == std::string::npos) continue;
+        try {
+          const Value e = minijson::parse(ev);
+          const Value* type = e.find("type");
+          const Value* obj = e.find("object");
+          if (!type || !obj || type->str() == "ERROR") {
+            restart = true;        // e.g. 410 Gone: list again
+            break;
+          }
+          Value res = Value::object();
+          if (type->str() != "DELETED")
+            if (const long long d = gpu_capacity(*obj, mixed, res)) return found(res, d);
+        } catch (const std::exception& e) {
+          throw NotHandled(std::string("watch event JSON: ") + e.what());
+        }
+      }
+    }
+    conn.reset();   // the watch ended (server timeout, ERROR, broken stream): a new connection for the list
   }
 }
 

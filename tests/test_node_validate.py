@@ -191,3 +191,48 @@ def test_plugin_hands_over_what_it_does_not_handle(tmp_path, node):
         assert not any(os.listdir(tmp_path / d) for d in "abcd" if os.path.isdir(tmp_path / d))
     finally:
         srv.stop()
+
+
+def test_plugin_watches_instead_of_polling(tmp_path, node):
+    """capacity that appears 10 s after the check starts costs one GET and one
+    watch on a kept-alive connection -- not a TLS connection every 100 ms (10 QPS per node)."""
+    srv, backing, kc = _api(tmp_path, {})
+    try:
+        import threading
+
+        def advertise():
+            time.sleep(10.0)
+            backing.patch("v1", "Node", "n1", {"status": {"capacity": {"amd.com/gpu": "8"}}})
+        threading.Thread(target=advertise, daemon=True).start()
+        t = time.monotonic()
+        rc, out, err = native("plugin", node, tmp_path / "n", {"KUBECONFIG": kc, "NODE_NAME": "n1",
+                                                               "WITH_WORKLOAD": "false"})
+        took = time.monotonic() - t
+        assert rc == 0, err
+        assert 9.5 < took < 13, took                         # the watch event, not a poll tick
+        assert srv.connections <= 5, srv.connections
+        assert len(srv.requests) <= 5, srv.requests
+        assert barriers(tmp_path / "n")["plugin-ready"]["devices"] == 8
+    finally:
+        srv.stop()
+
+
+def test_kubeconfig_current_context_selects_the_user(tmp_path, node):
+    """with two users the native check authenticates as the current context's user (the
+    Python client's choice), not as whichever token line came last; an unknown context is handed over."""
+    srv, backing, kc = _api(tmp_path, {"amd.com/gpu": "8"})
+    try:
+        text = open(kc).read().replace("current-context: t", "current-context: second")
+        text = text.replace("contexts:\n", "contexts:\n- context:\n    cluster: t\n    user: u2\n  name: second\n")
+        text += "- name: u2\n  user:\n    token: second-token\n- name: u3\n  user:\n    token: last-token\n"
+        (tmp_path / "kc2").write_text(text)
+        env = {"KUBECONFIG": str(tmp_path / "kc2"), "NODE_NAME": "n1", "WITH_WORKLOAD": "false"}
+        rc, out, err = native("plugin", node, tmp_path / "n", env)
+        assert rc == 0, err
+        assert set(srv.authorization) == {"Bearer second-token"}, srv.authorization
+        from gpu_operator_amd.k8s.rest import Config
+        assert Config.from_kubeconfig(str(tmp_path / "kc2")).bearer() == "second-token"    # the same choice
+        (tmp_path / "kc3").write_text(text.replace("current-context: second", "current-context: nope"))
+        assert native("plugin", node, tmp_path / "m", dict(env, KUBECONFIG=str(tmp_path / "kc3")))[0] == 3
+    finally:
+        srv.stop()

@@ -182,3 +182,98 @@ def test_watch_with_field_selector_sees_only_its_node(api):
     finally:
         stop()
     assert seen == [("ADDED", "b"), ("MODIFIED", "b")]
+
+
+class _ScriptedServer:
+    """A raw HTTP/1.1 server whose every request follows a script: "ok" (200, kept alive), "drop"
+    (the connection closes with no response byte, as a server closing an idle kept-alive
+    connection does) or "hang" (no response until the client gives up)."""
+
+    def __init__(self, script):
+        import socket as so
+        self.script, self.seen = list(script), []
+        self.sock = so.socket()
+        self.sock.bind(("127.0.0.1", 0))
+        self.sock.listen(8)
+        self.url = f"http://127.0.0.1:{self.sock.getsockname()[1]}"
+        threading.Thread(target=self._serve, daemon=True).start()
+
+    def _serve(self):
+        while True:
+            try:
+                c, _ = self.sock.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._conn, args=(c,), daemon=True).start()
+
+    def _conn(self, c):
+        buf = b""
+        while True:
+            while b"\r\n\r\n" not in buf:
+                d = c.recv(65536)
+                if not d:
+                    c.close()
+                    return
+                buf += d
+            head, buf = buf.split(b"\r\n\r\n", 1)
+            n = 0
+            for ln in head.split(b"\r\n")[1:]:
+                if ln.lower().startswith(b"content-length:"):
+                    n = int(ln.split(b":")[1])
+            while len(buf) < n:
+                buf += c.recv(65536)
+            buf = buf[n:]
+            self.seen.append(head.split(b" ")[0].decode())
+            what = self.script.pop(0) if self.script else "ok"
+            if what == "drop":
+                c.close()
+                return
+            if what == "hang":
+                time.sleep(3)
+                c.close()
+                return
+            body = b'{"kind":"Status","apiVersion":"v1","metadata":{"name":"x"}}'
+            c.sendall(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: " +
+                      str(len(body)).encode() + b"\r\n\r\n" + body)
+
+    def stop(self):
+        self.sock.close()
+
+
+def test_transport_retries_only_idempotent_requests_on_a_dropped_keepalive(monkeypatch):
+    """a dropped kept-alive connection is retried once for GET/PUT/DELETE; a POST is never
+    sent twice (it goes out on a fresh connection when the kept one may have gone stale); a timeout is
+    never retried (the request may have been applied)."""
+    from gpu_operator_amd.k8s import rest
+    srv = _ScriptedServer(["ok", "drop", "ok"])
+    t = rest._Transport(Config(srv.url, verify=False))
+    assert t.request("GET", "/api/v1/nodes/a", None, {}, 5).status_code == 200
+    assert t.request("GET", "/api/v1/nodes/a", None, {}, 5).status_code == 200     # dropped, retried once
+    assert srv.seen == ["GET", "GET", "GET"]
+    srv.stop()
+    # POST on a connection idle past the trust window: a fresh connection, one send
+    monkeypatch.setattr(rest, "_KEEPALIVE_TRUST_S", 0.0)
+    srv = _ScriptedServer(["ok", "ok"])
+    t = rest._Transport(Config(srv.url, verify=False))
+    t.request("GET", "/x", None, {}, 5)
+    assert t.request("POST", "/x", b"{}", {"Content-Type": "application/json"}, 5).status_code == 200
+    assert srv.seen == ["GET", "POST"]
+    srv.stop()
+    # a dropped POST is an error, not a second POST
+    monkeypatch.setattr(rest, "_KEEPALIVE_TRUST_S", 60.0)
+    srv = _ScriptedServer(["ok", "drop", "ok"])
+    t = rest._Transport(Config(srv.url, verify=False))
+    t.request("GET", "/x", None, {}, 5)
+    with pytest.raises(OSError):
+        t.request("POST", "/x", b"{}", {"Content-Type": "application/json"}, 5)
+    assert srv.seen == ["GET", "POST"]
+    srv.stop()
+    # a timed-out GET is not re-sent
+    srv = _ScriptedServer(["ok", "hang", "ok"])
+    t = rest._Transport(Config(srv.url, verify=False))
+    t.request("GET", "/x", None, {}, 5)
+    with pytest.raises(OSError):
+        t.request("GET", "/x", None, {}, 0.5)
+    time.sleep(0.2)
+    assert srv.seen == ["GET", "GET"]
+    srv.stop()
