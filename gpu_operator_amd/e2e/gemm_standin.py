@@ -13,6 +13,9 @@ Script (environment):
   GEMM_STANDIN_STATE    file counting the runs (also ``<state>.running`` exists while one runs)
   GEMM_STANDIN_RUNTIME_S  how long a run takes (default 1)
   GEMM_STANDIN_GPUS     GPUs without HIP_VISIBLE_DEVICES (default 8)
+  GEMM_STANDIN_SLOW_FILE  a file of node GPU indices ("3" or "3,5") read when the run reports: those
+                        GPUs are slow too (a tenant given the GPU mid-sweep shares it); the run waits
+                        up to 60 s for the file to exist
 """
 
 from __future__ import annotations
@@ -53,6 +56,14 @@ def main(argv=None) -> int:
     if "--smoke" in argv:
         print(json.dumps({"event": "hip-smoke", "devices": len(nodes), "elements": 50000, "ok": True}), flush=True)
     time.sleep(float(os.environ.get("GEMM_STANDIN_RUNTIME_S", "1")))
+    slow_file = os.environ.get("GEMM_STANDIN_SLOW_FILE", "")
+    if slow_file:
+        end = time.monotonic() + 60
+        while not os.path.exists(slow_file) and time.monotonic() < end:
+            time.sleep(0.05)
+        if os.path.exists(slow_file):
+            with open(slow_file) as f:
+                slow |= {int(x) for x in f.read().replace("\n", ",").split(",") if x.strip()}
     ok_all, total, lo = True, 0.0, None
     for i, node in enumerate(nodes):
         tf = 600.0 if node in slow else 1500.0

@@ -785,11 +785,72 @@ class E2E:
             raise StepFailed(f"the racing tenant did not start: {errs}")
         return out
 
+    def _standin_gemm(self, **env) -> Dict[str, str]:
+        """The scripted amd-gemm-validate (e2e/gemm_standin.py) on the node's PATH for the pods the
+        kubelet starts from now on: the validator's real HIP pod and workload entry run, the GEMM lines
+        are scripted. Returns the env it put in place."""
+        d = os.path.join(self.base, "standin")
+        os.makedirs(d, exist_ok=True)
+        for name, body in (("amd-gemm-validate", f'exec "{sys.executable}" -m gpu_operator_amd.e2e.gemm_standin "$@"\n'),
+                           ("rocprofv3", "exit 1\n")):            # no profiler on a CPU node
+            p = os.path.join(d, name)
+            with open(p, "w") as f:
+                f.write("#!/bin/sh\n" + body)
+            os.chmod(p, 0o755)
+        add = {"PATH": f"{d}:{self.kubelet.base_env.get('PATH', '')}", "AMDGO_BIN_DIR": d,
+               "GEMM_STANDIN_STATE": os.path.join(d, "runs"), **env}
+        self.kubelet.base_env.update(add)
+        return add
+
+    def _tenant_during_hip_sweep(self) -> Dict:
+        """Case (iv): a 1-GPU tenant is scheduled while the HIP pod's sweep runs (the pod is privileged
+        and requests no GPU, so the device plugin keeps advertising every GPU). The tenant's GPU then
+        measures slow -- the sharing -- and the validator must report it ``disturbed``, keep its numbers
+        out of the gates and open hip-ready: no floor failure, no re-measure."""
+        d = os.path.join(self.base, "standin")
+        slow_file = os.path.join(d, "tenant-gpu")
+        env = self._standin_gemm(GEMM_STANDIN_SCRIPT="fast", GEMM_STANDIN_RUNTIME_S="0.5",
+                                 GEMM_STANDIN_SLOW_FILE=slow_file)
+        running = env["GEMM_STANDIN_STATE"] + ".running"
+        errs: List[str] = []
+
+        def tenant():
+            try:
+                end = time.monotonic() + 120
+                while not os.path.exists(running) and time.monotonic() < end:
+                    time.sleep(0.02)
+                self._gpu_job("tenant-sweep", gpus=1)
+                pod = self.backing.get("v1", "Pod", "tenant-sweep", "default")
+                ids = [i for (uid, _, _), v in self.kubelet.plugins.assigned.items()
+                       if uid == pod["metadata"]["uid"] for i in v]
+                from ..devices import enumerate_gpus
+                from ..validator.components import _agent_of
+                gpus = enumerate_gpus(self.sys_root)
+                idx = sorted({_agent_of(i, gpus)["index"] for i in ids})
+                with open(slow_file + ".tmp", "w") as f:
+                    f.write(",".join(map(str, idx)))
+                os.rename(slow_file + ".tmp", slow_file)
+            except Exception as e:  # noqa: BLE001 - reported in the step's result
+                errs.append(f"{type(e).__name__}: {e}")
+                open(slow_file, "w").close()
+        th = threading.Thread(target=tenant, daemon=True)
+        th.start()
+        # the validator runs its HIP pod for real (no dry run) with the scripted GEMM
+        self._cp_update(lambda sp: sp["validator"]["hip"].update(env=[{"name": "HIP_VALIDATION_MODE", "value": "pod"}]))
+        out = self.restart_validator()
+        th.join(timeout=5)
+        if errs:
+            raise StepFailed(f"the tenant did not start during the sweep: {errs}")
+        with open(slow_file) as f:
+            out["tenant_gpus"] = [int(x) for x in f.read().split(",") if x]
+        return out
+
     def run_tenant_cases(self) -> Dict[str, Any]:
         """The validator beside tenants, on real processes: (i) a pod holds 2 GPUs
         -- the HIP pod's full sweep gets the 6 free GPUs, the 2 held ones a probe; (ii) pods hold all
         8 -- the probe only; (iii) a tenant lands between the fabric busy check and the fabric pod --
-        topology-only. The validator reaches Ready in each."""
+        topology-only; (iv) a tenant is given a GPU while the HIP sweep runs -- that GPU is reported
+        disturbed, out of the throughput gates. The validator reaches Ready in each."""
         self.setup()
         out: Dict[str, Any] = {}
         try:
@@ -808,6 +869,11 @@ class E2E:
                                                         if o.name(p).startswith("tenant-")])
             out["race"] = self.step("validator-restart[tenant before the fabric pod]", self._tenant_race)
             self.backing.delete("v1", "Pod", "tenant-race", "default")
+            self._wait("the race tenant gone", lambda: not [p for p in self.backing.list("v1", "Pod", "default")
+                                                            if o.name(p) == "tenant-race"])
+            out["during-sweep"] = self.step("validator-restart[tenant during the HIP sweep]",
+                                            self._tenant_during_hip_sweep)
+            self.backing.delete("v1", "Pod", "tenant-sweep", "default")
         except Exception as e:  # noqa: BLE001 - reported in the result
             self.result["error"] = f"{type(e).__name__}: {e}"
             self.result["logs_dir"] = self.base

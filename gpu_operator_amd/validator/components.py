@@ -60,6 +60,8 @@ class GateFailure:
 
 
 THROUGHPUT_KINDS = frozenset({"floor", "relative", "efficiency", "uniformity"})
+# (the fabric gates: "link" -- one xGMI pair below the node median, corrupted or without peer
+# access -- and "busbw" -- the all-reduce below its floor)
 
 
 @dataclass
@@ -217,7 +219,9 @@ def validate_toolkit(ctx: Context) -> Dict[str, Any]:
 GEMM_FLOOR_FRACTION = 0.50     # of the model's dense peak: healthy MI355X runs 0.63-0.68 on random data
 GEMM_MIN_RELATIVE = 0.85       # of the node median, same dtype and shape: boxes differ ~6 %, GPUs of one box ~2 %
 GEMM_MIN_EFFICIENCY = 0.90     # of N x the 1-GPU figure: independent GEMMs on separate GPUs scale at ~1.0
-BUSBW_FLOOR_FRACTION = 0.25    # of one xGMI link: a healthy 8-GPU mesh runs well above one link
+BUSBW_FLOOR_FRACTION = 0.25    # of one xGMI link (model): only when no link matrix was measured
+BUSBW_MESH_FRACTION = 0.30     # of the measured mesh bound (smallest per-GPU concurrent link ingress)
+LINK_MIN_RELATIVE = 0.80       # of the node median, per link and mode: one degraded xGMI link is named
 FABRIC_ANNOTATION = "amd.com/gpu.fabric-validation"   # read for records of older validators only
 
 
@@ -401,13 +405,51 @@ def gemm_floors(ctx: Context, gpus: Optional[List[Dict[str, Any]]] = None) -> Di
 
 
 def busbw_floor(ctx: Context) -> float:
-    """All-reduce bus-bandwidth floor (GB/s) for the largest rank count: ``RCCL_MIN_BUSBW_GBPS``
-    when set, else ``BUSBW_FLOOR_FRACTION`` of the model's per-link xGMI bandwidth."""
+    """The explicit all-reduce bus-bandwidth floor (GB/s): ``RCCL_MIN_BUSBW_GBPS`` when set, else 0 --
+    the floor is then mesh-aware (busbw_gate), from the link matrix the same run measures."""
     v = _env_float(ctx, "RCCL_MIN_BUSBW_GBPS")
-    if v is not None:
-        return v
+    return v if v is not None else 0.0
+
+
+def busbw_gate(ctx: Context, info: Dict[str, Any]) -> Dict[str, Any]:
+    """The floor the largest rank count's peak busBW must reach, and its basis (SURVEY §5.8 bounds):
+    ``env`` (RCCL_MIN_BUSBW_GBPS), ``measured-mesh`` (RCCL_MIN_BUSBW_MESH_FRACTION, default
+    BUSBW_MESH_FRACTION, x the smallest per-GPU ingress with every peer pulling at once -- what a
+    collective over this node's links can at best move), or ``model-link`` (BUSBW_FLOOR_FRACTION of
+    the model's per-link bandwidth, when no matrix was measured)."""
+    explicit = busbw_floor(ctx)
+    if explicit:
+        return {"min_busbw_gbps": explicit, "basis": "env"}
+    mesh = (info.get("links") or {}).get("min_gpu_ingress_gbps")
+    if mesh:
+        frac = _gate_value(ctx, "RCCL_MIN_BUSBW_MESH_FRACTION", BUSBW_MESH_FRACTION)
+        return {"min_busbw_gbps": round(frac * mesh, 1), "basis": "measured-mesh", "measured_mesh_bound_gbps": mesh,
+                "fraction": frac}
     model = node_model(ctx)
-    return round(model.xgmi_link_gbps * BUSBW_FLOOR_FRACTION, 1) if model else 0.0
+    return {"min_busbw_gbps": round(model.xgmi_link_gbps * BUSBW_FLOOR_FRACTION, 1) if model else 0.0,
+            "basis": "model-link"}
+
+
+def gate_links(links: Dict[str, Any], min_relative: float) -> List[GateFailure]:
+    """The xGMI link matrix's own gate, re-checked here: every ordered GPU pair whose isolated or
+    concurrent bandwidth is below ``min_relative`` x the node median of that mode, every pair whose
+    copy came back corrupted, every pair without peer access -- each one named ``src->dst``."""
+    if not links or links.get("skipped"):
+        return []
+    bad: List[GateFailure] = []
+    for mode in ("isolated", "concurrent"):
+        m = links.get(f"{mode}_gbps") or []
+        vals = [(s, d, float(v)) for s, row in enumerate(m) for d, v in enumerate(row) if s != d]
+        if not vals or not min_relative:
+            continue
+        med = sorted(v for _, _, v in vals)[len(vals) // 2]
+        for s, d, v in vals:
+            if med > 0 and v < min_relative * med:
+                bad.append(GateFailure("link", f"xGMI link {s}->{d} ({mode}): {v:.1f} GB/s is {v / med:.2f}x the node "
+                                               f"median {med:.1f} (floor {min_relative:g}x)"))
+    bad += [GateFailure("link", f"xGMI link {x}: copied data corrupted") for x in links.get("corrupt_links") or []]
+    bad += [GateFailure("link", f"xGMI link {x}: no peer access") for x in links.get("no_peer_access") or []]
+    return bad
 
 
 # ---------------------------------------------------------------------------------------------
@@ -829,7 +871,15 @@ def summarize_rccl(results: List[Dict[str, Any]]) -> Dict[str, Any]:
     per_ranks = {r["ranks"]: r.get("peak_busbw_gbps") for r in results if r.get("event") == "ranks_summary"}
     debug = next((r for r in results if r.get("event") == "rccl-debug"), {})
     summaries = [r for r in results if r.get("event") == "summary"]
+    mx = next((r for r in results if r.get("event") == "xgmi_matrix"), None)
+    links = None
+    if mx is not None:
+        links = {k: mx[k] for k in ("gpus", "skipped", "isolated_gbps", "concurrent_gbps", "median_isolated_gbps",
+                                    "median_concurrent_gbps", "gpu_ingress_gbps", "min_gpu_ingress_gbps", "min_ratio",
+                                    "slow_links", "corrupt_links", "no_peer_access", "ok") if k in mx}
     return {"sweep": sweep, "ranks": summ.get("ranks"), "peak_busbw_gbps": summ.get("peak_busbw_gbps"),
+            **({"links": links} if links is not None else {}),
+            "link_bound_gbps": summ.get("link_bound_gbps"), "mesh_bound_gbps": summ.get("mesh_bound_gbps"),
             "busbw_by_ranks": per_ranks, "fabric": fabric, "skipped": bool(summ.get("skipped")),
             "algo_proto": debug.get("algo_proto"),
             "ok": bool(summaries) and all(s.get("ok") for s in summaries) and all(r.get("ok") for r in sweep)
@@ -839,10 +889,40 @@ def summarize_rccl(results: List[Dict[str, Any]]) -> Dict[str, Any]:
 def _run_rccl_local(ctx: Context, ngpu: int, floor: float) -> List[Dict[str, Any]]:
     from .workload_main import RCCL_MAX_BYTES, RCCL_STEP_TIMEOUT_S, run_rccl
     ranks = ctx.env.get("RCCL_RANKS") or ",".join(str(n) for n in (2, 4, 8) if n <= ngpu) or str(ngpu)
-    # the same sweep (up to 8 GiB) and hang guard as the fabric pod's
+    # the same sweep (up to 8 GiB), link matrix, gates and hang guard as the fabric pod's
     return run_rccl(int(ctx.env.get("RCCL_MAX_BYTES", RCCL_MAX_BYTES)), ctx.env.get("RCCL_DTYPE", "bf16"), ranks=ranks,
                     min_busbw=floor or None,
-                    step_timeout=float(ctx.env.get("RCCL_TIMEOUT_S", RCCL_STEP_TIMEOUT_S)))
+                    step_timeout=float(ctx.env.get("RCCL_TIMEOUT_S", RCCL_STEP_TIMEOUT_S)),
+                    min_link_relative=_gate_value(ctx, "RCCL_MIN_LINK_RELATIVE", LINK_MIN_RELATIVE),
+                    mesh_fraction=None if floor else _gate_value(ctx, "RCCL_MIN_BUSBW_MESH_FRACTION", BUSBW_MESH_FRACTION))
+
+
+def judge_rccl(ctx: Context, results: List[Dict[str, Any]]) -> tuple:
+    """The fabric pod's lines -> (info, failures): the link matrix gate (each bad link named), the
+    busBW floor of the largest rank count (busbw_gate), and whatever else the workload failed on (a
+    wrong all-reduce result, a timeout) -- the binary gates the same way in the pod; this re-checks
+    so an older workload image cannot pass a bad fabric."""
+    info = summarize_rccl(results)
+    gate = busbw_gate(ctx, info)
+    info["min_busbw_gbps"] = gate["min_busbw_gbps"]
+    info["busbw_floor"] = gate
+    bad = gate_links(info.get("links") or {}, _gate_value(ctx, "RCCL_MIN_LINK_RELATIVE", LINK_MIN_RELATIVE))
+    peak, floor = info.get("peak_busbw_gbps"), gate["min_busbw_gbps"]
+    if not info["skipped"] and floor and peak is not None and peak < floor:
+        bad.append(GateFailure("busbw", f"peak busBW {peak} GB/s below the {floor} GB/s floor ({gate['basis']})"))
+    if not info["ok"] and not bad:
+        why = next((r.get("reason") or r.get("error") for r in results
+                    if r.get("event") in ("summary", "timeout", "async_error") and (r.get("reason") or r.get("error"))),
+                   None)
+        wrong = [r for r in info["sweep"] if not r.get("ok")]
+        if wrong:
+            why = f"{len(wrong)} all-reduce size(s) with wrong results, first at {wrong[0].get('bytes')} B on " \
+                  f"{wrong[0].get('ranks')} ranks"
+        bad.append(GateFailure("correctness", f"RCCL workload failed: {why or 'no passing summary'}"))
+    if bad:
+        info["ok"] = False
+        info["error"] = "; ".join(str(b) for b in bad[:8])
+    return info, bad
 
 
 def run_topology_check(ctx: Context) -> Dict[str, Any]:
@@ -882,6 +962,9 @@ def _record_full_fabric(ctx: Context, info: Dict[str, Any]) -> None:
     ctx.status.create(S.FABRIC_LAST_FULL, {
         "ts": round(time.time(), 3), "ranks": info.get("ranks"), "peak_busbw_gbps": info.get("peak_busbw_gbps"),
         "busbw_by_ranks": {str(k): v for k, v in (info.get("busbw_by_ranks") or {}).items()},
+        **({"links": {k: (info.get("links") or {}).get(k) for k in ("min_gpu_ingress_gbps", "min_ratio",
+                                                                      "median_isolated_gbps", "slow_links")}}
+           if info.get("links") else {}),
         "ok": bool(info.get("ok"))})
 
 
@@ -933,10 +1016,11 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
     floor = busbw_floor(ctx)
     mode = ctx.env.get("HIP_VALIDATION_MODE", "pod")
     if mode == "local":
-        info = summarize_rccl(_run_rccl_local(ctx, ngpu, floor))
-        info["min_busbw_gbps"] = floor
-        if not info.get("skipped") and not info["ok"]:
-            raise ValidationError(f"RCCL all-reduce validation failed: {info}")
+        info, bad = judge_rccl(ctx, _run_rccl_local(ctx, ngpu, floor))
+        if bad and not info.get("skipped"):
+            raise ValidationError(f"RCCL fabric validation failed: {[str(b) for b in bad[:8]]}", bad)
+        if not info["skipped"]:
+            _record_full_fabric(ctx, info)
         ctx.status.create(S.RCCL_READY, info)
         return info
     busy = gpu_pods_on_node(ctx)
@@ -955,12 +1039,17 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
     env = _validator_env(ctx)
     env.update({k: v for k, v in ctx.env.items() if k.startswith(("RCCL_", "NCCL_"))})
     env.update(plan["env"])
-    # the rank sweep stops at the node's physical GPU count; the busBW floor (models/ default or
-    # spec.validator.rccl.env RCCL_MIN_BUSBW_GBPS) gates the largest rank count
+    # the rank sweep stops at the node's physical GPU count; the busBW floor (spec.validator.rccl.env
+    # RCCL_MIN_BUSBW_GBPS, else a fraction of the mesh bound the pod's link matrix measures) gates the
+    # largest rank count; the link matrix names any pair below RCCL_MIN_LINK_RELATIVE x the median
     env.setdefault("RCCL_RANKS", ",".join(str(n) for n in (2, 4, 8) if n <= ngpu) or str(ngpu))
     if ngpu not in [int(x) for x in env["RCCL_RANKS"].split(",") if x]:
         env["RCCL_RANKS"] += f",{ngpu}"
-    env["RCCL_MIN_BUSBW_GBPS"] = f"{floor:g}"
+    if floor:
+        env["RCCL_MIN_BUSBW_GBPS"] = f"{floor:g}"
+    else:
+        env["RCCL_MIN_BUSBW_MESH_FRACTION"] = f"{_gate_value(ctx, 'RCCL_MIN_BUSBW_MESH_FRACTION', BUSBW_MESH_FRACTION):g}"
+    env["RCCL_MIN_LINK_RELATIVE"] = f"{_gate_value(ctx, 'RCCL_MIN_LINK_RELATIVE', LINK_MIN_RELATIVE):g}"
     if dry:
         env["RCCL_DRY_RUN"] = "1"
 
@@ -983,17 +1072,15 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
         now = gpu_pods_on_node(ctx)
         if e.admission or now:
             return _topology_only(ctx, node, ngpu, now, f"fabric pod not admitted beside GPU pod(s): {e}"[:400])
-        raise ValidationError(f"RCCL all-reduce validation failed: {e}")
+        if not e.results:
+            raise ValidationError(f"RCCL fabric validation failed: {e}"[:1000], [GateFailure("correctness", str(e)[:400])])
+        out = {"results": e.results}                 # the workload's own lines say what failed
     except (RuntimeError, TimeoutError) as e:
-        raise ValidationError(f"RCCL all-reduce validation failed: {e}")
-    info = summarize_rccl(out["results"])
-    info.update(mode="full", physical_gpus=ngpu, pod_shape=plan["shape"], min_busbw_gbps=floor)
+        raise ValidationError(f"RCCL fabric validation failed: {e}", [GateFailure("correctness", str(e)[:400])])
+    info, bad = judge_rccl(ctx, out["results"])
+    info.update(mode="full", physical_gpus=ngpu, pod_shape=plan["shape"])
     if plan.get("reason"):
         info["pod_shape_reason"] = plan["reason"]
-    peak = info.get("peak_busbw_gbps")
-    if info["ok"] and not info["skipped"] and floor and peak is not None and peak < floor:
-        info["ok"] = False
-        info["error"] = f"peak busBW {peak} GB/s below the {floor} GB/s floor"
     if plan["privileged"]:
         # the privileged-all pod holds no GPU resource: the device plugin kept advertising the GPUs,
         # so a tenant may have started during the collective -- its numbers (and any failure) then
@@ -1002,8 +1089,8 @@ def validate_rccl(ctx: Context) -> Dict[str, Any]:
         if after:
             return _topology_only(ctx, node, ngpu, after, "GPU pod(s) started during the collective: not measured",
                                   disturbed={k: info.get(k) for k in ("ok", "peak_busbw_gbps", "error") if k in info})
-    if not info["ok"]:
-        raise ValidationError(f"RCCL all-reduce validation failed: {info}")
+    if bad:
+        raise ValidationError(f"RCCL fabric validation failed: {[str(b) for b in bad[:8]]}", bad)
     if not info["skipped"]:
         _record_full_fabric(ctx, info)
     ctx.status.create(S.RCCL_READY, info)

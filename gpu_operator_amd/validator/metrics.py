@@ -66,6 +66,10 @@ class NodeMetrics:
                               node + ["dtype", "gpus"], registry=r)
         self.busbw = Gauge(p + "validator_allreduce_busbw_gbps", "validator RCCL all-reduce peak bus bandwidth",
                            node + ["ranks"], registry=r)
+        self.xgmi_link = Gauge(p + "validator_xgmi_link_gbps",
+                               "xGMI bandwidth of one ordered GPU pair (src -> dst) from the fabric pod's link matrix; "
+                               "mode isolated = that pair alone, concurrent = every pair at once",
+                               node + ["src", "dst", "mode"], registry=r)
         self._stop = threading.Event()
         self.ready_ts.labels(ctx.node_name).set(time.time())
 
@@ -102,6 +106,12 @@ class NodeMetrics:
         rc = sd.read(S.RCCL_READY) or {}
         if rc.get("peak_busbw_gbps") is not None:
             self.busbw.labels(n, str(rc.get("ranks"))).set(rc["peak_busbw_gbps"])
+        links = rc.get("links") or {}
+        for mode in ("isolated", "concurrent"):
+            for src, row in enumerate(links.get(f"{mode}_gbps") or []):
+                for dst, v in enumerate(row):
+                    if src != dst:
+                        self.xgmi_link.labels(n, str(src), str(dst), mode).set(v)
         for ranks, bw in (rc.get("busbw_by_ranks") or {}).items():     # the 2/4/8-rank sweep
             if bw is not None:
                 self.busbw.labels(n, str(ranks)).set(bw)

@@ -343,7 +343,8 @@ RCCL_STEP_TIMEOUT_S = 120.0   # the binary's hang guard: bound on one blocking s
 
 def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run, ranks: Optional[str] = None,
              min_busbw: Optional[float] = None, processes: int = 0, min_bytes: int = 1024,
-             timeout: float = 1200, step_timeout: float = RCCL_STEP_TIMEOUT_S) -> List[Dict]:
+             timeout: float = 1200, step_timeout: float = RCCL_STEP_TIMEOUT_S,
+             min_link_relative: Optional[float] = None, mesh_fraction: Optional[float] = None) -> List[Dict]:
     """The xGMI fabric proof: topology + fabric check, then a rank-count sweep in one process
     (``ranks`` "2,4,8") or, with ``processes`` N, one process per GPU joined through
     ncclCommInitRank. RCCL's INFO log is captured and summarised (algorithm/protocol per size).
@@ -354,6 +355,10 @@ def run_rccl(max_bytes: int, dtype: str, run: Callable = subprocess.run, ranks: 
     base = ["--max-bytes", str(max_bytes), "--dtype", dtype, "--min-bytes", str(min_bytes)]
     if min_busbw:
         base += ["--min-busbw", str(min_busbw)]
+    if min_link_relative is not None:
+        base += ["--min-link-relative", f"{min_link_relative:g}"]
+    if mesh_fraction:
+        base += ["--min-busbw-mesh-fraction", f"{mesh_fraction:g}"]
     if step_timeout:
         base += ["--timeout-s", f"{step_timeout:g}"]
     tmp = tempfile.mkdtemp(prefix="amdgo-rccl-")
@@ -468,7 +473,7 @@ def _run_rccl_mp(n: int, base: List[str], tmp: str, timeout: float) -> List[Dict
 
 TERMINATION_LOG_BYTES = 4000       # kubelet keeps at most 4 KiB of a termination message
 _SUMMARY_EVENTS = ("plan", "aggregate", "uniformity", "summary", "timeout", "async_error", "hip-smoke", "counters",
-                   "scaling", "fabric", "ranks_summary", "rccl-debug", "gpu_tflops")
+                   "scaling", "fabric", "ranks_summary", "rccl-debug", "gpu_tflops", "xgmi_matrix", "xgmi_link")
 
 
 def termination_message(results: List[Dict], limit: int = TERMINATION_LOG_BYTES) -> str:
@@ -536,6 +541,12 @@ def main(argv=None) -> int:
     r.add_argument("--ranks", default=os.environ.get("RCCL_RANKS", "2,4,8"))
     r.add_argument("--processes", type=int, default=int(os.environ.get("RCCL_PROCESSES", "0")))
     r.add_argument("--min-busbw", type=float, default=float(os.environ.get("RCCL_MIN_BUSBW_GBPS", "0") or 0))
+    r.add_argument("--min-link-relative", type=float,
+                   default=float(os.environ.get("RCCL_MIN_LINK_RELATIVE", "0.8") or 0),
+                   help="fail an xGMI link (GPU pair) below this fraction of the node median")
+    r.add_argument("--min-busbw-mesh-fraction", type=float,
+                   default=float(os.environ.get("RCCL_MIN_BUSBW_MESH_FRACTION", "0") or 0),
+                   help="without --min-busbw: the busBW floor as a fraction of the measured mesh bound")
     a = ap.parse_args(argv)
     if a.what == "hip":
         results = run_hip(a.gemm_shapes.split(","), counters=a.counters, iters=a.iters, dtype=a.gemm_dtype,
@@ -546,6 +557,7 @@ def main(argv=None) -> int:
         ok = hip_ok(results)
     else:
         results = run_rccl(a.max_bytes, a.dtype, ranks=a.ranks, min_busbw=a.min_busbw, processes=a.processes,
+                           min_link_relative=a.min_link_relative, mesh_fraction=a.min_busbw_mesh_fraction,
                            step_timeout=a.timeout_s)
         ok = all(x.get("ok", False) for x in results if x.get("event") == "summary")
     emit(results)

@@ -17,8 +17,19 @@
 //     rename), every rank joins with ncclCommInitRank. The launcher (amd-validator-workload
 //     rccl --processes N) starts the ranks from a parent that never touches the GPU.
 //
-// `ok` also requires the peak bus bandwidth of the largest rank count to reach --min-busbw
-// (the validator passes spec.validator.rccl.env RCCL_MIN_BUSBW_GBPS).
+//  4. The link matrix (before the rank sweep, 2+ GPUs): every ordered GPU pair (src -> dst) with
+//     peer access enabled, timed with a copy kernel on dst that reads src's HBM over xGMI (16 B per
+//     lane, wide enough to fill a link), first one pair at a time ("isolated"), then all N(N-1)
+//     pairs at once ("concurrent": each GPU pulls from every peer on its own stream). Every copy is
+//     checked (a link that corrupts data fails). A pair below --min-link-relative (0.8) x the node
+//     median of its mode fails and is NAMED (`slow_links`: "3->5"): an all-reduce over 8 ranks can
+//     hide one degraded link, this cannot. One compact `xgmi_matrix` line carries both 8x8 matrices
+//     (GB/s) and the per-GPU measured aggregate (the mesh bound the validator's busBW gate uses).
+//     1 GPU: a clean skip. --link-self-test times GPU 0 -> GPU 0 (the kernels on a 1-GPU box).
+//
+// `ok` also requires the peak bus bandwidth of the largest rank count to reach --min-busbw (an explicit
+// spec.validator.rccl.env RCCL_MIN_BUSBW_GBPS) or, without one, --min-busbw-mesh-fraction x the
+// measured mesh bound (the smallest per-GPU ingress of the concurrent link matrix).
 //
 // Hang guard (--timeout-s T): a watchdog thread bounds every blocking step -- communicator init, each
 // message size's all-reduces, each result check -- by T seconds and polls ncclCommGetAsyncError on the
@@ -30,7 +41,8 @@
 //
 //   amd-rccl-validate [--ranks 2,4,8] [--min-bytes 8] [--max-bytes 1073741824] [--iters 20]
 //                     [--warmup 5] [--dtype float|bf16] [--min-busbw GBPS] [--topology-only]
-//                     [--timeout-s T] [--sys-root /]
+//                     [--timeout-s T] [--sys-root /] [--link-bytes B] [--link-iters N]
+//                     [--min-link-relative R] [--no-links] [--links-only] [--link-self-test]
 //                     [--mp-rank R --mp-nranks N --mp-id-file F [--device D]]
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -45,6 +57,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iomanip>
 #include <mutex>
 #include <set>
 #include <sstream>
@@ -98,10 +111,29 @@ __global__ void check_bf16_kernel(const __bf16* p, size_t n, float expect, unsig
   if (c) atomicAdd(bad, c);
 }
 
+// The link probe: dst[i] = src[i] where src is a peer GPU's buffer (read over xGMI) -- launched on
+// the destination GPU, so the bytes cross the src -> dst direction of the link.
+__global__ void __launch_bounds__(256) peer_read_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+// src pattern of GPU g: word i = (g + 1) * 0x9E3779B1 ^ i
+__global__ void pattern_kernel(uint32_t* p, size_t n, uint32_t g) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = (g + 1u) * 0x9E3779B1u ^ (uint32_t)i;
+}
+__global__ void pattern_check_kernel(const uint32_t* p, size_t n, uint32_t g, unsigned long long* bad) {
+  unsigned long long c = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    c += p[i] != ((g + 1u) * 0x9E3779B1u ^ (uint32_t)i);
+  if (c) atomicAdd(bad, c);
+}
+
 // --- hang guard ------------------------------------------------------------------------------
 class Watchdog {
  public:
-  enum Phase { kIdle = 0, kInit, kAllreduce, kCheck };
+  enum Phase { kIdle = 0, kInit, kAllreduce, kCheck, kLinks };
 
   void start(double timeout_s, int rank) {
     timeout_s_ = timeout_s;
@@ -138,7 +170,7 @@ class Watchdog {
         .count();
   }
   static const char* phase_name(int p) {
-    return p == kInit ? "init" : p == kAllreduce ? "allreduce" : p == kCheck ? "check" : "idle";
+    return p == kInit ? "init" : p == kAllreduce ? "allreduce" : p == kCheck ? "check" : p == kLinks ? "links" : "idle";
   }
   void loop() {
     while (!stop_) {
@@ -206,6 +238,11 @@ struct Opts {
   std::string sys_root = "/";
   int mp_rank = -1, mp_nranks = 0, device = -1;
   std::string id_file;
+  size_t link_bytes = (size_t)256 << 20;
+  int link_iters = 5;
+  double min_link_relative = 0.8;
+  double mesh_fraction = 0;        // busBW floor as a fraction of the measured mesh bound (no --min-busbw)
+  bool links = true, links_only = false, link_self_test = false;
 };
 
 std::vector<int> parse_list(const std::string& s) {
@@ -269,6 +306,193 @@ bool fabric_check(const std::string& root) {
               ok ? "true" : "false", why.empty() ? "" : ",\"reason\":\"", why.c_str(), why.empty() ? "" : "\"");
   std::fflush(stdout);
   return ok;
+}
+
+// --- 4. the link matrix -------------------------------------------------------------------------
+struct LinkResult {
+  bool ok = true, skipped = false;
+  double min_aggregate = 0;   // smallest per-GPU concurrent ingress (GB/s): the measured mesh bound
+};
+
+static double median_of(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+// Times every ordered pair of `devs` (isolated, then concurrent) and prints the `xgmi_matrix` line.
+int link_matrix(const Opts& o, const std::vector<int>& devs, LinkResult& res) {
+  const int n = (int)devs.size();
+  const size_t bytes = o.link_bytes & ~(size_t)15, words = bytes / 4, vecs = bytes / 16;
+  std::vector<std::pair<int, int>> pairs;
+  for (int d = 0; d < n; ++d)
+    for (int s = 0; s < n; ++s)
+      if (s != d || o.link_self_test) pairs.push_back({s, d});
+  // peer access for every pair (the copy kernel on dst dereferences src's memory)
+  std::vector<std::string> no_peer;
+  for (auto [s, d] : pairs) {
+    if (s == d) continue;
+    int can = 0;
+    HIPCHECK(hipDeviceCanAccessPeer(&can, devs[d], devs[s]));
+    if (!can) {
+      no_peer.push_back(std::to_string(devs[s]) + "->" + std::to_string(devs[d]));
+      continue;
+    }
+    HIPCHECK(hipSetDevice(devs[d]));
+    const hipError_t e = hipDeviceEnablePeerAccess(devs[s], 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
+    (void)hipGetLastError();
+  }
+  // buffers: one patterned source per GPU, one destination per (dst, src) pair, a stream per pair
+  std::vector<void*> src(n, nullptr);
+  std::vector<std::vector<void*>> dst(n, std::vector<void*>(n, nullptr));
+  std::vector<std::vector<hipStream_t>> st(n, std::vector<hipStream_t>(n, nullptr));
+  std::vector<std::vector<hipEvent_t>> e0(n, std::vector<hipEvent_t>(n, nullptr)), e1 = e0;
+  std::vector<unsigned long long*> bad(n, nullptr);
+  for (int g = 0; g < n; ++g) {
+    HIPCHECK(hipSetDevice(devs[g]));
+    HIPCHECK(hipMalloc(&src[g], bytes));
+    HIPCHECK(hipMalloc(&bad[g], sizeof(unsigned long long)));
+    pattern_kernel<<<1024, 256>>>((uint32_t*)src[g], words, (uint32_t)devs[g]);
+    HIPCHECK(hipGetLastError());
+  }
+  for (auto [s, d] : pairs) {
+    HIPCHECK(hipSetDevice(devs[d]));
+    HIPCHECK(hipMalloc(&dst[d][s], bytes));
+    HIPCHECK(hipStreamCreateWithFlags(&st[d][s], hipStreamNonBlocking));
+    HIPCHECK(hipEventCreate(&e0[d][s]));
+    HIPCHECK(hipEventCreate(&e1[d][s]));
+  }
+  for (int g = 0; g < n; ++g) {
+    HIPCHECK(hipSetDevice(devs[g]));
+    HIPCHECK(hipDeviceSynchronize());
+  }
+  auto copy = [&](int s, int d) {
+    peer_read_kernel<<<2048, 256, 0, st[d][s]>>>((const uint4*)src[s], (uint4*)dst[d][s], vecs);
+  };
+  std::vector<std::vector<double>> iso(n, std::vector<double>(n, 0.0)), conc = iso;
+  std::vector<std::vector<unsigned long long>> errs(n, std::vector<unsigned long long>(n, 0));
+  g_watchdog.arm(Watchdog::kLinks, n, bytes);
+  // isolated: one pair at a time
+  for (auto [s, d] : pairs) {
+    HIPCHECK(hipSetDevice(devs[d]));
+    copy(s, d);
+    copy(s, d);
+    HIPCHECK(hipEventRecord(e0[d][s], st[d][s]));
+    for (int i = 0; i < o.link_iters; ++i) copy(s, d);
+    HIPCHECK(hipEventRecord(e1[d][s], st[d][s]));
+    HIPCHECK(hipEventSynchronize(e1[d][s]));
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, e0[d][s], e1[d][s]));
+    iso[d][s] = ms > 0 ? (double)bytes * o.link_iters / (ms * 1e-3) / 1e9 : 0;
+  }
+  // concurrent: every pair at once (each GPU pulls from all its peers, each link in both directions)
+  for (auto [s, d] : pairs) {
+    HIPCHECK(hipSetDevice(devs[d]));
+    copy(s, d);
+  }
+  for (int g = 0; g < n; ++g) {
+    HIPCHECK(hipSetDevice(devs[g]));
+    HIPCHECK(hipDeviceSynchronize());
+  }
+  for (auto [s, d] : pairs) {
+    HIPCHECK(hipSetDevice(devs[d]));
+    HIPCHECK(hipEventRecord(e0[d][s], st[d][s]));
+  }
+  for (int i = 0; i < o.link_iters; ++i)
+    for (auto [s, d] : pairs) {
+      HIPCHECK(hipSetDevice(devs[d]));
+      copy(s, d);
+    }
+  for (auto [s, d] : pairs) {
+    HIPCHECK(hipSetDevice(devs[d]));
+    HIPCHECK(hipEventRecord(e1[d][s], st[d][s]));
+  }
+  for (auto [s, d] : pairs) {
+    HIPCHECK(hipSetDevice(devs[d]));
+    HIPCHECK(hipEventSynchronize(e1[d][s]));
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, e0[d][s], e1[d][s]));
+    conc[d][s] = ms > 0 ? (double)bytes * o.link_iters / (ms * 1e-3) / 1e9 : 0;
+  }
+  // correctness: every destination holds its source's pattern
+  for (auto [s, d] : pairs) {
+    HIPCHECK(hipSetDevice(devs[d]));
+    HIPCHECK(hipMemsetAsync(bad[d], 0, sizeof(unsigned long long), st[d][s]));
+    pattern_check_kernel<<<1024, 256, 0, st[d][s]>>>((const uint32_t*)dst[d][s], words, (uint32_t)devs[s], bad[d]);
+    unsigned long long h = 0;
+    HIPCHECK(hipMemcpyAsync(&h, bad[d], sizeof h, hipMemcpyDeviceToHost, st[d][s]));
+    HIPCHECK(hipStreamSynchronize(st[d][s]));
+    errs[d][s] = h;
+  }
+  g_watchdog.disarm();
+  // the relative gate, per mode, against the node median of that mode
+  std::vector<double> iv, cv;
+  for (auto [s, d] : pairs) iv.push_back(iso[d][s]), cv.push_back(conc[d][s]);
+  const double imed = median_of(iv), cmed = median_of(cv);
+  std::vector<std::string> slow, corrupt;
+  double worst = 1e30;
+  for (auto [s, d] : pairs) {
+    const double ri = imed > 0 ? iso[d][s] / imed : 0, rc = cmed > 0 ? conc[d][s] / cmed : 0;
+    worst = std::min(worst, std::min(ri, rc));
+    const std::string name = std::to_string(devs[s]) + "->" + std::to_string(devs[d]);
+    if (errs[d][s]) corrupt.push_back(name);
+    if (o.min_link_relative > 0 && (ri < o.min_link_relative || rc < o.min_link_relative)) {
+      slow.push_back(name);
+      std::printf("{\"event\":\"xgmi_link\",\"src\":%d,\"dst\":%d,\"isolated_gbps\":%.1f,\"concurrent_gbps\":%.1f,"
+                  "\"isolated_ratio\":%.3f,\"concurrent_ratio\":%.3f,\"ok\":false,\"kind\":\"link\"}\n",
+                  devs[s], devs[d], iso[d][s], conc[d][s], ri, rc);
+    }
+  }
+  // per-GPU measured ingress with every peer pulling at once: the mesh bound of a collective
+  std::vector<double> agg(n, 0.0);
+  for (auto [s, d] : pairs) agg[d] += conc[d][s];
+  res.min_aggregate = n ? *std::min_element(agg.begin(), agg.end()) : 0;
+  res.ok = slow.empty() && corrupt.empty() && no_peer.empty();
+  auto matrix = [&](const std::vector<std::vector<double>>& m) {   // m[dst][src] -> rows = src, columns = dst
+    std::ostringstream js;
+    js << "[";
+    for (int row = 0; row < n; ++row) {
+      js << (row ? "," : "") << "[";
+      for (int col = 0; col < n; ++col) {
+        char b[24];
+        std::snprintf(b, sizeof b, "%.1f", m[col][row]);
+        js << (col ? "," : "") << b;
+      }
+      js << "]";
+    }
+    js << "]";
+    return js.str();
+  };
+  auto list = [](const std::vector<std::string>& v) {
+    std::string out;
+    for (const auto& x : v) out += (out.empty() ? "\"" : ",\"") + x + "\"";
+    return out;
+  };
+  std::ostringstream ag;
+  for (int g = 0; g < n; ++g) ag << (g ? "," : "") << std::fixed << std::setprecision(1) << agg[g];
+  std::printf("{\"event\":\"xgmi_matrix\",\"gpus\":%d,\"bytes\":%zu,\"iters\":%d,\"isolated_gbps\":%s,"
+              "\"concurrent_gbps\":%s,\"median_isolated_gbps\":%.1f,\"median_concurrent_gbps\":%.1f,"
+              "\"gpu_ingress_gbps\":[%s],\"min_gpu_ingress_gbps\":%.1f,\"min_ratio\":%.3f,\"min_link_relative\":%.2f,"
+              "\"slow_links\":[%s],\"corrupt_links\":[%s],\"no_peer_access\":[%s],\"self_test\":%s,\"ok\":%s%s}\n",
+              n, bytes, o.link_iters, matrix(iso).c_str(), matrix(conc).c_str(), imed, cmed, ag.str().c_str(),
+              res.min_aggregate, pairs.empty() ? 0.0 : worst, o.min_link_relative, list(slow).c_str(),
+              list(corrupt).c_str(), list(no_peer).c_str(), o.link_self_test ? "true" : "false",
+              res.ok ? "true" : "false", res.ok ? "" : ",\"kind\":\"link\"");
+  std::fflush(stdout);
+  for (auto [s, d] : pairs) {
+    (void)hipSetDevice(devs[d]);
+    (void)hipFree(dst[d][s]);
+    (void)hipStreamDestroy(st[d][s]);
+    (void)hipEventDestroy(e0[d][s]);
+    (void)hipEventDestroy(e1[d][s]);
+  }
+  for (int g = 0; g < n; ++g) {
+    (void)hipSetDevice(devs[g]);
+    (void)hipFree(src[g]);
+    (void)hipFree(bad[g]);
+  }
+  return 0;
 }
 
 // --- 2. one rank count in one process ---------------------------------------------------------
@@ -455,10 +679,18 @@ int main(int argc, char** argv) {
     else if (a == "--mp-id-file") o.id_file = next();
     else if (a == "--device") o.device = std::atoi(next().c_str());
     else if (a == "--timeout-s") o.timeout_s = std::atof(next().c_str());
+    else if (a == "--link-bytes") o.link_bytes = std::strtoull(next().c_str(), nullptr, 10);
+    else if (a == "--link-iters") o.link_iters = std::max(1, std::atoi(next().c_str()));
+    else if (a == "--min-link-relative") o.min_link_relative = std::atof(next().c_str());
+    else if (a == "--min-busbw-mesh-fraction") o.mesh_fraction = std::atof(next().c_str());
+    else if (a == "--no-links") o.links = false;
+    else if (a == "--links-only") o.links_only = true;
+    else if (a == "--link-self-test") o.link_self_test = true;
     else if (a == "-h" || a == "--help") {
       std::printf("usage: amd-rccl-validate [--ranks 2,4,8] [--min-bytes B] [--max-bytes B] [--iters N] "
                   "[--warmup N] [--dtype float|bf16] [--min-busbw GBPS] [--topology-only] [--timeout-s T] [--sys-root DIR] "
-                  "[--mp-rank R --mp-nranks N --mp-id-file F [--device D]]\n");
+                  "[--mp-rank R --mp-nranks N --mp-id-file F [--device D]] [--link-bytes B] [--link-iters N] "
+                  "[--min-link-relative R] [--min-busbw-mesh-fraction F] [--no-links] [--links-only] [--link-self-test]\n");
       return 0;
     } else {
       std::printf("{\"error\":\"unknown argument %s\"}\n", a.c_str());
@@ -495,6 +727,29 @@ int main(int argc, char** argv) {
               "\"dtype\":\"%s\",\"timeout_s\":%.1f}\n", ndev, ver, o.dtype.c_str(), o.timeout_s);
   g_watchdog.start(o.timeout_s, 0);
   bool all_ok = true;
+  // the link matrix over every visible GPU (one process: peer access between its devices)
+  LinkResult links;
+  if (o.links || o.links_only) {
+    std::vector<int> all(o.link_self_test ? 1 : ndev);
+    for (int d = 0; d < (int)all.size(); ++d) all[d] = d;
+    if ((int)all.size() >= 2 || o.link_self_test) {
+      if (link_matrix(o, all, links)) return 2;
+      all_ok = links.ok;
+    } else {
+      links.skipped = true;
+      std::printf("{\"event\":\"xgmi_matrix\",\"gpus\":%d,\"skipped\":\"%d GPU visible: no link to measure\","
+                  "\"ok\":true}\n", ndev, ndev);
+    }
+    if (o.links_only) {
+      std::printf("{\"event\":\"summary\",\"mode\":\"links-only\",\"skipped\":%s,\"min_gpu_ingress_gbps\":%.1f,"
+                  "\"ok\":%s}\n", links.skipped ? "true" : "false", links.min_aggregate, all_ok ? "true" : "false");
+      return all_ok ? 0 : 1;
+    }
+  }
+  // the busBW floor: --min-busbw when given, else --min-busbw-mesh-fraction of the measured mesh bound
+  Opts gated = o;
+  if (gated.min_busbw <= 0 && o.mesh_fraction > 0 && links.min_aggregate > 0 && !o.link_self_test)
+    gated.min_busbw = o.mesh_fraction * links.min_aggregate;
   int largest = 0;
   double largest_peak = 0;
   std::vector<int> run;
@@ -516,8 +771,8 @@ int main(int argc, char** argv) {
     for (auto c : comms) ncclCommDestroy(c);
     if (rc) return rc;
     const bool gate = n == *std::max_element(counts.begin(), counts.end()) || o.ranks.empty();
-    print_rank_summary(n, res, o.min_busbw, gate);
-    all_ok = all_ok && res.ok && (!gate || res.peak_busbw >= o.min_busbw);
+    print_rank_summary(n, res, gated.min_busbw, gate);
+    all_ok = all_ok && res.ok && (!gate || res.peak_busbw >= gated.min_busbw);
     run.push_back(n);
     if (n >= largest) {
       largest = n;
@@ -528,9 +783,12 @@ int main(int argc, char** argv) {
   const bool skipped = largest < 2;
   std::ostringstream rs;
   for (size_t i = 0; i < run.size(); ++i) rs << (i ? "," : "") << run[i];
+  // both bounds: the model's (one link / N-1 links of kLinkGBps) and the measured mesh
+  // bound (the smallest per-GPU ingress with every peer pulling at once, from the link matrix)
   std::printf("{\"event\":\"summary\",\"mode\":\"single-process\",\"ranks\":%d,\"ranks_run\":[%s],"
-              "\"peak_busbw_gbps\":%.2f,\"link_bound_gbps\":%.1f,\"mesh_bound_gbps\":%.1f,\"skipped\":%s,\"ok\":%s}\n",
+              "\"peak_busbw_gbps\":%.2f,\"link_bound_gbps\":%.1f,\"mesh_bound_gbps\":%.1f,"
+              "\"measured_mesh_bound_gbps\":%.1f,\"links_ok\":%s,\"skipped\":%s,\"ok\":%s}\n",
               largest, rs.str().c_str(), largest_peak, kLinkGBps, kLinkGBps * std::max(1, std::min(largest - 1, 7)),
-              skipped ? "true" : "false", all_ok ? "true" : "false");
+              links.min_aggregate, links.ok ? "true" : "false", skipped ? "true" : "false", all_ok ? "true" : "false");
   return all_ok ? 0 : 1;
 }

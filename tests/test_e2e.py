@@ -149,7 +149,8 @@ def test_validator_beside_tenants_on_real_processes(tmp_path):
     """VERDICT r3 item 1 on real processes (8 fake GPUs, GEMM and collective dry-run): (i) a tenant
     holds 2 GPUs -- the HIP pod's full sweep lists the 6 free ones (from the kubelet's pod-resources),
     the held 2 get the probe; (ii) tenants hold all 8 -- only the probe; (iii) a tenant lands between
-    the fabric busy check and the fabric pod -- topology-only within seconds. Ready in each."""
+    the fabric busy check and the fabric pod -- topology-only within seconds; (iv) a tenant given a GPU
+    during the HIP sweep -- that GPU disturbed, no floor failure. Ready in each."""
     node = str(fakesys.make_node(tmp_path / "root", n_gpus=8))
     r = E2E(sys_root=node, dev_root=node, hip_mode="skip", timeout=90).run_tenant_cases()
     assert r["ok"], r
@@ -166,3 +167,10 @@ def test_validator_beside_tenants_on_real_processes(tmp_path):
     race = r["race"]
     assert race["tenant_started_after_busy_check"] and race["rccl-ready"]["mode"] == "topology-only"
     assert race["rccl-ready"]["busy_pods"] == ["default/tenant-race"] and race["ready_s"] < 30
+    # (iv) a tenant given a GPU while the HIP sweep runs (real HIP pod, scripted GEMM): that GPU is
+    # disturbed, its slow number out of the gates -- hip-ready, no floor failure, no re-measure
+    sweep = r["during-sweep"]
+    hip = sweep["hip-ready"]
+    assert len(sweep["tenant_gpus"]) == 1 and hip["disturbed"]["devices"] == sweep["tenant_gpus"]
+    assert hip["disturbed"]["pods"] == ["default/tenant-sweep"] and hip["disturbed"]["attribution"] == "pod-resources"
+    assert "remeasured" not in hip and hip["pod_failed"]["exit_code"] == 1

@@ -488,7 +488,13 @@ def test_gemm_floors_come_from_the_model_and_env(tmp_path, node_root):
     assert comp.gemm_floors(ctx_for(tmp_path, cpx))["bf16"] == round(2516.6 * 0.50 / 8, 1)
     with pytest.raises(comp.ValidationError, match="not a number"):
         comp.gemm_floors(ctx_for(tmp_path, node_root, env={"GEMM_MIN_TFLOPS_BF16": "fast"}))
-    assert comp.busbw_floor(ctx_for(tmp_path, node_root)) == round(153.6 * 0.25, 1)
+    # the busBW floor: explicit env, else mesh-aware from the measured link matrix, else the model's link
+    ctx = ctx_for(tmp_path, node_root)
+    assert comp.busbw_floor(ctx) == 0.0
+    assert comp.busbw_gate(ctx, {}) == {"min_busbw_gbps": round(153.6 * 0.25, 1), "basis": "model-link"}
+    g = comp.busbw_gate(ctx, {"links": {"min_gpu_ingress_gbps": 700.0}})
+    assert g["basis"] == "measured-mesh" and g["min_busbw_gbps"] == 210.0
+    assert comp.busbw_gate(ctx_for(tmp_path, node_root, env={"RCCL_MIN_BUSBW_GBPS": "99"}), {})["basis"] == "env"
 
 
 def test_hip_below_floor_opens_no_barrier(tmp_path, node_root):
@@ -760,3 +766,65 @@ def test_local_mode_rccl_sweep_matches_the_pod(tmp_path, node_root, monkeypatch)
     ctx = ctx_for(tmp_path, node_root, client=c, env={"HIP_VALIDATION_MODE": "local"})
     comp.validate_rccl(ctx)
     assert seen["max_bytes"] == 8 << 30 and seen["step_timeout"] == 120.0 and seen["ranks"] == "2,4,8"
+
+
+# -- the xGMI link matrix ----------------------------------------------------------
+def _matrix_msg(slow=None, n=8, base=100.0, slow_gbps=55.0, busbw=320.0):
+    iso = [[0.0 if s == d else base for d in range(n)] for s in range(n)]
+    conc = [[0.0 if s == d else base * 0.9 for d in range(n)] for s in range(n)]
+    if slow:
+        s, d = slow
+        iso[s][d] = slow_gbps
+        conc[s][d] = slow_gbps * 0.9
+    ingress = [sum(conc[s][d] for s in range(n)) for d in range(n)]
+    return "\n".join(json.dumps(x) for x in [
+        {"event": "xgmi_matrix", "gpus": n, "isolated_gbps": iso, "concurrent_gbps": conc,
+         "median_isolated_gbps": base, "gpu_ingress_gbps": ingress, "min_gpu_ingress_gbps": min(ingress),
+         "slow_links": [f"{slow[0]}->{slow[1]}"] if slow else [], "corrupt_links": [], "no_peer_access": [],
+         "ok": not slow},
+        {"event": "ranks_summary", "ranks": 8, "peak_busbw_gbps": busbw, "ok": True},
+        {"event": "summary", "ranks": 8, "ranks_run": [2, 4, 8], "peak_busbw_gbps": busbw, "ok": not slow}])
+
+
+def test_one_slow_xgmi_link_is_named_and_opens_no_barrier(tmp_path, node_root):
+    """A rank output whose link matrix has one slow pair (3 -> 5 at 0.55x the median): no rccl-ready,
+    the pair in the error -- an 8-rank all-reduce at a healthy busBW would have hidden it."""
+    c = FakeClient([node_obj()])
+    k = FakeKubelet(c, {"amd-rccl-validator": _matrix_msg(slow=(3, 5))}, exit_code=1)
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    with pytest.raises(comp.ValidationError, match=r"3->5") as e:
+        comp.validate_rccl(ctx)
+    assert {f.kind for f in e.value.failures} == {"link"}
+    assert not ctx.status.exists(S.RCCL_READY)
+    env = _pod_env(k.seen[0])
+    assert env["RCCL_MIN_LINK_RELATIVE"] == "0.8" and env["RCCL_MIN_BUSBW_MESH_FRACTION"] == "0.3"
+    assert "RCCL_MIN_BUSBW_GBPS" not in env
+
+
+def test_healthy_matrix_sets_the_mesh_aware_busbw_floor_and_exports_links(tmp_path, node_root):
+    c = FakeClient([node_obj()])
+    FakeKubelet(c, {"amd-rccl-validator": _matrix_msg()})
+    ctx = ctx_for(tmp_path, node_root, client=c)
+    info = comp.validate_rccl(ctx)
+    # 7 peers x 90 GB/s concurrent ingress = 630 GB/s measured mesh bound; the floor is 0.3 of it
+    assert info["busbw_floor"]["basis"] == "measured-mesh" and info["min_busbw_gbps"] == 189.0
+    assert info["links"]["min_gpu_ingress_gbps"] == 630.0 and ctx.status.exists(S.RCCL_READY)
+    m = NodeMetrics(ctx)
+    m.refresh_status()
+    from prometheus_client import generate_latest
+    text = generate_latest(m.registry).decode()
+    assert 'amd_gpu_operator_validator_xgmi_link_gbps{dst="5",mode="isolated",node="n1",src="3"} 100.0' in text
+    assert len([x for x in text.splitlines() if x.startswith("amd_gpu_operator_validator_xgmi_link_gbps{")]) == 2 * 56
+    # the same matrix with an all-reduce below 0.3 of the mesh bound: a busBW failure, named as such
+    c2 = FakeClient([node_obj()])
+    FakeKubelet(c2, {"amd-rccl-validator": _matrix_msg(busbw=150.0)})
+    with pytest.raises(comp.ValidationError, match="busBW 150.0 GB/s below the 189.0 GB/s floor .measured-mesh"):
+        comp.validate_rccl(ctx_for(tmp_path / "b", node_root, client=c2))
+
+
+def test_link_gate_names_corrupt_and_unreachable_pairs():
+    links = {"isolated_gbps": [[0, 10], [10, 0]], "concurrent_gbps": [[0, 9], [9, 0]],
+             "corrupt_links": ["0->1"], "no_peer_access": ["1->0"]}
+    got = [str(f) for f in comp.gate_links(links, 0.8)]
+    assert got == ["xGMI link 0->1: copied data corrupted", "xGMI link 1->0: no peer access"]
+    assert comp.gate_links({"skipped": "1 GPU visible", "ok": True}, 0.8) == []

@@ -287,3 +287,20 @@ def test_gemm_validate_runs_one_worker_process_per_gpu():
     assert lines[-1] == {"event": "done", "ok": True}
     rc, lines, err = run("amd-gemm-validate", "--shapes", "2048", "--iters", "5", "--launch", "threads")
     assert rc == 0 and lines[0]["launch"] == "threads", err
+
+
+def test_xgmi_link_matrix_on_one_gpu_is_a_clean_skip_and_its_kernels_run():
+    """The link matrix needs 2+ GPUs: on the 1-GPU box it is a clean skip. --link-self-test runs the
+    peer-read copy, the pattern check and the matrix line on GPU 0 -> GPU 0 (its HBM), so the kernels
+    the 8-GPU node uses are exercised here."""
+    rc, lines, err = run("amd-rccl-validate", "--links-only", timeout=120)
+    assert rc == 0, err
+    mx = [x for x in lines if x.get("event") == "xgmi_matrix"][0]
+    assert mx["skipped"] and mx["ok"] and lines[-1]["event"] == "summary" and lines[-1]["skipped"]
+    rc, lines, err = run("amd-rccl-validate", "--links-only", "--link-self-test", "--link-bytes", str(256 << 20),
+                         timeout=120)
+    assert rc == 0, (lines, err)
+    mx = [x for x in lines if x.get("event") == "xgmi_matrix"][0]
+    print(f"GPU0 -> GPU0 copy: isolated {mx['isolated_gbps']} GB/s, concurrent {mx['concurrent_gbps']} GB/s")
+    assert mx["self_test"] and mx["ok"] and mx["corrupt_links"] == [] and mx["gpus"] == 1
+    assert mx["isolated_gbps"][0][0] > 1000          # an HBM3E copy kernel: TB/s, not PCIe
