@@ -78,7 +78,7 @@ def gemm_fp8(a, bt, out=None, *, generic: bool = False):
 
 # Production variant sets (native/hip/gemm_bf16.hip, gemm_fp8.hip): 0 = automatic dispatch, any
 # other member pins that kernel. Everything else lives in the tools-only lab library.
-BF16_VARIANTS = (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56)
+BF16_VARIANTS = (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61)
 FP8_VARIANTS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23)
 
 
@@ -90,6 +90,17 @@ def set_variant(v: int) -> None:
 
 def get_variant() -> int:
     return _lib.load().amdgo_gemm_get_variant()
+
+
+def set_split_target(t: int) -> None:
+    """v61 (split-K 128x128): aim for ``t`` workgroups per CU (1..8; per host thread)."""
+    if _lib.load().amdgo_gemm_set_split_target(int(t)) != 0:
+        raise ValueError(f"split target {t} outside 1..8")
+
+
+def small_splits(m: int, n: int, k: int, cus: int = 256) -> int:
+    """The K splits v61 uses for this shape on a device with ``cus`` CUs."""
+    return _lib.load().amdgo_gemm_small_splits(int(m), int(n), int(k), int(cus))
 
 
 def resolve_variant(m: int, n: int, k: int) -> int:

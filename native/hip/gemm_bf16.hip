@@ -35,14 +35,23 @@
 //        interleaves each half-pass's stores into the next one's staging, EPI 17 LEAN_ILV: 16384^2x1024
 //        +2.2 %, 8192^2x2048 +1.2 % over the plain pipeline, profiles/r4_sweep/lab_ilv_*.jsonl;
 //        gemm_w4ap.h): the power-of-two-K default for short K or one dispatch wave.
-//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 = that kernel pinned (no automatic switch; still falls back to a kernel
-//        that can run the shape or the device).
+//   60 (round 5) = 128x128 output tiles (gemm_small.h) for grids the 256x256 kernels leave mostly idle
+//        (a 256-tile grid of at most a quarter of the CUs) and for shapes only 128-tileable.
+//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 / 60 = that kernel pinned (no automatic switch; still falls back to a
+//        kernel that can run the shape or the device).
+// The automatic choice is the first matching row of the declarative table kBf16Rules below (each row
+// cites its sweep); what each kernel needs, and where a pinned one falls back, is kBf16Needs. Both are
+// checked against the round-4 rule code they replaced in tests/test_gemm_dispatch.py.
 // Every w4s / w4sp kernel here carries the K offset of its LDS-DMA pieces in the lane offset (VK: one VALU
 // add per K-tile, loop-invariant soffsets; 17 fewer SALU per K-tile, +0.6-0.8 % at 8192^3 and
 // 16384^3, profiles/r2_sched/sweep_vk.jsonl).
 // A bounds-checked generic kernel handles shapes that are not multiples of the tile.
 
+#include <map>
+#include <mutex>
+
 #include "gemm_bf16_kernels.h"
+#include "gemm_small.h"
 
 // K-tile schedules of the persistent asm pipeline (gemm_bf16_asm_loop.h, tools/gen_bf16_asm_loop.py):
 // g4 waits for the last R1 fragment read 4 MFMAs after it is issued (not 1), which takes the
@@ -58,80 +67,193 @@
 #define W4AP_SC_MAIN W4AP_SC_G4_ZC
 #define W4AP_SC_LONGK W4AP_SC_G6D6_ZC
 
-static int g_variant = 0;
+// The variant a caller pinned (amdgo_gemm_set_variant): per host thread, so threads driving
+// different GPUs (amd-gemm-validate --launch threads) never see each other's pin.
+static thread_local int g_variant = 0;
 
 // Persistent grid: one workgroup per CU (the 160 KiB LDS admits one), a multiple of the 8 XCDs,
 // never more workgroups than tiles. 0 when the device or the tile count is too small.
-static int persistent_grid(int nwg, hipStream_t s) {
-  const int cus = device_cu_count(s);
+static int persistent_grid(int nwg, int cus) {
   const int g = nwg < cus ? nwg : cus;
   return (g / NXCD) * NXCD;
 }
 
-// The kernel amdgo_gemm_bf16 runs for this shape on the device of stream `s` (0 = generic).
-static int resolve_variant(int M, int N, int K, hipStream_t s) {
-  if (M % BM || N % BN || K % BK || K < 2 * BK) return 0;
-  const int nwg = (M / BM) * (N / BN);
-  const int cus = device_cu_count(s);
-  const bool sq = (M / BM) % 16 == 0 && (N / BN) % 16 == 0;
-  int v = g_variant;
-  const bool pow2k = (K & (K - 1)) == 0;
-  if (v == 0 && cus == 256 && !pow2k && K % (2 * BK) == 0 && K >= 4 * BK && persistent_grid(nwg, s) >= NXCD) {
-    // K not a power of two: the asm pipeline in the VP DMA form (per-piece VGPR lane offsets, the K
-    // offset in one SGPR): 12288^3 1.02x hipBLASLt (v48 0.98x, the DM-0 asm form 0.88x),
-    // 8192^2x12288 1.07x (v47 1.02x), 12288^2x10240 1.03x (v48 1.03x); profiles/r3_s2/vp_bf16.jsonl.
-    // v54 = the same on the square cross-XCD raster for >= 8 dispatch waves on 16x16-tile multiples:
-    // 12288^3 1.05x (v53 1.03x), 12288^2x10240 1.07x (v53 1.04x); profiles/r3_s2/vpsq_bf16.jsonl
-    v = (sq && nwg >= 8 * cus) ? 54 : 53;
-  } else if (v == 0 && cus == 256 && pow2k && K >= 4 * BK && persistent_grid(nwg, s) >= NXCD) {
-    // The hand-scheduled asm K pipeline, persistent (profiles/r3_asm/): v50 everywhere it runs,
-    // ahead of v44 and v25 on every measured shape (8192^3 +2-3 %, 8192^2x2048 +7 %,
-    // 16384^2x1024 +14 % over v44); its square-raster form v51 for >= 8 dispatch waves with long K
-    // (16384^3 1.01x hipBLASLt, v45 0.98x); the DMA-spaced schedule v52 for one or two dispatch
-    // waves with very long K (with nontemporal C stores: 4096^2x32768 +1.0 % over v50, but v50 ahead
-    // at 4096^2x16384 by 1.9 % and at 4096x8192x8192 by 0.5 %; profiles/r3_s2/longk_bf16.jsonl).
-    v = 50;
-    if (sq && nwg >= 8 * cus && K >= 128 * BK) v = 51;
-    else if (nwg <= 2 * cus && K >= 512 * BK) v = 52;
-    // Round 4 (profiles/r4_lean/, r4_prod/): on 16x16-tile multiples with short K (<= 2048) or one
-    // dispatch wave, v56 (VP + PA DMA, pipelined LEAN epilogue, square raster): 16384^2x1024 1440 TF/s =
-    // 1.08x hipBLASLt (v50 1.06x), 8192^2x1024 1.09x (1.02x), 8192^2x2048 1.05x (1.03x), 4096^2x2048
-    // 1.03x (1.00x); other one-wave grids v55 (VP + PA, LEAN, linear raster).
-    else if (sq && (K <= 32 * BK || nwg <= cus)) v = 56;
-    else if (nwg <= cus) v = 55;
-  } else if (v == 0) {
-    v = 44;
-    // Short K (K-loop of <= 64 K-tiles) with several tiles per CU: the persistent v25 hides each
-    // tile's prologue and epilogue under the neighbouring K-loops (16384x16384x1024: +10 %;
-    // K = 3072 +1.2 %, K = 4096 +0.3-0.7 %: profiles/r2_sched/sweep_persistent_midk.jsonl).
-    if (K <= 64 * BK && nwg >= 2 * cus) v = 25;
-    // Big grids (>= 8 dispatch waves) with long K: the square cross-XCD raster (v45) streams fewer
-    // distinct panels per wave (profiles/r1_s6_sq: 12288^3 +5.5 %, 16384x8192x8192 +2.9 %,
-    // 16384^3 +3.4 %; at 4 waves or K = 4096 it measured 1 % behind v44, so those stay on v44).
-    else if (sq && nwg >= 8 * cus && K >= 128 * BK) v = 45;
+// What the dispatch knows about a shape on a device.
+struct Bf16Shape {
+  int M, N, K, cus;
+  bool tiles256;   // M, N multiples of 256, K of 64, K >= 128: the 256x256 kernels can run it
+  bool tiles128;   // M, N multiples of 128, K of 64: the 128x128 kernel (v60) can run it
+  int nwg;         // 256x256 output tiles
+  int pgrid;       // persistent grid of the 256x256 kernels
+  bool sq;         // 16x16-tile multiples (the square cross-XCD raster)
+  bool pow2k;
+  bool mi355;      // the 256-CU MI355X every w4ap / serpentine schedule was measured on
+};
+
+static Bf16Shape bf16_shape(int M, int N, int K, int cus) {
+  Bf16Shape c{M, N, K, cus};
+  c.tiles256 = M % BM == 0 && N % BN == 0 && K % BK == 0 && K >= 2 * BK;
+  c.tiles128 = M % S_BM == 0 && N % S_BN == 0 && K % S_BK == 0 && K >= S_BK;
+  c.nwg = (M / BM) * (N / BN);
+  c.pgrid = persistent_grid(c.nwg, cus);
+  c.sq = (M / BM) % 16 == 0 && (N / BN) % 16 == 0;
+  c.pow2k = (K & (K - 1)) == 0;
+  c.mi355 = cus == 256;
+  return c;
+}
+
+// The automatic dispatch, one row per shape class, first match wins. Each row names the sweep that
+// put it there (every number: our kernel against hipBLASLt in the same process on MI355X).
+struct Bf16Rule {
+  int variant;
+  bool (*match)(const Bf16Shape&);
+  const char* evidence;
+};
+static constexpr Bf16Rule kBf16Rules[] = {
+    // a 256x256 grid of at most a quarter of the CUs (or a shape only 128-tileable): 4x the workgroups
+    {60, [](const Bf16Shape& c) { return c.tiles128 && (!c.tiles256 || 4 * c.nwg <= c.cus); },
+     "profiles/r5_small/sweep_small_bf16.jsonl (1024^3 0.94x -> see README)"},
+    {0, [](const Bf16Shape& c) { return !c.tiles256; }, "generic bounds-checked kernel"},
+    // K not a power of two (even K-tile count >= 4): the asm pipeline in the VP DMA form
+    {54, [](const Bf16Shape& c) { return c.mi355 && !c.pow2k && c.K % (2 * BK) == 0 && c.K >= 4 * BK &&
+                                         c.pgrid >= NXCD && c.sq && c.nwg >= 8 * c.cus; },
+     "profiles/r3_s2/vpsq_bf16.jsonl (12288^3 1.05x, 12288^2x10240 1.07x)"},
+    {53, [](const Bf16Shape& c) { return c.mi355 && !c.pow2k && c.K % (2 * BK) == 0 && c.K >= 4 * BK &&
+                                         c.pgrid >= NXCD; },
+     "profiles/r3_s2/vp_bf16.jsonl (12288^3 1.02x, 8192^2x12288 1.07x)"},
+    // power-of-two K: the persistent asm K pipeline and its forms
+    {51, [](const Bf16Shape& c) { return c.mi355 && c.pow2k && c.K >= 4 * BK && c.pgrid >= NXCD && c.sq &&
+                                         c.nwg >= 8 * c.cus && c.K >= 128 * BK; },
+     "profiles/r3_asm/ (16384^3 1.01x)"},
+    {52, [](const Bf16Shape& c) { return c.mi355 && c.pow2k && c.K >= 4 * BK && c.pgrid >= NXCD &&
+                                         c.nwg <= 2 * c.cus && c.K >= 512 * BK; },
+     "profiles/r3_s2/longk_bf16.jsonl (4096^2x32768 +1.0 %)"},
+    {56, [](const Bf16Shape& c) { return c.mi355 && c.pow2k && c.K >= 4 * BK && c.pgrid >= NXCD && c.sq &&
+                                         (c.K <= 32 * BK || c.nwg <= c.cus); },
+     "profiles/r4_lean/, r4_sweep/ (16384^2x1024 1.08x, 8192^2x2048 1.05x)"},
+    {55, [](const Bf16Shape& c) { return c.mi355 && c.pow2k && c.K >= 4 * BK && c.pgrid >= NXCD && c.nwg <= c.cus; },
+     "profiles/r4_lean/ (one-wave grids off the 16x16-tile multiples)"},
+    {50, [](const Bf16Shape& c) { return c.mi355 && c.pow2k && c.K >= 4 * BK && c.pgrid >= NXCD; },
+     "profiles/r3_asm/asm8_summary.jsonl (8192^3 +2-3 % over v44)"},
+    // the C++ w4s family (short K without a persistent asm grid, other devices)
+    {25, [](const Bf16Shape& c) { return c.K <= 64 * BK && c.nwg >= 2 * c.cus && c.pgrid >= NXCD; },
+     "profiles/r2_sched/sweep_persistent_midk.jsonl (16384^2x1024 +10 %)"},
+    {48, [](const Bf16Shape& c) { return c.mi355 && !c.pow2k && c.sq && c.nwg >= 8 * c.cus && c.K >= 128 * BK; },
+     "profiles/r2_sched/sweep_pa.jsonl (PA rows, K not a power of two)"},
+    {45, [](const Bf16Shape& c) { return c.mi355 && c.sq && c.nwg >= 8 * c.cus && c.K >= 128 * BK; },
+     "profiles/r1_s6_sq (12288^3 +5.5 %, 16384^3 +3.4 %)"},
+    {47, [](const Bf16Shape& c) { return c.mi355 && !c.pow2k; }, "profiles/r2_sched/sweep_pa.jsonl (12288^3 +11 %)"},
+    {44, [](const Bf16Shape& c) { return c.mi355; }, "profiles/r1_* (serpentine K + loop rotation)"},
+    {42, [](const Bf16Shape&) { return true; }, "devices without 256 CUs: rotation only"},
+};
+
+// What a kernel needs from the shape and device, and where a pinned variant goes when it cannot run.
+struct Bf16Need {
+  int variant;
+  bool (*ok)(const Bf16Shape&);
+  int fallback;
+};
+static constexpr Bf16Need kBf16Needs[] = {
+    {60, [](const Bf16Shape& c) { return c.tiles128; }, 0},
+    {61, [](const Bf16Shape& c) { return c.tiles128; }, 0},
+    {45, [](const Bf16Shape& c) { return c.sq; }, 44},
+    {48, [](const Bf16Shape& c) { return c.sq; }, 47},
+    {47, [](const Bf16Shape& c) { return c.mi355; }, 42},
+    {48, [](const Bf16Shape& c) { return c.mi355; }, 42},
+    {25, [](const Bf16Shape& c) { return c.pgrid >= NXCD; }, 44},
+    // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups
+    {50, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    {51, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    {52, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    {53, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    {54, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    {55, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    {56, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    // the square raster needs 16x16 super-tiles and exactly 256 workgroups
+    {54, [](const Bf16Shape& c) { return c.sq && c.mi355; }, 53},
+    {56, [](const Bf16Shape& c) { return c.sq && c.mi355; }, 55},
+    {51, [](const Bf16Shape& c) { return c.sq && c.mi355; }, 50},
+    // serpentine K assumes 32 co-resident workgroups per XCD
+    {44, [](const Bf16Shape& c) { return c.mi355; }, 42},
+    {45, [](const Bf16Shape& c) { return c.mi355; }, 42},
+};
+
+// v61 split count: enough workgroups for one per CU (g_split_target x CUs), each split at least 4
+// K-tiles deep; 1 = no split.
+static thread_local int g_split_target = 1;
+static int small_splits(int tiles, int nk, int cus) {
+  int s = (g_split_target * cus) / (tiles > 0 ? tiles : 1);
+  if (s > nk / 4) s = nk / 4;
+  return s < 1 ? 1 : s;
+}
+
+// v61's fp32 partials and per-tile arrival counters, one set per (device, stream): two GEMMs in
+// flight on different streams never share them; a launch on one stream resets its counters before it
+// ends, so the next launch there finds them zero. Allocated on first use, never shrunk.
+struct SplitWorkspace {
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  size_t floats = 0;
+  int counters = 0;
+};
+static std::mutex g_split_mu;
+static std::map<std::pair<int, hipStream_t>, SplitWorkspace> g_split_ws;
+
+static SplitWorkspace* split_workspace(hipStream_t s, size_t floats, int tiles) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_split_mu);
+  SplitWorkspace& w = g_split_ws[{dev, s}];
+  if (w.floats < floats) {
+    // a larger partial buffer: the old one may still be read by a launch in flight on this stream
+    if (w.ws && hipStreamSynchronize(s) != hipSuccess) return nullptr;
+    if (w.ws) (void)hipFree(w.ws);
+    w.ws = nullptr;
+    w.floats = 0;
+    if (hipMalloc(&w.ws, floats * sizeof(float)) != hipSuccess) return nullptr;
+    w.floats = floats;
   }
-  if (v == 45 && !sq) v = 44;                           // square raster needs 16x16 super-tiles
-  if (v == 48 && !sq) v = 47;
-  if ((v == 47 || v == 48) && cus != 256) v = 42;
-  if (v == 25 && persistent_grid(nwg, s) < NXCD) v = 44;
-  // w4ap runs an even number of K-tiles (>= 4) on a grid of whole XCD groups; its square raster
-  // (v51) needs exactly 256 workgroups over 16x16 super-tiles
-  if ((v == 50 || v == 51 || v == 52 || v == 53 || v == 54 || v == 55 || v == 56) &&
-      (K % (2 * BK) != 0 || K < 4 * BK || persistent_grid(nwg, s) < NXCD))
-    v = 44;
-  if (v == 54 && (!sq || cus != 256)) v = 53;
-  if (v == 56 && (!sq || cus != 256)) v = 55;
-  if (v == 51 && (!sq || cus != 256)) v = 50;
-  if ((v == 44 || v == 45) && cus != 256) v = 42;       // serpentine K assumes 32 co-resident WGs / XCD
-  // K not a power of two: A-panel DMA instructions read rows 32 apart (PA, v47 / v48). At a 24 KiB
-  // row stride adjacent rows cost 8-11 % (12288^3 1405 -> 1557 TF, 8192^2x12288 1457 -> 1579,
-  // 12288^2x10240 +5 %); at power-of-two K it is neutral (8192) or worse (16384: -8 %).
-  // profiles/r2_sched/sweep_pa.jsonl
-  if (g_variant == 0 && !pow2k) {
-    if (v == 44) v = 47;
-    else if (v == 45) v = 48;
+  if (w.counters < tiles) {
+    if (w.cnt && hipStreamSynchronize(s) != hipSuccess) return nullptr;
+    if (w.cnt) (void)hipFree(w.cnt);
+    w.cnt = nullptr;
+    w.counters = 0;
+    const int n = tiles < 1024 ? 1024 : tiles;
+    if (hipMalloc(&w.cnt, n * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(w.cnt, 0, n * sizeof(int), s) != hipSuccess) return nullptr;
+    w.counters = n;
+  }
+  return &w;
+}
+
+// The kernel for a shape on a device with `cus` CUs: the pinned variant (walked down its fallbacks
+// until it can run), or the first matching row of kBf16Rules. 0 = the generic kernel.
+static int plan_bf16(int M, int N, int K, int cus, int pinned) {
+  const Bf16Shape c = bf16_shape(M, N, K, cus);
+  int v = pinned;
+  if (v == 0) {
+    for (const auto& r : kBf16Rules)
+      if (r.match(c)) {
+        v = r.variant;
+        break;
+      }
+    return v;
+  }
+  if (v != 60 && v != 61 && !c.tiles256) return 0;
+  for (bool moved = true; moved && v;) {
+    moved = false;
+    for (const auto& n : kBf16Needs)
+      if (n.variant == v && !n.ok(c)) {
+        v = n.fallback;
+        moved = true;
+        break;
+      }
   }
   return v;
+}
+
+static int resolve_variant(int M, int N, int K, hipStream_t s) {
+  return plan_bf16(M, N, K, device_cu_count(s), g_variant);
 }
 
 extern "C" {
@@ -139,13 +261,32 @@ extern "C" {
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
   if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50 &&
-      v != 51 && v != 52 && v != 53 && v != 54 && v != 55 && v != 56)
+      v != 51 && v != 52 && v != 53 && v != 54 && v != 55 && v != 56 && v != 60 && v != 61)
     return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
 }
 int amdgo_gemm_get_variant() { return g_variant; }
+// v61: split-K workgroups per CU to aim for (1 = one wave of the chip); per host thread like the pin.
+int amdgo_gemm_set_split_target(int t) {
+  if (t < 1 || t > 8) return (int)hipErrorInvalidValue;
+  g_split_target = t;
+  return 0;
+}
+int amdgo_gemm_small_splits(int M, int N, int K, int cus) {
+  return small_splits((M / S_BM) * (N / S_BN), K / S_BK, cus);
+}
 int amdgo_gemm_resolve_variant(int M, int N, int K) { return resolve_variant(M, N, K, nullptr); }
+// The dispatch as a pure function of the shape, the device's CU count and a pinned variant (no GPU
+// needed: the CPU tests check the table against the rules it replaced).
+int amdgo_gemm_plan_bf16(int M, int N, int K, int cus, int pinned) { return plan_bf16(M, N, K, cus, pinned); }
+// The evidence row behind the automatic choice (the sweep file that put it there).
+const char* amdgo_gemm_plan_bf16_evidence(int M, int N, int K, int cus) {
+  const Bf16Shape c = bf16_shape(M, N, K, cus);
+  for (const auto& r : kBf16Rules)
+    if (r.match(c)) return r.evidence;
+  return "";
+}
 
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
@@ -155,13 +296,32 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   const auto* b = (const __bf16*)Bt;
   auto* c = (__bf16*)C;
   const int nwg = (M / BM) * (N / BN);
+  const int cus = device_cu_count(s);
+  auto persistent = [&](int n) { return persistent_grid(n, cus); };
   switch (resolve_variant(M, N, K, s)) {
+    case 60:
+      hipLaunchKernelGGL(gemm_bf16_128x128_t<false>, dim3((M / S_BM) * (N / S_BN)), dim3(S_THREADS), 0, s, a, b, c, M, N,
+                         K, 1, nullptr, nullptr);
+      break;
+    case 61: {
+      const int tiles = (M / S_BM) * (N / S_BN);
+      const int splits = small_splits(tiles, K / S_BK, cus);
+      SplitWorkspace* w = splits > 1 ? split_workspace(s, (size_t)tiles * splits * S_BM * S_BN, tiles) : nullptr;
+      if (!w) {
+        hipLaunchKernelGGL(gemm_bf16_128x128_t<false>, dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K, 1, nullptr,
+                           nullptr);
+        break;
+      }
+      hipLaunchKernelGGL(gemm_bf16_128x128_t<true>, dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
+                         splits, w->ws, w->cnt);
+      break;
+    }
     case 18:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 25:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, false, true>), dim3(persistent_grid(nwg, s)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, false, true>), dim3(persistent(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 42:
@@ -185,7 +345,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          0, s, a, b, c, M, N, K);
       break;
     case 50:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg, s)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 51:
@@ -193,7 +353,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          a, b, c, M, N, K);
       break;
     case 53:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 1>), dim3(persistent_grid(nwg, s)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 1>), dim3(persistent(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 54:
@@ -201,7 +361,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          0, s, a, b, c, M, N, K);
       break;
     case 55:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN, 2>), dim3(persistent_grid(nwg, s)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN, 2>), dim3(persistent(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 56:
@@ -209,7 +369,7 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
                          0, s, a, b, c, M, N, K);
       break;
     case 52:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent_grid(nwg, s)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {

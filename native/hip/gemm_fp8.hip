@@ -36,46 +36,109 @@
 
 #include "gemm_fp8_kernels.h"
 
-static int g_fp8_variant = 0;
+// The variant a caller pinned (amdgo_gemm_fp8_set_variant): per host thread (see gemm_bf16.hip).
+static thread_local int g_fp8_variant = 0;
 
 // q16 schedule (lab v28 / v32): free barrier after slot 17, DMA pieces at slots 18, 21, .., 63,
 // landing wait at 34, B0' reads from slot 35, A0' reads from 43 (block 2 walks A0 slowly).
 #define Q16(SERP, SQ) (gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, SERP, SQ, 2, 2, true>)
 
-// The kernel amdgo_gemm_fp8 runs for this shape on the device of stream `s` (0 = generic).
-static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
-  if (M % F8_BM || N % F8_BN || K % F8_BK || K < 2 * F8_BK) return 0;
-  const int nwg = (M / F8_BM) * (N / F8_BN);
-  const int cus = device_cu_count(s);
-  const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;     // persistent grid: one WG per CU
-  const bool sq = (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0;
-  int v = g_fp8_variant;
-  const bool ap_ok = cus == 256 && K % (2 * F8_BK) == 0 && K >= 4 * F8_BK && pgrid >= NXCD;
-  if (v == 0 && ap_ok) {
-    // v22 on multi-wave square grids needs >= 32 tiles on both sides or K >= 4096: with a 16-tile side
-    // and short K it measured 3-6 % behind v21 (12288x4096x1024 2129 vs 2253 TF/s, 8192x4096x1024 1958
-    // vs 2072; profiles/r4_sweep/rules2_fp8.jsonl). One dispatch wave: v22, or v23 off the 16x16-tile
-    // multiples (4096^3 2996 vs v20 2957, 4096^2x8192 +1.3 %, 2048x4096x4096 1.010x vs 0.997x;
-    // profiles/r4_sweep/onewave_fp8.jsonl).
-    const bool wide = M / F8_BM >= 32 && N / F8_BN >= 32;
-    if (nwg <= cus) v = sq ? 22 : 23;
-    else if (sq && nwg >= 2 * cus) v = (wide || K >= 4096) ? 22 : 21;
-    else v = 20;
-  } else if (v == 0) {
-    v = sq ? 16 : 15;
-    // Short K (<= 12 K-tiles) with several tiles per CU: the persistent block-scaled kernel hides
-    // each tile's prologue and epilogue under the neighbouring K-loops; up to 64 K-tiles with >= 4
-    // tiles per CU the persistent q16 does (it loses to v10 at K = 1024-1536 and to the square
-    // raster at K = 16384).
-    if (K <= 12 * F8_BK && nwg >= 2 * cus) v = 10;
-    else if (K <= 64 * F8_BK && nwg >= 4 * cus) v = 18;
+// What the dispatch knows about a shape on a device.
+struct Fp8Shape {
+  int M, N, K, cus;
+  bool tiles;      // M, N multiples of 256, K of 128, K >= 256: the 256x256 kernels can run it
+  int nwg, pgrid;  // 256x256 output tiles; the persistent grid (one WG per CU, whole XCD groups)
+  bool sq;         // 16x16-tile multiples (the square cross-XCD raster)
+  bool wide;       // >= 32 tiles on both sides
+  bool ap;         // the q16ap asm frame can run it: the 256-CU MI355X, an even K-tile count >= 4
+};
+
+static Fp8Shape fp8_shape(int M, int N, int K, int cus) {
+  Fp8Shape c{M, N, K, cus};
+  c.tiles = M % F8_BM == 0 && N % F8_BN == 0 && K % F8_BK == 0 && K >= 2 * F8_BK;
+  c.nwg = (M / F8_BM) * (N / F8_BN);
+  c.pgrid = ((c.nwg < cus ? c.nwg : cus) / NXCD) * NXCD;
+  c.sq = (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0;
+  c.wide = M / F8_BM >= 32 && N / F8_BN >= 32;
+  c.ap = cus == 256 && K % (2 * F8_BK) == 0 && K >= 4 * F8_BK && c.pgrid >= NXCD;
+  return c;
+}
+
+// The automatic dispatch, first match wins; each row names the sweep that put it there.
+struct Fp8Rule {
+  int variant;
+  bool (*match)(const Fp8Shape&);
+  const char* evidence;
+};
+static constexpr Fp8Rule kFp8Rules[] = {
+    {0, [](const Fp8Shape& c) { return !c.tiles; }, "generic bounds-checked kernel"},
+    // one dispatch wave: v22 (v23 off the 16x16-tile multiples)
+    {22, [](const Fp8Shape& c) { return c.ap && c.nwg <= c.cus && c.sq; },
+     "profiles/r4_sweep/onewave_fp8.jsonl (4096^3 2996 vs v20 2957)"},
+    {23, [](const Fp8Shape& c) { return c.ap && c.nwg <= c.cus; },
+     "profiles/r4_sweep/onewave_fp8.jsonl (2048x4096x4096 1.010x vs 0.997x)"},
+    // multi-wave square grids: v22 needs >= 32 tiles on both sides or K >= 4096, else v21
+    {22, [](const Fp8Shape& c) { return c.ap && c.sq && c.nwg >= 2 * c.cus && (c.wide || c.K >= 4096); },
+     "profiles/r4_lean/ (16384^2x1024 1.19x, 12288^3 1.02x)"},
+    {21, [](const Fp8Shape& c) { return c.ap && c.sq && c.nwg >= 2 * c.cus; },
+     "profiles/r4_sweep/rules2_fp8.jsonl (12288x4096x1024 2253 vs v22 2129)"},
+    {20, [](const Fp8Shape& c) { return c.ap; }, "profiles/r3_s2/zc_fp8.jsonl (4096^3 1.04x)"},
+    // off the asm frame (other devices, K not an even K-tile count): the C++ q16 family
+    {10, [](const Fp8Shape& c) { return c.K <= 12 * F8_BK && c.nwg >= 2 * c.cus && c.pgrid >= NXCD; },
+     "profiles/r2_fp8_q16/ (persistent block-scaled kernel, short K)"},
+    {18, [](const Fp8Shape& c) { return c.K <= 64 * F8_BK && c.nwg >= 4 * c.cus && c.pgrid >= NXCD; },
+     "profiles/r2_fp8_q16/sweep_q16p*.jsonl (8192^3 +0.7-1.2 %, 16384^2x4096 +2.9 %)"},
+    {16, [](const Fp8Shape& c) { return c.sq && c.cus == 256; }, "profiles/r2_fp8_q16/ (square raster)"},
+    {15, [](const Fp8Shape& c) { return c.cus == 256; }, "profiles/r2_fp8_q16/ (q16 vs block-scaled +3-5 %)"},
+    {17, [](const Fp8Shape&) { return true; }, "devices without 256 CUs: q16 without serpentine K"},
+};
+
+// What a kernel needs, and where a pinned variant goes when it cannot run.
+struct Fp8Need {
+  int variant;
+  bool (*ok)(const Fp8Shape&);
+  int fallback;   // -1: 16 on the square raster, else 15
+};
+static constexpr Fp8Need kFp8Needs[] = {
+    {20, [](const Fp8Shape& c) { return c.ap; }, -1},
+    {21, [](const Fp8Shape& c) { return c.ap; }, -1},
+    {22, [](const Fp8Shape& c) { return c.ap; }, -1},
+    {23, [](const Fp8Shape& c) { return c.ap; }, -1},
+    {21, [](const Fp8Shape& c) { return c.sq; }, 20},
+    {22, [](const Fp8Shape& c) { return c.sq; }, 23},
+    {16, [](const Fp8Shape& c) { return c.sq; }, 15},
+    {10, [](const Fp8Shape& c) { return c.pgrid >= NXCD; }, 15},
+    {18, [](const Fp8Shape& c) { return c.pgrid >= NXCD; }, 15},
+    // serpentine K assumes 32 co-resident tiles per XCD
+    {15, [](const Fp8Shape& c) { return c.cus == 256; }, 17},
+    {16, [](const Fp8Shape& c) { return c.cus == 256; }, 17},
+};
+
+// The kernel for a shape on a device with `cus` CUs (0 = generic): the pinned variant walked down its
+// fallbacks, or the first matching row of kFp8Rules.
+static int plan_fp8(int M, int N, int K, int cus, int pinned) {
+  const Fp8Shape c = fp8_shape(M, N, K, cus);
+  if (!c.tiles) return 0;
+  if (pinned == 0) {
+    for (const auto& r : kFp8Rules)
+      if (r.match(c)) return r.variant;
+    return 0;
   }
-  if ((v == 20 || v == 21 || v == 22 || v == 23) && !ap_ok) v = sq ? 16 : 15;
-  if ((v == 21 || v == 22) && !sq) v = v == 22 ? 23 : 20;
-  if (v == 16 && !sq) v = 15;
-  if ((v == 10 || v == 18) && pgrid < NXCD) v = 15;
-  if ((v == 15 || v == 16) && cus != 256) v = 17;   // serpentine K assumes 32 co-resident tiles per XCD
+  int v = pinned;
+  for (bool moved = true; moved;) {
+    moved = false;
+    for (const auto& n : kFp8Needs)
+      if (n.variant == v && !n.ok(c)) {
+        v = n.fallback < 0 ? (c.sq ? 16 : 15) : n.fallback;
+        moved = true;
+        break;
+      }
+  }
   return v;
+}
+
+static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
+  return plan_fp8(M, N, K, device_cu_count(s), g_fp8_variant);
 }
 
 extern "C" {
@@ -89,6 +152,13 @@ int amdgo_gemm_fp8_set_variant(int v) {
 }
 int amdgo_gemm_fp8_get_variant() { return g_fp8_variant; }
 int amdgo_gemm_fp8_resolve_variant(int M, int N, int K) { return resolve_fp8_variant(M, N, K, nullptr); }
+int amdgo_gemm_plan_fp8(int M, int N, int K, int cus, int pinned) { return plan_fp8(M, N, K, cus, pinned); }
+const char* amdgo_gemm_plan_fp8_evidence(int M, int N, int K, int cus) {
+  const Fp8Shape c = fp8_shape(M, N, K, cus);
+  for (const auto& r : kFp8Rules)
+    if (r.match(c)) return r.evidence;
+  return "";
+}
 
 // Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
 int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {

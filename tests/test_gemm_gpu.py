@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -153,7 +153,7 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
@@ -167,7 +167,8 @@ def test_production_variant_set_is_closed(cuda_device):
                                         (12288, 12288, 8192, 51), (16384, 16384, 16384, 51),
                                         (4096, 4096, 16384, 56), (4096, 8192, 8192, 50), (4096, 4096, 32768, 52),
                                         (4096, 4096, 4096, 56),
-                                        (8192, 8192, 128, 25), (256, 256, 64, 0), (300, 256, 256, 0)])
+                                        (8192, 8192, 128, 25), (256, 256, 64, 60), (300, 256, 256, 0),
+                                        (1024, 1024, 1024, 60), (2048, 2048, 2048, 60), (1152, 1152, 1024, 60)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""
     import torch
@@ -243,3 +244,60 @@ def test_asm_square_raster_is_bitwise_v45(cuda_device, m, n, k):
     assert torch.equal(c45, c54)
     assert torch.equal(c45, c56)
     assert torch.equal(c50, c52)      # same pipeline, different instruction placement
+
+
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (1024, 1024, 1024), (1152, 1280, 576), (2048, 2048, 2048),
+                                   (384, 640, 4160), (1024, 1024, 8192)])
+def test_small_grid_kernel_v60_matches_fp32_reference(cuda_device, m, n, k):
+    """v60 (128x128 tiles, gemm_small.h) on shapes only it or the generic kernel can run, and on the
+    small grids the automatic dispatch now sends it; A = I checks its C mapping exactly."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    old = G.get_variant()
+    G.set_variant(60)
+    try:
+        assert G.resolve_variant(m, n, k) == 60
+        g = torch.Generator(device=cuda_device).manual_seed(m * 3 + n + k)
+        a = (torch.rand((m, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand((n, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        c = G.gemm_bf16(a, bt)
+        torch.testing.assert_close(c.float(), _ref(a, bt), atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+        eye = torch.eye(m, k, device=cuda_device, dtype=torch.bfloat16)      # C = Bt^T rows (exact)
+        idx = torch.arange(k, device=cuda_device)
+        bt2 = ((torch.arange(n, device=cuda_device)[:, None] * 5 + idx[None, :] * 3) % 41 - 20).to(torch.bfloat16)
+        assert torch.equal(G.gemm_bf16(eye, bt2), (eye.float() @ bt2.float().t()).to(torch.bfloat16))
+    finally:
+        G.set_variant(old)
+    assert G.resolve_variant(1024, 1024, 1024) == 60          # the automatic choice for a 16-tile grid
+
+
+@pytest.mark.parametrize("m,n,k,target", [(1024, 1024, 1024, 1), (1024, 1024, 8192, 1), (128, 128, 4096, 1),
+                                          (2048, 2048, 2048, 2), (1152, 1280, 4160, 4), (256, 384, 64, 1)])
+def test_split_k_kernel_v61_matches_fp32_reference_on_repeat(cuda_device, m, n, k, target):
+    """v61: the K splits of a tile meet at a per-tile counter; the last one adds the others' fp32
+    partials. Three launches in a row on one stream (each must find the counters reset) and a launch
+    on a second stream, all against the fp32 reference."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    old = G.get_variant()
+    G.set_variant(61)
+    G.set_split_target(target)
+    try:
+        assert G.resolve_variant(m, n, k) == 61
+        g = torch.Generator(device=cuda_device).manual_seed(m + 7 * n + k)
+        a = (torch.rand((m, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand((n, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        ref = _ref(a, bt)
+        outs = [G.gemm_bf16(a, bt) for _ in range(3)]
+        side = torch.cuda.Stream(device=cuda_device)
+        with torch.cuda.stream(side):
+            outs.append(G.gemm_bf16(a, bt))
+        torch.cuda.synchronize()
+        for c in outs:
+            torch.testing.assert_close(c.float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+        assert all(torch.equal(outs[0], c) for c in outs[1:3])     # same splits, same summation order
+    finally:
+        G.set_split_target(1)
+        G.set_variant(old)

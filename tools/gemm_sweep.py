@@ -35,7 +35,11 @@ class _Pinned:
 
     def __init__(self, G, spec: str, dtype: str):
         self.G, self.dtype = G, dtype
-        if spec.startswith("p"):
+        self.split = None
+        if spec.startswith("p") and "s" in spec[1:]:          # p61s2: v61 aiming at 2 workgroups per CU
+            v, t = spec[1:].split("s")
+            self.v, self.lab, self.split = int(v), None, int(t)
+        elif spec.startswith("p"):
             self.v, self.lab = int(spec[1:]), None
         else:
             import gemm_lab
@@ -44,6 +48,8 @@ class _Pinned:
     def select(self):
         if self.lab is None:
             (self.G.set_variant if self.dtype == "bf16" else self.G.set_fp8_variant)(self.v)
+            if self.dtype == "bf16":
+                self.G.set_split_target(self.split or 1)
 
     def __call__(self, A, Bt, C):
         if self.lab is not None:
