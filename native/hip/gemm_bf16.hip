@@ -78,6 +78,15 @@ static int persistent_grid(int nwg, int cus) {
   return (g / NXCD) * NXCD;
 }
 
+// v61 split count: enough workgroups for one per CU (g_split_target x CUs), each split at least 16
+// K-tiles deep (gemm_small.h: shorter splits cost more in the reduction than the idle CUs); 1 = none.
+static thread_local int g_split_target = 1;
+static int small_splits(int tiles, int nk, int cus) {
+  int s = (g_split_target * cus) / (tiles > 0 ? tiles : 1);
+  if (s > nk / 16) s = nk / 16;
+  return s < 1 ? 1 : s;
+}
+
 // What the dispatch knows about a shape on a device.
 struct Bf16Shape {
   int M, N, K, cus;
@@ -110,9 +119,14 @@ struct Bf16Rule {
   const char* evidence;
 };
 static constexpr Bf16Rule kBf16Rules[] = {
-    // a 256x256 grid of at most a quarter of the CUs (or a shape only 128-tileable): 4x the workgroups
+    // a 256x256 grid of at most a quarter of the CUs (or a shape only 128-tileable): 128x128 tiles, 4x
+    // the workgroups; split-K too when the 128x128 grid is still far below the chip and K is long
+    {61, [](const Bf16Shape& c) {
+       return c.tiles128 && (!c.tiles256 || 4 * c.nwg <= c.cus) &&
+              small_splits((c.M / S_BM) * (c.N / S_BN), c.K / S_BK, c.cus) > 1; },
+     "profiles/r5_small/sweep_v62.jsonl (1024^2x8192 458 vs 207 TF/s unsplit)"},
     {60, [](const Bf16Shape& c) { return c.tiles128 && (!c.tiles256 || 4 * c.nwg <= c.cus); },
-     "profiles/r5_small/sweep_small_bf16.jsonl (1024^3 0.94x -> see README)"},
+     "profiles/r5_small/sweep_v62.jsonl (1024^3 1.36x, 1536^3 1.01x, 2048^2x1024 1.35x hipBLASLt)"},
     {0, [](const Bf16Shape& c) { return !c.tiles256; }, "generic bounds-checked kernel"},
     // K not a power of two (even K-tile count >= 4): the asm pipeline in the VP DMA form
     {54, [](const Bf16Shape& c) { return c.mi355 && !c.pow2k && c.K % (2 * BK) == 0 && c.K >= 4 * BK &&
@@ -178,14 +192,6 @@ static constexpr Bf16Need kBf16Needs[] = {
     {45, [](const Bf16Shape& c) { return c.mi355; }, 42},
 };
 
-// v61 split count: enough workgroups for one per CU (g_split_target x CUs), each split at least 4
-// K-tiles deep; 1 = no split.
-static thread_local int g_split_target = 1;
-static int small_splits(int tiles, int nk, int cus) {
-  int s = (g_split_target * cus) / (tiles > 0 ? tiles : 1);
-  if (s > nk / 4) s = nk / 4;
-  return s < 1 ? 1 : s;
-}
 
 // v61's fp32 partials and per-tile arrival counters, one set per (device, stream): two GEMMs in
 // flight on different streams never share them; a launch on one stream resets its counters before it
@@ -239,7 +245,7 @@ static int plan_bf16(int M, int N, int K, int cus, int pinned) {
       }
     return v;
   }
-  if (v != 60 && v != 61 && !c.tiles256) return 0;
+  if (v < 60 && !c.tiles256) return 0;
   for (bool moved = true; moved && v;) {
     moved = false;
     for (const auto& n : kBf16Needs)
@@ -300,20 +306,19 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   auto persistent = [&](int n) { return persistent_grid(n, cus); };
   switch (resolve_variant(M, N, K, s)) {
     case 60:
-      hipLaunchKernelGGL(gemm_bf16_128x128_t<false>, dim3((M / S_BM) * (N / S_BN)), dim3(S_THREADS), 0, s, a, b, c, M, N,
-                         K, 1, nullptr, nullptr);
+      hipLaunchKernelGGL(gemm_bf16_128x128<false>, dim3((M / S_BM) * (N / S_BN)), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
+                         1, nullptr, nullptr);
       break;
     case 61: {
       const int tiles = (M / S_BM) * (N / S_BN);
       const int splits = small_splits(tiles, K / S_BK, cus);
       SplitWorkspace* w = splits > 1 ? split_workspace(s, (size_t)tiles * splits * S_BM * S_BN, tiles) : nullptr;
-      if (!w) {
-        hipLaunchKernelGGL(gemm_bf16_128x128_t<false>, dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K, 1, nullptr,
+      if (w)
+        hipLaunchKernelGGL(gemm_bf16_128x128<true>, dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K, splits,
+                           w->ws, w->cnt);
+      else
+        hipLaunchKernelGGL(gemm_bf16_128x128<false>, dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K, 1, nullptr,
                            nullptr);
-        break;
-      }
-      hipLaunchKernelGGL(gemm_bf16_128x128_t<true>, dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
-                         splits, w->ws, w->cnt);
       break;
     }
     case 18:

@@ -7,20 +7,18 @@
 // bound by the per-CU MFMA time of a few CUs, not by the chip. This kernel cuts the work 4x finer:
 //
 //   * 128x128 output tile per 256-thread workgroup, 4 waves as 2x2, each wave a 64x64 sub-tile =
-//     4x4 v_mfma_f32_16x16x32_bf16 accumulators (64 VGPRs); launch_bounds(256, 2): two workgroups
-//     share a CU when the grid is larger than the chip;
-//   * K-step 64: one K-tile of A and of B is 16 KiB each, double-buffered in 64 KiB of LDS;
-//   * the next K-tile's global loads (16 B per lane, 4 per operand per thread) are issued before the
-//     current K-tile's 32 MFMAs per wave and written to the other LDS buffer after them: one barrier
-//     per K-tile, the HBM/L2 latency under the matrix work;
-//   * LDS rows of 128 B hold 8 16-B chunks XOR-swizzled by (row & 7): the ds_write_b128 of a wave (8
-//     rows x 8 chunks) and the ds_read_b128 fragment reads (16 rows, one chunk column) spread over
-//     the banks -- 2-way at worst on the reads, the minimum for a 16-row b128 read;
+//     4x4 v_mfma_f32_16x16x32_bf16 accumulators (64 AGPRs);
+//   * K-step 64: one K-tile of A and of B is 16 KiB each, in a ring of 3 LDS buffers (below);
+//   * LDS rows of 128 B hold 8 16-B chunks XOR-swizzled by (row & 7): the ds_read_b128 fragment reads
+//     (16 rows, one chunk column) spread over the banks -- 2-way at worst, the minimum for a 16-row
+//     b128 read;
 //   * XCD-aware tile order (bijective remap): the tiles one XCD runs are contiguous row-major, so
 //     they share A row panels in that XCD's L2.
 //
 // Shapes: M % 128 == 0, N % 128 == 0, K % 64 == 0 (host checks). v60 runs the whole K per tile;
 // v61 splits K over several workgroups per tile (below).
+//
+// (launch_bounds(256, 1): the 96 KiB ring admits one workgroup per CU.)
 #pragma once
 
 #include "gemm_tile_common.h"
@@ -33,62 +31,102 @@ typedef float s_floatx4 __attribute__((ext_vector_type(4)));
 // byte offset of 16-B chunk q (0..7) of row r in a [rows][64] bf16 panel (128-B rows), swizzled
 __device__ __forceinline__ int s_swz(int r, int q) { return r * 128 + ((q ^ (r & 7)) << 4); }
 
-// SPLIT (v61): split-K for grids smaller than the chip. The grid is tiles x `splits` workgroups; item
-// (tile, s) runs K-tiles [s nk / splits, (s + 1) nk / splits). Every workgroup stores its fp32 partial
-// tile to `ws` (thread-major float4s: one coalesced KiB per wave and accumulator), releases it
-// (__threadfence, device scope) and counts itself in `cnt[tile]`; the workgroup that arrives last
-// acquires, adds the other partials to its registers, writes the bf16 tile and resets the counter for
-// the next launch (stream order). The splits of a tile are adjacent items, so the bijective XCD remap
-// keeps them on one XCD and the partials in one L2.
+// The in-launch split-K combine (cdna_hip_programming.md "Projection GEMM at M = 256" item 2): every
+// split stores its fp32 slab with plain 16-B stores, drains them, and after a workgroup barrier ONE
+// lane releases at agent scope and draws a ticket from the tile's counter; the split that draws the
+// last ticket acquires (one lane, agent scope) and sums ALL the tile's slabs in split order -- its own
+// included, re-read -- so the result does not depend on which split finished last. Returns true in the
+// reducing workgroup (acc then holds the full sum), false in the others. `flag` is LDS scratch.
+template <class Acc>
+__device__ __forceinline__ bool small_split_reduce(Acc& acc, float* __restrict__ ws, int* __restrict__ cnt, int item,
+                                                   int tile, int splits, int tid, int* flag) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4* slab = (f4*)(ws + (size_t)item * (128 * 128));
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) slab[(i * 4 + j) * 256 + tid] = acc[i][j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ticket = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = ticket == splits - 1;
+    if (ticket == splits - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!*flag) return false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; ++s) {
+    const f4* part = (const f4*)(ws + ((size_t)tile * splits + s) * (128 * 128));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += part[(i * 4 + j) * 256 + tid];
+  }
+  if (tid == 0) cnt[tile] = 0;   // ready for the next launch on this stream
+  return true;
+}
+
+// Staging: LDS-DMA (global_load_lds_dwordx4): each wave-instruction writes 1 KiB (8 rows of 128 B)
+// straight to LDS, lane-linear, so the XOR swizzle goes on the SOURCE address (lane L of a chunk loads
+// global chunk (L & 7) ^ (L >> 3) of its row; the fragment reads use s_swz). A ring of 3 K-tile buffers
+// (96 KiB) keeps two K-tiles in flight: at K-tile t a counted vmcnt retires tile t only, a raw s_barrier
+// (no __syncthreads, whose fence would drain the DMA) publishes it, and the DMA of tile t + 2 goes into
+// the buffer every wave finished reading at t - 1. The loads' latency hides under two K-tiles of MFMA
+// work instead of one -- these grids have one workgroup per CU and no other wave to hide it. Against
+// register staging (one tile ahead, ds_write_b128 pass) the same tile measured 1024^3 +6 %, 1536^3
+// +9 %, 2048^3 +9 %, 2048^2x1024 +8 % (profiles/r5_small/sweep_v62.jsonl).
+//
+// SPLIT (v61): split-K for grids far below the chip. The grid is tiles x `splits` workgroups; item
+// (tile, s) runs K-tiles [s nk / splits, (s + 1) nk / splits), stores its fp32 partial (thread-major
+// float4s: one coalesced KiB per wave and accumulator) and the last split of the tile sums them
+// (small_split_reduce) and writes the bf16 tile. The splits of a tile are adjacent items, so the
+// bijective XCD remap keeps them on one XCD and the partials in one L2. Splits keep >= 16 K-tiles each:
+// at 4 K-tiles (1024^3 in 4 splits) the reduction costs more than the idle CUs (110 vs 167 TF/s), at 32
+// (1024^2x8192 in 4 splits) it pays 2.2x (458 vs 207 TF/s).
+typedef __attribute__((address_space(3))) void* s_lds_ptr;
+
 template <bool SPLIT>
-__global__ void __launch_bounds__(S_THREADS, 2)
-gemm_bf16_128x128_t(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C, int M,
+__global__ void __launch_bounds__(S_THREADS, 1)
+gemm_bf16_128x128(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C, int M,
                     int N, int K, int splits, float* __restrict__ ws, int* __restrict__ cnt) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * S_BM * S_BK * 2];   // [buf][A|B] 64 KiB
-  __shared__ int arrived;
+  constexpr int NBUF = 3, OPB = S_BM * S_BK * 2, TILEB = 2 * OPB;     // 16 KiB per operand, 32 KiB per K-tile
+  __shared__ __attribute__((aligned(16))) char lds[NBUF * TILEB];     // the only LDS object (trap 4a)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = N / S_BN, ntiles = (M / S_BM) * tiles_n;
   const int item = xcd_remap(blockIdx.x, ntiles * (SPLIT ? splits : 1));
   const int tile = SPLIT ? item / splits : item, split = SPLIT ? item % splits : 0;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const __bf16* Ab = A + (size_t)tm * S_BM * K;
-  const __bf16* Bb = Bt + (size_t)tn * S_BN * K;
+  const int nk_all = K / S_BK;
+  const int kt0 = SPLIT ? split * nk_all / splits : 0;
+  const int nk = SPLIT ? (split + 1) * nk_all / splits - kt0 : nk_all;
 
-  // global -> register staging: chunk c = tid + 256 i covers row c >> 3, 16-B chunk c & 7
-  // (straight-line code, no lambdas: an array a lambda captures by reference lives in scratch)
-  const int r0 = tid >> 3, q0 = tid & 7;        // chunk i: row r0 + 32 i, chunk q0
-  const __bf16* ga = Ab + (size_t)r0 * K + q0 * 8;
-  const __bf16* gb = Bb + (size_t)r0 * K + q0 * 8;
-  const size_t rstep = (size_t)32 * K;
-  int soff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) soff[i] = s_swz(r0 + 32 * i, q0);
-  uint4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
-#define S_GLOAD(kt)                                                   \
-  do {                                                                \
-    const size_t k0_ = (size_t)(kt) * S_BK;                           \
-    ra0 = *(const uint4*)(ga + k0_);                                  \
-    ra1 = *(const uint4*)(ga + rstep + k0_);                          \
-    ra2 = *(const uint4*)(ga + 2 * rstep + k0_);                      \
-    ra3 = *(const uint4*)(ga + 3 * rstep + k0_);                      \
-    rb0 = *(const uint4*)(gb + k0_);                                  \
-    rb1 = *(const uint4*)(gb + rstep + k0_);                          \
-    rb2 = *(const uint4*)(gb + 2 * rstep + k0_);                      \
-    rb3 = *(const uint4*)(gb + 3 * rstep + k0_);                      \
-  } while (0)
-#define S_LSTORE(buf)                                                 \
-  do {                                                                \
-    char* la_ = lds + (buf) * (2 * S_BM * S_BK * 2);                  \
-    char* lb_ = la_ + S_BM * S_BK * 2;                                \
-    *(uint4*)(la_ + soff[0]) = ra0;                                   \
-    *(uint4*)(la_ + soff[1]) = ra1;                                   \
-    *(uint4*)(la_ + soff[2]) = ra2;                                   \
-    *(uint4*)(la_ + soff[3]) = ra3;                                   \
-    *(uint4*)(lb_ + soff[0]) = rb0;                                   \
-    *(uint4*)(lb_ + soff[1]) = rb1;                                   \
-    *(uint4*)(lb_ + soff[2]) = rb2;                                   \
-    *(uint4*)(lb_ + soff[3]) = rb3;                                   \
+  // DMA sources: wave w issues the 8-row chunks c = w + 4 i (i = 0..3) of each operand
+  const int lr = lane >> 3, lq = (lane & 7) ^ lr;
+  const __bf16* srcA = A + ((size_t)tm * S_BM + 8 * wave + lr) * K + (size_t)kt0 * S_BK + lq * 8;
+  const __bf16* srcB = Bt + ((size_t)tn * S_BN + 8 * wave + lr) * K + (size_t)kt0 * S_BK + lq * 8;
+  const size_t chunk_step = (size_t)32 * K;        // 4 chunks of 8 rows further
+#define S_DMA(kt, buf)                                                                                         \
+  do {                                                                                                        \
+    char* base_ = lds + (buf) * TILEB + wave * 1024;                                                          \
+    const size_t ko_ = (size_t)(kt) * S_BK;                                                                   \
+    __builtin_amdgcn_global_load_lds((const void*)(srcA + ko_), (s_lds_ptr)(base_), 16, 0, 0);                \
+    __builtin_amdgcn_global_load_lds((const void*)(srcA + chunk_step + ko_), (s_lds_ptr)(base_ + 4096), 16, 0, 0); \
+    __builtin_amdgcn_global_load_lds((const void*)(srcA + 2 * chunk_step + ko_), (s_lds_ptr)(base_ + 8192), 16, 0, 0); \
+    __builtin_amdgcn_global_load_lds((const void*)(srcA + 3 * chunk_step + ko_), (s_lds_ptr)(base_ + 12288), 16, 0, 0); \
+    __builtin_amdgcn_global_load_lds((const void*)(srcB + ko_), (s_lds_ptr)(base_ + OPB), 16, 0, 0);          \
+    __builtin_amdgcn_global_load_lds((const void*)(srcB + chunk_step + ko_), (s_lds_ptr)(base_ + OPB + 4096), 16, 0, 0); \
+    __builtin_amdgcn_global_load_lds((const void*)(srcB + 2 * chunk_step + ko_), (s_lds_ptr)(base_ + OPB + 8192), 16, 0, 0); \
+    __builtin_amdgcn_global_load_lds((const void*)(srcB + 3 * chunk_step + ko_), (s_lds_ptr)(base_ + OPB + 12288), 16, 0, 0); \
   } while (0)
 
   s_floatx4 acc[4][4];
@@ -97,20 +135,20 @@ gemm_bf16_128x128_t(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = s_floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk_all = K / S_BK;
-  const int kt0 = SPLIT ? split * nk_all / splits : 0;
-  const int nk = SPLIT ? (split + 1) * nk_all / splits - kt0 : nk_all;
-  S_GLOAD(kt0);
-  S_LSTORE(0);
-  __syncthreads();
+  S_DMA(0, 0);
+  if (nk > 1) S_DMA(1, 1);
+  int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) S_GLOAD(kt0 + kt + 1);
-    const char* la = lds + buf * (2 * S_BM * S_BK * 2);
-    const char* lb = la + S_BM * S_BK * 2;
+    // retire K-tile kt (8 DMAs per thread per tile; tile kt + 1's stay in flight), then publish it
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // every wave is past K-tile kt - 1's reads: its buffer takes tile kt + 2
+    if (kt + 2 < nk) S_DMA(kt + 2, buf == 0 ? 2 : buf - 1);
+    const char* la = lds + buf * TILEB;
+    const char* lb = la + OPB;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      // lane l: row (l & 15) of its 16-row block, k = 32 kk + 8 (l >> 4) .. + 7 = chunk 4 kk + (l >> 4)
       const int q = kk * 4 + (lane >> 4);
       s_bf16x8 af[4], bf[4];
 #pragma unroll
@@ -122,34 +160,14 @@ gemm_bf16_128x128_t(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) S_LSTORE(buf ^ 1);
-    __syncthreads();
+    buf = buf == 2 ? 0 : buf + 1;
   }
+#undef S_DMA
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();     // every wave done with the ring (the split reduce reuses lds)
   if constexpr (SPLIT) {
-    if (splits > 1) {
-      s_floatx4* part = (s_floatx4*)(ws + (size_t)item * (S_BM * S_BN));
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) part[(i * 4 + j) * S_THREADS + tid] = acc[i][j];
-      __threadfence();                     // release: the partial is visible device-wide
-      __syncthreads();
-      if (tid == 0) arrived = atomicAdd(&cnt[tile], 1);
-      __syncthreads();
-      if (arrived != splits - 1) return;   // not the last of the tile's splits
-      __threadfence();                     // acquire: every other split's partial
-      for (int s2 = 0; s2 < splits; ++s2) {
-        if (s2 == split) continue;
-        const s_floatx4* other = (const s_floatx4*)(ws + ((size_t)tile * splits + s2) * (S_BM * S_BN));
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] += other[(i * 4 + j) * S_THREADS + tid];
-      }
-      if (tid == 0) cnt[tile] = 0;         // ready for the next launch on this stream
-    }
+    if (splits > 1 && !small_split_reduce(acc, ws, cnt, item, tile, splits, tid, (int*)lds)) return;
   }
-  // epilogue: D of block (i, j): column l & 15, rows 4 (l >> 4) + e
   const int row0 = tm * S_BM + wm * 64 + (lane >> 4) * 4, col0 = tn * S_BN + wn * 64 + (lane & 15);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -158,6 +176,4 @@ gemm_bf16_128x128_t(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         C[(size_t)(row0 + i * 16 + e) * N + col0 + j * 16] = (__bf16)acc[i][j][e];
-#undef S_GLOAD
-#undef S_LSTORE
 }

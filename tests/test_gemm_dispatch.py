@@ -69,10 +69,15 @@ def _r4_bf16(M, N, K, cus, g):
 
 
 def _small(M, N, K, cus):
-    """The round-5 row: 128x128 tiles when the 256x256 grid fills at most a quarter of the CUs."""
+    """The round-5 rows: 128x128 tiles when the 256x256 grid fills at most a quarter of the CUs -- v61
+    (split-K) when the 128x128 grid is still under the CU count and every split keeps >= 16 K-tiles,
+    else v60. None when neither applies."""
     tiles256 = M % BM == 0 and N % BN == 0 and K % BK == 0 and K >= 2 * BK
     tiles128 = M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and K >= 64
-    return tiles128 and (not tiles256 or 4 * (M // BM) * (N // BN) <= cus)
+    if not (tiles128 and (not tiles256 or 4 * (M // BM) * (N // BN) <= cus)):
+        return None
+    splits = max(1, min(cus // ((M // 128) * (N // 128)), (K // 64) // 16))
+    return 61 if splits > 1 else 60
 
 
 DIMS = [128, 256, 384, 512, 1024, 1536, 2048, 3072, 4096, 6144, 8192, 12288, 16384]
@@ -94,7 +99,8 @@ def test_bf16_table_reproduces_the_round4_rules(lib):
     for M, N in itertools.product(DIMS, DIMS[::2]):
         for K, cus, pin in itertools.product(KS, CUS, BF16_PINS):
             got = lib.amdgo_gemm_plan_bf16(M, N, K, cus, pin)
-            want = 60 if pin == 0 and _small(M, N, K, cus) else _r4_bf16(M, N, K, cus, pin)
+            small = _small(M, N, K, cus) if pin == 0 else None
+            want = small if small is not None else _r4_bf16(M, N, K, cus, pin)
             if got != want:
                 bad.append((M, N, K, cus, pin, got, want))
     assert not bad, bad[:20]
@@ -108,6 +114,9 @@ def test_bf16_small_grid_row_and_its_evidence(lib):
     assert lib.amdgo_gemm_plan_bf16(1024, 1024, 1024, 256, 60) == 60    # pinned
     assert lib.amdgo_gemm_plan_bf16(1000, 1024, 1024, 256, 60) == 0     # pinned, cannot run: generic
     assert lib.amdgo_gemm_plan_bf16(8192, 8192, 8192, 256, 0) == 50
+    assert lib.amdgo_gemm_plan_bf16(1024, 1024, 8192, 256, 0) == 61     # split-K: 4 splits of 32 K-tiles
+    assert lib.amdgo_gemm_small_splits(1024, 1024, 8192, 256) == 4
+    assert lib.amdgo_gemm_small_splits(1024, 1024, 1024, 256) == 1      # 16 K-tiles: no split
     ev = lib.amdgo_gemm_plan_bf16_evidence(1024, 1024, 1024, 256).decode()
     assert ev.startswith("profiles/r5_small/")
     assert lib.amdgo_gemm_plan_bf16_evidence(16384, 16384, 1024, 256).decode().startswith("profiles/r4_lean/")

@@ -168,7 +168,8 @@ def test_production_variant_set_is_closed(cuda_device):
                                         (4096, 4096, 16384, 56), (4096, 8192, 8192, 50), (4096, 4096, 32768, 52),
                                         (4096, 4096, 4096, 56),
                                         (8192, 8192, 128, 25), (256, 256, 64, 60), (300, 256, 256, 0),
-                                        (1024, 1024, 1024, 60), (2048, 2048, 2048, 60), (1152, 1152, 1024, 60)])
+                                        (1024, 1024, 1024, 60), (2048, 2048, 2048, 60), (1152, 1152, 1024, 60),
+                                        (1024, 1024, 8192, 61), (1024, 1024, 2048, 61), (1024, 1024, 512, 60)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""
     import torch
@@ -246,18 +247,19 @@ def test_asm_square_raster_is_bitwise_v45(cuda_device, m, n, k):
     assert torch.equal(c50, c52)      # same pipeline, different instruction placement
 
 
-@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (1024, 1024, 1024), (1152, 1280, 576), (2048, 2048, 2048),
-                                   (384, 640, 4160), (1024, 1024, 8192)])
-def test_small_grid_kernel_v60_matches_fp32_reference(cuda_device, m, n, k):
+@pytest.mark.parametrize("v", [60])
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (128, 128, 128), (1024, 1024, 1024), (1152, 1280, 576),
+                                   (2048, 2048, 2048), (384, 640, 4160), (1024, 1024, 8192)])
+def test_small_grid_kernel_v60_matches_fp32_reference(cuda_device, v, m, n, k):
     """v60 (128x128 tiles, gemm_small.h) on shapes only it or the generic kernel can run, and on the
     small grids the automatic dispatch now sends it; A = I checks its C mapping exactly."""
     import torch
     from gpu_operator_amd.ops import gemm as G
 
     old = G.get_variant()
-    G.set_variant(60)
+    G.set_variant(v)
     try:
-        assert G.resolve_variant(m, n, k) == 60
+        assert G.resolve_variant(m, n, k) == v
         g = torch.Generator(device=cuda_device).manual_seed(m * 3 + n + k)
         a = (torch.rand((m, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
         bt = (torch.rand((n, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
@@ -272,9 +274,10 @@ def test_small_grid_kernel_v60_matches_fp32_reference(cuda_device, m, n, k):
     assert G.resolve_variant(1024, 1024, 1024) == 60          # the automatic choice for a 16-tile grid
 
 
+@pytest.mark.parametrize("v", [61])
 @pytest.mark.parametrize("m,n,k,target", [(1024, 1024, 1024, 1), (1024, 1024, 8192, 1), (128, 128, 4096, 1),
                                           (2048, 2048, 2048, 2), (1152, 1280, 4160, 4), (256, 384, 64, 1)])
-def test_split_k_kernel_v61_matches_fp32_reference_on_repeat(cuda_device, m, n, k, target):
+def test_split_k_kernel_v61_matches_fp32_reference_on_repeat(cuda_device, v, m, n, k, target):
     """v61: the K splits of a tile meet at a per-tile counter; the last one adds the others' fp32
     partials. Three launches in a row on one stream (each must find the counters reset) and a launch
     on a second stream, all against the fp32 reference."""
@@ -282,10 +285,10 @@ def test_split_k_kernel_v61_matches_fp32_reference_on_repeat(cuda_device, m, n, 
     from gpu_operator_amd.ops import gemm as G
 
     old = G.get_variant()
-    G.set_variant(61)
+    G.set_variant(v)
     G.set_split_target(target)
     try:
-        assert G.resolve_variant(m, n, k) == 61
+        assert G.resolve_variant(m, n, k) == v
         g = torch.Generator(device=cuda_device).manual_seed(m + 7 * n + k)
         a = (torch.rand((m, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
         bt = (torch.rand((n, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
