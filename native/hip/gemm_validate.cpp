@@ -25,8 +25,9 @@
 //   3. every GPU of the set meets at the rendezvous -- a GPU that stabilised early idles there
 //      until the slowest one arrives, and its clock drops while it waits;
 //   4. the re-ramp, untimed: at least 10 dispatches and --ramp-ms of work, enqueued back to back
-//      right after the rendezvous, with no host sync between them and the timed loop (with
-//      --no-stabilise neither step 2 nor this one runs: exactly --iters dispatches are issued);
+//      right after the rendezvous, with no host sync between them and the timed loop -- on sets of
+//      2+ GPUs (a 1-GPU set waits for nobody); with --no-stabilise neither step 2 nor this one runs:
+//      exactly --iters dispatches are issued;
 //   5. the timed loop: at least --iters dispatches and at least --min-window-ms of work (sized from
 //      the stabilised per-dispatch time), between two events -- a residual ramp is a small part of
 //      a 100 ms window, not half of a 30 ms one.
@@ -333,7 +334,7 @@ static bool stabilise(const DType& dt, const Shape& s, Resources& res, const Opt
 // One GPU's probe of one (dtype, shape). `barrier` is the set's rendezvous; it is reached exactly once
 // on every path, also when setup fails early, or the other GPUs of the set would wait forever.
 static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, const std::function<void()>& barrier,
-                    Result& r) {
+                    int set_size, Result& r) {
   r.device = dev;
   r.s = s;
   struct Arrive {
@@ -390,11 +391,14 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   CHECK(hipStreamSynchronize(res.st));
   if (o.stabilise && !stabilise(dt, s, res, o, r)) return false;
   // the re-ramp and the timed window, sized from the stabilised dispatch time; without the clock
-  // protocol (--no-stabilise: a correctness probe, a profiled single dispatch) exactly --iters
-  r.ramp = o.stabilise ? 10 : 0;
+  // protocol (--no-stabilise: a correctness probe, a profiled single dispatch) exactly --iters. A
+  // one-GPU set waits for nobody at its rendezvous (tens of microseconds through the pipes): no idle,
+  // no re-ramp -- unless the test hook injects one.
+  const bool ramp = o.stabilise && (set_size > 1 || o.pre_idle_ms > 0);
+  r.ramp = ramp ? 10 : 0;
   r.iters = o.iters;
   if (o.stabilise && r.stab_ms > 0) {
-    r.ramp = std::max(r.ramp, (int)std::ceil(o.ramp_ms / r.stab_ms));
+    if (ramp) r.ramp = std::max(r.ramp, (int)std::ceil(o.ramp_ms / r.stab_ms));
     r.iters = std::max(r.iters, (int)std::ceil(o.min_window_ms / r.stab_ms));
   }
   hipEvent_t e0, e1;
@@ -639,7 +643,9 @@ static bool run_plan(const std::vector<Set>& plan, size_t ndev, double min_tflop
 //   W <set>                                                       at the set's rendezvous
 //   R <set> <launched> <ok> <oom> <tflops> <ms> <max_rel_err> <stab dispatches> <stab spread>
 //     <need bytes> <free bytes> <iters> <ramp> <error...>         the set's result
-// Launcher -> worker: "g\n" on its stdin releases the rendezvous. EOF on stdin ends the worker.
+// Launcher -> worker: "P <sets>\n" once, after the start (and smoke) lines -- the worker's part of the
+// plan, built over the workers that saw their GPU -- then "g\n" releases each rendezvous. EOF on stdin
+// ends the worker.
 struct Worker {
   int slot = 0;
   pid_t pid = -1;
@@ -785,9 +791,10 @@ static bool parse_opts(const std::string& s, Options& o) {
   return n == 8;
 }
 
-// --worker: one GPU (HIP device 0 under the HIP_VISIBLE_DEVICES the launcher set). `sets` is
-// "<id>:<dtype>:<m>x<n>x<k>;..." -- the sets of the plan this GPU takes part in, in plan order.
-static int worker_main(const std::string& sets, const Options& o, bool run_smoke) {
+// --worker: one GPU (HIP device 0 under the HIP_VISIBLE_DEVICES the launcher set). After its start
+// (and smoke) line it reads its part of the plan from stdin, "P <id>:<dtype>:<m>x<n>x<k>:<gpus>;..." --
+// the sets it takes part in, in plan order, with their sizes -- or "Q" (no part: the launcher dropped it).
+static int worker_main(const Options& o, bool run_smoke) {
   std::signal(SIGPIPE, SIG_IGN);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
@@ -807,15 +814,23 @@ static int worker_main(const std::string& sets, const Options& o, bool run_smoke
     std::printf("H %d\n", smoke_failures({0}) == 0 ? 1 : 0);
     std::fflush(stdout);
   }
+  std::string sets;
+  {
+    std::vector<char> line(1 << 16);
+    if (!std::fgets(line.data(), (int)line.size(), stdin) || line[0] != 'P') return 0;
+    sets = line.data() + 1;
+    while (!sets.empty() && (sets.back() == '\n' || sets.back() == '\r' || sets.back() == ' ')) sets.pop_back();
+    while (!sets.empty() && sets.front() == ' ') sets.erase(0, 1);
+  }
   size_t pos = 0;
   while (pos < sets.size()) {
     size_t e = sets.find(';', pos);
     const std::string item = sets.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
     pos = e == std::string::npos ? sets.size() : e + 1;
-    int id = 0;
+    int id = 0, set_size = 1;
     char dtn[32] = "";
     Shape s{};
-    if (std::sscanf(item.c_str(), "%d:%31[^:]:%dx%dx%d", &id, dtn, &s.m, &s.n, &s.k) != 5) return 2;
+    if (std::sscanf(item.c_str(), "%d:%31[^:]:%dx%dx%d:%d", &id, dtn, &s.m, &s.n, &s.k, &set_size) != 6) return 2;
     const DType* dt = dtype_by_name(dtn);
     if (!dt) return 2;
     const std::function<void()> barrier = [&] {
@@ -825,7 +840,7 @@ static int worker_main(const std::string& sets, const Options& o, bool run_smoke
       if (!std::fgets(go, sizeof go, stdin)) std::_Exit(4);   // the launcher is gone
     };
     Result r;
-    run_one(*dt, 0, s, o, barrier, r);
+    run_one(*dt, 0, s, o, barrier, set_size, r);
     std::string err = r.error;
     for (char& c : err)
       if (c == '\n' || c == '\r') c = ' ';
@@ -850,53 +865,59 @@ static bool parse_result_line(const std::string& ln, int& id, Result& r) {
 
 static constexpr double kWorkerReplyS = 600.0;   // one set's worst case is seconds; a GPU hang is not
 
-// The launcher: one worker per selected GPU, the plan driven through their pipes.
-static int launch_processes(const std::vector<int>& devs, const std::vector<std::string>& bdf,
+// The launcher: one worker per selected GPU, the plan driven through their pipes. `all`: the
+// device list is every agent sysfs showed (no --devices); an agent whose worker then sees no GPU
+// (a container whose device cgroup hides it from the runtime but not from sysfs) is dropped and
+// reported, not failed. With an explicit --devices it is a failure.
+static int launch_processes(const std::vector<int>& devs_in, bool all, const std::vector<std::string>& bdf,
                             const std::vector<int>& hip_index, const std::vector<const DType*>& dtypes,
                             const std::vector<Shape>& shapes, const std::vector<int>& counts, const Options& o,
                             bool run_smoke, double min_tflops, double min_tflops_fp8, double min_eff, double min_rel) {
   std::signal(SIGPIPE, SIG_IGN);
-  std::vector<std::string> sel_bdf;
-  for (int d : devs) sel_bdf.push_back(bdf[d]);
-  const std::vector<Set> plan = make_plan(dtypes, shapes, counts, devs.size(), sel_bdf);
-  std::vector<Worker> ws(devs.size());
-  for (size_t i = 0; i < devs.size(); ++i) {
-    ws[i].slot = devs[i];
-    std::string sets;
-    for (const Set& st : plan)
-      if (std::find(st.slots.begin(), st.slots.end(), (int)i) != st.slots.end()) {
-        char buf[96];
-        std::snprintf(buf, sizeof buf, "%s%d:%s:%dx%dx%d", sets.empty() ? "" : ";", st.id, st.dt->name, st.s.m, st.s.n,
-                      st.s.k);
-        sets += buf;
-      }
-    std::vector<std::string> args = {"amd-gemm-validate", "--worker", sets, "--worker-opts", fmt_opts(o)};
+  std::vector<Worker> spawned(devs_in.size());
+  for (size_t i = 0; i < devs_in.size(); ++i) {
+    spawned[i].slot = devs_in[i];
+    std::vector<std::string> args = {"amd-gemm-validate", "--worker", "--worker-opts", fmt_opts(o)};
     if (run_smoke) args.push_back("--smoke");
-    if (!spawn_worker(ws[i], hip_index[devs[i]], args)) ws[i].why = "worker for GPU " + std::to_string(devs[i]) + ": " + ws[i].why;
+    if (!spawn_worker(spawned[i], hip_index[devs_in[i]], args))
+      spawned[i].why = "worker for GPU " + std::to_string(devs_in[i]) + ": " + spawned[i].why;
   }
   // start lines: the runtime's view of each worker's GPU, checked against the sysfs agent
-  std::string arch = "unknown";
+  std::string arch = "unknown", dropped;
   int cus = 0;
   size_t lds = 0;
-  for (auto& w : ws) {
+  std::vector<Worker> ws;
+  for (auto& w : spawned) {
     std::string ln;
-    if (!w.line(ln, 300.0)) continue;
-    int n = 0, c = 0;
-    size_t l = 0;
-    char bus[64] = "", a[96] = "";
-    if (std::sscanf(ln.c_str(), "S %d %63s %95s %d %zu", &n, bus, a, &c, &l) != 5 || n < 1) {
-      w.fail("saw no GPU (" + ln + ")");
-      continue;
+    if (w.line(ln, 300.0)) {
+      int n = 0, c = 0;
+      size_t l = 0;
+      char bus[64] = "", a[96] = "";
+      const bool parsed = std::sscanf(ln.c_str(), "S %d %63s %95s %d %zu", &n, bus, a, &c, &l) == 5;
+      if (parsed && n < 1 && all) {
+        dropped += (dropped.empty() ? "" : ",") + std::to_string(w.slot);
+        w.fail("dropped: the runtime sees no GPU there");
+        continue;
+      }
+      if (!parsed || n < 1) w.fail("saw no GPU (" + ln + ")");
+      else if (!bdf[w.slot].empty() && std::string(bus) != "-" && bdf[w.slot] != bus)
+        w.fail(std::string("opened ") + bus + ", not " + bdf[w.slot]);
+      else if (arch == "unknown") arch = a, cus = c, lds = l;
     }
-    if (!bdf[w.slot].empty() && std::string(bus) != "-" && bdf[w.slot] != bus) {
-      w.fail(std::string("opened ") + bus + ", not " + bdf[w.slot]);
-      continue;
-    }
-    if (arch == "unknown") arch = a, cus = c, lds = l;
+    ws.push_back(w);
   }
+  if (ws.empty()) {
+    std::printf("{\"error\":\"no AMD GPU visible to the runtime (sysfs agents %s)\"}\n", dropped.c_str());
+    return 3;
+  }
+  std::vector<int> devs;
+  std::vector<std::string> sel_bdf;
+  for (const auto& w : ws) devs.push_back(w.slot), sel_bdf.push_back(bdf[w.slot]);
+  const std::vector<Set> plan = make_plan(dtypes, shapes, counts, devs.size(), sel_bdf);
   std::printf("{\"event\":\"start\",\"devices\":%zu,\"visible\":%zu,\"gcn_arch\":\"%s\",\"cus\":%d,"
-              "\"lds_per_block\":%zu,\"iters\":%d,\"stabilise\":%s,\"launch\":\"processes\",\"min_window_ms\":%.0f}\n",
-              devs.size(), bdf.size(), arch.c_str(), cus, lds, o.iters, o.stabilise ? "true" : "false", o.min_window_ms);
+              "\"lds_per_block\":%zu,\"iters\":%d,\"stabilise\":%s,\"launch\":\"processes\",\"min_window_ms\":%.0f%s%s%s}\n",
+              devs.size(), bdf.size(), arch.c_str(), cus, lds, o.iters, o.stabilise ? "true" : "false", o.min_window_ms,
+              dropped.empty() ? "" : ",\"dropped\":[", dropped.c_str(), dropped.empty() ? "" : "]");
   std::fflush(stdout);
   bool all_ok = true;
   if (run_smoke) {
@@ -907,6 +928,18 @@ static int launch_processes(const std::vector<int>& devs, const std::vector<std:
     }
     print_smoke(devs.size(), failures);
     all_ok = failures == 0;
+  }
+  // each worker's part of the plan
+  for (size_t i = 0; i < ws.size(); ++i) {
+    std::string sets;
+    for (const Set& st : plan)
+      if (std::find(st.slots.begin(), st.slots.end(), (int)i) != st.slots.end()) {
+        char buf[96];
+        std::snprintf(buf, sizeof buf, "%s%d:%s:%dx%dx%d:%zu", sets.empty() ? "" : ";", st.id, st.dt->name, st.s.m,
+                      st.s.n, st.s.k, st.slots.size());
+        sets += buf;
+      }
+    ws[i].send(("P " + sets + "\n").c_str());
   }
   auto lost = [&](Result& r, const Worker& w) {
     r.launched = false;
@@ -956,7 +989,7 @@ static bool under_profiler() {
 }
 
 int main(int argc, char** argv) {
-  std::string shapes = "8192", devices = "all", dtype = "bf16", scaling, launch = "processes", worker_sets;
+  std::string shapes = "8192", devices = "all", dtype = "bf16", scaling, launch = "processes";
   std::string worker_opts;
   bool worker = false;
   Options o;
@@ -983,7 +1016,7 @@ int main(int argc, char** argv) {
     else if (a == "--pre-timed-idle-ms") o.pre_idle_ms = std::max(0.0, std::atof(next().c_str()));
     else if (a == "--launch") launch = next();
     else if (a == "--smoke") run_smoke = true;
-    else if (a == "--worker") worker = true, worker_sets = next();
+    else if (a == "--worker") worker = true;
     else if (a == "--worker-opts") worker_opts = next();
     else if (a == "-h" || a == "--help") {
       std::printf("usage: amd-gemm-validate [--shapes 8192,4096,MxNxK] [--dtype bf16|fp8|both] [--iters N] "
@@ -998,7 +1031,7 @@ int main(int argc, char** argv) {
   }
   if (worker) {
     if (!worker_opts.empty() && !parse_opts(worker_opts, o)) return 2;
-    return worker_main(worker_sets, o, run_smoke);
+    return worker_main(o, run_smoke);
   }
   if (launch != "processes" && launch != "threads") {
     std::printf("{\"error\":\"unknown --launch %s (processes or threads)\"}\n", json_safe(launch).c_str());
@@ -1049,7 +1082,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   if (launch == "processes")
-    return launch_processes(devs, bdf, hip_index, dtypes, shape_list, counts, o, run_smoke, min_tflops,
+    return launch_processes(devs, devices == "all", bdf, hip_index, dtypes, shape_list, counts, o, run_smoke, min_tflops,
                             min_tflops_fp8, min_eff, min_rel);
 
   // --launch threads: one process, one host thread per GPU
@@ -1077,7 +1110,9 @@ int main(int argc, char** argv) {
                       const std::function<void()> barrier = [&] { sync.arrive_and_wait(); };
                       std::vector<std::thread> th;
                       for (size_t i = 0; i < set.slots.size(); ++i)
-                        th.emplace_back([&, i] { run_one(*set.dt, devs[set.slots[i]], set.s, o, barrier, res[i]); });
+                        th.emplace_back([&, i] {
+                          run_one(*set.dt, devs[set.slots[i]], set.s, o, barrier, (int)set.slots.size(), res[i]);
+                        });
                       for (auto& t : th) t.join();
                     }) && all_ok;
   // the last line: every result is out and every device synchronised. The validator reads up to

@@ -240,7 +240,9 @@ def test_idle_before_the_timed_loop_does_not_droop_the_number():
     idle, _ = _tflops("--pre-timed-idle-ms", "200")
     print(f"no idle {base['tflops']} TF/s, 200 ms idle {idle['tflops']} TF/s; ramp {idle['ramp_dispatches']}, "
           f"iters {idle['iters']}")
-    assert base["iters"] * base["ms"] >= 99.0 and base["ramp_dispatches"] >= 10
+    assert base["iters"] * base["ms"] >= 99.0
+    # a 1-GPU set waits for nobody at its rendezvous: no re-ramp; the injected idle gets one
+    assert base["ramp_dispatches"] == 0 and idle["ramp_dispatches"] >= 10
     assert abs(idle["tflops"] - base["tflops"]) <= 0.02 * base["tflops"], (base, idle)
 
 
