@@ -79,7 +79,7 @@ def gemm_fp8(a, bt, out=None, *, generic: bool = False):
 # Production variant sets (native/hip/gemm_bf16.hip, gemm_fp8.hip): 0 = automatic dispatch, any
 # other member pins that kernel. Everything else lives in the tools-only lab library.
 BF16_VARIANTS = (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61)
-FP8_VARIANTS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23)
+FP8_VARIANTS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61)
 
 
 def set_variant(v: int) -> None:
@@ -99,7 +99,7 @@ def set_split_target(t: int) -> None:
 
 
 def small_splits(m: int, n: int, k: int, cus: int = 256) -> int:
-    """The K splits v61 uses for this shape on a device with ``cus`` CUs."""
+    """The K pieces per tile v61 uses for this bf16 shape on a device with ``cus`` CUs (1: none)."""
     return _lib.load().amdgo_gemm_small_splits(int(m), int(n), int(k), int(cus))
 
 

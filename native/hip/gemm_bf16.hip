@@ -51,7 +51,7 @@
 #include <mutex>
 
 #include "gemm_bf16_kernels.h"
-#include "gemm_small.h"
+#include "gemm_small_host.h"
 
 // K-tile schedules of the persistent asm pipeline (gemm_bf16_asm_loop.h, tools/gen_bf16_asm_loop.py):
 // g4 waits for the last R1 fragment read 4 MFMAs after it is issued (not 1), which takes the
@@ -76,15 +76,6 @@ static thread_local int g_variant = 0;
 static int persistent_grid(int nwg, int cus) {
   const int g = nwg < cus ? nwg : cus;
   return (g / NXCD) * NXCD;
-}
-
-// v61 split count: enough workgroups for one per CU (g_split_target x CUs), each split at least 16
-// K-tiles deep (gemm_small.h: shorter splits cost more in the reduction than the idle CUs); 1 = none.
-static thread_local int g_split_target = 1;
-static int small_splits(int tiles, int nk, int cus) {
-  int s = (g_split_target * cus) / (tiles > 0 ? tiles : 1);
-  if (s > nk / 16) s = nk / 16;
-  return s < 1 ? 1 : s;
 }
 
 // What the dispatch knows about a shape on a device.
@@ -170,6 +161,7 @@ struct Bf16Need {
 static constexpr Bf16Need kBf16Needs[] = {
     {60, [](const Bf16Shape& c) { return c.tiles128; }, 0},
     {61, [](const Bf16Shape& c) { return c.tiles128; }, 0},
+
     {45, [](const Bf16Shape& c) { return c.sq; }, 44},
     {48, [](const Bf16Shape& c) { return c.sq; }, 47},
     {47, [](const Bf16Shape& c) { return c.mi355; }, 42},
@@ -192,45 +184,6 @@ static constexpr Bf16Need kBf16Needs[] = {
     {45, [](const Bf16Shape& c) { return c.mi355; }, 42},
 };
 
-
-// v61's fp32 partials and per-tile arrival counters, one set per (device, stream): two GEMMs in
-// flight on different streams never share them; a launch on one stream resets its counters before it
-// ends, so the next launch there finds them zero. Allocated on first use, never shrunk.
-struct SplitWorkspace {
-  float* ws = nullptr;
-  int* cnt = nullptr;
-  size_t floats = 0;
-  int counters = 0;
-};
-static std::mutex g_split_mu;
-static std::map<std::pair<int, hipStream_t>, SplitWorkspace> g_split_ws;
-
-static SplitWorkspace* split_workspace(hipStream_t s, size_t floats, int tiles) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(g_split_mu);
-  SplitWorkspace& w = g_split_ws[{dev, s}];
-  if (w.floats < floats) {
-    // a larger partial buffer: the old one may still be read by a launch in flight on this stream
-    if (w.ws && hipStreamSynchronize(s) != hipSuccess) return nullptr;
-    if (w.ws) (void)hipFree(w.ws);
-    w.ws = nullptr;
-    w.floats = 0;
-    if (hipMalloc(&w.ws, floats * sizeof(float)) != hipSuccess) return nullptr;
-    w.floats = floats;
-  }
-  if (w.counters < tiles) {
-    if (w.cnt && hipStreamSynchronize(s) != hipSuccess) return nullptr;
-    if (w.cnt) (void)hipFree(w.cnt);
-    w.cnt = nullptr;
-    w.counters = 0;
-    const int n = tiles < 1024 ? 1024 : tiles;
-    if (hipMalloc(&w.cnt, n * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(w.cnt, 0, n * sizeof(int), s) != hipSuccess) return nullptr;
-    w.counters = n;
-  }
-  return &w;
-}
 
 // The kernel for a shape on a device with `cus` CUs: the pinned variant (walked down its fallbacks
 // until it can run), or the first matching row of kBf16Rules. 0 = the generic kernel.
@@ -276,7 +229,7 @@ int amdgo_gemm_get_variant() { return g_variant; }
 // v61: split-K workgroups per CU to aim for (1 = one wave of the chip); per host thread like the pin.
 int amdgo_gemm_set_split_target(int t) {
   if (t < 1 || t > 8) return (int)hipErrorInvalidValue;
-  g_split_target = t;
+  small_split_target() = t;
   return 0;
 }
 int amdgo_gemm_small_splits(int M, int N, int K, int cus) {
@@ -303,24 +256,13 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   auto* c = (__bf16*)C;
   const int nwg = (M / BM) * (N / BN);
   const int cus = device_cu_count(s);
-  auto persistent = [&](int n) { return persistent_grid(n, cus); };
-  switch (resolve_variant(M, N, K, s)) {
+  auto persistent = [&](int n) { return persistent_launch_grid(n, cus); };
+  const int variant_now = resolve_variant(M, N, K, s);
+  switch (variant_now) {
     case 60:
-      hipLaunchKernelGGL(gemm_bf16_128x128<false>, dim3((M / S_BM) * (N / S_BN)), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
-                         1, nullptr, nullptr);
+    case 61:
+      launch_small<false>(a, b, c, M, N, K, s, cus, variant_now == 61);
       break;
-    case 61: {
-      const int tiles = (M / S_BM) * (N / S_BN);
-      const int splits = small_splits(tiles, K / S_BK, cus);
-      SplitWorkspace* w = splits > 1 ? split_workspace(s, (size_t)tiles * splits * S_BM * S_BN, tiles) : nullptr;
-      if (w)
-        hipLaunchKernelGGL(gemm_bf16_128x128<true>, dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K, splits,
-                           w->ws, w->cnt);
-      else
-        hipLaunchKernelGGL(gemm_bf16_128x128<false>, dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K, 1, nullptr,
-                           nullptr);
-      break;
-    }
     case 18:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
                          a, b, c, M, N, K);

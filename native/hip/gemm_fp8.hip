@@ -28,13 +28,17 @@
 //       16384^2x1024 1.19x hipBLASLt (v21 1.13x), 12288^3 1.02x (v21 1.00x), 8192^2x2048 1.10x (1.08x),
 //       16384^3 1.035x (1.031x), 8192^3 1.035x (1.023x); profiles/r4_lean/. One dispatch wave: v22 (v23 off the
 //       16x16-tile multiples).
-//   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 = that kernel pinned (no automatic switch; falls back when the
+//   60 / 61 (round 5): the 128x128 small-grid kernel of the bf16 v60 / v61 (gemm_small.h) on the
+//       double-rate v_mfma_f32_16x16x128_f8f6f4, whole-tile or split-K, for grids the 256x256 tiling
+//       leaves mostly idle (and shapes only 128-tileable).
+//   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 / 60 / 61 = that kernel pinned (no automatic switch; falls back when the
 //       shape or the device cannot run it).
 // q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
 // (profiles/r2_fp8_q16/): 8192^3 +5.3 %, 16384^3 +3.1 %, 4096^3 +4.1 %, 16384x8192x8192 +2.2 %.
 // Fast path: M % 256 == 0, N % 256 == 0, K % 128 == 0, K >= 256; otherwise the generic kernel.
 
 #include "gemm_fp8_kernels.h"
+#include "gemm_small_host.h"
 
 // The variant a caller pinned (amdgo_gemm_fp8_set_variant): per host thread (see gemm_bf16.hip).
 static thread_local int g_fp8_variant = 0;
@@ -47,6 +51,7 @@ static thread_local int g_fp8_variant = 0;
 struct Fp8Shape {
   int M, N, K, cus;
   bool tiles;      // M, N multiples of 256, K of 128, K >= 256: the 256x256 kernels can run it
+  bool tiles128;   // M, N multiples of 128, K of 128: the 128x128 kernels (v60 / v61, gemm_small.h)
   int nwg, pgrid;  // 256x256 output tiles; the persistent grid (one WG per CU, whole XCD groups)
   bool sq;         // 16x16-tile multiples (the square cross-XCD raster)
   bool wide;       // >= 32 tiles on both sides
@@ -56,6 +61,7 @@ struct Fp8Shape {
 static Fp8Shape fp8_shape(int M, int N, int K, int cus) {
   Fp8Shape c{M, N, K, cus};
   c.tiles = M % F8_BM == 0 && N % F8_BN == 0 && K % F8_BK == 0 && K >= 2 * F8_BK;
+  c.tiles128 = M % S_BM == 0 && N % S_BN == 0 && K % 128 == 0 && K >= 128;
   c.nwg = (M / F8_BM) * (N / F8_BN);
   c.pgrid = ((c.nwg < cus ? c.nwg : cus) / NXCD) * NXCD;
   c.sq = (M / F8_BM) % 16 == 0 && (N / F8_BN) % 16 == 0;
@@ -71,6 +77,14 @@ struct Fp8Rule {
   const char* evidence;
 };
 static constexpr Fp8Rule kFp8Rules[] = {
+    // a 256x256 grid of at most a quarter of the CUs (or a shape only 128-tileable): the 128x128
+    // kernel, split-K when the 128x128 grid is under the CU count (the bf16 rows' rule, same kernel frame)
+    {61, [](const Fp8Shape& c) {
+       return c.tiles128 && (!c.tiles || 4 * c.nwg <= c.cus) &&
+              small_splits((c.M / S_BM) * (c.N / S_BN), c.K / 128, c.cus) > 1; },
+     "profiles/r5_small/ (fp8 128x128 split-K)"},
+    {60, [](const Fp8Shape& c) { return c.tiles128 && (!c.tiles || 4 * c.nwg <= c.cus); },
+     "profiles/r5_small/ (fp8 128x128)"},
     {0, [](const Fp8Shape& c) { return !c.tiles; }, "generic bounds-checked kernel"},
     // one dispatch wave: v22 (v23 off the 16x16-tile multiples)
     {22, [](const Fp8Shape& c) { return c.ap && c.nwg <= c.cus && c.sq; },
@@ -100,6 +114,8 @@ struct Fp8Need {
   int fallback;   // -1: 16 on the square raster, else 15
 };
 static constexpr Fp8Need kFp8Needs[] = {
+    {60, [](const Fp8Shape& c) { return c.tiles128; }, 0},
+    {61, [](const Fp8Shape& c) { return c.tiles128; }, 0},
     {20, [](const Fp8Shape& c) { return c.ap; }, -1},
     {21, [](const Fp8Shape& c) { return c.ap; }, -1},
     {22, [](const Fp8Shape& c) { return c.ap; }, -1},
@@ -118,12 +134,13 @@ static constexpr Fp8Need kFp8Needs[] = {
 // fallbacks, or the first matching row of kFp8Rules.
 static int plan_fp8(int M, int N, int K, int cus, int pinned) {
   const Fp8Shape c = fp8_shape(M, N, K, cus);
-  if (!c.tiles) return 0;
+  if (!c.tiles && !c.tiles128) return 0;
   if (pinned == 0) {
     for (const auto& r : kFp8Rules)
       if (r.match(c)) return r.variant;
     return 0;
   }
+  if (!c.tiles && pinned != 60 && pinned != 61) return 0;
   int v = pinned;
   for (bool moved = true; moved;) {
     moved = false;
@@ -145,7 +162,8 @@ extern "C" {
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
-  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21 && v != 22 && v != 23)
+  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21 && v != 22 && v != 23 &&
+      v != 60 && v != 61)
     return (int)hipErrorInvalidValue;
   g_fp8_variant = v;
   return 0;
@@ -169,8 +187,13 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
   auto* c = (__bf16*)C;
   const int nwg = (M / F8_BM) * (N / F8_BN);
   const int cus = device_cu_count(s);
-  const int pgrid = ((nwg < cus ? nwg : cus) / NXCD) * NXCD;
-  switch (resolve_fp8_variant(M, N, K, s)) {
+  const int pgrid = persistent_launch_grid(nwg, cus);
+  const int variant_now = resolve_fp8_variant(M, N, K, s);
+  switch (variant_now) {
+    case 60:
+    case 61:
+      launch_small<true>(a, b, c, M, N, K, s, cus, variant_now == 61);
+      break;
     case 10:
       hipLaunchKernelGGL((gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>), dim3(pgrid), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);

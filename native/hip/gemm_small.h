@@ -1,179 +1,258 @@
-// gfx950 bf16 GEMM for small output grids (v60):
+// gfx950 bf16 / fp8 GEMM for small output grids (v60, v61):
 //
-//   C[M,N] (bf16) = A[M,K] (bf16, K-major) * Bt[N,K]^T (bf16, K-major), fp32 accumulation.
+//   C[M,N] (bf16) = A[M,K] * Bt[N,K]^T, A and Bt K-major, both bf16 or both fp8 e4m3fn, fp32 accumulation.
+//
+// A K-tile is 128 bytes of every row -- 64 bf16 or 128 fp8 elements -- so the LDS image, the DMA and the
+// fragment reads are the same bytes for both dtypes: a lane reads 16-byte chunks g and g + 4 of a row
+// (g = lane >> 4). bf16 runs them as two k-steps of v_mfma_f32_16x16x32_bf16; fp8 feeds both chunks to
+// one v_mfma_f32_16x16x128_f8f6f4 (the unscaled double-rate form; any lane -> k map gives the same sums
+// when A and B share it, as in gemm_fp8_kernels.h F8Q_CHUNK). The accumulator layout is the same.
 //
 // The 256x256 kernels own one output tile per CU: on a grid of 16 such tiles (1024^3) 16 of the 256
 // CUs work and each runs a 134 MFLOP tile alone (~14 us at one CU's matrix rate), so the dispatch is
 // bound by the per-CU MFMA time of a few CUs, not by the chip. This kernel cuts the work 4x finer:
 //
-//   * 128x128 output tile per 256-thread workgroup, 4 waves as 2x2, each wave a 64x64 sub-tile =
-//     4x4 v_mfma_f32_16x16x32_bf16 accumulators (64 AGPRs);
-//   * K-step 64: one K-tile of A and of B is 16 KiB each, in a ring of 3 LDS buffers (below);
+//   * 128x128 output tile per workgroup; WAVES = 4: 2x2 waves of 64x64 (4x4 v_mfma_f32_16x16x32_bf16
+//     accumulators, 64 AGPRs); WAVES = 8: 2x4 waves of 64x32 (4x2 accumulators), two waves per SIMD;
+//   * K-step 64: one K-tile of A and of B is 16 KiB each, in a ring of 4 LDS buffers (below);
 //   * LDS rows of 128 B hold 8 16-B chunks XOR-swizzled by (row & 7): the ds_read_b128 fragment reads
 //     (16 rows, one chunk column) spread over the banks -- 2-way at worst, the minimum for a 16-row
 //     b128 read;
 //   * XCD-aware tile order (bijective remap): the tiles one XCD runs are contiguous row-major, so
 //     they share A row panels in that XCD's L2.
 //
-// Shapes: M % 128 == 0, N % 128 == 0, K % 64 == 0 (host checks). v60 runs the whole K per tile;
+// Shapes: M % 128 == 0, N % 128 == 0, K a multiple of one K-tile (host checks). v60 runs the whole K per tile;
 // v61 splits K over several workgroups per tile (below).
 //
-// (launch_bounds(256, 1): the 96 KiB ring admits one workgroup per CU.)
+// (the 128 KiB ring admits one workgroup per CU.)
 #pragma once
 
 #include "gemm_tile_common.h"
 
-constexpr int S_BM = 128, S_BN = 128, S_BK = 64, S_THREADS = 256;
+constexpr int S_BM = 128, S_BN = 128, S_BK = 64, S_WAVES = 8, S_THREADS = S_WAVES * 64, S_NBUF = 4;
 
 typedef __bf16 s_bf16x8 __attribute__((ext_vector_type(8)));
+typedef int s_i32x4 __attribute__((ext_vector_type(4)));
+typedef int s_i32x8 __attribute__((ext_vector_type(8)));
 typedef float s_floatx4 __attribute__((ext_vector_type(4)));
 
-// byte offset of 16-B chunk q (0..7) of row r in a [rows][64] bf16 panel (128-B rows), swizzled
+// byte offset of 16-B chunk q (0..7) of row r in a panel of 128-B rows, swizzled
 __device__ __forceinline__ int s_swz(int r, int q) { return r * 128 + ((q ^ (r & 7)) << 4); }
 
-// The in-launch split-K combine (cdna_hip_programming.md "Projection GEMM at M = 256" item 2): every
-// split stores its fp32 slab with plain 16-B stores, drains them, and after a workgroup barrier ONE
-// lane releases at agent scope and draws a ticket from the tile's counter; the split that draws the
-// last ticket acquires (one lane, agent scope) and sums ALL the tile's slabs in split order -- its own
-// included, re-read -- so the result does not depend on which split finished last. Returns true in the
-// reducing workgroup (acc then holds the full sum), false in the others. `flag` is LDS scratch.
-template <class Acc>
-__device__ __forceinline__ bool small_split_reduce(Acc& acc, float* __restrict__ ws, int* __restrict__ cnt, int item,
-                                                   int tile, int splits, int tid, int* flag) {
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  f4* slab = (f4*)(ws + (size_t)item * (128 * 128));
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) slab[(i * 4 + j) * 256 + tid] = acc[i][j];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int ticket = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = ticket == splits - 1;
-    if (ticket == splits - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!*flag) return false;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < splits; ++s) {
-    const f4* part = (const f4*)(ws + ((size_t)tile * splits + s) * (128 * 128));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] += part[(i * 4 + j) * 256 + tid];
-  }
-  if (tid == 0) cnt[tile] = 0;   // ready for the next launch on this stream
-  return true;
-}
-
-// Staging: LDS-DMA (global_load_lds_dwordx4): each wave-instruction writes 1 KiB (8 rows of 128 B)
+// Staging: LDS-DMA (buffer_load_dwordx4 ... lds): each wave-instruction writes 1 KiB (8 rows of 128 B)
 // straight to LDS, lane-linear, so the XOR swizzle goes on the SOURCE address (lane L of a chunk loads
-// global chunk (L & 7) ^ (L >> 3) of its row; the fragment reads use s_swz). A ring of 3 K-tile buffers
-// (96 KiB) keeps two K-tiles in flight: at K-tile t a counted vmcnt retires tile t only, a raw s_barrier
-// (no __syncthreads, whose fence would drain the DMA) publishes it, and the DMA of tile t + 2 goes into
-// the buffer every wave finished reading at t - 1. The loads' latency hides under two K-tiles of MFMA
-// work instead of one -- these grids have one workgroup per CU and no other wave to hide it. Against
-// register staging (one tile ahead, ds_write_b128 pass) the same tile measured 1024^3 +6 %, 1536^3
-// +9 %, 2048^3 +9 %, 2048^2x1024 +8 % (profiles/r5_small/sweep_v62.jsonl).
+// global chunk (L & 7) ^ (L >> 3) of its row; the fragment reads use s_swz). One buffer descriptor per
+// operand panel; the lane's byte offset is one VGPR for the whole K loop and the K-tile / chunk offsets
+// are SGPRs, so a DMA costs no address VALU -- every VALU op sits in the MFMA issue stream: buffer
+// loads against global_load_lds with 64-bit lane addresses measured +10-12 % on every shape
+// (2048^2x8192 838 -> 937 TF/s, 9.6e6 -> 7.4e6 VALU instructions; profiles/r5_small/).
+// A ring of 4 K-tile buffers (128 KiB) keeps three K-tiles in flight: at K-tile t a counted vmcnt
+// retires tile t only, a raw s_barrier (no __syncthreads, whose fence would drain the DMA) publishes it,
+// and the DMA of tile t + 3 goes into the buffer every wave finished reading at t - 1.
 //
-// SPLIT (v61): split-K for grids far below the chip. The grid is tiles x `splits` workgroups; item
-// (tile, s) runs K-tiles [s nk / splits, (s + 1) nk / splits), stores its fp32 partial (thread-major
-// float4s: one coalesced KiB per wave and accumulator) and the last split of the tile sums them
-// (small_split_reduce) and writes the bf16 tile. The splits of a tile are adjacent items, so the
-// bijective XCD remap keeps them on one XCD and the partials in one L2. Splits keep >= 16 K-tiles each:
-// at 4 K-tiles (1024^3 in 4 splits) the reduction costs more than the idle CUs (110 vs 167 TF/s), at 32
-// (1024^2x8192 in 4 splits) it pays 2.2x (458 vs 207 TF/s).
+// Waves: 8 (two per SIMD, 2x4 of 64x32) against 4 (one per SIMD, 2x2 of 64x64): +4-10 % on every
+// shape (2048^3 802 -> 834, 1536^3 450 -> 490 TF/s) -- a SIMD's second wave issues MFMAs while the
+// first waits on its fragment reads or at the barrier.
+//
+// Fragments: a K-tile's A reads and its first k-step's B reads go out at once, then the first k-step's
+// MFMAs (each waits only for its own operands: counted lgkmcnt), then the second k-step's B reads and
+// MFMAs (+2-5 % over one k-step at a time). The kernel arguments are read into SGPRs before the loop:
+// a scalar load still pending at the loop header turns every counted fragment wait into lgkmcnt(0).
 typedef __attribute__((address_space(3))) void* s_lds_ptr;
 
-template <bool SPLIT>
-__global__ void __launch_bounds__(S_THREADS, 1)
-gemm_bf16_128x128(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C, int M,
-                    int N, int K, int splits, float* __restrict__ ws, int* __restrict__ cnt) {
-  constexpr int NBUF = 3, OPB = S_BM * S_BK * 2, TILEB = 2 * OPB;     // 16 KiB per operand, 32 KiB per K-tile
-  __shared__ __attribute__((aligned(16))) char lds[NBUF * TILEB];     // the only LDS object (trap 4a)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_n = N / S_BN, ntiles = (M / S_BM) * tiles_n;
-  const int item = xcd_remap(blockIdx.x, ntiles * (SPLIT ? splits : 1));
-  const int tile = SPLIT ? item / splits : item, split = SPLIT ? item % splits : 0;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int nk_all = K / S_BK;
-  const int kt0 = SPLIT ? split * nk_all / splits : 0;
-  const int nk = SPLIT ? (split + 1) * nk_all / splits - kt0 : nk_all;
+constexpr int S_OPB = S_BM * S_BK * 2, S_TILEB = 2 * S_OPB;   // 16 KiB per operand, 32 KiB per K-tile
+constexpr int S_LDS = S_NBUF * S_TILEB + 16;                  // the ring + the split reduction's flag
+constexpr int S_WN = S_WAVES / 2, S_TN = S_BN / S_WN, S_NJ = S_TN / 16;   // wave grid 2 x S_WN, 64 x S_TN each
+constexpr int S_NACC = 4 * S_NJ;                              // 16x16 accumulators per thread
+static_assert(S_WAVES == 4 || S_WAVES == 8, "2x2 waves of 64x64 or 2x4 waves of 64x32");
+typedef s_floatx4 SmallAcc[4][S_NJ];
 
-  // DMA sources: wave w issues the 8-row chunks c = w + 4 i (i = 0..3) of each operand
+// wait until at most `ahead` K-tiles (PT DMAs each) of this thread are in flight; ahead <= S_NBUF - 2
+template <int PT>
+__device__ __forceinline__ void s_wait_tiles(int ahead) {
+  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PT) : "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PT) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// acc = A[tile rows, K-tiles kt0 .. kt0 + nk) * Bt[...]^T for output tile (tm, tn); row_b = bytes per
+// operand row. Ends with every wave past its last fragment read (the ring is free again).
+template <bool F8>
+__device__ __forceinline__ void small_mainloop(const char* __restrict__ A, const char* __restrict__ Bt, uint32_t row_b,
+                                               int tm, int tn, int kt0, int nk, char* lds, SmallAcc& acc) {
+  constexpr int NBUF = S_NBUF, WAVES = S_WAVES, NJ = S_NJ, TN = S_TN;
+  constexpr int CPW = 16 / WAVES;            // 8-row chunks per operand a wave DMAs per K-tile
+  constexpr int PT = 2 * CPW;                // DMAs per thread per K-tile
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: LDS-DMA bases stay scalar
+  const int wm = wave / S_WN, wn = wave % S_WN;
+  // DMA pieces: wave w issues the 8-row chunks c = w + WAVES i (i < CPW) of each operand
   const int lr = lane >> 3, lq = (lane & 7) ^ lr;
-  const __bf16* srcA = A + ((size_t)tm * S_BM + 8 * wave + lr) * K + (size_t)kt0 * S_BK + lq * 8;
-  const __bf16* srcB = Bt + ((size_t)tn * S_BN + 8 * wave + lr) * K + (size_t)kt0 * S_BK + lq * 8;
-  const size_t chunk_step = (size_t)32 * K;        // 4 chunks of 8 rows further
-#define S_DMA(kt, buf)                                                                                         \
-  do {                                                                                                        \
-    char* base_ = lds + (buf) * TILEB + wave * 1024;                                                          \
-    const size_t ko_ = (size_t)(kt) * S_BK;                                                                   \
-    __builtin_amdgcn_global_load_lds((const void*)(srcA + ko_), (s_lds_ptr)(base_), 16, 0, 0);                \
-    __builtin_amdgcn_global_load_lds((const void*)(srcA + chunk_step + ko_), (s_lds_ptr)(base_ + 4096), 16, 0, 0); \
-    __builtin_amdgcn_global_load_lds((const void*)(srcA + 2 * chunk_step + ko_), (s_lds_ptr)(base_ + 8192), 16, 0, 0); \
-    __builtin_amdgcn_global_load_lds((const void*)(srcA + 3 * chunk_step + ko_), (s_lds_ptr)(base_ + 12288), 16, 0, 0); \
-    __builtin_amdgcn_global_load_lds((const void*)(srcB + ko_), (s_lds_ptr)(base_ + OPB), 16, 0, 0);          \
-    __builtin_amdgcn_global_load_lds((const void*)(srcB + chunk_step + ko_), (s_lds_ptr)(base_ + OPB + 4096), 16, 0, 0); \
-    __builtin_amdgcn_global_load_lds((const void*)(srcB + 2 * chunk_step + ko_), (s_lds_ptr)(base_ + OPB + 8192), 16, 0, 0); \
-    __builtin_amdgcn_global_load_lds((const void*)(srcB + 3 * chunk_step + ko_), (s_lds_ptr)(base_ + OPB + 12288), 16, 0, 0); \
-  } while (0)
-
-  s_floatx4 acc[4][4];
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)tm * S_BM * row_b), 0, (int)(S_BM * row_b), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bt + (size_t)tn * S_BN * row_b), 0, (int)(S_BN * row_b), 0x00020000);
+  const uint32_t voff = (uint32_t)(8 * wave + lr) * row_b + (uint32_t)kt0 * 128u + (uint32_t)lq * 16u;
+  const uint32_t cstep = 8u * WAVES * row_b;
+  auto dma = [&](int kt, int b) {
+    char* base = lds + b * S_TILEB + wave * 1024;
+    const uint32_t kb = (uint32_t)kt * 128u;
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (s_lds_ptr)(base + i * WAVES * 1024), 16, voff, kb + i * cstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (s_lds_ptr)(base + S_OPB + i * WAVES * 1024), 16, voff,
+                                               kb + i * cstep, 0, 0);
+    }
+  };
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = s_floatx4{0.f, 0.f, 0.f, 0.f};
-
-  S_DMA(0, 0);
-  if (nk > 1) S_DMA(1, 1);
+    for (int j = 0; j < NJ; ++j) acc[i][j] = s_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t)
+    if (t < nk) dma(t, t);
   int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    // retire K-tile kt (8 DMAs per thread per tile; tile kt + 1's stay in flight), then publish it
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // retire K-tile kt (the younger tiles stay in flight), then publish it
+    s_wait_tiles<PT>(min(NBUF - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
-    // every wave is past K-tile kt - 1's reads: its buffer takes tile kt + 2
-    if (kt + 2 < nk) S_DMA(kt + 2, buf == 0 ? 2 : buf - 1);
-    const char* la = lds + buf * TILEB;
-    const char* lb = la + OPB;
+    // every wave is past K-tile kt - 1's reads: its buffer takes tile kt + NBUF - 1
+    if (kt + NBUF - 1 < nk) dma(kt + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
+    const char* la = lds + buf * S_TILEB;
+    const char* lb = la + S_OPB;
+    s_i32x4 af[2][4], bf[2][NJ];
+    const int q0 = lane >> 4, q1 = 4 + (lane >> 4);
+    auto rd = [&](const char* base, int row, int q) { return *(const s_i32x4*)(base + s_swz(row + (lane & 15), q)); };
+    af[0][0] = rd(la, wm * 64, q0);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int q = kk * 4 + (lane >> 4);
-      s_bf16x8 af[4], bf[4];
+    for (int j = 0; j < NJ; ++j) bf[0][j] = rd(lb, wn * TN + j * 16, q0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *(const s_bf16x8*)(la + s_swz(wm * 64 + i * 16 + (lane & 15), q));
+    for (int i = 1; i < 4; ++i) af[0][i] = rd(la, wm * 64 + i * 16, q0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = *(const s_bf16x8*)(lb + s_swz(wn * 64 + j * 16 + (lane & 15), q));
+    for (int i = 0; i < 4; ++i) af[1][i] = rd(la, wm * 64 + i * 16, q1);
+    if constexpr (F8) {
+      // one 16x16x128 MFMA per accumulator over both chunks
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bf[1][j] = rd(lb, wn * TN + j * 16, q1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const s_i32x8 b8 = __builtin_shufflevector(bf[0][j], bf[1][j], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const s_i32x8 a8 = __builtin_shufflevector(af[0][i], af[1][i], 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[i][j], 0, 0, 0, 0, 0, 0);
+        }
+      }
+    } else {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((s_bf16x8)af[0][i], (s_bf16x8)bf[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bf[1][j] = rd(lb, wn * TN + j * 16, q1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((s_bf16x8)af[1][i], (s_bf16x8)bf[1][j], acc[i][j], 0, 0, 0);
     }
-    buf = buf == 2 ? 0 : buf + 1;
+    buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
-#undef S_DMA
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();     // every wave done with the ring (the split reduce reuses lds)
-  if constexpr (SPLIT) {
-    if (splits > 1 && !small_split_reduce(acc, ws, cnt, item, tile, splits, tid, (int*)lds)) return;
-  }
-  const int row0 = tm * S_BM + wm * 64 + (lane >> 4) * 4, col0 = tn * S_BN + wn * 64 + (lane & 15);
+  __builtin_amdgcn_s_barrier();     // every wave done with the ring
+}
+
+__device__ __forceinline__ void small_store_c(__bf16* __restrict__ C, int N, int tm, int tn, const SmallAcc& acc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / S_WN, wn = wave % S_WN;
+  const int row0 = tm * S_BM + wm * 64 + (lane >> 4) * 4, col0 = tn * S_BN + wn * S_TN + (lane & 15);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < S_NJ; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         C[(size_t)(row0 + i * 16 + e) * N + col0 + j * 16] = (__bf16)acc[i][j][e];
+}
+
+// v60: one workgroup per output tile, the whole K. F8: A, Bt are fp8 e4m3fn bytes.
+template <bool F8>
+__global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
+gemm_mfma_128x128(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
+                  int K) {
+  __shared__ __attribute__((aligned(16))) char lds[S_LDS];     // the only LDS object (trap 4a)
+  const int tiles_n = N / S_BN, ntiles = (M / S_BM) * tiles_n;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const uint32_t row_b = (uint32_t)K * (F8 ? 1u : 2u);
+  asm volatile("" ::"s"(C), "s"(N));   // kernel arguments in SGPRs before the loop (see "Fragments")
+  SmallAcc acc;
+  small_mainloop<F8>((const char*)A, (const char*)Bt, row_b, tm, tn, 0, (int)(row_b / 128u), lds, acc);
+  small_store_c(C, N, tm, tn, acc);
+}
+
+// v61, split-K: `splits` workgroups per output tile; piece s of a tile runs K-tiles
+// [s nk / splits, (s + 1) nk / splits), so every tile is cut at the same K offsets and the workgroups
+// sharing an A or B panel stream the same K-slices at the same time (L2 hits). A piece stores its fp32
+// slab (thread-major float4s: one coalesced KiB per wave and accumulator) and draws a ticket from the
+// tile's counter (cdna_hip_programming.md "Projection GEMM at M = 256" item 2: plain 16-B stores, drain,
+// barrier, ONE lane releases at agent scope and counts; the last arriver acquires). The tile's last
+// arriver sums every piece's slab in piece order -- its own included, re-read -- so the result does not
+// depend on arrival order, and writes the bf16 tile. Nobody waits for anybody: the grid needs no
+// co-residency. The pieces of a tile are adjacent items: the XCD remap keeps them on one XCD and the
+// slabs in one L2. Pieces keep >= 16 K-tiles (gemm_small_host.h): at 4 K-tiles (1024^3 in 4 pieces)
+// the reduction costs more than the idle CUs (110 vs 167 TF/s), at 32 (1024^2x8192 in 4) it pays 2.2x
+// (458 vs 207). A stream-K even share of grids larger than the chip (pieces cut at offsets that differ
+// from workgroup to workgroup) lost the panel sharing and ran 35-40 % below v60
+// (profiles/r5_small/sweep_streamk.jsonl).
+template <bool F8>
+__global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
+gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
+                     int K, int splits, float* __restrict__ ws, int* __restrict__ cnt) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char lds[S_LDS];     // the only LDS object (trap 4a)
+  int* flag = (int*)(lds + S_NBUF * S_TILEB);
+  const int tid = threadIdx.x;
+  const int tiles_n = N / S_BN, ntiles = (M / S_BM) * tiles_n;
+  const uint32_t row_b = (uint32_t)K * (F8 ? 1u : 2u);
+  const int nk = (int)(row_b / 128u);
+  const int item = xcd_remap(blockIdx.x, ntiles * splits);
+  const int tile = item / splits, piece = item - tile * splits;
+  const int kt0 = piece * nk / splits, kt1 = (piece + 1) * nk / splits;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  asm volatile("" ::"s"(C), "s"(N), "s"(ws), "s"(cnt), "s"(splits));   // see "Fragments"
+  SmallAcc acc;
+  small_mainloop<F8>((const char*)A, (const char*)Bt, row_b, tm, tn, kt0, kt1 - kt0, lds, acc);
+  if (splits > 1) {
+    f4* flat = (f4*)&acc[0][0];
+    f4* slab = (f4*)(ws + (size_t)item * (S_BM * S_BN));
+#pragma unroll
+    for (int a = 0; a < S_NACC; ++a) slab[a * S_THREADS + tid] = flat[a];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = ticket == splits - 1;
+      if (ticket == splits - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!*flag) return;
+#pragma unroll
+    for (int a = 0; a < S_NACC; ++a) flat[a] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < splits; ++s) {
+      const f4* part = (const f4*)(ws + ((size_t)tile * splits + s) * (S_BM * S_BN));
+#pragma unroll
+      for (int a = 0; a < S_NACC; ++a) flat[a] += part[a * S_THREADS + tid];
+    }
+    if (tid == 0) cnt[tile] = 0;   // ready for the next launch on this stream
+  }
+  small_store_c(C, N, tm, tn, acc);
 }

@@ -48,6 +48,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return start + bid / NXCD;
 }
 
+// Launch grid of the persistent 256x256 kernels: one workgroup per CU, a multiple of 8 (whole XCD
+// groups), and every tile in the first round when the grid has fewer tiles than CUs -- rounding
+// down instead (100 tiles on 96 workgroups) ran 4 tiles in a second round at half the chip's
+// throughput (2560^3 416 TF/s; profiles/r5_small/). Workgroups past their XCD's tiles exit at once.
+__host__ inline int persistent_launch_grid(int nwg, int cus) {
+  const int whole = (cus / NXCD) * NXCD;
+  if (nwg >= whole) return whole;
+  const int up = (nwg + NXCD - 1) / NXCD * NXCD;
+  return up <= whole ? up : whole;
+}
+
 // Grouped raster: GROUP_M tile rows walk the N tiles together.
 __device__ __forceinline__ void tile_coords(int wgid, int tiles_m, int tiles_n, int& tm, int& tn) {
   const int per_group = GROUP_M * tiles_n;

@@ -68,16 +68,20 @@ def _r4_bf16(M, N, K, cus, g):
     return v
 
 
+def _splits(tiles, nk, cus, target=1):
+    """v61's K pieces per tile (gemm_small_host.h small_splits): target x CUs / tiles, >= 16 K-tiles
+    a piece, 1 = none."""
+    return max(1, min(target * cus // tiles, nk // 16))
+
+
 def _small(M, N, K, cus):
     """The round-5 rows: 128x128 tiles when the 256x256 grid fills at most a quarter of the CUs -- v61
-    (split-K) when the 128x128 grid is still under the CU count and every split keeps >= 16 K-tiles,
-    else v60. None when neither applies."""
+    (split-K) when the 128x128 grid leaves pieces to give, else v60. None when neither applies."""
     tiles256 = M % BM == 0 and N % BN == 0 and K % BK == 0 and K >= 2 * BK
     tiles128 = M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and K >= 64
     if not (tiles128 and (not tiles256 or 4 * (M // BM) * (N // BN) <= cus)):
         return None
-    splits = max(1, min(cus // ((M // 128) * (N // 128)), (K // 64) // 16))
-    return 61 if splits > 1 else 60
+    return 61 if _splits((M // 128) * (N // 128), K // 64, cus) > 1 else 60
 
 
 DIMS = [128, 256, 384, 512, 1024, 1536, 2048, 3072, 4096, 6144, 8192, 12288, 16384]
@@ -114,9 +118,10 @@ def test_bf16_small_grid_row_and_its_evidence(lib):
     assert lib.amdgo_gemm_plan_bf16(1024, 1024, 1024, 256, 60) == 60    # pinned
     assert lib.amdgo_gemm_plan_bf16(1000, 1024, 1024, 256, 60) == 0     # pinned, cannot run: generic
     assert lib.amdgo_gemm_plan_bf16(8192, 8192, 8192, 256, 0) == 50
-    assert lib.amdgo_gemm_plan_bf16(1024, 1024, 8192, 256, 0) == 61     # split-K: 4 splits of 32 K-tiles
+    assert lib.amdgo_gemm_plan_bf16(1024, 1024, 8192, 256, 0) == 61     # split-K: 4 pieces of 32 K-tiles
     assert lib.amdgo_gemm_small_splits(1024, 1024, 8192, 256) == 4
     assert lib.amdgo_gemm_small_splits(1024, 1024, 1024, 256) == 1      # 16 K-tiles: no split
+    assert lib.amdgo_gemm_plan_bf16(2560, 2560, 2560, 256, 0) == 53     # 100 tiles: the 256x256 frame (VP, K 2560)
     ev = lib.amdgo_gemm_plan_bf16_evidence(1024, 1024, 1024, 256).decode()
     assert ev.startswith("profiles/r5_small/")
     assert lib.amdgo_gemm_plan_bf16_evidence(16384, 16384, 1024, 256).decode().startswith("profiles/r4_lean/")
@@ -158,8 +163,20 @@ def _r4_fp8(M, N, K, cus, g):
     return v
 
 
-FP8_PINS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23)
+FP8_PINS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61)
 FP8_KS = [128, 256, 384, 512, 640, 1024, 1536, 1664, 2048, 4096, 8192, 8320, 16384, 32768]
+
+
+def _small_fp8(M, N, K, cus, pin):
+    """The round-5 fp8 rows (the bf16 rule on 128-byte K-tiles of fp8) and the pins 60 / 61; None
+    where round 4's rules apply unchanged."""
+    tiles256 = M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and K >= 256
+    tiles128 = M % 128 == 0 and N % 128 == 0 and K % 128 == 0 and K >= 128
+    if pin in (60, 61):
+        return pin if tiles128 else 0
+    if pin == 0 and tiles128 and (not tiles256 or 4 * (M // 256) * (N // 256) <= cus):
+        return 61 if _splits((M // 128) * (N // 128), K // 128, cus) > 1 else 60
+    return None
 
 
 def test_fp8_table_reproduces_the_round4_rules(lib):
@@ -167,7 +184,8 @@ def test_fp8_table_reproduces_the_round4_rules(lib):
     for M, N in itertools.product(DIMS, DIMS[::2]):
         for K, cus, pin in itertools.product(FP8_KS, CUS, FP8_PINS):
             got = lib.amdgo_gemm_plan_fp8(M, N, K, cus, pin)
-            want = _r4_fp8(M, N, K, cus, pin)
+            small = _small_fp8(M, N, K, cus, pin)
+            want = small if small is not None else _r4_fp8(M, N, K, cus, pin)
             if got != want:
                 bad.append((M, N, K, cus, pin, got, want))
     assert not bad, bad[:20]
