@@ -78,8 +78,8 @@ def gemm_fp8(a, bt, out=None, *, generic: bool = False):
 
 # Production variant sets (native/hip/gemm_bf16.hip, gemm_fp8.hip): 0 = automatic dispatch, any
 # other member pins that kernel. Everything else lives in the tools-only lab library.
-BF16_VARIANTS = (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61)
-FP8_VARIANTS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61)
+BF16_VARIANTS = (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61, 62)
+FP8_VARIANTS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61, 62)
 
 
 def set_variant(v: int) -> None:

@@ -119,6 +119,9 @@ static constexpr Bf16Rule kBf16Rules[] = {
     {60, [](const Bf16Shape& c) { return c.tiles128 && (!c.tiles256 || 4 * c.nwg <= c.cus); },
      "profiles/r5_small/sweep_v62.jsonl (1024^3 1.36x, 1536^3 1.01x, 2048^2x1024 1.35x hipBLASLt)"},
     {0, [](const Bf16Shape& c) { return !c.tiles256; }, "generic bounds-checked kernel"},
+    // a quarter to a half of the CUs in 256x256 tiles: 256x128 tiles fill the chip in one wave
+    {62, [](const Bf16Shape& c) { return 4 * c.nwg > c.cus && 2 * c.nwg <= c.cus; },
+     "profiles/r5_small/sweep_tile256x128.jsonl, sweep_tile256x128_mid.jsonl (2560^3 878 vs 773, 2816^3 1060 vs 969)"},
     // K not a power of two (even K-tile count >= 4): the asm pipeline in the VP DMA form
     {54, [](const Bf16Shape& c) { return c.mi355 && !c.pow2k && c.K % (2 * BK) == 0 && c.K >= 4 * BK &&
                                          c.pgrid >= NXCD && c.sq && c.nwg >= 8 * c.cus; },
@@ -161,6 +164,7 @@ struct Bf16Need {
 static constexpr Bf16Need kBf16Needs[] = {
     {60, [](const Bf16Shape& c) { return c.tiles128; }, 0},
     {61, [](const Bf16Shape& c) { return c.tiles128; }, 0},
+    {62, [](const Bf16Shape& c) { return c.tiles128 && c.M % 256 == 0; }, 0},
 
     {45, [](const Bf16Shape& c) { return c.sq; }, 44},
     {48, [](const Bf16Shape& c) { return c.sq; }, 47},
@@ -220,7 +224,7 @@ extern "C" {
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
   if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50 &&
-      v != 51 && v != 52 && v != 53 && v != 54 && v != 55 && v != 56 && v != 60 && v != 61)
+      v != 51 && v != 52 && v != 53 && v != 54 && v != 55 && v != 56 && v != 60 && v != 61 && v != 62)
     return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
@@ -262,6 +266,9 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
     case 60:
     case 61:
       launch_small<false>(a, b, c, M, N, K, s, cus, variant_now == 61);
+      break;
+    case 62:
+      launch_small<false, 256>(a, b, c, M, N, K, s, cus, false);
       break;
     case 18:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,

@@ -86,6 +86,9 @@ static constexpr Fp8Rule kFp8Rules[] = {
     {60, [](const Fp8Shape& c) { return c.tiles128 && (!c.tiles || 4 * c.nwg <= c.cus); },
      "profiles/r5_small/ (fp8 128x128)"},
     {0, [](const Fp8Shape& c) { return !c.tiles; }, "generic bounds-checked kernel"},
+    // a quarter to a half of the CUs in 256x256 tiles: 256x128 tiles fill the chip in one wave
+    {62, [](const Fp8Shape& c) { return 4 * c.nwg > c.cus && 2 * c.nwg <= c.cus; },
+     "profiles/r5_small/sweep_tile256x128_mid_fp8.jsonl (2560^3 1591 vs 1412, 2560^2x8192 2032 vs 1713)"},
     // one dispatch wave: v22 (v23 off the 16x16-tile multiples)
     {22, [](const Fp8Shape& c) { return c.ap && c.nwg <= c.cus && c.sq; },
      "profiles/r4_sweep/onewave_fp8.jsonl (4096^3 2996 vs v20 2957)"},
@@ -116,6 +119,7 @@ struct Fp8Need {
 static constexpr Fp8Need kFp8Needs[] = {
     {60, [](const Fp8Shape& c) { return c.tiles128; }, 0},
     {61, [](const Fp8Shape& c) { return c.tiles128; }, 0},
+    {62, [](const Fp8Shape& c) { return c.tiles128 && c.M % 256 == 0; }, 0},
     {20, [](const Fp8Shape& c) { return c.ap; }, -1},
     {21, [](const Fp8Shape& c) { return c.ap; }, -1},
     {22, [](const Fp8Shape& c) { return c.ap; }, -1},
@@ -140,7 +144,7 @@ static int plan_fp8(int M, int N, int K, int cus, int pinned) {
       if (r.match(c)) return r.variant;
     return 0;
   }
-  if (!c.tiles && pinned != 60 && pinned != 61) return 0;
+  if (!c.tiles && pinned != 60 && pinned != 61 && pinned != 62) return 0;
   int v = pinned;
   for (bool moved = true; moved;) {
     moved = false;
@@ -163,7 +167,7 @@ extern "C" {
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
   if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21 && v != 22 && v != 23 &&
-      v != 60 && v != 61)
+      v != 60 && v != 61 && v != 62)
     return (int)hipErrorInvalidValue;
   g_fp8_variant = v;
   return 0;
@@ -193,6 +197,9 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
     case 60:
     case 61:
       launch_small<true>(a, b, c, M, N, K, s, cus, variant_now == 61);
+      break;
+    case 62:
+      launch_small<true, 256>(a, b, c, M, N, K, s, cus, false);
       break;
     case 10:
       hipLaunchKernelGGL((gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>), dim3(pgrid), dim3(F8_THREADS), 0, s,

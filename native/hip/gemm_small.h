@@ -29,7 +29,7 @@
 
 #include "gemm_tile_common.h"
 
-constexpr int S_BM = 128, S_BN = 128, S_BK = 64, S_WAVES = 8, S_THREADS = S_WAVES * 64, S_NBUF = 4;
+constexpr int S_BM = 128, S_BN = 128, S_BK = 64, S_WAVES = 8, S_THREADS = S_WAVES * 64;
 
 typedef __bf16 s_bf16x8 __attribute__((ext_vector_type(8)));
 typedef int s_i32x4 __attribute__((ext_vector_type(4)));
@@ -60,14 +60,27 @@ __device__ __forceinline__ int s_swz(int r, int q) { return r * 128 + ((q ^ (r &
 // a scalar load still pending at the loop header turns every counted fragment wait into lgkmcnt(0).
 typedef __attribute__((address_space(3))) void* s_lds_ptr;
 
-constexpr int S_OPB = S_BM * S_BK * 2, S_TILEB = 2 * S_OPB;   // 16 KiB per operand, 32 KiB per K-tile
-constexpr int S_LDS = S_NBUF * S_TILEB + 16;                  // the ring + the split reduction's flag
-constexpr int S_WN = S_WAVES / 2, S_TN = S_BN / S_WN, S_NJ = S_TN / 16;   // wave grid 2 x S_WN, 64 x S_TN each
-constexpr int S_NACC = 4 * S_NJ;                              // 16x16 accumulators per thread
-static_assert(S_WAVES == 4 || S_WAVES == 8, "2x2 waves of 64x64 or 2x4 waves of 64x32");
-typedef s_floatx4 SmallAcc[4][S_NJ];
+// Tile shapes: BMT x 128 output tiles (BMT = 128: v60 / v61; 256: v62, for 256x256 grids of a quarter
+// to a half of the CUs, where 256x128 tiles fill the chip in one wave: 2560^3 878 vs 773 TF/s, 2816^3
+// 1060 vs 969, 4096x2048x4096 1145 vs 1074; fp8 2560^3 1591 vs 1412 -- profiles/r5_small/),
+// 8 waves as WM x WN of 64 x TN each; a ring of NBUF K-tiles of OPA (A: BMT rows) + OPB (B: 128 rows)
+// bytes: 4 x 32 KiB for 128, 3 x 48 KiB for 256.
+template <int BMT>
+struct SmallCfg {
+  static_assert(BMT == 128 || BMT == 256, "128- or 256-row tiles");
+  static constexpr int WM = BMT / 64, WN = S_WAVES / WM, TN = S_BN / WN, NJ = TN / 16;
+  static constexpr int NBUF = BMT == 128 ? 4 : 3;
+  static constexpr int OPA = BMT * 128, OPB = S_BN * 128, TILEB = OPA + OPB;
+  static constexpr int LDS = NBUF * TILEB + 16;                // the ring + the split reduction's flag
+  static constexpr int CPA = BMT / 8 / S_WAVES, CPB = S_BN / 8 / S_WAVES;   // 8-row DMA chunks per wave
+  static constexpr int PT = CPA + CPB;                         // DMAs per thread per K-tile
+  static constexpr int NACC = 4 * NJ;                          // 16x16 accumulators per thread
+  static_assert(LDS <= 160 * 1024, "one CU's LDS");
+};
+template <int BMT>
+using SmallAcc = s_floatx4[4][SmallCfg<BMT>::NJ];
 
-// wait until at most `ahead` K-tiles (PT DMAs each) of this thread are in flight; ahead <= S_NBUF - 2
+// wait until at most `ahead` K-tiles (PT DMAs each) of this thread are in flight; ahead <= 2
 template <int PT>
 __device__ __forceinline__ void s_wait_tiles(int ahead) {
   if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PT) : "memory");
@@ -77,32 +90,32 @@ __device__ __forceinline__ void s_wait_tiles(int ahead) {
 
 // acc = A[tile rows, K-tiles kt0 .. kt0 + nk) * Bt[...]^T for output tile (tm, tn); row_b = bytes per
 // operand row. Ends with every wave past its last fragment read (the ring is free again).
-template <bool F8>
+template <bool F8, int BMT>
 __device__ __forceinline__ void small_mainloop(const char* __restrict__ A, const char* __restrict__ Bt, uint32_t row_b,
-                                               int tm, int tn, int kt0, int nk, char* lds, SmallAcc& acc) {
-  constexpr int NBUF = S_NBUF, WAVES = S_WAVES, NJ = S_NJ, TN = S_TN;
-  constexpr int CPW = 16 / WAVES;            // 8-row chunks per operand a wave DMAs per K-tile
-  constexpr int PT = 2 * CPW;                // DMAs per thread per K-tile
+                                               int tm, int tn, int kt0, int nk, char* lds, SmallAcc<BMT>& acc) {
+  using Cfg = SmallCfg<BMT>;
+  constexpr int NBUF = Cfg::NBUF, WAVES = S_WAVES, NJ = Cfg::NJ, TN = Cfg::TN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: LDS-DMA bases stay scalar
-  const int wm = wave / S_WN, wn = wave % S_WN;
-  // DMA pieces: wave w issues the 8-row chunks c = w + WAVES i (i < CPW) of each operand
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  // DMA pieces: wave w issues the 8-row chunks c = w + WAVES i of each operand
   const int lr = lane >> 3, lq = (lane & 7) ^ lr;
   const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)tm * S_BM * row_b), 0, (int)(S_BM * row_b), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)tm * BMT * row_b), 0, (int)(BMT * row_b), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)(Bt + (size_t)tn * S_BN * row_b), 0, (int)(S_BN * row_b), 0x00020000);
   const uint32_t voff = (uint32_t)(8 * wave + lr) * row_b + (uint32_t)kt0 * 128u + (uint32_t)lq * 16u;
   const uint32_t cstep = 8u * WAVES * row_b;
   auto dma = [&](int kt, int b) {
-    char* base = lds + b * S_TILEB + wave * 1024;
+    char* base = lds + b * Cfg::TILEB + wave * 1024;
     const uint32_t kb = (uint32_t)kt * 128u;
 #pragma unroll
-    for (int i = 0; i < CPW; ++i) {
+    for (int i = 0; i < Cfg::CPA; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (s_lds_ptr)(base + i * WAVES * 1024), 16, voff, kb + i * cstep, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (s_lds_ptr)(base + S_OPB + i * WAVES * 1024), 16, voff,
+#pragma unroll
+    for (int i = 0; i < Cfg::CPB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (s_lds_ptr)(base + Cfg::OPA + i * WAVES * 1024), 16, voff,
                                                kb + i * cstep, 0, 0);
-    }
   };
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -114,12 +127,12 @@ __device__ __forceinline__ void small_mainloop(const char* __restrict__ A, const
   int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // retire K-tile kt (the younger tiles stay in flight), then publish it
-    s_wait_tiles<PT>(min(NBUF - 2, nk - 1 - kt));
+    s_wait_tiles<Cfg::PT>(min(NBUF - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
     // every wave is past K-tile kt - 1's reads: its buffer takes tile kt + NBUF - 1
     if (kt + NBUF - 1 < nk) dma(kt + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
-    const char* la = lds + buf * S_TILEB;
-    const char* lb = la + S_OPB;
+    const char* la = lds + buf * Cfg::TILEB;
+    const char* lb = la + Cfg::OPA;
     s_i32x4 af[2][4], bf[2][NJ];
     const int q0 = lane >> 4, q1 = 4 + (lane >> 4);
     auto rd = [&](const char* base, int row, int q) { return *(const s_i32x4*)(base + s_swz(row + (lane & 15), q)); };
@@ -165,33 +178,36 @@ __device__ __forceinline__ void small_mainloop(const char* __restrict__ A, const
   __builtin_amdgcn_s_barrier();     // every wave done with the ring
 }
 
-__device__ __forceinline__ void small_store_c(__bf16* __restrict__ C, int N, int tm, int tn, const SmallAcc& acc) {
+template <int BMT>
+__device__ __forceinline__ void small_store_c(__bf16* __restrict__ C, int N, int tm, int tn, const SmallAcc<BMT>& acc) {
+  using Cfg = SmallCfg<BMT>;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave / S_WN, wn = wave % S_WN;
-  const int row0 = tm * S_BM + wm * 64 + (lane >> 4) * 4, col0 = tn * S_BN + wn * S_TN + (lane & 15);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int row0 = tm * BMT + wm * 64 + (lane >> 4) * 4, col0 = tn * S_BN + wn * Cfg::TN + (lane & 15);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < S_NJ; ++j)
+    for (int j = 0; j < Cfg::NJ; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         C[(size_t)(row0 + i * 16 + e) * N + col0 + j * 16] = (__bf16)acc[i][j][e];
 }
 
-// v60: one workgroup per output tile, the whole K. F8: A, Bt are fp8 e4m3fn bytes.
-template <bool F8>
+// v60 (BMT = 128) / v62 (BMT = 256: BMT x 128 tiles despite the name): one workgroup per output tile,
+// the whole K. F8: A, Bt are fp8 e4m3fn bytes.
+template <bool F8, int BMT = 128>
 __global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
 gemm_mfma_128x128(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
                   int K) {
-  __shared__ __attribute__((aligned(16))) char lds[S_LDS];     // the only LDS object (trap 4a)
-  const int tiles_n = N / S_BN, ntiles = (M / S_BM) * tiles_n;
+  __shared__ __attribute__((aligned(16))) char lds[SmallCfg<BMT>::LDS];     // the only LDS object (trap 4a)
+  const int tiles_n = N / S_BN, ntiles = (M / BMT) * tiles_n;
   const int tile = xcd_remap(blockIdx.x, ntiles);
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const uint32_t row_b = (uint32_t)K * (F8 ? 1u : 2u);
   asm volatile("" ::"s"(C), "s"(N));   // kernel arguments in SGPRs before the loop (see "Fragments")
-  SmallAcc acc;
-  small_mainloop<F8>((const char*)A, (const char*)Bt, row_b, tm, tn, 0, (int)(row_b / 128u), lds, acc);
-  small_store_c(C, N, tm, tn, acc);
+  SmallAcc<BMT> acc;
+  small_mainloop<F8, BMT>((const char*)A, (const char*)Bt, row_b, tm, tn, 0, (int)(row_b / 128u), lds, acc);
+  small_store_c<BMT>(C, N, tm, tn, acc);
 }
 
 // v61, split-K: `splits` workgroups per output tile; piece s of a tile runs K-tiles
@@ -208,15 +224,16 @@ gemm_mfma_128x128(const void* __restrict__ A, const void* __restrict__ Bt, __bf1
 // (458 vs 207). A stream-K even share of grids larger than the chip (pieces cut at offsets that differ
 // from workgroup to workgroup) lost the panel sharing and ran 35-40 % below v60
 // (profiles/r5_small/sweep_streamk.jsonl).
-template <bool F8>
+template <bool F8, int BMT = 128>
 __global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
 gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
                      int K, int splits, float* __restrict__ ws, int* __restrict__ cnt) {
   typedef float f4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) char lds[S_LDS];     // the only LDS object (trap 4a)
-  int* flag = (int*)(lds + S_NBUF * S_TILEB);
+  using Cfg = SmallCfg<BMT>;
+  __shared__ __attribute__((aligned(16))) char lds[Cfg::LDS];     // the only LDS object (trap 4a)
+  int* flag = (int*)(lds + Cfg::NBUF * Cfg::TILEB);
   const int tid = threadIdx.x;
-  const int tiles_n = N / S_BN, ntiles = (M / S_BM) * tiles_n;
+  const int tiles_n = N / S_BN, ntiles = (M / BMT) * tiles_n;
   const uint32_t row_b = (uint32_t)K * (F8 ? 1u : 2u);
   const int nk = (int)(row_b / 128u);
   const int item = xcd_remap(blockIdx.x, ntiles * splits);
@@ -224,13 +241,14 @@ gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __
   const int kt0 = piece * nk / splits, kt1 = (piece + 1) * nk / splits;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   asm volatile("" ::"s"(C), "s"(N), "s"(ws), "s"(cnt), "s"(splits));   // see "Fragments"
-  SmallAcc acc;
-  small_mainloop<F8>((const char*)A, (const char*)Bt, row_b, tm, tn, kt0, kt1 - kt0, lds, acc);
+  SmallAcc<BMT> acc;
+  small_mainloop<F8, BMT>((const char*)A, (const char*)Bt, row_b, tm, tn, kt0, kt1 - kt0, lds, acc);
   if (splits > 1) {
+    constexpr size_t SLAB = (size_t)BMT * S_BN;     // floats per tile
     f4* flat = (f4*)&acc[0][0];
-    f4* slab = (f4*)(ws + (size_t)item * (S_BM * S_BN));
+    f4* slab = (f4*)(ws + (size_t)item * SLAB);
 #pragma unroll
-    for (int a = 0; a < S_NACC; ++a) slab[a * S_THREADS + tid] = flat[a];
+    for (int a = 0; a < Cfg::NACC; ++a) slab[a * S_THREADS + tid] = flat[a];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -246,13 +264,13 @@ gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __
     __syncthreads();
     if (!*flag) return;
 #pragma unroll
-    for (int a = 0; a < S_NACC; ++a) flat[a] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < Cfg::NACC; ++a) flat[a] = f4{0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < splits; ++s) {
-      const f4* part = (const f4*)(ws + ((size_t)tile * splits + s) * (S_BM * S_BN));
+      const f4* part = (const f4*)(ws + ((size_t)tile * splits + s) * SLAB);
 #pragma unroll
-      for (int a = 0; a < S_NACC; ++a) flat[a] += part[a * S_THREADS + tid];
+      for (int a = 0; a < Cfg::NACC; ++a) flat[a] += part[a * S_THREADS + tid];
     }
     if (tid == 0) cnt[tile] = 0;   // ready for the next launch on this stream
   }
-  small_store_c(C, N, tm, tn, acc);
+  small_store_c<BMT>(C, N, tm, tn, acc);
 }

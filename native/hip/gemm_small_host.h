@@ -64,15 +64,15 @@ inline SmallWorkspace* small_workspace(hipStream_t s, size_t floats, int tiles) 
 
 // v60 (split = false) or v61: split-K when the grid has pieces to give, else v60. Host guarantees M, N multiples
 // of 128 and K a whole number of 128-byte K-tiles.
-template <bool F8>
+template <bool F8, int BMT = 128>
 inline void launch_small(const void* a, const void* b, __bf16* c, int M, int N, int K, hipStream_t s, int cus, bool split) {
-  const int tiles = (M / S_BM) * (N / S_BN);
+  const int tiles = (M / BMT) * (N / S_BN);
   const int nk = (int)((size_t)K * (F8 ? 1 : 2) / 128);
   const int splits = split ? small_splits(tiles, nk, cus) : 1;
-  SmallWorkspace* w = splits > 1 ? small_workspace(s, (size_t)tiles * splits * S_BM * S_BN, tiles) : nullptr;
+  SmallWorkspace* w = splits > 1 ? small_workspace(s, (size_t)tiles * splits * BMT * S_BN, tiles) : nullptr;
   if (w)
-    hipLaunchKernelGGL(gemm_mfma_128x128_sk<F8>, dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K, splits,
-                       w->ws, w->cnt);
+    hipLaunchKernelGGL((gemm_mfma_128x128_sk<F8, BMT>), dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
+                       splits, w->ws, w->cnt);
   else
-    hipLaunchKernelGGL(gemm_mfma_128x128<F8>, dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K);
+    hipLaunchKernelGGL((gemm_mfma_128x128<F8, BMT>), dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K);
 }

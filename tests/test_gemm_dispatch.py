@@ -79,7 +79,10 @@ def _small(M, N, K, cus):
     (split-K) when the 128x128 grid leaves pieces to give, else v60. None when neither applies."""
     tiles256 = M % BM == 0 and N % BN == 0 and K % BK == 0 and K >= 2 * BK
     tiles128 = M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and K >= 64
-    if not (tiles128 and (not tiles256 or 4 * (M // BM) * (N // BN) <= cus)):
+    nwg = (M // BM) * (N // BN)
+    if tiles256 and 4 * nwg > cus and 2 * nwg <= cus:
+        return 62                                   # 256x128 tiles: one wave of the chip
+    if not (tiles128 and (not tiles256 or 4 * nwg <= cus)):
         return None
     return 61 if _splits((M // 128) * (N // 128), K // 64, cus) > 1 else 60
 
@@ -121,7 +124,7 @@ def test_bf16_small_grid_row_and_its_evidence(lib):
     assert lib.amdgo_gemm_plan_bf16(1024, 1024, 8192, 256, 0) == 61     # split-K: 4 pieces of 32 K-tiles
     assert lib.amdgo_gemm_small_splits(1024, 1024, 8192, 256) == 4
     assert lib.amdgo_gemm_small_splits(1024, 1024, 1024, 256) == 1      # 16 K-tiles: no split
-    assert lib.amdgo_gemm_plan_bf16(2560, 2560, 2560, 256, 0) == 53     # 100 tiles: the 256x256 frame (VP, K 2560)
+    assert lib.amdgo_gemm_plan_bf16(2560, 2560, 2560, 256, 0) == 62     # 100 256x256 tiles: 200 of 256x128
     ev = lib.amdgo_gemm_plan_bf16_evidence(1024, 1024, 1024, 256).decode()
     assert ev.startswith("profiles/r5_small/")
     assert lib.amdgo_gemm_plan_bf16_evidence(16384, 16384, 1024, 256).decode().startswith("profiles/r4_lean/")
@@ -163,7 +166,7 @@ def _r4_fp8(M, N, K, cus, g):
     return v
 
 
-FP8_PINS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61)
+FP8_PINS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61, 62)
 FP8_KS = [128, 256, 384, 512, 640, 1024, 1536, 1664, 2048, 4096, 8192, 8320, 16384, 32768]
 
 
@@ -174,8 +177,13 @@ def _small_fp8(M, N, K, cus, pin):
     tiles128 = M % 128 == 0 and N % 128 == 0 and K % 128 == 0 and K >= 128
     if pin in (60, 61):
         return pin if tiles128 else 0
-    if pin == 0 and tiles128 and (not tiles256 or 4 * (M // 256) * (N // 256) <= cus):
+    if pin == 62:
+        return 62 if tiles128 and M % 256 == 0 else 0
+    nwg = (M // 256) * (N // 256)
+    if pin == 0 and tiles128 and (not tiles256 or 4 * nwg <= cus):
         return 61 if _splits((M // 128) * (N // 128), K // 128, cus) > 1 else 60
+    if pin == 0 and tiles256 and 4 * nwg > cus and 2 * nwg <= cus:
+        return 62
     return None
 
 

@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61])   # the production set (gemm.FP8_VARIANTS)
+@pytest.fixture(params=[0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61, 62])   # the production set (gemm.FP8_VARIANTS)
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 
@@ -162,7 +162,7 @@ def test_fp8_production_variant_set_is_closed(cuda_device):
         assert G.resolve_fp8_variant(12288, 12288, 12288) == 22
         assert G.resolve_fp8_variant(12288, 4096, 1024) == 21            # a 16-tile side keeps v21
         assert G.resolve_fp8_variant(4096, 4096, 4096) == 22                # one dispatch wave
-        assert G.resolve_fp8_variant(2048, 4096, 4096) == 23                # one wave, not 16x16-tile multiples
+        assert G.resolve_fp8_variant(2048, 4096, 4096) == 62                # 128 tiles: 256x128 tiles fill the chip
         assert G.resolve_fp8_variant(4096, 8192, 4096) == 22                # a 16-tile side, K >= 4096
         assert G.resolve_fp8_variant(4096 + 256, 4096, 4096) == 20
         assert G.resolve_fp8_variant(8192, 8192, 8192 + 128) in (16, 18)   # odd K-tile count

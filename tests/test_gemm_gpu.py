@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61, 62])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -153,7 +153,7 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61, 62)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
@@ -161,7 +161,7 @@ def test_production_variant_set_is_closed(cuda_device):
 
 
 @pytest.mark.parametrize("m,n,k,want", [(8192, 8192, 8192, 50), (16384, 16384, 1024, 56), (8192, 8192, 4096, 50),
-                                        (8192, 8192, 2048, 56), (4096, 8192, 1024, 56), (4096, 4096, 2048, 56), (2048, 4096, 512, 55),
+                                        (8192, 8192, 2048, 56), (4096, 8192, 1024, 56), (4096, 4096, 2048, 56), (2048, 4096, 512, 62),
                                         (12288, 12288, 12288, 54), (8192, 8192, 12288, 53), (8192, 8192, 8256, 47),
                                         (12288, 12288, 8256, 48),
                                         (12288, 12288, 8192, 51), (16384, 16384, 16384, 51),
@@ -169,7 +169,8 @@ def test_production_variant_set_is_closed(cuda_device):
                                         (4096, 4096, 4096, 56),
                                         (8192, 8192, 128, 25), (256, 256, 64, 60), (300, 256, 256, 0),
                                         (1024, 1024, 1024, 60), (2048, 2048, 2048, 60), (1152, 1152, 1024, 60),
-                                        (1024, 1024, 8192, 61), (1024, 1024, 2048, 61), (1024, 1024, 512, 60)])
+                                        (1024, 1024, 8192, 61), (1024, 1024, 2048, 61), (1024, 1024, 512, 60),
+                                        (2560, 2560, 2560, 62), (4096, 2048, 4096, 62), (3072, 3072, 3072, 53)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""
     import torch
