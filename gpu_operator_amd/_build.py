@@ -90,7 +90,8 @@ def _pyext_name(stem: str) -> str:
 # Production builds read the generated headers with the shipped schedules only; the lab libraries
 # read the *_lab.h headers (every schedule), which mask the production ones (tools/gen_*_asm_loop.py).
 GEMM_HEADERS = ["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h",
-                "hip/gemm_fp8_kernels.h", "hip/gemm_fp8_asm_loop.h", "hip/gemm_w4ap.h"]
+                "hip/gemm_fp8_kernels.h", "hip/gemm_fp8_asm_loop.h", "hip/gemm_w4ap.h", "hip/gemm_small.h",
+                "hip/gemm_small_host.h"]
 LAB_HEADERS = GEMM_HEADERS + ["hip/gemm_bf16_asm_loop_lab.h", "hip/gemm_fp8_asm_loop_lab.h"]
 
 TARGETS: List[Target] = [

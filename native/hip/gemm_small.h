@@ -218,8 +218,13 @@ gemm_mfma_128x128(const void* __restrict__ A, const void* __restrict__ Bt, __bf1
 // barrier, ONE lane releases at agent scope and counts; the last arriver acquires). The tile's last
 // arriver sums every piece's slab in piece order -- its own included, re-read -- so the result does not
 // depend on arrival order, and writes the bf16 tile. Nobody waits for anybody: the grid needs no
-// co-residency. The pieces of a tile are adjacent items: the XCD remap keeps them on one XCD and the
-// slabs in one L2. Pieces keep >= 16 K-tiles (gemm_small_host.h): at 4 K-tiles (1024^3 in 4 pieces)
+// co-residency. Item order: pieces of >= 32 K-tiles go piece-major (item = piece x tiles + tile), so
+// the XCD remap gives an XCD a run of neighbouring tiles at ONE K range -- 1024^2x16384 in 4 pieces
+// streams 6 MiB of A and B per XCD instead of 18 (tile-major, every XCD read all of B): bf16 617 ->
+// 709 TF/s (1.07x hipBLASLt), 1024^2x8192 485 -> 518, fp8 1024^2x16384 974 -> 1048; the slabs then
+// cross XCDs (the agent-scope release / acquire covers that), which costs more than it saves on
+// shorter pieces (1024^2x4096, 16 K-tiles: 327 -> 316), so those stay tile-major (the pieces of a
+// tile adjacent, on one XCD; profiles/r5_small/sweep_piece_major.jsonl). Pieces keep >= 16 K-tiles (gemm_small_host.h): at 4 K-tiles (1024^3 in 4 pieces)
 // the reduction costs more than the idle CUs (110 vs 167 TF/s), at 32 (1024^2x8192 in 4) it pays 2.2x
 // (458 vs 207). A stream-K even share of grids larger than the chip (pieces cut at offsets that differ
 // from workgroup to workgroup) lost the panel sharing and ran 35-40 % below v60
@@ -227,7 +232,7 @@ gemm_mfma_128x128(const void* __restrict__ A, const void* __restrict__ Bt, __bf1
 template <bool F8, int BMT = 128>
 __global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
 gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
-                     int K, int splits, float* __restrict__ ws, int* __restrict__ cnt) {
+                     int K, int splits, int pmajor, float* __restrict__ ws, int* __restrict__ cnt) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   using Cfg = SmallCfg<BMT>;
   __shared__ __attribute__((aligned(16))) char lds[Cfg::LDS];     // the only LDS object (trap 4a)
@@ -237,7 +242,8 @@ gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __
   const uint32_t row_b = (uint32_t)K * (F8 ? 1u : 2u);
   const int nk = (int)(row_b / 128u);
   const int item = xcd_remap(blockIdx.x, ntiles * splits);
-  const int tile = item / splits, piece = item - tile * splits;
+  const int piece = pmajor ? item / ntiles : item % splits;      // item order: see v61 above
+  const int tile = pmajor ? item - piece * ntiles : item / splits;
   const int kt0 = piece * nk / splits, kt1 = (piece + 1) * nk / splits;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   asm volatile("" ::"s"(C), "s"(N), "s"(ws), "s"(cnt), "s"(splits));   // see "Fragments"
@@ -246,7 +252,7 @@ gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __
   if (splits > 1) {
     constexpr size_t SLAB = (size_t)BMT * S_BN;     // floats per tile
     f4* flat = (f4*)&acc[0][0];
-    f4* slab = (f4*)(ws + (size_t)item * SLAB);
+    f4* slab = (f4*)(ws + ((size_t)tile * splits + piece) * SLAB);
 #pragma unroll
     for (int a = 0; a < Cfg::NACC; ++a) slab[a * S_THREADS + tid] = flat[a];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
