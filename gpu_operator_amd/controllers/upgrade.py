@@ -113,9 +113,14 @@ class UpgradeStateManager:
         self._pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="upgrade") if run_async else None
         self._inflight: Set[str] = set()
         self._lock = threading.Lock()
+        self._worker = threading.local()     # .deferred: the state a running worker moves its node to
 
     # -- node label/annotation provider (durable state) ----------------------------------------
     def set_state(self, node: Dict, state: str) -> None:
+        deferred = getattr(self._worker, "deferred", None)
+        if deferred is not None:
+            deferred.append((node, state))    # applied once the worker has left _inflight (_schedule)
+            return
         name = o.name(node)
         self.client.patch("v1", "Node", name, {"metadata": {"labels": {UPGRADE_STATE_LABEL: state or None}}})
         o.labels(node)[UPGRADE_STATE_LABEL] = state
@@ -536,13 +541,21 @@ class UpgradeStateManager:
             self._inflight.add(node)
 
         def run():
+            # The worker's state change is the event that drives the next reconcile; published while
+            # the node is still in _inflight, a next step that is async too (pod deletion -> drain)
+            # would be skipped by that reconcile and wait for the 2-minute requeue. So the label is
+            # written only after the node has left _inflight.
+            self._worker.deferred = []
             try:
                 fn()
             except Exception:  # noqa: BLE001
                 log.exception("upgrade worker for node %s failed", node)
             finally:
+                deferred, self._worker.deferred = self._worker.deferred, None
                 with self._lock:
                     self._inflight.discard(node)
+                for n, st in deferred:
+                    self.set_state(n, st)
         if self._pool is None:
             run()
         else:

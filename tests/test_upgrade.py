@@ -458,3 +458,41 @@ def test_daemonset_gpu_pod_with_drain_completes_the_upgrade():
             break
     assert states(c)["n0"] == U.DONE, seen
     assert U.DRAIN_REQUIRED in seen and seen.count(U.POD_DELETION_REQUIRED) <= 2, seen
+
+
+def test_async_worker_publishes_its_state_after_leaving_inflight():
+    """A worker's state label is the event that drives the next reconcile. Published while its node
+    was still in _inflight, an async next step (pod deletion -> drain) was skipped by that reconcile
+    and the node waited for the 2-minute requeue (the e2e upgrade timed out under load). The label
+    is now written after the node has left _inflight."""
+    import threading
+    from gpu_operator_amd.k8s.fake import FakeClient
+
+    node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": "n0", "labels": {}}}
+    c = FakeClient([node])
+    mgr = U.UpgradeStateManager(c, NS, run_async=True, workers=2)
+    seen = []
+    orig_patch = c.patch
+
+    def patch(av, kind, name, body, *a, **kw):
+        labels = ((body.get("metadata") or {}).get("labels") or {})
+        if U.UPGRADE_STATE_LABEL in labels:
+            with mgr._lock:
+                seen.append((labels[U.UPGRADE_STATE_LABEL], name in mgr._inflight))
+        return orig_patch(av, kind, name, body, *a, **kw)
+    c.patch = patch
+
+    def work():
+        mgr.set_state(c.get("v1", "Node", "n0"), U.DRAIN_REQUIRED)
+        assert o.get_labels(c.get("v1", "Node", "n0")).get(U.UPGRADE_STATE_LABEL) is None   # not yet
+    mgr._schedule("n0", work)
+    for _ in range(200):
+        if seen:
+            break
+        threading.Event().wait(0.01)
+    assert seen == [(U.DRAIN_REQUIRED, False)]
+    assert o.get_labels(c.get("v1", "Node", "n0"))[U.UPGRADE_STATE_LABEL] == U.DRAIN_REQUIRED
+    # and the reconcile that label triggers can schedule the next async step at once
+    ran = threading.Event()
+    mgr._schedule("n0", ran.set)
+    assert ran.wait(2)
