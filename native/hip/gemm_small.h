@@ -193,11 +193,11 @@ __device__ __forceinline__ void small_store_c(__bf16* __restrict__ C, int N, int
         C[(size_t)(row0 + i * 16 + e) * N + col0 + j * 16] = (__bf16)acc[i][j][e];
 }
 
-// v60 (BMT = 128) / v62 (BMT = 256: BMT x 128 tiles despite the name): one workgroup per output tile,
+// v60 (BMT = 128) / v62 (BMT = 256): one workgroup per BMT x 128 output tile,
 // the whole K. F8: A, Bt are fp8 e4m3fn bytes.
 template <bool F8, int BMT = 128>
 __global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
-gemm_mfma_128x128(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
+gemm_mfma_small(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
                   int K) {
   __shared__ __attribute__((aligned(16))) char lds[SmallCfg<BMT>::LDS];     // the only LDS object (trap 4a)
   const int tiles_n = N / S_BN, ntiles = (M / BMT) * tiles_n;
@@ -231,7 +231,7 @@ gemm_mfma_128x128(const void* __restrict__ A, const void* __restrict__ Bt, __bf1
 // (profiles/r5_small/sweep_streamk.jsonl).
 template <bool F8, int BMT = 128>
 __global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
-gemm_mfma_128x128_sk(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
+gemm_mfma_small_sk(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
                      int K, int splits, int pmajor, float* __restrict__ ws, int* __restrict__ cnt) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   using Cfg = SmallCfg<BMT>;

@@ -71,8 +71,8 @@ inline void launch_small(const void* a, const void* b, __bf16* c, int M, int N, 
   const int splits = split ? small_splits(tiles, nk, cus) : 1;
   SmallWorkspace* w = splits > 1 ? small_workspace(s, (size_t)tiles * splits * BMT * S_BN, tiles) : nullptr;
   if (w)
-    hipLaunchKernelGGL((gemm_mfma_128x128_sk<F8, BMT>), dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
+    hipLaunchKernelGGL((gemm_mfma_small_sk<F8, BMT>), dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
                        splits, nk / splits >= 32 ? 1 : 0, w->ws, w->cnt);
   else
-    hipLaunchKernelGGL((gemm_mfma_128x128<F8, BMT>), dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K);
+    hipLaunchKernelGGL((gemm_mfma_small<F8, BMT>), dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K);
 }

@@ -18,4 +18,9 @@ echo "bench (defaults)"; timeout -k 10 300 python bench.py > $OUT/bench.log 2>&1
 tail -1 $OUT/bench.log
 cd /tmp && export TMPDIR=/tmp
 echo "rocprof"; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 20 --no-extras > $GRAFT_REPO_ROOT/$OUT/bench_prof.log 2>&1
+echo "small-grid traces"
+for spec in "bf16 1024" "fp8 1024" "bf16 1024x1024x8192" "fp8 1024x1024x16384" "bf16 2560"; do
+  set -- $spec
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/trace_$1_$2 --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/gemm_prof.py --dtype $1 --variant p0 --size $2 --iters 100 > $GRAFT_REPO_ROOT/$OUT/trace_$1_$2.log 2>&1
+done
 echo done
