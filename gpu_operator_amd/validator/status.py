@@ -48,9 +48,19 @@ class StatusDir:
         return os.path.join(self.path, name)
 
     def create(self, name: str, payload: Optional[Dict[str, Any]] = None) -> None:
+        """Write barrier ``name`` atomically. A barrier that already exists keeps its first ``ts`` (the
+        moment the gate first opened, as the native writer in node_validate.cpp does) and records the
+        re-validation as ``revalidated_ts``."""
         self.ensure()
         body = dict(payload or {})
-        body.setdefault("ts", time.time())
+        now = time.time()
+        if "ts" not in body:
+            old = self.read(name)
+            first = old.get("ts") if isinstance(old, dict) else None
+            if isinstance(first, (int, float)):
+                body["ts"], body["revalidated_ts"] = first, now
+            else:
+                body["ts"] = now
         tmp = self.file(f".{name}.tmp.{os.getpid()}")
         with open(tmp, "w") as f:
             json.dump(body, f)
