@@ -6,7 +6,9 @@
 * bf16 operands: ``native/hip/gemm_bf16.hip`` (``gemm_bf16``);
 * fp8 OCP e4m3fn operands: ``native/hip/gemm_fp8.hip`` (``gemm_fp8``), the unscaled double-rate
   ``v_mfma_f32_16x16x128_f8f6f4`` (the block-scaled 32x32x64 form for short K), i.e. the matrix
-  cores' fp8 rate.
+  cores' fp8 rate;
+* small grids, both dtypes: ``native/hip/gemm_small.h`` (variants 60 / 61 / 62: 128x128 tiles,
+  their split-K form, 256x128 tiles).
 
 Replaces the reference validator's ``vectorAdd`` pass/fail probe
 (reference: validator/cuda-workload-validation.yaml:20) with a matrix-core

@@ -36,8 +36,10 @@
 //        +2.2 %, 8192^2x2048 +1.2 % over the plain pipeline, profiles/r4_sweep/lab_ilv_*.jsonl;
 //        gemm_w4ap.h): the power-of-two-K default for short K or one dispatch wave.
 //   60 (round 5) = 128x128 output tiles (gemm_small.h) for grids the 256x256 kernels leave mostly idle
-//        (a 256-tile grid of at most a quarter of the CUs) and for shapes only 128-tileable.
-//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 / 60 = that kernel pinned (no automatic switch; still falls back to a
+//        (a 256-tile grid of at most a quarter of the CUs) and for shapes only 128-tileable; 61 = its
+//        split-K form when the 128x128 grid is under the CU count and K leaves pieces of >= 16
+//        K-tiles; 62 = 256x128 tiles for 256-tile grids of a quarter to a half of the CUs.
+//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 / 60 / 61 / 62 = that kernel pinned (no automatic switch; still falls back to a
 //        kernel that can run the shape or the device).
 // The automatic choice is the first matching row of the declarative table kBf16Rules below (each row
 // cites its sweep); what each kernel needs, and where a pinned one falls back, is kBf16Needs. Both are
@@ -71,8 +73,9 @@
 // different GPUs (amd-gemm-validate --launch threads) never see each other's pin.
 static thread_local int g_variant = 0;
 
-// Persistent grid: one workgroup per CU (the 160 KiB LDS admits one), a multiple of the 8 XCDs,
-// never more workgroups than tiles. 0 when the device or the tile count is too small.
+// Persistent grid as the dispatch rules see it: one workgroup per CU (the 160 KiB LDS admits one), a
+// multiple of the 8 XCDs, never more workgroups than tiles. 0 when the device or the tile count is too
+// small. (The launch rounds up instead: persistent_launch_grid, gemm_tile_common.h.)
 static int persistent_grid(int nwg, int cus) {
   const int g = nwg < cus ? nwg : cus;
   return (g / NXCD) * NXCD;

@@ -31,7 +31,8 @@
 //   60 / 61 (round 5): the 128x128 small-grid kernel of the bf16 v60 / v61 (gemm_small.h) on the
 //       double-rate v_mfma_f32_16x16x128_f8f6f4, whole-tile or split-K, for grids the 256x256 tiling
 //       leaves mostly idle (and shapes only 128-tileable).
-//   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 / 60 / 61 = that kernel pinned (no automatic switch; falls back when the
+//   62 (round 5): the same frame in 256x128 tiles for 256-tile grids of a quarter to a half of the CUs.
+//   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 / 60 / 61 / 62 = that kernel pinned (no automatic switch; falls back when the
 //       shape or the device cannot run it).
 // q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
 // (profiles/r2_fp8_q16/): 8192^3 +5.3 %, 16384^3 +3.1 %, 4096^3 +4.1 %, 16384x8192x8192 +2.2 %.
