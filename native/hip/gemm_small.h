@@ -136,18 +136,25 @@ __device__ __forceinline__ void small_mainloop(const char* __restrict__ A, const
     s_i32x4 af[2][4], bf[2][NJ];
     const int q0 = lane >> 4, q1 = 4 + (lane >> 4);
     auto rd = [&](const char* base, int row, int q) { return *(const s_i32x4*)(base + s_swz(row + (lane & 15), q)); };
-    af[0][0] = rd(la, wm * 64, q0);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bf[0][j] = rd(lb, wn * TN + j * 16, q0);
-#pragma unroll
-    for (int i = 1; i < 4; ++i) af[0][i] = rd(la, wm * 64 + i * 16, q0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) af[1][i] = rd(la, wm * 64 + i * 16, q1);
     if constexpr (F8) {
-      // one 16x16x128 MFMA per accumulator over both chunks
+      // one 16x16x128 MFMA per accumulator over both chunks. Reads in the order the MFMAs (B column
+      // j outer, A row i inner) first need them -- A0, B0, A1, A2, A3, B1.. -- so each MFMA waits
+      // only for its own operands' reads
+      auto rda = [&](int i) { af[0][i] = rd(la, wm * 64 + i * 16, q0); af[1][i] = rd(la, wm * 64 + i * 16, q1); };
+      auto rdb = [&](int j) { bf[0][j] = rd(lb, wn * TN + j * 16, q0); bf[1][j] = rd(lb, wn * TN + j * 16, q1); };
+      rda(0);
+      rdb(0);
+      __builtin_amdgcn_sched_barrier(0);     // (pins the read order: the scheduler would reorder them)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bf[1][j] = rd(lb, wn * TN + j * 16, q1);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int i = 1; i < 4; ++i) {
+        rda(i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int j = 1; j < NJ; ++j) {
+        rdb(j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const s_i32x8 b8 = __builtin_shufflevector(bf[0][j], bf[1][j], 0, 1, 2, 3, 4, 5, 6, 7);
@@ -158,14 +165,22 @@ __device__ __forceinline__ void small_mainloop(const char* __restrict__ A, const
         }
       }
     } else {
+      af[0][0] = rd(la, wm * 64, q0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bf[0][j] = rd(lb, wn * TN + j * 16, q0);
+#pragma unroll
+      for (int i = 1; i < 4; ++i) af[0][i] = rd(la, wm * 64 + i * 16, q0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[1][i] = rd(la, wm * 64 + i * 16, q1);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bf[1][j] = rd(lb, wn * TN + j * 16, q1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((s_bf16x8)af[0][i], (s_bf16x8)bf[0][j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) bf[1][j] = rd(lb, wn * TN + j * 16, q1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
