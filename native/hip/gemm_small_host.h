@@ -19,6 +19,14 @@ inline int small_splits(int tiles, int nk, int cus) {
   if (tiles <= 0) return 1;
   int splits = small_split_target() * cus / tiles;
   if (splits > nk / 16) splits = nk / 16;
+  // pieces as short as 16 K-tiles only while that keeps the grid within half the chip: their
+  // reduction outweighs the extra CUs (1024^2x4096: 4 pieces of 16 on 256 CUs 330 TF/s, 2 of 32 on
+  // 128 CUs 355; fp8 1024^2x8192 661 -> 724; 512^2x8192 keeps 8 of 16 on 128 CUs;
+  // profiles/r5_small/sweep_piece32.jsonl)
+  if (splits > 1 && nk / splits <= 16) {
+    const int half = small_split_target() * cus / 2 / tiles;
+    if (half < splits) splits = half;
+  }
   return splits > 1 ? splits : 1;
 }
 

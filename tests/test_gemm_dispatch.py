@@ -70,8 +70,11 @@ def _r4_bf16(M, N, K, cus, g):
 
 def _splits(tiles, nk, cus, target=1):
     """v61's K pieces per tile (gemm_small_host.h small_splits): target x CUs / tiles, >= 16 K-tiles
-    a piece, 1 = none."""
-    return max(1, min(target * cus // tiles, nk // 16))
+    a piece, pieces of 16 only within half the chip, 1 = none."""
+    s = min(target * cus // tiles, nk // 16)
+    if s > 1 and nk // s <= 16:                 # 16-K-tile pieces only within half the chip
+        s = min(s, target * cus // 2 // tiles)
+    return max(1, s)
 
 
 def _small(M, N, K, cus):
