@@ -1,4 +1,4 @@
-// gfx950 bf16 / fp8 GEMM for small output grids (v60, v61):
+// gfx950 bf16 / fp8 GEMM for small output grids (v60, v61, v62):
 //
 //   C[M,N] (bf16) = A[M,K] * Bt[N,K]^T, A and Bt K-major, both bf16 or both fp8 e4m3fn, fp32 accumulation.
 //
@@ -10,21 +10,19 @@
 //
 // The 256x256 kernels own one output tile per CU: on a grid of 16 such tiles (1024^3) 16 of the 256
 // CUs work and each runs a 134 MFLOP tile alone (~14 us at one CU's matrix rate), so the dispatch is
-// bound by the per-CU MFMA time of a few CUs, not by the chip. This kernel cuts the work 4x finer:
+// bound by the per-CU MFMA time of a few CUs, not by the chip. This frame cuts the work finer:
 //
-//   * 128x128 output tile per workgroup; WAVES = 4: 2x2 waves of 64x64 (4x4 v_mfma_f32_16x16x32_bf16
-//     accumulators, 64 AGPRs); WAVES = 8: 2x4 waves of 64x32 (4x2 accumulators), two waves per SIMD;
-//   * K-step 64: one K-tile of A and of B is 16 KiB each, in a ring of 4 LDS buffers (below);
+//   * BMT x 128 output tiles (BMT = 128: v60 / v61; 256: v62), one 512-thread workgroup each, 8 waves
+//     (two per SIMD) of 64 x TN (SmallCfg below);
+//   * K-step 128 bytes, in an LDS ring of 4 K-tiles (128 rows) or 3 (256 rows);
 //   * LDS rows of 128 B hold 8 16-B chunks XOR-swizzled by (row & 7): the ds_read_b128 fragment reads
-//     (16 rows, one chunk column) spread over the banks -- 2-way at worst, the minimum for a 16-row
-//     b128 read;
+//     (16 rows, one chunk column) spread over the banks (SQ_LDS_BANK_CONFLICT 0, profiles/r5_small/);
 //   * XCD-aware tile order (bijective remap): the tiles one XCD runs are contiguous row-major, so
 //     they share A row panels in that XCD's L2.
 //
-// Shapes: M % 128 == 0, N % 128 == 0, K a multiple of one K-tile (host checks). v60 runs the whole K per tile;
-// v61 splits K over several workgroups per tile (below).
-//
-// (the 128 KiB ring admits one workgroup per CU.)
+// Shapes: M % BMT == 0, N % 128 == 0, K a multiple of one K-tile (host checks). v60 / v62 run the whole
+// K per tile; v61 splits K over several workgroups per tile (below). One workgroup per CU (the ring is
+// 128 or 144 KiB of the CU's 160).
 #pragma once
 
 #include "gemm_tile_common.h"
