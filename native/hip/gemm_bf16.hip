@@ -242,6 +242,8 @@ int amdgo_gemm_set_split_target(int t) {
 int amdgo_gemm_small_splits(int M, int N, int K, int cus) {
   return small_splits((M / S_BM) * (N / S_BN), K / S_BK, cus);
 }
+// The launch grid of the persistent 256x256 kernels for `nwg` tiles on `cus` CUs (gemm_tile_common.h).
+int amdgo_gemm_persistent_launch_grid(int nwg, int cus) { return persistent_launch_grid(nwg, cus); }
 int amdgo_gemm_resolve_variant(int M, int N, int K) { return resolve_variant(M, N, K, nullptr); }
 // The dispatch as a pure function of the shape, the device's CU count and a pinned variant (no GPU
 // needed: the CPU tests check the table against the rules it replaced).

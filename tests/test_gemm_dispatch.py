@@ -224,3 +224,18 @@ def test_the_pinned_variant_is_per_thread(lib):
     t.join()
     assert got == [0] and lib.amdgo_gemm_fp8_get_variant() == 22
     lib.amdgo_gemm_fp8_set_variant(0)
+
+
+def test_persistent_launch_grid_rounds_up_to_whole_xcd_groups(lib):
+    """A grid of fewer tiles than CUs gets every tile in the first round: 100 tiles -> 104 workgroups
+    (13 per XCD; rounding down to 96 had run 4 tiles in a second round at half the throughput)."""
+    g = lib.amdgo_gemm_persistent_launch_grid
+    assert g(100, 256) == 104 and g(81, 256) == 88 and g(64, 256) == 64 and g(1, 256) == 8
+    assert g(256, 256) == 256 and g(1024, 256) == 256          # one workgroup per CU
+    assert g(300, 304) == 304 and g(303, 304) == 304            # 304 CUs: 38 per XCD
+    for nwg in range(1, 600):
+        for cus in (80, 256, 304):
+            n = g(nwg, cus)
+            assert n % 8 == 0 and n <= cus
+            if nwg <= (cus // 8) * 8:
+                assert n // 8 >= -(-nwg // 8)           # workgroups per XCD >= its tiles: one round
