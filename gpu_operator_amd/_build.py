@@ -91,12 +91,12 @@ def _pyext_name(stem: str) -> str:
 # read the *_lab.h headers (every schedule), which mask the production ones (tools/gen_*_asm_loop.py).
 GEMM_HEADERS = ["include/gemm_tile_common.h", "hip/gemm_bf16_kernels.h", "hip/gemm_bf16_asm_loop.h",
                 "hip/gemm_fp8_kernels.h", "hip/gemm_fp8_asm_loop.h", "hip/gemm_w4ap.h", "hip/gemm_small.h",
-                "hip/gemm_small_host.h"]
+                "hip/gemm_small_host.h", "hip/gemm_raster_host.h"]
 LAB_HEADERS = GEMM_HEADERS + ["hip/gemm_bf16_asm_loop_lab.h", "hip/gemm_fp8_asm_loop_lab.h"]
 
 TARGETS: List[Target] = [
     # GPU compute: validator workloads (GEMM, smoke). Loaded via ctypes by ops/.
-    Target("libamdgo_hip.so", ["hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/smoke.hip"], "hip-shared",
+    Target("libamdgo_hip.so", ["hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/gemm_abft.hip", "hip/smoke.hip"], "hip-shared",
            headers=GEMM_HEADERS),
     # Node agent library (sysfs/KFD topology, partitions, telemetry, inotify barriers).
     Target(_pyext_name("_amdnode"), ["node/pybind.cpp", "node/amdnode.cpp"], "pyext",
@@ -105,8 +105,8 @@ TARGETS: List[Target] = [
            flags=["-static-libstdc++", "-static-libgcc"], headers=["include/amdnode.h"]),
     # Validator workload binaries (run inside the validation pods).
     # (one worker process per GPU: the launcher enumerates the GPUs from KFD sysfs, libamdnode)
-    Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/smoke.hip",
-                                     "node/amdnode.cpp"],
+    Target("bin/amd-gemm-validate", ["hip/gemm_validate.cpp", "hip/gemm_bf16.hip", "hip/gemm_fp8.hip", "hip/gemm_abft.hip",
+                                     "hip/smoke.hip", "node/amdnode.cpp"],
            "hip-exe", flags=["-x", "hip"], headers=GEMM_HEADERS + ["include/amdnode.h"]),
     Target("bin/amd-hip-smoke", ["hip/hip_smoke_main.cpp", "hip/smoke.hip"], "hip-exe", flags=["-x", "hip"]),
     Target("bin/amd-rccl-validate", ["hip/rccl_validate.cpp", "node/amdnode.cpp"], "hip-exe", flags=["-x", "hip"],

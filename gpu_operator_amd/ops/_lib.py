@@ -63,6 +63,25 @@ def load() -> ctypes.CDLL:
             getattr(lib, f).restype = i
         lib.amdgo_gemm_fp8_get_variant.restype = i
         lib.amdgo_gemm_get_variant.restype = i
+        ip = ctypes.POINTER(ctypes.c_int)
+        for f in ("amdgo_gemm_bf16_raster", "amdgo_gemm_fp8_raster"):
+            getattr(lib, f).argtypes = [i, i, i, ip, ip, ip, i]
+            getattr(lib, f).restype = i
+        for f in ("amdgo_gemm_bf16_raster_for", "amdgo_gemm_fp8_raster_for"):
+            getattr(lib, f).argtypes = [i, i, i, i, ip, ip, ip, i]
+            getattr(lib, f).restype = i
+        for f in ("amdgo_gemm_bf16_placed", "amdgo_gemm_fp8_placed"):
+            getattr(lib, f).argtypes = [vp, vp, vp, i, i, i, vp, vp]
+            getattr(lib, f).restype = i
+        lib.amdgo_abft_workspace_bytes.argtypes = [i, i, i, i, i]
+        lib.amdgo_abft_workspace_bytes.restype = ctypes.c_longlong
+        lib.amdgo_abft_check.argtypes = [i, vp, vp, vp, i, i, i, i, i, vp, ctypes.c_longlong, ip,
+                                         ctypes.POINTER(ctypes.c_float), vp]
+        lib.amdgo_abft_check.restype = i
+        lib.amdgo_abft_inject.argtypes = [vp, i, i, i, i, ctypes.c_float, vp]
+        lib.amdgo_abft_inject.restype = i
+        lib.amdgo_gemm_small_workspace_count.argtypes = [i]
+        lib.amdgo_gemm_small_workspace_count.restype = i
         for f in ("amdgo_gemm_tile_m", "amdgo_gemm_tile_n", "amdgo_gemm_tile_k",
                   "amdgo_gemm_fp8_tile_m", "amdgo_gemm_fp8_tile_n", "amdgo_gemm_fp8_tile_k"):
             getattr(lib, f).restype = i

@@ -203,5 +203,113 @@ def verify(a, bt, c, nrows: int = 64, seed: int = 0, rows: Optional[list] = None
     return GemmCheck(float(err.max()), max_rel, tol, max_rel <= tol)
 
 
+# ---------------------------------------------------------------------------------------------
+# The dispatch's raster and the ABFT check (native/hip/gemm_raster_host.h, gemm_abft.hip)
+# ---------------------------------------------------------------------------------------------
+RASTER_KINDS = ("generic", "grid", "grid_sq", "persistent", "persistent_sq", "small")
+
+
+@dataclass
+class Raster:
+    """Which workgroup of a launch computes which output tile: ``owner[tm][tn][piece]`` is the linear
+    block id, ``round`` the iteration of its tile loop (persistent grids)."""
+    variant: int
+    kind: str
+    tile_m: int
+    tile_n: int
+    tiles_m: int
+    tiles_n: int
+    grid: int
+    pieces: int
+    owner: list
+    round: list
+
+
+def raster(m: int, n: int, k: int, dtype: str = "bf16", cus: Optional[int] = None) -> Raster:
+    """The raster of the kernel the dispatch picks for this shape -- on a device with ``cus`` CUs
+    (no GPU needed), or on the current device."""
+    import ctypes
+
+    lib = _lib.load()
+    info = (ctypes.c_int * 8)()
+    ip = ctypes.POINTER(ctypes.c_int)
+    fn_for = lib.amdgo_gemm_fp8_raster_for if dtype == "fp8" else lib.amdgo_gemm_bf16_raster_for
+    fn_cur = lib.amdgo_gemm_fp8_raster if dtype == "fp8" else lib.amdgo_gemm_bf16_raster
+
+    def call(owners, rounds, cap):
+        if cus is None:
+            return fn_cur(m, n, k, info, owners, rounds, cap)
+        return fn_for(m, n, k, cus, info, owners, rounds, cap)
+
+    call(ctypes.cast(None, ip), ctypes.cast(None, ip), 0)
+    cap = info[4] * info[5] * info[7]
+    owners, rounds = (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+    if call(owners, rounds, cap) < 0:
+        raise RuntimeError("raster: capacity")
+    tm, tn, p = info[4], info[5], info[7]
+    own = [[[owners[(a * tn + b) * p + q] for q in range(p)] for b in range(tn)] for a in range(tm)]
+    rnd = [[[rounds[(a * tn + b) * p + q] for q in range(p)] for b in range(tn)] for a in range(tm)]
+    return Raster(info[0], RASTER_KINDS[info[1]], info[2], info[3], tm, tn, info[6], p, own, rnd)
+
+
+def gemm_placed(a, bt, out, placement, fp8: bool = False):
+    """One GEMM through the placement-recording kernels: workgroup b writes its HW_REG_XCC_ID and
+    HW_REG_HW_ID to ``placement[2b]``, ``[2b+1]`` (an int32 GPU tensor with room for the raster's grid)."""
+    import torch
+
+    m, k = a.shape
+    n = bt.shape[0]
+    lib = _lib.load()
+    fn = lib.amdgo_gemm_fp8_placed if fp8 else lib.amdgo_gemm_bf16_placed
+    _lib.check(fn(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k, placement.data_ptr(),
+                  _stream_ptr(torch, a.device)), "gemm_placed")
+    return out
+
+
+@dataclass
+class AbftResult:
+    tile_flags: list         # [tiles_m][tiles_n]: bit 0 a row sum failed, bit 1 a column sum
+    worst_ratio: float       # max |sum - expected| / tolerance (< 1 when clean)
+
+    @property
+    def bad_tiles(self) -> list:
+        return [(i, j) for i, row in enumerate(self.tile_flags) for j, f in enumerate(row) if f]
+
+
+def abft_check(a, bt, c, tile_m: int, tile_n: int) -> AbftResult:
+    """The ABFT check of ``c == a @ bt.T`` in ``tile_m`` x ``tile_n`` tiles (native/hip/gemm_abft.hip):
+    every element covered by one row and one column checksum, the failing tiles named."""
+    import ctypes
+    import torch
+
+    m, k = a.shape
+    n = bt.shape[0]
+    lib = _lib.load()
+    nbytes = lib.amdgo_abft_workspace_bytes(m, n, k, tile_m, tile_n)
+    ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=a.device)
+    tm, tn = -(-m // tile_m), -(-n // tile_n)
+    flags = (ctypes.c_int * (tm * tn))()
+    worst = ctypes.c_float(0.0)
+    dt = 1 if a.dtype == torch.float8_e4m3fn else 0
+    _lib.check(lib.amdgo_abft_check(dt, a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, tile_m, tile_n,
+                                    ws.data_ptr(), nbytes, flags, ctypes.byref(worst),
+                                    _stream_ptr(torch, a.device)), "abft_check")
+    return AbftResult([[flags[i * tn + j] for j in range(tn)] for i in range(tm)], float(worst.value))
+
+
+def abft_inject_(c, row: int, col: int, delta: float) -> None:
+    """Test hook: ``c[row, col] += delta`` on the GPU, ordered on the current stream."""
+    import torch
+
+    m, n = c.shape
+    _lib.check(_lib.load().amdgo_abft_inject(c.data_ptr(), m, n, row, col, float(delta),
+                                             _stream_ptr(torch, c.device)), "abft_inject")
+
+
+def small_workspace_count(device: int) -> int:
+    """v61 split-K workspace sets the library holds for ``device`` (capped, LRU)."""
+    return _lib.load().amdgo_gemm_small_workspace_count(int(device))
+
+
 def tflops(m: int, n: int, k: int, seconds: float) -> float:
     return 2.0 * m * n * k / seconds / 1e12

@@ -53,6 +53,7 @@
 #include <mutex>
 
 #include "gemm_bf16_kernels.h"
+#include "gemm_raster_host.h"
 #include "gemm_small_host.h"
 
 // K-tile schedules of the persistent asm pipeline (gemm_bf16_asm_loop.h, tools/gen_bf16_asm_loop.py):
@@ -224,6 +225,9 @@ static int resolve_variant(int M, int N, int K, hipStream_t s) {
 
 extern "C" {
 
+int amdgo_ref_rows(int dtype, const void* A, const void* Bt, const int* rows, int nrows, float* out, int N, int K,
+                   void* stream);
+
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
   if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50 &&
@@ -242,6 +246,8 @@ int amdgo_gemm_set_split_target(int t) {
 int amdgo_gemm_small_splits(int M, int N, int K, int cus) {
   return small_splits((M / S_BM) * (N / S_BN), K / S_BK, cus);
 }
+// v61 split-K workspace sets held for device `dev` (at most kSmallWorkspaces; gemm_small_host.h).
+int amdgo_gemm_small_workspace_count(int dev) { return small_workspace_count(dev); }
 // The launch grid of the persistent 256x256 kernels for `nwg` tiles on `cus` CUs (gemm_tile_common.h).
 int amdgo_gemm_persistent_launch_grid(int nwg, int cus) { return persistent_launch_grid(nwg, cus); }
 int amdgo_gemm_resolve_variant(int M, int N, int K) { return resolve_variant(M, N, K, nullptr); }
@@ -256,10 +262,14 @@ const char* amdgo_gemm_plan_bf16_evidence(int M, int N, int K, int cus) {
   return "";
 }
 
-// Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
-int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
+}  // extern "C"
+
+// The dispatch of one GEMM. REC: the placement-recording instantiations of the same kernels (the
+// checked dispatch of amd-gemm-validate, gemm_tile_common.h note_placement); REC = kTimed is every
+// other launch, and its kernels carry no record code.
+template <Rec REC>
+static int gemm_bf16_dispatch(const void* A, const void* Bt, void* C, int M, int N, int K, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
-  hipStream_t s = (hipStream_t)stream;
   const auto* a = (const __bf16*)A;
   const auto* b = (const __bf16*)Bt;
   auto* c = (__bf16*)C;
@@ -270,73 +280,129 @@ int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K,
   switch (variant_now) {
     case 60:
     case 61:
-      launch_small<false>(a, b, c, M, N, K, s, cus, variant_now == 61);
+      launch_small<false, 128, REC>(a, b, c, M, N, K, s, cus, variant_now == 61);
       break;
     case 62:
-      launch_small<false, 256>(a, b, c, M, N, K, s, cus, false);
+      launch_small<false, 256, REC>(a, b, c, M, N, K, s, cus, false);
       break;
     case 18:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
-                         a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, false, false, true, false, REC>), dim3(nwg),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 25:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, false, true>), dim3(persistent(nwg)),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4sp<17, 19, 5, 80, 40, false, true, REC>), dim3(persistent(nwg)),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 42:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
-                         a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 0, true, false, true, false, REC>), dim3(nwg),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 44:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true>), dim3(nwg), dim3(W4_THREADS), 0, s,
-                         a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true, false, REC>), dim3(nwg),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 47:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true, true>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true, true, REC>), dim3(nwg),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 48:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, true, true>), dim3(nwg),
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, true, true, REC>), dim3(nwg),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 45:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, true>), dim3(nwg), dim3(W4_THREADS),
-                         0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, true, true, false, REC>), dim3(nwg),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 50:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent(nwg)),
-                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, false, W4AP_EPI_STAGED_ZC, 0, REC>),
+                         dim3(persistent(nwg)), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 51:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(W4_THREADS), 0, s,
-                         a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_MAIN, true, true, W4AP_EPI_STAGED_ZC, 0, REC>), dim3(256),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 53:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 1>), dim3(persistent(nwg)),
-                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_STAGED_ZC, 1, REC>),
+                         dim3(persistent(nwg)), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 54:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC, 1>), dim3(256), dim3(W4_THREADS),
-                         0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_STAGED_ZC, 1, REC>), dim3(256),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 55:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN, 2>), dim3(persistent(nwg)),
-                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, false, W4AP_EPI_LEAN, 2, REC>),
+                         dim3(persistent(nwg)), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 56:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN_ILV, 2>), dim3(256), dim3(W4_THREADS),
-                         0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4VP_SC_G4_ZC, true, true, W4AP_EPI_LEAN_ILV, 2, REC>), dim3(256),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 52:
-      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC>), dim3(persistent(nwg)),
-                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC, 0, REC>),
+                         dim3(persistent(nwg)), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {
       dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
-      hipLaunchKernelGGL(gemm_bf16_generic, grid, dim3(256), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL(gemm_bf16_generic<REC>, grid, dim3(256), 0, s, a, b, c, M, N, K);
     }
   }
   return (int)hipGetLastError();
+}
+
+// The raster of the kernel the dispatch picks for a shape on the current device: output tile, launch
+// grid and how workgroups walk the tiles (gemm_raster_host.h) -- what the ABFT check needs to name the
+// workgroup behind a bad tile.
+static GemmRaster raster_bf16(int M, int N, int K, int cus) {
+  const int v = plan_bf16(M, N, K, cus, g_variant);
+  const int nwg = (M / BM) * (N / BN);
+  switch (v) {
+    case 60:
+    case 61: {
+      const int tiles = (M / S_BM) * (N / S_BN);
+      const int nk = K * 2 / 128;
+      const int splits = v == 61 ? small_splits(tiles, nk, cus) : 1;
+      return GemmRaster::small(v, S_BM, S_BN, splits, small_piece_major(nk, splits));
+    }
+    case 62:
+      return GemmRaster::small(v, 256, S_BN, 1, 0);
+    case 18: case 42: case 44: case 47:
+      return GemmRaster::grid_of(v, BM, BN, nwg, false);
+    case 45: case 48:
+      return GemmRaster::grid_of(v, BM, BN, nwg, true);
+    case 25: case 50: case 52: case 53: case 55:
+      return GemmRaster::persistent(v, BM, BN, persistent_launch_grid(nwg, cus), false);
+    case 51: case 54: case 56:
+      return GemmRaster::persistent(v, BM, BN, 256, true);
+    default:
+      return GemmRaster::generic(v, GBM, GBN);
+  }
+}
+
+extern "C" {
+
+// Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
+int amdgo_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
+  return gemm_bf16_dispatch<kTimed>(A, Bt, C, M, N, K, (hipStream_t)stream);
+}
+
+// The same GEMM through the placement-recording kernels: workgroup b of the dispatch writes
+// {HW_REG_XCC_ID, HW_REG_HW_ID} to placement[2b], [2b+1] (device memory, room for the raster's grid).
+int amdgo_gemm_bf16_placed(const void* A, const void* Bt, void* C, int M, int N, int K, uint32_t* placement,
+                           void* stream) {
+  const hipError_t e = set_placement_record((hipStream_t)stream, placement);
+  if (e != hipSuccess) return (int)e;
+  return gemm_bf16_dispatch<kRecord>(A, Bt, C, M, N, K, (hipStream_t)stream);
+}
+
+// The dispatch's raster for a shape on the current device: fills `info` (GemmRasterInfo fields, see
+// gemm_raster_host.h) and, when `owners` is non-null, the owning workgroup and round of every
+// (tile, piece) -- `cap` ints per array. Returns the tile count, or -1 when `cap` is too small.
+int amdgo_gemm_bf16_raster(int M, int N, int K, int* info, int* owners, int* rounds, int cap) {
+  return raster_fill(raster_bf16(M, N, K, device_cu_count(nullptr)), M, N, info, owners, rounds, cap);
+}
+// The same for a device with `cus` CUs (no GPU needed: the CPU tests check every raster is a bijection).
+int amdgo_gemm_bf16_raster_for(int M, int N, int K, int cus, int* info, int* owners, int* rounds, int cap) {
+  return raster_fill(raster_bf16(M, N, K, cus), M, N, info, owners, rounds, cap);
 }
 
 // Force the generic kernel (independent implementation used by tests).
@@ -344,17 +410,15 @@ int amdgo_gemm_bf16_generic(const void* A, const void* Bt, void* C, int M, int N
                             void* stream) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
-  hipLaunchKernelGGL(gemm_bf16_generic, grid, dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(gemm_bf16_generic<kTimed>, grid, dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
   return (int)hipGetLastError();
 }
 
-int amdgo_gemm_ref_rows(const void* A, const void* Bt, const int* rows, int nrows, float* out,
-                        int N, int K, void* stream) {
-  dim3 grid((N + 255) / 256, nrows);
-  hipLaunchKernelGGL(gemm_ref_rows, grid, dim3(256), 0, (hipStream_t)stream,
-                     (const __bf16*)A, (const __bf16*)Bt, rows, nrows, out, N, K);
-  return (int)hipGetLastError();
+// fp32 reference of sampled rows (gemm_abft.hip, one wave per output column).
+int amdgo_gemm_ref_rows(const void* A, const void* Bt, const int* rows, int nrows, float* out, int N, int K,
+                        void* stream) {
+  return amdgo_ref_rows(0, A, Bt, rows, nrows, out, N, K, stream);
 }
 
 int amdgo_fill_uniform_bf16(void* p, size_t n, uint32_t seed, void* stream) {

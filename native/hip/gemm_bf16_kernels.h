@@ -8,7 +8,7 @@
 //                               without 256 CUs), v18 = neither;
 //   * gemm_bf16_256x256_w4sp -- v25: v18 made persistent (short K, several tiles per CU);
 //   * gemm_bf16_generic      -- bounds-checked 64x64-tile MFMA kernel for every other shape;
-//   * gemm_ref_rows / fill_uniform_bf16 -- scalar fp32 reference rows and the operand filler.
+//   * fill_uniform_bf16 -- the operand filler (the fp32 reference rows live in gemm_abft.hip).
 // Design notes and measurements: docs/validator-gemm.md, profiles/r1_*.
 #pragma once
 
@@ -85,12 +85,13 @@ __host__ __device__ constexpr int w4s_r0_at(int b2, int rs, int i) {
 // (The round-2 knock-out timings that priced each of these parts are recorded in
 // profiles/r2_sched/README.md; the knock-out builds themselves were retired from the tree.)
 template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, int SERP = 0, bool ROT = false,
-          bool SQ = false, bool VK = false, bool PA = false>
+          bool SQ = false, bool VK = false, bool PA = false, Rec REC = kTimed>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4s(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
   static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  note_placement<REC>();
 
   const int tiles_m = M / BM;
   const int tiles_n = N / BN;
@@ -701,11 +702,12 @@ gemm_bf16_256x256_w4a(const __bf16* __restrict__ A, const __bf16* __restrict__ B
 }
 
 // w4ap (v50-v52): w4a made persistent; the frame is shared with the fp8 kernel (gemm_w4ap.h).
-template <int SC = 0, bool SERP = true, bool SQ = false, int EPI = 0, int DM = 0>
+template <int SC = 0, bool SERP = true, bool SQ = false, int EPI = 0, int DM = 0, Rec REC = kTimed>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
+  note_placement<REC>();
   w4ap_run<SC, SERP, SQ, false, EPI, DM>((const char*)A, (const char*)Bt, C, M, N, K, smem);
 }
 
@@ -721,12 +723,14 @@ gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ 
 constexpr int W4P_EPI_WAVE = 8192;                       // 32 rows x 128 cols x bf16
 constexpr int W4P_LDS = LDS_BYTES + 4 * W4P_EPI_WAVE;     // 160 KiB
 
-template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, bool SERP = false, bool VK = false>
+template <int B1 = 17, int D0 = 19, int DS = 5, int B2 = 80, int RS = 40, bool SERP = false, bool VK = false,
+          Rec REC = kTimed>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
   static_assert(B1 >= 16 && D0 > B1 && D0 + 15 * DS < 127 && B2 > B1 && B2 + RS < 127, "schedule");
   __shared__ __attribute__((aligned(16))) char smem[W4P_LDS];
+  note_placement<REC>();
 
   const int tiles_m = M / BM;
   const int tiles_n = N / BN;
@@ -927,11 +931,13 @@ gemm_bf16_256x256_w4sp(const __bf16* __restrict__ A, const __bf16* __restrict__ 
 // implementation for cross-checking the fast path.
 constexpr int GBM = 64, GBN = 64, GBK = 32;
 
+template <Rec REC = kTimed>
 __global__ void __launch_bounds__(256)
 gemm_bf16_generic(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                   __bf16* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) __bf16 sa[GBM][GBK + 8];
   __shared__ __attribute__((aligned(16))) __bf16 sb[GBN][GBK + 8];
+  note_placement<REC>();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -981,20 +987,6 @@ gemm_bf16_generic(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
         const int col = n0 + wc * 32 + j * 16 + 4 * (lane >> 4) + e;
         if (row < M && col < N) C[(size_t)row * N + col] = (__bf16)acc[i][j][e];
       }
-}
-
-// fp32-accumulating reference (one thread per output element; sampled rows only).
-__global__ void gemm_ref_rows(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                              const int* __restrict__ rows, int nrows, float* __restrict__ out,
-                              int N, int K) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ri = blockIdx.y;
-  if (col >= N || ri >= nrows) return;
-  const __bf16* a = A + (size_t)rows[ri] * K;
-  const __bf16* b = Bt + (size_t)col * K;
-  float s = 0.f;
-  for (int k = 0; k < K; ++k) s += (float)a[k] * (float)b[k];
-  out[(size_t)ri * N + col] = s;
 }
 
 // Deterministic uniform [-1,1) bf16 fill (counter-based hash), so validator runs on

@@ -39,6 +39,7 @@
 // Fast path: M % 256 == 0, N % 256 == 0, K % 128 == 0, K >= 256; otherwise the generic kernel.
 
 #include "gemm_fp8_kernels.h"
+#include "gemm_raster_host.h"
 #include "gemm_small_host.h"
 
 // The variant a caller pinned (amdgo_gemm_fp8_set_variant): per host thread (see gemm_bf16.hip).
@@ -46,7 +47,7 @@ static thread_local int g_fp8_variant = 0;
 
 // q16 schedule (lab v28 / v32): free barrier after slot 17, DMA pieces at slots 18, 21, .., 63,
 // landing wait at 34, B0' reads from slot 35, A0' reads from 43 (block 2 walks A0 slowly).
-#define Q16(SERP, SQ) (gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, SERP, SQ, 2, 2, true>)
+#define Q16(SERP, SQ, REC) (gemm_fp8_256x256_q16<16, 18, 3, 34, 35, 43, SERP, SQ, 2, 2, true, false, REC>)
 
 // What the dispatch knows about a shape on a device.
 struct Fp8Shape {
@@ -165,6 +166,9 @@ static int resolve_fp8_variant(int M, int N, int K, hipStream_t s) {
 
 extern "C" {
 
+int amdgo_ref_rows(int dtype, const void* A, const void* Bt, const int* rows, int nrows, float* out, int N, int K,
+                   void* stream);
+
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
   if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21 && v != 22 && v != 23 &&
@@ -183,10 +187,12 @@ const char* amdgo_gemm_plan_fp8_evidence(int M, int N, int K, int cus) {
   return "";
 }
 
-// Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
-int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
+}  // extern "C"
+
+// The dispatch of one GEMM; REC: the placement-recording instantiations (see gemm_bf16.hip).
+template <Rec REC>
+static int gemm_fp8_dispatch(const void* A, const void* Bt, void* C, int M, int N, int K, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
-  hipStream_t s = (hipStream_t)stream;
   const auto* a = (const uint8_t*)A;
   const auto* b = (const uint8_t*)Bt;
   auto* c = (__bf16*)C;
@@ -197,65 +203,115 @@ int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, 
   switch (variant_now) {
     case 60:
     case 61:
-      launch_small<true>(a, b, c, M, N, K, s, cus, variant_now == 61);
+      launch_small<true, 128, REC>(a, b, c, M, N, K, s, cus, variant_now == 61);
       break;
     case 62:
-      launch_small<true, 256>(a, b, c, M, N, K, s, cus, false);
+      launch_small<true, 256, REC>(a, b, c, M, N, K, s, cus, false);
       break;
     case 10:
-      hipLaunchKernelGGL((gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6>), dim3(pgrid), dim3(F8_THREADS), 0, s,
+      hipLaunchKernelGGL((gemm_fp8_256x256_w4sp<6, 7, 16, 24, 6, false, REC>), dim3(pgrid), dim3(F8_THREADS), 0, s,
                          a, b, c, M, N, K);
       break;
     case 18:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16p<>), dim3(pgrid), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16p<16, 18, 3, 34, 35, 43, false, 2, 2, true, REC>), dim3(pgrid),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 20:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, false, false, W4AP_EPI_STAGED_ZC>), dim3(pgrid), dim3(F8_THREADS), 0, s,
-                         a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, false, false, W4AP_EPI_STAGED_ZC, 0, REC>), dim3(pgrid),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 21:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC>), dim3(256), dim3(F8_THREADS), 0, s,
-                         a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8AP_SC_P_ZC, true, true, W4AP_EPI_STAGED_ZC, 0, REC>), dim3(256),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 22:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN_ILV, 2>), dim3(256), dim3(F8_THREADS), 0, s,
-                         a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, true, true, W4AP_EPI_LEAN_ILV, 2, REC>), dim3(256),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 23:
-      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, false, false, W4AP_EPI_LEAN, 2>), dim3(pgrid), dim3(F8_THREADS),
-                         0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, false, false, W4AP_EPI_LEAN, 2, REC>), dim3(pgrid),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 15:
-      hipLaunchKernelGGL(Q16(32, false), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL(Q16(32, false, REC), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 16:
-      hipLaunchKernelGGL(Q16(32, true), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL(Q16(32, true, REC), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     case 17:
-      hipLaunchKernelGGL(Q16(0, false), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL(Q16(0, false, REC), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
     default: {
       dim3 grid((N + G8 - 1) / G8, (M + G8 - 1) / G8);
-      hipLaunchKernelGGL(gemm_fp8_generic, grid, dim3(256), 0, s, a, b, c, M, N, K);
+      hipLaunchKernelGGL(gemm_fp8_generic<REC>, grid, dim3(256), 0, s, a, b, c, M, N, K);
     }
   }
   return (int)hipGetLastError();
 }
 
+// The raster of the kernel the dispatch picks for a shape on the current device (gemm_raster_host.h).
+static GemmRaster raster_fp8(int M, int N, int K, int cus) {
+  const int v = plan_fp8(M, N, K, cus, g_fp8_variant);
+  const int nwg = (M / F8_BM) * (N / F8_BN);
+  switch (v) {
+    case 60:
+    case 61: {
+      const int tiles = (M / S_BM) * (N / S_BN);
+      const int nk = K / 128;
+      const int splits = v == 61 ? small_splits(tiles, nk, cus) : 1;
+      return GemmRaster::small(v, S_BM, S_BN, splits, small_piece_major(nk, splits));
+    }
+    case 62:
+      return GemmRaster::small(v, 256, S_BN, 1, 0);
+    case 15: case 17:
+      return GemmRaster::grid_of(v, F8_BM, F8_BN, nwg, false);
+    case 16:
+      return GemmRaster::grid_of(v, F8_BM, F8_BN, nwg, true);
+    case 10: case 18: case 20: case 23:
+      return GemmRaster::persistent(v, F8_BM, F8_BN, persistent_launch_grid(nwg, cus), false);
+    case 21: case 22:
+      return GemmRaster::persistent(v, F8_BM, F8_BN, 256, true);
+    default:
+      return GemmRaster::generic(v, G8, G8);
+  }
+}
+
+extern "C" {
+
+// Returns 0 on success, a hipError_t value otherwise. `stream` may be null.
+int amdgo_gemm_fp8(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
+  return gemm_fp8_dispatch<kTimed>(A, Bt, C, M, N, K, (hipStream_t)stream);
+}
+
+// The placement-recording dispatch (amdgo_gemm_bf16_placed).
+int amdgo_gemm_fp8_placed(const void* A, const void* Bt, void* C, int M, int N, int K, uint32_t* placement,
+                          void* stream) {
+  const hipError_t e = set_placement_record((hipStream_t)stream, placement);
+  if (e != hipSuccess) return (int)e;
+  return gemm_fp8_dispatch<kRecord>(A, Bt, C, M, N, K, (hipStream_t)stream);
+}
+
+// The dispatch's raster (amdgo_gemm_bf16_raster).
+int amdgo_gemm_fp8_raster(int M, int N, int K, int* info, int* owners, int* rounds, int cap) {
+  return raster_fill(raster_fp8(M, N, K, device_cu_count(nullptr)), M, N, info, owners, rounds, cap);
+}
+// The same for a device with `cus` CUs (no GPU needed: the CPU tests check every raster is a bijection).
+int amdgo_gemm_fp8_raster_for(int M, int N, int K, int cus, int* info, int* owners, int* rounds, int cap) {
+  return raster_fill(raster_fp8(M, N, K, cus), M, N, info, owners, rounds, cap);
+}
+
 int amdgo_gemm_fp8_generic(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((N + G8 - 1) / G8, (M + G8 - 1) / G8);
-  hipLaunchKernelGGL(gemm_fp8_generic, grid, dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(gemm_fp8_generic<kTimed>, grid, dim3(256), 0, (hipStream_t)stream,
                      (const uint8_t*)A, (const uint8_t*)Bt, (__bf16*)C, M, N, K);
   return (int)hipGetLastError();
 }
 
-int amdgo_gemm_fp8_ref_rows(const void* A, const void* Bt, const int* rows, int nrows, float* out,
-                            int N, int K, void* stream) {
-  dim3 grid((N + 255) / 256, nrows);
-  hipLaunchKernelGGL(gemm_fp8_ref_rows, grid, dim3(256), 0, (hipStream_t)stream,
-                     (const uint8_t*)A, (const uint8_t*)Bt, rows, nrows, out, N, K);
-  return (int)hipGetLastError();
+// fp32 reference of sampled rows (gemm_abft.hip, software e4m3 decode).
+int amdgo_gemm_fp8_ref_rows(const void* A, const void* Bt, const int* rows, int nrows, float* out, int N, int K,
+                            void* stream) {
+  return amdgo_ref_rows(1, A, Bt, rows, nrows, out, N, K, stream);
 }
 
 int amdgo_fill_uniform_fp8(void* p, size_t n, uint32_t seed, void* stream) {

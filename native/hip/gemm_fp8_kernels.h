@@ -303,10 +303,11 @@ __device__ __forceinline__ void f8q_mfma(const i32x8& b, const i32x8& a) {
 // a0 dies at slot 35, a1 at 39, ... (else every A0 fragment lives to slot 47). Block 1 always walks
 // B0 slowly (b0 dies at slot 19, b1 at 23, ...).
 template <int W1 = 16, int D0 = 18, int DS = 1, int W2 = 34, int RB0 = 36, int RA0 = 48, int SERP = 0,
-          bool SQ = false, int RBS = 2, int RAS = 2, bool ASLOW = false, bool VK = false>
+          bool SQ = false, int RBS = 2, int RAS = 2, bool ASLOW = false, bool VK = false, Rec REC = kTimed>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                      __bf16* __restrict__ C, int M, int N, int K) {
+  note_placement<REC>();
   constexpr int SLOTS = 64;
   constexpr auto rb_ok = [] {
     for (int j = 0; j < 4; ++j) {
@@ -480,10 +481,11 @@ gemm_fp8_256x256_q16(const uint8_t* __restrict__ A, const uint8_t* __restrict__ 
 constexpr int F8P_EPI_WAVE = 8192;                        // 32 rows x 128 cols x bf16
 constexpr int F8P_LDS = F8_LDS + 4 * F8P_EPI_WAVE;        // 160 KiB
 
-template <int B1 = 6, int D0 = 7, int DSPAN = 16, int B2 = 24, int RS = 6, bool SERP = false>
+template <int B1 = 6, int D0 = 7, int DSPAN = 16, int B2 = 24, int RS = 6, bool SERP = false, Rec REC = kTimed>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
+  note_placement<REC>();
   constexpr int SLOTS = 32;
   static_assert(B1 >= 4 && D0 >= B1 && D0 + DSPAN <= SLOTS && B2 >= 16 && B2 > B1 && B2 + RS < SLOTS,
                 "schedule");
@@ -704,10 +706,11 @@ gemm_fp8_256x256_w4sp(const uint8_t* __restrict__ A, const uint8_t* __restrict__
 // that zeroes the accumulators as it reads them) around the q16 iteration (unscaled 16x16x128,
 // quarter-block slot order, the production placement). For short K with several tiles per CU.
 template <int W1 = 16, int D0 = 18, int DS = 3, int W2 = 34, int RB0 = 35, int RA0 = 43, bool SERP = false,
-          int RBS = 2, int RAS = 2, bool ASLOW = true>
+          int RBS = 2, int RAS = 2, bool ASLOW = true, Rec REC = kTimed>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                       __bf16* __restrict__ C, int M, int N, int K) {
+  note_placement<REC>();
   constexpr int SLOTS = 64;
   static_assert(W1 >= 15 && D0 > W1 && D0 + 15 * DS < SLOTS && W2 > W1 && RB0 > W2 && RA0 > W2, "schedule");
   __shared__ __attribute__((aligned(16))) char smem[F8P_LDS];
@@ -908,11 +911,12 @@ gemm_fp8_256x256_q16p(const uint8_t* __restrict__ A, const uint8_t* __restrict__
 // q16 K-tile body as one hand-scheduled asm block per output tile (tools/gen_fp8_asm_loop.py,
 // gemm_fp8_asm_loop.h): the same MFMAs, operands and accumulators as q16p, waits computed per
 // fragment instead of hipcc's, no per-piece SALU address arithmetic or s_nop.
-template <int SC = 0, bool SERP = false, bool SQ = false, int EPI = 0, int DM = 0>
+template <int SC = 0, bool SERP = false, bool SQ = false, int EPI = 0, int DM = 0, Rec REC = kTimed>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_q16ap(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                        __bf16* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
+  note_placement<REC>();
   w4ap_run<SC, SERP, SQ, true, EPI, DM>((const char*)A, (const char*)Bt, C, M, N, K, smem);
 }
 
@@ -930,11 +934,13 @@ __device__ __forceinline__ float e4m3_to_f32(uint8_t v) {
 constexpr int G8 = 64, G8K = 32;
 
 // Bounds-checked 64x64 tiles, operands decoded to fp32 in LDS, 4x4 outputs per thread.
+template <Rec REC = kTimed>
 __global__ void __launch_bounds__(256)
 gemm_fp8_generic(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
                  __bf16* __restrict__ C, int M, int N, int K) {
   __shared__ float sa[G8K][G8 + 1];
   __shared__ float sb[G8K][G8 + 1];
+  note_placement<REC>();
   const int m0 = blockIdx.y * G8, n0 = blockIdx.x * G8;
   const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
   float acc[4][4] = {};
@@ -968,20 +974,6 @@ gemm_fp8_generic(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
       const int r = m0 + tr * 4 + i, c = n0 + tc * 4 + j;
       if (r < M && c < N) C[(size_t)r * N + c] = (__bf16)acc[i][j];
     }
-}
-
-// fp32 reference of sampled output rows (one thread per output element).
-__global__ void gemm_fp8_ref_rows(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt,
-                                  const int* __restrict__ rows, int nrows, float* __restrict__ out,
-                                  int N, int K) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ri = blockIdx.y;
-  if (col >= N || ri >= nrows) return;
-  const uint8_t* a = A + (size_t)rows[ri] * K;
-  const uint8_t* b = Bt + (size_t)col * K;
-  float s = 0.f;
-  for (int k = 0; k < K; ++k) s = fmaf(e4m3_to_f32(a[k]), e4m3_to_f32(b[k]), s);
-  out[(size_t)ri * N + col] = s;
 }
 
 // Deterministic uniform [-1,1) fill, rounded to e4m3fn by the hardware converter (OCP on gfx950).

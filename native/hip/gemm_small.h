@@ -208,11 +208,12 @@ __device__ __forceinline__ void small_store_c(__bf16* __restrict__ C, int N, int
 
 // v60 (BMT = 128) / v62 (BMT = 256): one workgroup per BMT x 128 output tile,
 // the whole K. F8: A, Bt are fp8 e4m3fn bytes.
-template <bool F8, int BMT = 128>
+template <bool F8, int BMT = 128, Rec REC = kTimed>
 __global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
 gemm_mfma_small(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
                   int K) {
   __shared__ __attribute__((aligned(16))) char lds[SmallCfg<BMT>::LDS];     // the only LDS object (trap 4a)
+  note_placement<REC>();
   const int tiles_n = N / S_BN, ntiles = (M / BMT) * tiles_n;
   const int tile = xcd_remap(blockIdx.x, ntiles);
   const int tm = tile / tiles_n, tn = tile % tiles_n;
@@ -242,13 +243,14 @@ gemm_mfma_small(const void* __restrict__ A, const void* __restrict__ Bt, __bf16*
 // (458 vs 207). A stream-K even share of grids larger than the chip (pieces cut at offsets that differ
 // from workgroup to workgroup) lost the panel sharing and ran 35-40 % below v60
 // (profiles/r5_small/sweep_streamk.jsonl).
-template <bool F8, int BMT = 128>
+template <bool F8, int BMT = 128, Rec REC = kTimed>
 __global__ void __launch_bounds__(S_THREADS, 1) __attribute__((amdgpu_waves_per_eu(S_WAVES / 4, S_WAVES / 4)))
 gemm_mfma_small_sk(const void* __restrict__ A, const void* __restrict__ Bt, __bf16* __restrict__ C, int M, int N,
                      int K, int splits, int pmajor, float* __restrict__ ws, int* __restrict__ cnt) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   using Cfg = SmallCfg<BMT>;
   __shared__ __attribute__((aligned(16))) char lds[Cfg::LDS];     // the only LDS object (trap 4a)
+  note_placement<REC>();
   int* flag = (int*)(lds + Cfg::NBUF * Cfg::TILEB);
   const int tid = threadIdx.x;
   const int tiles_n = N / S_BN, ntiles = (M / BMT) * tiles_n;

@@ -4,6 +4,8 @@
 
 #include <map>
 #include <mutex>
+#include <thread>
+#include <tuple>
 #include <utility>
 
 #include "gemm_small.h"
@@ -30,57 +32,144 @@ inline int small_splits(int tiles, int nk, int cus) {
   return splits > 1 ? splits : 1;
 }
 
+// v61's item order: piece-major for pieces of >= 32 K-tiles (gemm_small.h, gemm_mfma_small_sk).
+inline int small_piece_major(int nk, int splits) { return nk / splits >= 32 ? 1 : 0; }
+
 // v61's fp32 partials (one 128x128 slab per workgroup) and per-tile arrival counters, one set per
 // (device, stream): two GEMMs in flight on different streams never share them; a launch on one stream
-// resets its counters before it ends, so the next launch there finds them zero. Allocated on first
-// use, never shrunk.
+// resets its counters before it ends, so the next launch there finds them zero. The device is the
+// stream's (hipStreamGetDevice), not the caller's current one, and the allocation is made on it: a
+// launch on a cuda:1 stream while the current device is 0 must not get GPU 0 memory. The per-thread
+// stream handle names a different stream in every host thread, so its key includes the thread.
+// At most kSmallWorkspaces sets per device, least recently used evicted: a process that cycles streams
+// (torch side streams, a stream per request) would otherwise grow HBM use without bound. Each set
+// carries an event recorded after its last launch; eviction waits on that event, never on the stream
+// (which the caller may have destroyed).
 struct SmallWorkspace {
   float* ws = nullptr;
   int* cnt = nullptr;
   size_t floats = 0;
   int counters = 0;
+  hipEvent_t done = nullptr;   // after the last launch that used this set
+  uint64_t used = 0;           // LRU clock
 };
 
+constexpr int kSmallWorkspaces = 16;   // per device
+
+struct SmallWorkspaceKey {
+  int dev;
+  hipStream_t s;
+  std::thread::id tid;   // only for the per-thread stream handle
+  bool operator<(const SmallWorkspaceKey& o) const { return std::tie(dev, s, tid) < std::tie(o.dev, o.s, o.tid); }
+};
+
+// Runs `f` with `dev` current, then restores the caller's device.
+template <class F>
+inline auto on_device(int dev, F&& f) {
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != dev) (void)hipSetDevice(dev);
+  auto r = f();
+  if (prev != dev && prev >= 0) (void)hipSetDevice(prev);
+  return r;
+}
+
+inline void small_workspace_release(SmallWorkspace& w) {
+  if (w.done) (void)hipEventSynchronize(w.done);
+  if (w.ws) (void)hipFree(w.ws);
+  if (w.cnt) (void)hipFree(w.cnt);
+  if (w.done) (void)hipEventDestroy(w.done);
+  w = SmallWorkspace{};
+}
+
+struct SmallWorkspaces {
+  std::mutex mu;
+  std::map<SmallWorkspaceKey, SmallWorkspace> all;
+  uint64_t clock = 0;
+};
+
+inline SmallWorkspaces& small_workspaces() {
+  static SmallWorkspaces* w = new SmallWorkspaces();   // never destroyed: no teardown-order hazard at exit
+  return *w;
+}
+
+// Workspace sets currently held for `dev` (the GPU test of the LRU cap reads it).
+inline int small_workspace_count(int dev) {
+  SmallWorkspaces& W = small_workspaces();
+  std::lock_guard<std::mutex> lk(W.mu);
+  int n = 0;
+  for (const auto& kv : W.all) n += kv.first.dev == dev;
+  return n;
+}
+
 inline SmallWorkspace* small_workspace(hipStream_t s, size_t floats, int tiles) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SmallWorkspace> all;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  SmallWorkspace& w = all[{dev, s}];
-  if (w.floats < floats) {
-    // a larger partial buffer: the old one may still be read by a launch in flight on this stream
-    if (w.ws && hipStreamSynchronize(s) != hipSuccess) return nullptr;
-    if (w.ws) (void)hipFree(w.ws);
-    w.ws = nullptr;
-    w.floats = 0;
-    if (hipMalloc(&w.ws, floats * sizeof(float)) != hipSuccess) return nullptr;
-    w.floats = floats;
+  if (s != nullptr && s != hipStreamPerThread) {
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) return nullptr;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    return nullptr;
   }
-  if (w.counters < tiles) {
-    if (w.cnt && hipStreamSynchronize(s) != hipSuccess) return nullptr;
-    if (w.cnt) (void)hipFree(w.cnt);
-    w.cnt = nullptr;
-    w.counters = 0;
-    const int n = tiles < 1024 ? 1024 : tiles;
-    if (hipMalloc(&w.cnt, n * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(w.cnt, 0, n * sizeof(int), s) != hipSuccess) return nullptr;
-    w.counters = n;
+  const SmallWorkspaceKey key{dev, s, s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id()};
+  SmallWorkspaces& W = small_workspaces();
+  std::lock_guard<std::mutex> lk(W.mu);
+  auto it = W.all.find(key);
+  if (it == W.all.end()) {
+    // a new set: evict this device's least recently used one at the cap
+    int held = 0;
+    auto lru = W.all.end();
+    for (auto j = W.all.begin(); j != W.all.end(); ++j)
+      if (j->first.dev == dev) {
+        ++held;
+        if (lru == W.all.end() || j->second.used < lru->second.used) lru = j;
+      }
+    if (held >= kSmallWorkspaces && lru != W.all.end()) {
+      on_device(dev, [&] { small_workspace_release(lru->second); return 0; });
+      W.all.erase(lru);
+    }
+    it = W.all.emplace(key, SmallWorkspace{}).first;
   }
-  return &w;
+  SmallWorkspace& w = it->second;
+  w.used = ++W.clock;
+  const bool ok = on_device(dev, [&] {
+    if (!w.done && hipEventCreateWithFlags(&w.done, hipEventDisableTiming) != hipSuccess) return false;
+    if (w.floats < floats) {
+      // a larger partial buffer: the old one may still be read by a launch in flight on this stream
+      if (w.ws && hipEventSynchronize(w.done) != hipSuccess) return false;
+      if (w.ws) (void)hipFree(w.ws);
+      w.ws = nullptr;
+      w.floats = 0;
+      if (hipMalloc(&w.ws, floats * sizeof(float)) != hipSuccess) return false;
+      w.floats = floats;
+    }
+    if (w.counters < tiles) {
+      if (w.cnt && hipEventSynchronize(w.done) != hipSuccess) return false;
+      if (w.cnt) (void)hipFree(w.cnt);
+      w.cnt = nullptr;
+      w.counters = 0;
+      const int n = tiles < 1024 ? 1024 : tiles;
+      if (hipMalloc(&w.cnt, n * sizeof(int)) != hipSuccess) return false;
+      if (hipMemsetAsync(w.cnt, 0, n * sizeof(int), s) != hipSuccess) return false;
+      w.counters = n;
+    }
+    return true;
+  });
+  return ok ? &w : nullptr;
 }
 
 // v60 (split = false) or v61: split-K when the grid has pieces to give, else v60. Host guarantees M, N multiples
 // of 128 and K a whole number of 128-byte K-tiles.
-template <bool F8, int BMT = 128>
+// REC: the placement-recording instantiations (gemm_tile_common.h note_placement).
+template <bool F8, int BMT = 128, Rec REC = kTimed>
 inline void launch_small(const void* a, const void* b, __bf16* c, int M, int N, int K, hipStream_t s, int cus, bool split) {
   const int tiles = (M / BMT) * (N / S_BN);
   const int nk = (int)((size_t)K * (F8 ? 1 : 2) / 128);
   const int splits = split ? small_splits(tiles, nk, cus) : 1;
   SmallWorkspace* w = splits > 1 ? small_workspace(s, (size_t)tiles * splits * BMT * S_BN, tiles) : nullptr;
-  if (w)
-    hipLaunchKernelGGL((gemm_mfma_small_sk<F8, BMT>), dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N, K,
-                       splits, nk / splits >= 32 ? 1 : 0, w->ws, w->cnt);
-  else
-    hipLaunchKernelGGL((gemm_mfma_small<F8, BMT>), dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K);
+  if (w) {
+    hipLaunchKernelGGL((gemm_mfma_small_sk<F8, BMT, REC>), dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N,
+                       K, splits, small_piece_major(nk, splits), w->ws, w->cnt);
+    (void)hipEventRecord(w->done, s);
+  } else {
+    hipLaunchKernelGGL((gemm_mfma_small<F8, BMT, REC>), dim3(tiles), dim3(S_THREADS), 0, s, a, b, c, M, N, K);
+  }
 }

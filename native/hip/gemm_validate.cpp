@@ -4,7 +4,8 @@
 //
 // Runs the hand-written CDNA4 MFMA GEMMs -- bf16 (gemm_bf16.hip) and/or fp8 e4m3fn on the
 // double-rate matrix-core path (gemm_fp8.hip) -- concurrently on the selected GPUs on uniform
-// [-1,1) operands; checks sampled output rows against an independent fp32 reference kernel; prints
+// [-1,1) operands; checks every output element (ABFT tile checksums, below) and sampled rows against an
+// independent fp32 reference kernel; prints
 // one JSON line per (dtype, GPU, shape) and an aggregate line.
 //
 // One process per GPU (--launch processes, the default): this process never
@@ -66,7 +67,16 @@
 //                     [--warmup 5] [--devices all|0,1,...] [--scaling 1,2,4,8] [--check-rows 32]
 //                     [--min-tflops X] [--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R]
 //                     [--stabilise-max-s 6] [--no-stabilise] [--smoke] [--launch processes|threads]
-//                     [--min-window-ms 100] [--ramp-ms 60] [--pre-timed-idle-ms 0]
+//                     [--min-window-ms 100] [--ramp-ms 60] [--pre-timed-idle-ms 0] [--inject-fault TM,TN[,DELTA]]
+//
+// Correctness (every set, every GPU): after the timed loop, C is poisoned with NaN and one more dispatch
+// runs through the placement-recording instantiation of the same kernel (each workgroup stores the XCD
+// and CU it ran on); the ABFT check (gemm_abft.hip) then verifies every output element through per-tile
+// row and column checksums and names each bad tile, the workgroup that computed it (the dispatch's raster,
+// gemm_raster_host.h), its XCD and CU: {"kind":"correctness","tile":[TM,TN],"xcd":X,"cu":{..}}. The
+// --check-rows sampled rows against an independent fp32 reference stay as a second opinion.
+// --inject-fault TM,TN[,DELTA] adds DELTA (default 64) to one element of tile (TM, TN) of that C, between
+// the dispatch and the check (the GPU test of the naming).
 //
 // --smoke first runs hip-smoke (smoke.hip: the vectorAdd analogue, every element checked on the
 // host) on each selected GPU and prints its `hip-smoke` line -- in the workers, so the validator's
@@ -110,6 +120,16 @@ int amdgo_gemm_fp8_ref_rows(const void* A, const void* Bt, const int* rows, int 
                             int K, void* stream);
 int amdgo_fill_uniform_fp8(void* p, size_t n, uint32_t seed, void* stream);
 int amdgo_vector_add_f32(const float* a, const float* b, float* c, size_t n, void* stream);
+int amdgo_gemm_bf16_placed(const void* A, const void* Bt, void* C, int M, int N, int K, uint32_t* placement,
+                           void* stream);
+int amdgo_gemm_fp8_placed(const void* A, const void* Bt, void* C, int M, int N, int K, uint32_t* placement,
+                          void* stream);
+int amdgo_gemm_bf16_raster(int M, int N, int K, int* info, int* owners, int* rounds, int cap);
+int amdgo_gemm_fp8_raster(int M, int N, int K, int* info, int* owners, int* rounds, int cap);
+long long amdgo_abft_workspace_bytes(int M, int N, int K, int TM, int TN);
+int amdgo_abft_check(int dtype, const void* A, const void* Bt, const void* C, int M, int N, int K, int TM, int TN,
+                     void* ws, long long ws_bytes, int* tile_flags, float* worst_ratio, void* stream);
+int amdgo_abft_inject(void* C, int M, int N, int row, int col, float delta, void* stream);
 }
 
 static constexpr size_t kSmokeElements = 50000;
@@ -146,16 +166,22 @@ static void print_smoke(size_t devices, int failures) {
   std::fflush(stdout);
 }
 
-// One operand precision: element size plus its GEMM, reference and fill entry points.
+// One operand precision: element size plus its GEMM, reference and fill entry points, the
+// placement-recording dispatch and raster of the checked dispatch, and its ABFT operand code.
 struct DType {
   const char* name;
   size_t esize;
   int (*gemm)(const void*, const void*, void*, int, int, int, void*);
   int (*ref_rows)(const void*, const void*, const int*, int, float*, int, int, void*);
   int (*fill)(void*, size_t, uint32_t, void*);
+  int (*placed)(const void*, const void*, void*, int, int, int, uint32_t*, void*);
+  int (*raster)(int, int, int, int*, int*, int*, int);
+  int abft_dtype;
 };
-static const DType kBf16{"bf16", 2, amdgo_gemm_bf16, amdgo_gemm_ref_rows, amdgo_fill_uniform_bf16};
-static const DType kFp8{"fp8_e4m3fn", 1, amdgo_gemm_fp8, amdgo_gemm_fp8_ref_rows, amdgo_fill_uniform_fp8};
+static const DType kBf16{"bf16", 2, amdgo_gemm_bf16, amdgo_gemm_ref_rows, amdgo_fill_uniform_bf16,
+                         amdgo_gemm_bf16_placed, amdgo_gemm_bf16_raster, 0};
+static const DType kFp8{"fp8_e4m3fn", 1, amdgo_gemm_fp8, amdgo_gemm_fp8_ref_rows, amdgo_fill_uniform_fp8,
+                        amdgo_gemm_fp8_placed, amdgo_gemm_fp8_raster, 1};
 
 static const DType* dtype_by_name(const std::string& n) {
   if (n == kBf16.name) return &kBf16;
@@ -202,6 +228,8 @@ struct Shape {
 
 struct Options {
   int iters = 50, warmup = 5, check_rows = 32;
+  int inject_tm = -1, inject_tn = -1;   // --inject-fault TM,TN[,DELTA]: perturb one element of that tile
+  double inject_delta = 64.0;
   double stabilise_max_s = 6.0;
   double min_window_ms = 100.0;   // the timed loop covers at least this much GPU time
   double ramp_ms = 60.0;          // re-ramp after the rendezvous: at least this much GPU time (profiles/r5_ramp)
@@ -209,27 +237,42 @@ struct Options {
   bool stabilise = true;
 };
 
+// The ABFT check of the checked dispatch (gemm_abft.hip): every output element covered, a failing
+// tile named with the workgroup that computed it and, from that dispatch's placement record, the
+// XCD and CU it ran on.
+struct AbftOut {
+  bool ran = false;
+  int variant = -1, tile_m = 0, tile_n = 0, bad_tiles = 0;
+  double worst_ratio = 0, checked_fraction = 0, check_ms = 0, abft_ms = 0;
+  // the first bad tile (row-major order): its workgroup (piece 0), round, XCD (-1: pieces of a split-K
+  // tile ran on different XCDs, see `list`) and hardware id fields
+  int tm = -1, tn = -1, wg = -1, round = -1, xcd = -1, se = -1, sh = -1, cu = -1;
+  std::string list;   // up to 8 bad tiles "tm.tn.xcd" joined by ';' ("-": none)
+};
+
 struct Result {
   int device = 0;
   Shape s{};
-  double tflops = 0, ms = 0, max_rel_err = 0, stab_spread = -1, stab_ms = 0;
+  double tflops = 0, ms = 0, max_rel_err = 0, stab_spread = -1, stab_ms = 0, probe_ms = 0;
   int stab_dispatches = 0, iters = 0, ramp = 0;
   bool launched = false, ok = false, oom = false;
   size_t need_bytes = 0, free_bytes = 0;
+  AbftOut abft;
   std::string error;
 };
 
 // Every device object of one run_one call; freed on every return path.
 struct Resources {
-  void *A = nullptr, *B = nullptr, *C = nullptr;
+  void *A = nullptr, *B = nullptr, *C = nullptr, *abft_ws = nullptr;
   float* ref = nullptr;
   int* rows = nullptr;
+  uint32_t* placement = nullptr;
   hipStream_t st = nullptr;
   std::vector<hipEvent_t> events;
   ~Resources() {
     if (st) (void)hipStreamSynchronize(st);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
-    for (void* p : {A, B, C, (void*)ref, (void*)rows})
+    for (void* p : {A, B, C, abft_ws, (void*)ref, (void*)rows, (void*)placement})
       if (p) (void)hipFree(p);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -349,10 +392,26 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   CHECK(hipSetDevice(dev));
   Resources res;  // declared after Arrive: freed (and the stream drained) before the rendezvous
   CHECK(hipStreamCreateWithFlags(&res.st, hipStreamNonBlocking));
+  const auto t_probe = std::chrono::steady_clock::now();
   const size_t na = (size_t)s.m * s.k, nb = (size_t)s.n * s.k, nc = (size_t)s.m * s.n;
   const int check_rows = std::max(1, std::min(o.check_rows, s.m));
+  // the checked dispatch's raster: its output tile (the ABFT strips), launch grid (the placement
+  // record's size) and the ABFT workspace
+  int info[8] = {0};
+  dt.raster(s.m, s.n, s.k, info, nullptr, nullptr, 0);
+  const int tile_m = info[2], tile_n = info[3], tiles_m = info[4], tiles_n = info[5], grid = info[6],
+            pieces = info[7];
+  const long long abft_bytes = amdgo_abft_workspace_bytes(s.m, s.n, s.k, tile_m, tile_n);
+  if (abft_bytes < 0 || grid <= 0) {
+    r.error = "no ABFT layout for this shape";
+    return false;
+  }
+  r.abft.variant = info[0];
+  r.abft.tile_m = tile_m;
+  r.abft.tile_n = tile_n;
   // what this shape needs against what the GPU has free: a tenant may hold most of the HBM
-  r.need_bytes = na * dt.esize + nb * dt.esize + nc * 2 + (size_t)check_rows * s.n * 4 + (size_t)check_rows * 4;
+  r.need_bytes = na * dt.esize + nb * dt.esize + nc * 2 + (size_t)check_rows * s.n * 4 + (size_t)check_rows * 4 +
+                 (size_t)abft_bytes + (size_t)grid * 8;
   size_t total = 0;
   CHECK(hipMemGetInfo(&r.free_bytes, &total));
   if (r.need_bytes > r.free_bytes) {
@@ -371,7 +430,8 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
     return false;
   };
   if (!alloc(&res.A, na * dt.esize, "A") || !alloc(&res.B, nb * dt.esize, "B") || !alloc(&res.C, nc * 2, "C") ||
-      !alloc((void**)&res.ref, (size_t)check_rows * s.n * 4, "ref") || !alloc((void**)&res.rows, check_rows * 4, "rows"))
+      !alloc((void**)&res.ref, (size_t)check_rows * s.n * 4, "ref") || !alloc((void**)&res.rows, check_rows * 4, "rows") ||
+      !alloc(&res.abft_ws, (size_t)abft_bytes, "abft") || !alloc((void**)&res.placement, (size_t)grid * 8, "placement"))
     return false;
   if (dt.fill(res.A, na, 1000 + dev, res.st) || dt.fill(res.B, nb, 2000 + dev, res.st)) {
     r.error = "fill failed";
@@ -420,7 +480,69 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   r.ms = ms / r.iters;
   r.tflops = 2.0 * s.m * s.n * (double)s.k / (r.ms * 1e-3) / 1e12;
   r.launched = true;
-  // correctness on sampled rows against the independent fp32 reference kernel
+  // The checked dispatch: C poisoned with NaN (a tile nobody writes fails, a stale one cannot pass
+  // for fresh), one dispatch through the placement-recording instantiation of the same kernel, then
+  // the ABFT check of every output element; the sampled fp32 rows are a second opinion on that C.
+  const auto t_check = std::chrono::steady_clock::now();
+  CHECK(hipMemsetAsync(res.C, 0xFF, nc * 2, res.st));
+  CHECK(hipMemsetAsync(res.placement, 0xFF, (size_t)grid * 8, res.st));
+  if (const int err = dt.placed(res.A, res.B, res.C, s.m, s.n, s.k, res.placement, res.st)) {
+    r.error = std::string("checked dispatch: ") + hipGetErrorString((hipError_t)err);
+    return false;
+  }
+  if (o.inject_tm >= 0 && o.inject_tn >= 0) {
+    const int row = std::min(s.m - 1, o.inject_tm * tile_m + tile_m / 2);
+    const int col = std::min(s.n - 1, o.inject_tn * tile_n + tile_n / 3);
+    if (amdgo_abft_inject(res.C, s.m, s.n, row, col, (float)o.inject_delta, res.st)) {
+      r.error = "inject failed";
+      return false;
+    }
+  }
+  std::vector<int> flags((size_t)tiles_m * tiles_n, 0);
+  float worst = 0.f;
+  const auto t_abft = std::chrono::steady_clock::now();
+  if (const int err = amdgo_abft_check(dt.abft_dtype, res.A, res.B, res.C, s.m, s.n, s.k, tile_m, tile_n, res.abft_ws,
+                                       abft_bytes, flags.data(), &worst, res.st)) {
+    r.error = std::string("ABFT check: ") + hipGetErrorString((hipError_t)err);
+    return false;
+  }
+  const auto ms_since = [](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  };
+  AbftOut& ab = r.abft;
+  ab.abft_ms = ms_since(t_abft);
+  ab.ran = true;
+  ab.worst_ratio = worst;
+  ab.checked_fraction = 1.0;   // every element is in one row sum and one column sum (gemm_abft.hip)
+  for (int f : flags) ab.bad_tiles += f != 0;
+  if (ab.bad_tiles) {
+    // name the bad tiles: raster -> workgroup (per piece) -> that workgroup's placement record
+    std::vector<int> owners((size_t)tiles_m * tiles_n * pieces), rounds(owners.size());
+    std::vector<uint32_t> place((size_t)grid * 2);
+    dt.raster(s.m, s.n, s.k, info, owners.data(), rounds.data(), (int)owners.size());
+    CHECK(hipMemcpy(place.data(), res.placement, place.size() * 4, hipMemcpyDeviceToHost));
+    int listed = 0;
+    for (int t = 0; t < tiles_m * tiles_n; ++t) {
+      if (!flags[t]) continue;
+      int xcd = -2, wg = -1, round = -1;
+      uint32_t hw = 0xFFFFFFFFu;
+      for (int p = 0; p < pieces; ++p) {
+        const int b = owners[(size_t)t * pieces + p];
+        const int x = b >= 0 && b < grid && place[2 * b] != 0xFFFFFFFFu ? (int)(place[2 * b] & 0xF) : -1;
+        if (p == 0) wg = b, round = rounds[(size_t)t * pieces], hw = b >= 0 && b < grid ? place[2 * b + 1] : hw;
+        xcd = xcd == -2 ? x : (xcd == x ? xcd : -1);
+      }
+      if (ab.tm < 0) {
+        ab.tm = t / tiles_n, ab.tn = t % tiles_n, ab.wg = wg, ab.round = round, ab.xcd = xcd;
+        if (hw != 0xFFFFFFFFu) ab.cu = (hw >> 8) & 0xF, ab.sh = (hw >> 12) & 1, ab.se = (hw >> 13) & 7;
+      }
+      if (listed++ < 8)
+        ab.list += (ab.list.empty() ? "" : ";") + std::to_string(t / tiles_n) + "." + std::to_string(t % tiles_n) + "." +
+                   std::to_string(xcd);
+    }
+  }
+  if (ab.list.empty()) ab.list = "-";
+  // second opinion: sampled rows against the independent fp32 reference kernel
   std::vector<int> hrows(check_rows);
   for (int i = 0; i < check_rows; ++i) hrows[i] = (int)(((uint64_t)i * 2654435761u + dev) % s.m);
   CHECK(hipMemcpyAsync(res.rows, hrows.data(), check_rows * 4, hipMemcpyHostToDevice, res.st));
@@ -432,18 +554,28 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   std::vector<uint16_t> hc((size_t)s.n);
   CHECK(hipMemcpyAsync(href.data(), res.ref, href.size() * 4, hipMemcpyDeviceToHost, res.st));
   CHECK(hipStreamSynchronize(res.st));
-  double worst = 0;
+  double worst_rel = 0;
   for (int i = 0; i < check_rows; ++i) {
     CHECK(hipMemcpy(hc.data(), (uint16_t*)res.C + (size_t)hrows[i] * s.n, s.n * 2, hipMemcpyDeviceToHost));
     for (int j = 0; j < s.n; ++j) {
       const double got = bf16_to_f32(hc[j]), want = href[(size_t)i * s.n + j];
       const double rel = std::fabs(got - want) / std::max(1.0, std::fabs(want));
-      worst = std::max(worst, rel);
+      worst_rel = std::isnan(rel) ? INFINITY : std::max(worst_rel, rel);
     }
   }
-  r.max_rel_err = worst;
-  r.ok = std::isfinite(worst) && worst <= 1.0 / 128;
-  if (!r.ok) r.error = "check failed: max_rel_err " + std::to_string(worst);
+  r.max_rel_err = worst_rel;
+  ab.check_ms = ms_since(t_check);
+  const bool rows_ok = std::isfinite(worst_rel) && worst_rel <= 1.0 / 128;
+  r.ok = rows_ok && ab.bad_tiles == 0;
+  if (ab.bad_tiles) {
+    char buf[192];
+    std::snprintf(buf, sizeof buf, "ABFT: %d bad tile(s), first [%d,%d] (workgroup %d, XCD %d)%s", ab.bad_tiles, ab.tm,
+                  ab.tn, ab.wg, ab.xcd, rows_ok ? "" : "; sampled rows also wrong");
+    r.error = buf;
+  } else if (!rows_ok) {
+    r.error = "check failed: max_rel_err " + std::to_string(worst_rel);
+  }
+  r.probe_ms = ms_since(t_probe);
   return true;
 }
 
@@ -520,6 +652,46 @@ static const char* failure_kind(const Result& r, bool floor_ok) {
   return "";
 }
 
+// The ABFT fields of a gemm line: coverage, margin, cost, and the first bad tile named by workgroup,
+// XCD and CU (gemm_abft.hip; the placement record of the checked dispatch).
+static std::string abft_json(const Result& r) {
+  const AbftOut& a = r.abft;
+  if (!a.ran) return "";
+  char buf[512];
+  std::snprintf(buf, sizeof buf,
+                ",\"checked_fraction\":%.3f,\"abft_worst_ratio\":%.4f,\"bad_tiles\":%d,\"variant\":%d,\"tile_m\":%d,"
+                "\"tile_n\":%d,\"check_ms\":%.3f,\"abft_ms\":%.3f,\"probe_ms\":%.1f",
+                a.checked_fraction, std::isfinite(a.worst_ratio) ? a.worst_ratio : 1e30, a.bad_tiles, a.variant, a.tile_m,
+                a.tile_n, a.check_ms, a.abft_ms, r.probe_ms);
+  std::string out = buf;
+  if (a.bad_tiles > 0) {
+    std::snprintf(buf, sizeof buf, ",\"tile\":[%d,%d],\"workgroup\":%d,\"round\":%d,\"xcd\":", a.tm, a.tn, a.wg,
+                  a.round);
+    out += buf;
+    out += a.xcd >= 0 ? std::to_string(a.xcd) : "null";
+    if (a.cu >= 0) {
+      std::snprintf(buf, sizeof buf, ",\"cu\":{\"se\":%d,\"sh\":%d,\"cu\":%d}", a.se, a.sh, a.cu);
+      out += buf;
+    }
+    // "tm.tn.xcd;..." -> [[tm,tn,xcd],...]
+    std::string lst = ",\"bad_tile_list\":[";
+    size_t pos = 0;
+    bool first = true;
+    while (a.list != "-" && pos < a.list.size()) {
+      size_t e = a.list.find(';', pos);
+      std::string item = a.list.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
+      pos = e == std::string::npos ? a.list.size() : e + 1;
+      int tm = 0, tn = 0, x = 0;
+      if (std::sscanf(item.c_str(), "%d.%d.%d", &tm, &tn, &x) != 3) continue;
+      lst += (first ? "[" : ",[") + std::to_string(tm) + "," + std::to_string(tn) + "," +
+             (x >= 0 ? std::to_string(x) : std::string("null")) + "]";
+      first = false;
+    }
+    out += lst + "]";
+  }
+  return out;
+}
+
 // The per-GPU lines and the aggregate of one set (results in slot order).
 static Aggregate report_set(const Set& set, std::vector<Result>& res, double floor, double single, double min_eff) {
   const DType& dt = *set.dt;
@@ -547,9 +719,10 @@ static Aggregate report_set(const Set& set, std::vector<Result>& res, double flo
     const std::string kind = ok ? "" : std::string(",\"kind\":\"") + failure_kind(r, floor_ok) + "\"";
     std::printf("{\"event\":\"gemm\",\"dtype\":\"%s\",\"device\":%d%s,\"m\":%d,\"n\":%d,\"k\":%d,\"ms\":%.4f,"
                 "\"tflops\":%.1f,\"max_rel_err\":%.3e,\"stabilise_dispatches\":%d,\"stabilise_spread\":%.4f,"
-                "\"iters\":%d,\"ramp_dispatches\":%d,\"min_tflops\":%.1f,\"ok\":%s%s%s%s%s%s}\n",
-                dt.name, r.device, scal.c_str(), s.m, s.n, s.k, r.ms, r.tflops, r.max_rel_err, r.stab_dispatches,
-                r.stab_spread, r.iters, r.ramp, floor_applies(s) ? floor : 0.0, ok ? "true" : "false", kind.c_str(), oom,
+                "\"iters\":%d,\"ramp_dispatches\":%d,\"min_tflops\":%.1f%s,\"ok\":%s%s%s%s%s%s}\n",
+                dt.name, r.device, scal.c_str(), s.m, s.n, s.k, r.ms, r.tflops,
+                std::isfinite(r.max_rel_err) ? r.max_rel_err : 1e30, r.stab_dispatches, r.stab_spread, r.iters, r.ramp,
+                floor_applies(s) ? floor : 0.0, abft_json(r).c_str(), ok ? "true" : "false", kind.c_str(), oom,
                 err.empty() ? "" : ",\"error\":\"", err.c_str(), err.empty() ? "" : "\"");
     if (r.launched && r.ok) {
       double& best = g_best[{dt.name, s.m, s.n, s.k}][r.device];
@@ -779,18 +952,20 @@ static bool spawn_worker(Worker& w, int hip_index, const std::vector<std::string
 }
 
 static std::string fmt_opts(const Options& o) {
-  char buf[256];
-  std::snprintf(buf, sizeof buf, "%d %d %d %.17g %.17g %.17g %.17g %d", o.iters, o.warmup, o.check_rows,
-                o.stabilise_max_s, o.min_window_ms, o.ramp_ms, o.pre_idle_ms, o.stabilise ? 1 : 0);
+  char buf[320];
+  std::snprintf(buf, sizeof buf, "%d %d %d %.17g %.17g %.17g %.17g %d %d %d %.17g", o.iters, o.warmup, o.check_rows,
+                o.stabilise_max_s, o.min_window_ms, o.ramp_ms, o.pre_idle_ms, o.stabilise ? 1 : 0, o.inject_tm,
+                o.inject_tn, o.inject_delta);
   return buf;
 }
 
 static bool parse_opts(const std::string& s, Options& o) {
   int stab = 1;
-  const int n = std::sscanf(s.c_str(), "%d %d %d %lf %lf %lf %lf %d", &o.iters, &o.warmup, &o.check_rows,
-                            &o.stabilise_max_s, &o.min_window_ms, &o.ramp_ms, &o.pre_idle_ms, &stab);
+  const int n = std::sscanf(s.c_str(), "%d %d %d %lf %lf %lf %lf %d %d %d %lf", &o.iters, &o.warmup, &o.check_rows,
+                            &o.stabilise_max_s, &o.min_window_ms, &o.ramp_ms, &o.pre_idle_ms, &stab, &o.inject_tm,
+                            &o.inject_tn, &o.inject_delta);
   o.stabilise = stab != 0;
-  return n == 8;
+  return n == 11;
 }
 
 // --worker: one GPU (HIP device 0 under the HIP_VISIBLE_DEVICES the launcher set). After its start
@@ -846,21 +1021,34 @@ static int worker_main(const Options& o, bool run_smoke) {
     std::string err = r.error;
     for (char& c : err)
       if (c == '\n' || c == '\r') c = ' ';
-    std::printf("R %d %d %d %d %.17g %.17g %.17g %d %.17g %zu %zu %d %d %s\n", id, r.launched, r.ok, r.oom, r.tflops,
-                r.ms, r.max_rel_err, r.stab_dispatches, r.stab_spread, r.need_bytes, r.free_bytes, r.iters, r.ramp,
-                err.c_str());
+    const AbftOut& a = r.abft;
+    std::printf("R %d %d %d %d %.17g %.17g %.17g %d %.17g %zu %zu %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %.17g "
+                "%.17g %.17g %.17g %.17g %s %s\n",
+                id, r.launched, r.ok, r.oom, r.tflops, r.ms, r.max_rel_err, r.stab_dispatches, r.stab_spread, r.need_bytes,
+                r.free_bytes, r.iters, r.ramp, a.ran, a.variant, a.tile_m, a.tile_n, a.bad_tiles, a.tm, a.tn, a.wg, a.round,
+                a.xcd, a.se, a.sh, a.cu, a.worst_ratio, a.checked_fraction, a.check_ms, a.abft_ms, r.probe_ms,
+                a.list.empty() ? "-" : a.list.c_str(), err.c_str());
     std::fflush(stdout);
   }
   return 0;
 }
 
+// One worker result line (worker_main's "R" format). False when it does not parse; the error text is
+// whatever follows the last field (possibly empty).
 static bool parse_result_line(const std::string& ln, int& id, Result& r) {
-  int launched = 0, ok = 0, oom = 0, off = 0;
-  if (std::sscanf(ln.c_str(), "R %d %d %d %d %lf %lf %lf %d %lf %zu %zu %d %d %n", &id, &launched, &ok, &oom, &r.tflops,
-                  &r.ms, &r.max_rel_err, &r.stab_dispatches, &r.stab_spread, &r.need_bytes, &r.free_bytes, &r.iters,
-                  &r.ramp, &off) < 13)
-    return false;
-  r.launched = launched, r.ok = ok, r.oom = oom;
+  int launched = 0, ok = 0, oom = 0, ran = 0, off = 0;
+  char list[256] = "";
+  AbftOut& a = r.abft;
+  const int n = std::sscanf(ln.c_str(),
+                            "R %d %d %d %d %lf %lf %lf %d %lf %zu %zu %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %lf %lf "
+                            "%lf %lf %lf %255s %n",
+                            &id, &launched, &ok, &oom, &r.tflops, &r.ms, &r.max_rel_err, &r.stab_dispatches,
+                            &r.stab_spread, &r.need_bytes, &r.free_bytes, &r.iters, &r.ramp, &ran, &a.variant, &a.tile_m,
+                            &a.tile_n, &a.bad_tiles, &a.tm, &a.tn, &a.wg, &a.round, &a.xcd, &a.se, &a.sh, &a.cu,
+                            &a.worst_ratio, &a.checked_fraction, &a.check_ms, &a.abft_ms, &r.probe_ms, list, &off);
+  if (n < 32) return false;
+  r.launched = launched, r.ok = ok, r.oom = oom, a.ran = ran;
+  a.list = list;
   r.error = off > 0 && (size_t)off <= ln.size() ? ln.substr((size_t)off) : "";
   return true;
 }
@@ -1016,6 +1204,16 @@ int main(int argc, char** argv) {
     else if (a == "--min-window-ms") o.min_window_ms = std::max(0.0, std::atof(next().c_str()));
     else if (a == "--ramp-ms") o.ramp_ms = std::max(0.0, std::atof(next().c_str()));
     else if (a == "--pre-timed-idle-ms") o.pre_idle_ms = std::max(0.0, std::atof(next().c_str()));
+    else if (a == "--inject-fault") {
+      const std::string v = next();
+      double d = o.inject_delta;
+      const int got = std::sscanf(v.c_str(), "%d,%d,%lf", &o.inject_tm, &o.inject_tn, &d);
+      if (got < 2 || o.inject_tm < 0 || o.inject_tn < 0) {
+        std::printf("{\"error\":\"--inject-fault wants TM,TN[,DELTA], got %s\"}\n", json_safe(v).c_str());
+        return 2;
+      }
+      o.inject_delta = d;
+    }
     else if (a == "--launch") launch = next();
     else if (a == "--smoke") run_smoke = true;
     else if (a == "--worker") worker = true;
@@ -1024,7 +1222,8 @@ int main(int argc, char** argv) {
       std::printf("usage: amd-gemm-validate [--shapes 8192,4096,MxNxK] [--dtype bf16|fp8|both] [--iters N] "
                   "[--warmup N] [--devices all|0,1] [--scaling 1,2,4,8] [--check-rows N] [--min-tflops X] "
                   "[--min-tflops-fp8 Y] [--min-efficiency E] [--min-relative R] [--stabilise-max-s S] [--no-stabilise] "
-                  "[--smoke] [--launch processes|threads] [--min-window-ms MS] [--ramp-ms MS] [--pre-timed-idle-ms MS]\n");
+                  "[--smoke] [--launch processes|threads] [--min-window-ms MS] [--ramp-ms MS] [--pre-timed-idle-ms MS] "
+                  "[--inject-fault TM,TN[,DELTA]]\n");
       return 0;
     } else {
       std::printf("{\"error\":\"unknown argument %s\"}\n", json_safe(a).c_str());

@@ -40,7 +40,7 @@ constexpr int NXCD = 8;      // MI355X: 8 XCDs, each with a private 4 MiB L2
 
 // Bijective for any nwg: blocks b and b+8 share an XCD (observed round-robin dispatch); give
 // each XCD a contiguous run of logical tiles so co-resident tiles share A/B panels in its L2.
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+__host__ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid % NXCD;
   const int q = nwg / NXCD;
   const int r = nwg % NXCD;
@@ -60,11 +60,11 @@ __host__ inline int persistent_launch_grid(int nwg, int cus) {
 }
 
 // Grouped raster: GROUP_M tile rows walk the N tiles together.
-__device__ __forceinline__ void tile_coords(int wgid, int tiles_m, int tiles_n, int& tm, int& tn) {
+__host__ __device__ __forceinline__ void tile_coords(int wgid, int tiles_m, int tiles_n, int& tm, int& tn) {
   const int per_group = GROUP_M * tiles_n;
   const int group = wgid / per_group;
   const int first_m = group * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int gsize = tiles_m - first_m < GROUP_M ? tiles_m - first_m : GROUP_M;
   const int in_group = wgid - group * per_group;
   tm = first_m + in_group % gsize;
   tn = in_group / gsize;
@@ -77,7 +77,7 @@ __device__ __forceinline__ void tile_coords(int wgid, int tiles_m, int tiles_n, 
 // panel K-slices at the same time (MALL hits). Consecutive waves walk N inside a super-row (an
 // XCD keeps its A panels, so serpentine K still finds their K-slices in L2); super-rows snake.
 // Host guarantees tiles_m % 16 == 0 and tiles_n % 16 == 0, so the map is a bijection.
-__device__ __forceinline__ void tile_coords_sq(int bid, int tiles_n, int& tm, int& tn) {
+__host__ __device__ __forceinline__ void tile_coords_sq(int bid, int tiles_n, int& tm, int& tn) {
   const int wave = bid >> 8;
   const int xcd = bid & (NXCD - 1);
   const int slot = (bid & 255) >> 3;
@@ -87,6 +87,36 @@ __device__ __forceinline__ void tile_coords_sq(int bid, int tiles_n, int& tm, in
   if (sr & 1) sc = sn - 1 - sc;
   tm = (sr << 4) + ((xcd & 1) << 3) + (slot & 7);
   tn = (sc << 4) + ((xcd >> 1) << 2) + (slot >> 3);
+}
+
+// The rasters above are __host__ too: the host mirrors a dispatch's tile -> workgroup map with the very
+// functions the kernels run (gemm_raster_host.h), so amd-gemm-validate can name the workgroup behind a
+// bad output tile.
+
+// Placement record (REC instantiations only, amd-gemm-validate's checked dispatch): workgroup b stores
+// the XCD it ran on (HW_REG_XCC_ID) and its hardware id (HW_REG_HW_ID: CU, SH and SE) at
+// g_wg_placement[2b], [2b+1]. blockIdx % 8 only says which workgroups share an XCD, not which XCD
+// (MI355X_MICROARCH.md, "Workgroup dispatch"); the record says which one, and which CU. One lane, two
+// plain vector stores, before anything else -- the REC=false kernels (every timed dispatch) do not
+// contain it. One copy of the pointer per TU and device; set from the host before a REC launch.
+__device__ uint32_t* g_wg_placement = nullptr;
+
+// A kernel's instantiation: timed (every production launch) or placement-recording. An enum, not a
+// bool, so the two are told apart by name in the code object (tests/test_gemm_build.py).
+enum Rec : int { kTimed = 0, kRecord = 1 };
+
+template <Rec REC>
+__device__ __forceinline__ void note_placement() {
+  if constexpr (REC == kRecord) {
+    if (threadIdx.x == 0 && g_wg_placement != nullptr) {
+      uint32_t xcc, hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      const uint32_t b = blockIdx.x + blockIdx.y * gridDim.x;
+      g_wg_placement[2 * b] = xcc;
+      g_wg_placement[2 * b + 1] = hw;
+    }
+  }
 }
 
 // Raw s_barrier pinned in place (no implicit vmcnt(0) as __syncthreads() would emit).

@@ -37,8 +37,10 @@ def asm_fp8(tmp_path_factory):
     return _compile(tmp_path_factory, "gemm_fp8.hip")
 
 
-def _kernels(asm: str, name: str):
-    starts = list(re.finditer(rf"^(_Z\w*{name}\w*):", asm, re.M))
+def _kernels(asm: str, name: str, rec: bool = False):
+    """The kernels whose mangled name contains `name`: the timed instantiations, or with `rec` the
+    placement-recording ones (test_placement_record_only_in_rec_kernels audits those)."""
+    starts = [m for m in re.finditer(rf"^(_Z\w*{name}\w*):", asm, re.M) if _is_rec(m.group(1)) == rec]
     assert starts, name
     return [_kernel_at(asm, m) for m in starts]
 
@@ -67,8 +69,10 @@ def test_production_library_kernel_set(asm):
     """The shipped code object holds exactly the production kernels: w4s for v18/v42/v44/v45, the
     persistent w4sp (v25) and the generic kernel -- no superseded generation, no knock-out build."""
     names = re.findall(r"^(_Z\w+):", asm, re.M)
-    assert len([x for x in names if "w4sI" in x]) == 6     # v18, v42, v44, v45, v47, v48
-    assert len([x for x in names if "w4spI" in x]) == 1
+    # every production kernel twice: the timed instantiation and the placement-recording one (REC,
+    # the last template argument) that amd-gemm-validate's checked dispatch runs
+    assert len([x for x in names if "w4sI" in x]) == 2 * 6     # v18, v42, v44, v45, v47, v48
+    assert len([x for x in names if "w4spI" in x]) == 2 * 1
     assert not [x for x in names if re.search(r"w4I|w4rI|_ppI|256x256_v2|256x256P", x)], names
     assert "AMDGO_GEMM" not in asm
 
@@ -330,3 +334,28 @@ def test_production_asm_headers_carry_only_shipped_schedules():
         text = open(os.path.join(hip, f), errors="replace").read()
         if "_asm_loop_lab.h\"" in text and not f.endswith("_lab.h"):
             assert f.endswith("_lab.hip"), f"{f} includes a lab header"
+
+
+def _is_rec(name: str) -> bool:
+    """A placement-recording instantiation: template argument Rec::kRecord (gemm_tile_common.h)."""
+    return "3RecE1E" in name
+
+
+@pytest.mark.parametrize("which", ["asm", "asm_fp8"])
+def test_placement_record_only_in_rec_kernels(request, which):
+    """The placement record (HW_REG_XCC_ID / HW_REG_HW_ID read, two vector stores by one lane) is in the
+    REC instantiations only: the timed kernels are the code they were before it existed."""
+    asm = request.getfixturevalue(which)
+    names = [n for n in re.findall(r"^(_Z\w*gemm_\w+):", asm, re.M) if "ref_rows" not in n and "fill_" not in n]
+    rec = [n for n in names if _is_rec(n)]
+    timed = [n for n in names if "3RecE0E" in n]
+    assert rec and len(rec) == len(timed) == len(names) // 2, (len(rec), len(timed), len(names))
+    for n in names:
+        body = asm[asm.index(n + ":"):asm.index(".end_amdhsa_kernel", asm.index(n + ":"))]
+        has = "hwreg(HW_REG_XCC_ID" in body
+        assert has == _is_rec(n), n
+        if _is_rec(n):
+            # the record costs no scratch and leaves the pinned accumulators to the asm blocks
+            assert "scratch_" not in body and "ScratchSize: 0" in asm[asm.index(n + ":"):][:200000], n
+            if "256x256" in n:      # the asm-pinned families (the small kernels' accumulators are hipcc's)
+                _no_compiler_agpr_access(body)

@@ -1,0 +1,83 @@
+"""The host mirror of the GEMM dispatch's rasters (native/hip/gemm_raster_host.h), CPU only.
+
+amd-gemm-validate names the workgroup behind a bad output tile from this mirror, so it must be a
+bijection between (tile, K piece) and the launch's (workgroup, round) slots for every kernel the
+dispatch can pick, and it must agree with the launch grid the dispatch uses."""
+
+import itertools
+
+import pytest
+
+from gpu_operator_amd.ops import _lib
+
+try:
+    _lib.load()
+    HAVE_LIB = True
+except Exception:  # noqa: BLE001 -- not built: the build test reports that
+    HAVE_LIB = False
+
+pytestmark = pytest.mark.skipif(not HAVE_LIB, reason="libamdgo_hip.so not built")
+
+SHAPES = [
+    (8192, 8192, 8192), (16384, 16384, 16384), (4096, 4096, 4096), (2560, 2560, 2560), (1024, 1024, 4096),
+    (1024, 1024, 16384), (512, 512, 8192), (2048, 2048, 8192), (12288, 12288, 12288), (8192, 8192, 2048),
+    (4096, 4096, 32768), (16384, 16384, 1024), (1000, 1000, 1000), (768, 512, 1024), (4096, 8192, 12288),
+    (2816, 2816, 2816), (1536, 1536, 1536), (256, 256, 256), (3000, 200, 4096),
+]
+
+
+def _check_bijection(r):
+    slots = set()
+    for tm, tn, p in itertools.product(range(r.tiles_m), range(r.tiles_n), range(r.pieces)):
+        b, rnd = r.owner[tm][tn][p], r.round[tm][tn][p]
+        assert 0 <= b < r.grid, (r.variant, tm, tn, p, b, r.grid)
+        assert rnd >= 0
+        assert (b, rnd) not in slots, (r.variant, tm, tn, p, b, rnd)   # one tile per workgroup round
+        slots.add((b, rnd))
+    return slots
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_raster_is_a_bijection(dtype, shape):
+    from gpu_operator_amd.ops import gemm as G
+
+    m, n, k = shape
+    r = G.raster(m, n, k, dtype, cus=256)
+    slots = _check_bijection(r)
+    assert len(slots) == r.tiles_m * r.tiles_n * r.pieces
+    assert r.tile_n in (64, 128, 256, 512)            # the ABFT strip widths gemm_abft.hip supports
+    if r.kind in ("generic", "grid", "grid_sq", "small"):
+        assert {b for b, _ in slots} == set(range(r.grid))          # every workgroup owns exactly one item
+        assert all(rnd == 0 for _, rnd in slots)
+    if r.kind == "persistent":
+        # whole XCD groups; a workgroup's tiles all come from its XCD's contiguous run: the rounds of one
+        # workgroup are consecutive and start at 0
+        assert r.grid % 8 == 0
+        per_wg = {}
+        for b, rnd in slots:
+            per_wg.setdefault(b, []).append(rnd)
+        for rounds in per_wg.values():
+            assert sorted(rounds) == list(range(len(rounds)))
+
+
+def test_raster_kinds_follow_the_dispatch():
+    from gpu_operator_amd.ops import gemm as G
+
+    lib = _lib.load()
+    for dtype, plan in (("bf16", lib.amdgo_gemm_plan_bf16), ("fp8", lib.amdgo_gemm_plan_fp8)):
+        for m, n, k in SHAPES:
+            r = G.raster(m, n, k, dtype, cus=256)
+            assert r.variant == plan(m, n, k, 256, 0), (dtype, m, n, k)
+            want = {60: "small", 61: "small", 62: "small", 0: "generic"}.get(r.variant)
+            if want:
+                assert r.kind == want, (dtype, m, n, k, r.variant, r.kind)
+            if r.variant == 61:
+                assert r.pieces == G.small_splits(m, n, k, 256) or dtype == "fp8"
+    # the headline shape: v50 on 256 persistent workgroups, 4 rounds of 256x256 tiles
+    r = G.raster(8192, 8192, 8192, "bf16", cus=256)
+    assert (r.variant, r.kind, r.grid, r.tile_m, r.tiles_m) == (50, "persistent", 256, 256, 32)
+    assert max(x[0] for row in r.round for x in row) == 3
+    # a CPX partition (32 CUs) gets its own raster: a persistent grid of 32
+    r = G.raster(8192, 8192, 8192, "bf16", cus=32)
+    assert r.grid in (0, 32) or r.kind != "persistent"
