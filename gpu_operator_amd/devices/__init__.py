@@ -76,7 +76,8 @@ def read_telemetry(root: Optional[str] = None) -> List[Dict]:
         out.append({k: getattr(t, k) for k in ("index", "power_w", "temp_edge_c", "temp_junction_c",
                                                "temp_mem_c", "gpu_busy_pct", "mem_busy_pct", "vram_used",
                                                "vram_total", "sclk_mhz", "mclk_mhz", "ecc_correctable",
-                                               "ecc_uncorrectable", "pcie_bw_bytes")})
+                                               "ecc_uncorrectable", "pcie_bw_bytes", "ras_ue_total", "ras_ce_total",
+                                               "ras_ue_blocks", "bad_pages_retired", "bad_pages_pending")})
     return out
 
 

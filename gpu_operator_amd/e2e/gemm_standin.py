@@ -9,7 +9,9 @@ its output are visible indices, as the binary's are).
 
 Script (environment):
   GEMM_STANDIN_SCRIPT   runs separated by ";" -- "fast", or "slow:3,5" (node GPUs 3 and 5 at 600
-                        TF/s, the others at 1500); run k uses entry k, the last entry repeats
+                        TF/s, the others at 1500), or "badtile:3@5.7.2" (node GPU 3 computes a wrong
+                        output tile [5,7] on XCD 2: the ABFT failure line of the binary); run k uses
+                        entry k, the last entry repeats
   GEMM_STANDIN_STATE    file counting the runs (also ``<state>.running`` exists while one runs)
   GEMM_STANDIN_RUNTIME_S  how long a run takes (default 1)
   GEMM_STANDIN_GPUS     GPUs without HIP_VISIBLE_DEVICES (default 8)
@@ -45,6 +47,12 @@ def main(argv=None) -> int:
     script = [x for x in os.environ.get("GEMM_STANDIN_SCRIPT", "fast").split(";") if x] or ["fast"]
     entry = script[min(runs, len(script) - 1)]
     slow = {int(x) for x in entry.split(":", 1)[1].split(",") if x} if entry.startswith("slow:") else set()
+    bad = {}                                       # node GPU -> (tm, tn, xcd)
+    if entry.startswith("badtile:"):
+        for item in entry.split(":", 1)[1].split(","):
+            gpu, where = item.split("@")
+            tm, tn, xcd = (int(x) for x in where.split("."))
+            bad[int(gpu)] = (tm, tn, xcd)
     vis = os.environ.get("HIP_VISIBLE_DEVICES", "")
     nodes = [int(x) for x in vis.split(",") if x.strip()] if vis else \
         list(range(int(os.environ.get("GEMM_STANDIN_GPUS", "8"))))
@@ -69,9 +77,17 @@ def main(argv=None) -> int:
         tf = 600.0 if node in slow else 1500.0
         ok = not (floors_apply and floor and tf < floor)
         line = {"event": "gemm", "dtype": "bf16", "device": i, "m": m, "n": n, "k": k, "tflops": tf,
-                "max_rel_err": 1e-3, "ok": ok}
+                "max_rel_err": 1e-3, "checked_fraction": 1.0, "abft_worst_ratio": 0.3, "bad_tiles": 0, "variant": 50,
+                "tile_m": 256, "tile_n": 256, "ok": ok}
         if not ok:
             line.update(kind="floor", error=f"below floor: {tf:.1f} < {floor:.1f} TFLOP/s")
+        if node in bad:
+            tm, tn, xcd = bad[node]
+            ok = False
+            line.update(ok=False, kind="correctness", bad_tiles=1, abft_worst_ratio=55.0, tile=[tm, tn],
+                        workgroup=8 * tm + xcd, round=0, xcd=xcd, cu={"se": 1, "sh": 0, "cu": 4},
+                        bad_tile_list=[[tm, tn, xcd]],
+                        error=f"ABFT: 1 bad tile(s), first [{tm},{tn}] (workgroup {8 * tm + xcd}, XCD {xcd})")
         print(json.dumps(line), flush=True)
         ok_all = ok_all and ok
         total += tf

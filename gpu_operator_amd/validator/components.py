@@ -54,6 +54,9 @@ class GateFailure:
     (a scaling step below the gate), ``uniformity`` (the workload's own node-median gate)."""
     kind: str
     text: str
+    # where a correctness failure happened, when the workload could say (amd-gemm-validate's ABFT check:
+    # device, dtype, tile, workgroup, xcd, cu); not part of the failure's identity
+    where: Optional[Dict[str, Any]] = field(default=None, compare=False, hash=False)
 
     def __str__(self) -> str:
         return self.text
@@ -502,6 +505,11 @@ def summarize_gemm(results: List[Dict[str, Any]]) -> Dict[str, Any]:
         out["scaling_skipped"] = sorted({r["gpus"] for r in sc if r.get("skipped")})
     if smoke:
         out["smoke_ok"] = all(s.get("ok") for s in smoke)
+    # the ABFT coverage of the run: the least covered GEMM and the closest any sum came to its bound
+    checked = [r for r in per + probe if "checked_fraction" in r]
+    if checked:
+        out["checked_fraction"] = min(float(r["checked_fraction"]) for r in checked)
+        out["abft_worst_ratio"] = max(float(r.get("abft_worst_ratio", 0.0)) for r in checked)
     out["counters"] = [r for r in results if r.get("event") == "counters"]
     return out
 
@@ -546,6 +554,24 @@ def _line_kind(r: Dict[str, Any]) -> str:
     return "oom" if r.get("oom") else "correctness"
 
 
+def _bad_tile(r: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    """The location of a wrong GEMM result, from the workload's ABFT fields (amd-gemm-validate names
+    the first bad output tile, the workgroup that computed it and -- from the checked dispatch's
+    placement record -- its XCD and CU); None for a line without them."""
+    if "tile" not in r:
+        return None
+    return {k: r[k] for k in ("device", "dtype", "tile", "workgroup", "xcd", "cu", "bad_tiles", "variant") if k in r}
+
+
+def _where_text(w: Dict[str, Any]) -> str:
+    cu = w.get("cu") or {}
+    on = f"XCD {w['xcd']}" if w.get("xcd") is not None else "several XCDs (split-K pieces)"
+    if cu:
+        on += f", CU se{cu.get('se')}.sh{cu.get('sh')}.cu{cu.get('cu')}"
+    return (f" [bad output tile {w.get('tile')} of {w.get('bad_tiles', 1)}, workgroup {w.get('workgroup')}"
+            f" on {on}]")
+
+
 def _set_devices(info: Dict[str, Any]) -> Dict[tuple, set]:
     """(dtype, m, n, k, gpus) -> the devices whose per-GPU lines belong to that set."""
     out: Dict[tuple, set] = {}
@@ -579,8 +605,10 @@ def gate_gemm(info: Dict[str, Any], floors: Dict[str, float], busy: List[str] = 
         kind = _line_kind(r)
         if kind in THROUGHPUT_KINDS and r.get("device") in disturbed:
             continue
+        where = _bad_tile(r) if kind == "correctness" else None
         bad.append(GateFailure(kind, f"gemm {r.get('dtype', 'bf16')} device {r.get('device')}: "
-                                     f"{r.get('error', 'check failed')}"))
+                                     f"{r.get('error', 'check failed')}" + (_where_text(where) if where else ""),
+                               where))
     bad += [GateFailure("correctness", f"probe device {p['device']}: {p.get('error', 'check failed')}")
             for p in info.get("probe", []) if not p["ok"] and "skipped" not in p]
     bad += [GateFailure("correctness", f"aggregate {r.get('dtype', 'bf16')} x{r.get('gpus')}: not ok")

@@ -61,6 +61,12 @@ class NodeMetrics:
         self.gemm_gpu_tflops = Gauge(p + "validator_gemm_gpu_tflops",
                                      "validator MFMA GEMM throughput of one GPU (its best over the sweep's sets)",
                                      node + ["gpu", "dtype", "m", "n", "k"], registry=r)
+        self.gemm_checked = Gauge(p + "validator_gemm_checked_fraction",
+                                  "fraction of the validator GEMM's output elements verified (ABFT tile checksums; "
+                                  "the least covered GEMM of the last passing run)", node, registry=r)
+        self.gemm_abft_ratio = Gauge(p + "validator_gemm_abft_worst_ratio",
+                                     "largest |checksum - expected| / tolerance of the last passing run (< 1)",
+                                     node, registry=r)
         self.gemm_eff = Gauge(p + "validator_gemm_scaling_efficiency",
                               "aggregate GEMM TFLOP/s on `gpus` GPUs / (gpus x the 1-GPU figure)",
                               node + ["dtype", "gpus"], registry=r)
@@ -99,6 +105,9 @@ class NodeMetrics:
             g = str(hip.get("gpus") or "")
             self.gemm_tflops.labels(n, "node", "bf16", g).set(hip["gemm_tflops_total"])
             self.gemm_tflops.labels(n, "per_gpu", "bf16", g).set(hip.get("gemm_tflops_per_gpu", 0))
+        if "checked_fraction" in hip:
+            self.gemm_checked.labels(n).set(hip["checked_fraction"])
+            self.gemm_abft_ratio.labels(n).set(hip.get("abft_worst_ratio", 0.0))
         for line in hip.get("gpu_tflops") or []:      # one series per GPU: a GPU failing the median shows
             for gpu, v in (line.get("tflops") or {}).items():
                 self.gemm_gpu_tflops.labels(n, str(gpu), comp._dtype_key(line.get("dtype", "bf16")), str(line.get("m")),

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstring>
 
 namespace {
@@ -71,31 +72,81 @@ abft_strip_sums(const T* __restrict__ X, int R, int K, int S, float* __restrict_
   Wabs[(size_t)t * K + k] = a;
 }
 
-// E[r][j] = sum_k X[r][k] W[j][k] and Eabs[r][j] = sum_k |X[r][k] W[j][k]| for r < R, j < J.
-// A 32-row x 32-strip block, 256 threads: thread (ty, tx) owns row tx and strips 4ty..4ty+3; K in
-// chunks of 64 staged through LDS (X as fp32 [row][k], padded; W transposed [k][strip], so a
-// thread's four strips are one 16-byte broadcast read).
+// 8 consecutive elements X[i..i+7] as fp32: one 16-byte (bf16) / 8-byte (fp8) load when `vec`
+// (in bounds and aligned), else guarded scalar loads up to `n` elements.
+__device__ __forceinline__ void abft_ld8(const __bf16* p, size_t i, int n, bool vec, float* out) {
+  if (vec) {
+    const uint4 q = *(const uint4*)(p + i);
+    const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      out[2 * e] = __uint_as_float(u[e] << 16);
+      out[2 * e + 1] = __uint_as_float(u[e] & 0xFFFF0000u);
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[e] = e < n ? abft_ld(p, i + e) : 0.f;
+}
+__device__ __forceinline__ void abft_ld8(const uint8_t* p, size_t i, int n, bool vec, float* out) {
+  if (vec) {
+    const uint2 q = *(const uint2*)(p + i);
+    const uint8_t b[8] = {(uint8_t)q.x, (uint8_t)(q.x >> 8), (uint8_t)(q.x >> 16), (uint8_t)(q.x >> 24),
+                          (uint8_t)q.y, (uint8_t)(q.y >> 8), (uint8_t)(q.y >> 16), (uint8_t)(q.y >> 24)};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[e] = abft_ld(b, e);
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[e] = e < n ? abft_ld(p, i + e) : 0.f;
+}
+
+// E[z][r][j] = sum over K-slice z of X[r][k] W[j][k], Eabs the same of |X[r][k] W[j][k]|, for r < R,
+// j < J. A 32-row x 32-strip block of 256 threads: thread (ty, tx) owns row tx and strips 4ty..4ty+3;
+// the block's K-slice (blockIdx.z, `kper` long, a multiple of 64) in chunks of 64 staged through LDS
+// by one 8-element vector load per thread and operand (X as fp32 [row][k], padded; W transposed
+// [k][strip], so a thread's four strips are one 16-byte broadcast read). K is sliced so the grid has
+// ~1024 blocks (a 32-strip check of 8192 rows is 256 blocks, one wave per SIMD and a global-load wait
+// per chunk: 1 ms; sliced, 4 blocks per CU hide each other's loads); the compare sums the slices in
+// order, so the result does not depend on scheduling.
 constexpr int EX_R = 32, EX_J = 32, EX_KC = 64;
 
 template <class T>
 __global__ void __launch_bounds__(ABFT_THREADS)
-abft_expect(const T* __restrict__ X, int R, int K, const float* __restrict__ W, int J, float* __restrict__ E,
-            float* __restrict__ Eabs) {
+abft_expect(const T* __restrict__ X, int R, int K, const float* __restrict__ W, int J, int kper,
+            float* __restrict__ E, float* __restrict__ Eabs) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   __shared__ float xs[EX_R][EX_KC + 1];
   __shared__ __attribute__((aligned(16))) float ws[EX_KC][EX_J + 4];
   const int tid = threadIdx.x;
   const int tx = tid & 31, ty = tid >> 5;
   const int r0 = blockIdx.x * EX_R, j0 = blockIdx.y * EX_J;
+  const int kb = blockIdx.z * kper, ke = min(K, kb + kper);
+  const int lr = tid >> 3, lk = (tid & 7) * 8;      // staging: row / strip lr, elements lk..lk+7
+  const bool xvec = (K & 7) == 0, wvec = (K & 3) == 0;
   f4 acc = {0.f, 0.f, 0.f, 0.f}, aab = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < K; k0 += EX_KC) {
-    for (int e = tid; e < EX_R * EX_KC; e += ABFT_THREADS) {
-      const int r = e / EX_KC, k = e % EX_KC;
-      xs[r][k] = (r0 + r < R && k0 + k < K) ? abft_ld(X, (size_t)(r0 + r) * K + k0 + k) : 0.f;
+  for (int k0 = kb; k0 < ke; k0 += EX_KC) {
+    {
+      float v[8];
+      const int k = k0 + lk, n = min(8, ke - k);
+      if (r0 + lr < R && n > 0) abft_ld8(X, (size_t)(r0 + lr) * K + k, n, xvec && n == 8, v);
+      else
+        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xs[lr][lk + e] = v[e];
     }
-    for (int e = tid; e < EX_J * EX_KC; e += ABFT_THREADS) {
-      const int j = e / EX_KC, k = e % EX_KC;
-      ws[k][j] = (j0 + j < J && k0 + k < K) ? W[(size_t)(j0 + j) * K + k0 + k] : 0.f;
+    {
+      float v[8];
+      const int k = k0 + lk, n = min(8, ke - k);
+      const float* w = W + (size_t)(j0 + lr) * K + k;
+      if (j0 + lr < J && n == 8 && wvec) {
+        const f4 a = *(const f4*)w, b = *(const f4*)(w + 4);
+        for (int e = 0; e < 4; ++e) v[e] = a[e], v[e + 4] = b[e];
+      } else {
+        for (int e = 0; e < 8; ++e) v[e] = (j0 + lr < J && e < n) ? w[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ws[lk + e][lr] = v[e];
     }
     __syncthreads();
 #pragma unroll 8
@@ -112,14 +163,28 @@ abft_expect(const T* __restrict__ X, int R, int K, const float* __restrict__ W, 
   }
   const int r = r0 + tx;
   if (r >= R) return;
+  const size_t base = ((size_t)blockIdx.z * R + r) * J;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = j0 + ty * 4 + q;
     if (j < J) {
-      E[(size_t)r * J + j] = acc[q];
-      Eabs[(size_t)r * J + j] = aab[q];
+      E[base + j] = acc[q];
+      Eabs[base + j] = aab[q];
     }
   }
+}
+
+// The K slicing of an expect launch: slices of a multiple of 64 elements, enough of them for ~1024
+// blocks, at most 8.
+struct ExSplit {
+  int kper, slices;
+};
+ExSplit ex_split(int R, int J, int K) {
+  const long long blocks = (long long)((R + EX_R - 1) / EX_R) * ((J + EX_J - 1) / EX_J);
+  int want = (int)std::max(1LL, std::min(8LL, 1024 / std::max(1LL, blocks)));
+  int kper = (K + want - 1) / want;
+  kper = (kper + EX_KC - 1) / EX_KC * EX_KC;
+  return {kper, (K + kper - 1) / kper};
 }
 
 // ulp(x)^2 of a bf16 from its bits: 2^(2(e - 134)) for biased exponent e (7 stored mantissa bits),
@@ -203,14 +268,19 @@ abft_c_sums(const __bf16* __restrict__ C, int M, int N, int TM, int J, int I, fl
 // per wave; a failing sum also sets bit (1 << col) of its tile's flag.
 __global__ void __launch_bounds__(ABFT_THREADS)
 abft_compare(const float* __restrict__ S, const float* __restrict__ U, const float* __restrict__ E,
-             const float* __restrict__ Eabs, int R, int J, int rows_per_tile, int tiles_n, int col, float k_sigma,
-             float rel_slack, int* __restrict__ flags, int* __restrict__ worst) {
+             const float* __restrict__ Eabs, int slices, int R, int J, int rows_per_tile, int tiles_n, int col,
+             float k_sigma, float rel_slack, int* __restrict__ flags, int* __restrict__ worst) {
   const size_t idx = (size_t)blockIdx.x * ABFT_THREADS + threadIdx.x;
   float ratio = 0.f;
   if (idx < (size_t)R * J) {
     const int r = (int)(idx / J), j = (int)(idx % J);
-    const float d = fabsf(S[idx] - E[idx]);
-    const float tol = k_sigma * sqrtf(U[idx]) + rel_slack * Eabs[idx] + 1e-30f;
+    float e = 0.f, ea = 0.f;
+    for (int z = 0; z < slices; ++z) {
+      e += E[(size_t)z * R * J + idx];
+      ea += Eabs[(size_t)z * R * J + idx];
+    }
+    const float d = fabsf(S[idx] - e);
+    const float tol = k_sigma * sqrtf(U[idx]) + rel_slack * ea + 1e-30f;
     const bool bad = !(d <= tol);
     ratio = bad && !(d == d && d < __builtin_inff()) ? __builtin_inff() : d / tol;
     if (bad) {
@@ -222,53 +292,43 @@ abft_compare(const float* __restrict__ S, const float* __restrict__ U, const flo
   if ((threadIdx.x & 63) == 0) atomicMax(worst, __float_as_int(ratio));
 }
 
-// fp32 reference of sampled output rows -- the validator's second opinion next to the checksums, and
-// ops.gemm.reference_rows. One wave per output column: lane l multiplies K-elements 4l..4l+3 of every
-// 256-wide K chunk (coalesced reads of the Bt row, the sampled A rows shared through L2 by the whole
-// grid), 32 rows at a time, then a wave reduction per row. Vector ALU fp32 only, software fp8 decode.
-// (A thread-per-column form read Bt with a stride of K per lane: 20 ms for 32 rows at 8192^3; this
-// form reads each Bt row once per 32 rows.)
-constexpr int REF_ROWS = 32;
-
+// fp32 reference of sampled output rows (the validator's second opinion next to the checksums, and
+// ops.gemm.reference_rows): out[i][n] = sum_k A[rows[i]][k] Bt[n][k] is the expectation product above
+// with X = Bt and the gathered A rows as W -- vector-ALU fp32, software fp8 decode, no matrix core.
+// (A thread-per-column kernel read Bt with a stride of K per lane: 20 ms for 32 rows at 8192^3.)
 template <class T>
 __global__ void __launch_bounds__(ABFT_THREADS)
-ref_rows_wave(const T* __restrict__ A, const T* __restrict__ Bt, const int* __restrict__ rows, int nrows,
-              float* __restrict__ out, int N, int K) {
-  const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int r0 = blockIdx.y * REF_ROWS;
-  if (n >= N) return;                       // uniform over the wave
-  const int nr = min(REF_ROWS, nrows - r0);
-  size_t arow[REF_ROWS];
-#pragma unroll
-  for (int i = 0; i < REF_ROWS; ++i) arow[i] = i < nr ? (size_t)rows[r0 + i] * K : 0;
-  float acc[REF_ROWS];
-#pragma unroll
-  for (int i = 0; i < REF_ROWS; ++i) acc[i] = 0.f;
-  const size_t brow = (size_t)n * K;
-  for (int k0 = 0; k0 < K; k0 += 256) {
-    float b[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = k0 + lane * 4 + e;
-      b[e] = k < K ? abft_ld(Bt, brow + k) : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < REF_ROWS; ++i) {
-      if (i >= nr) break;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = k0 + lane * 4 + e;
-        if (k < K) acc[i] = fmaf(abft_ld(A, arow[i] + k), b[e], acc[i]);
-      }
-    }
+gather_rows_f32(const T* __restrict__ A, const int* __restrict__ rows, int nrows, int K, float* __restrict__ out) {
+  const int i = blockIdx.y;
+  for (int k = blockIdx.x * ABFT_THREADS + threadIdx.x; k < K; k += gridDim.x * ABFT_THREADS)
+    out[(size_t)i * K + k] = abft_ld(A, (size_t)rows[i] * K + k);
+}
+
+// out[i][n] = sum of the slices E[z][n][i]
+__global__ void __launch_bounds__(ABFT_THREADS)
+ref_rows_finish(const float* __restrict__ E, int slices, int N, int nrows, float* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * ABFT_THREADS + threadIdx.x;
+  if (idx >= (size_t)N * nrows) return;
+  const int n = (int)(idx / nrows), i = (int)(idx % nrows);
+  float v = 0.f;
+  for (int z = 0; z < slices; ++z) v += E[(size_t)z * N * nrows + idx];
+  out[(size_t)i * N + n] = v;
+}
+
+// max over the sampled rows of |C - ref| / max(1, |ref|) (NaN -> +inf), as int bits in *worst
+__global__ void __launch_bounds__(ABFT_THREADS)
+rows_max_rel_err(const __bf16* __restrict__ C, const int* __restrict__ rows, int nrows, const float* __restrict__ ref,
+                 int N, int* __restrict__ worst) {
+  const size_t idx = (size_t)blockIdx.x * ABFT_THREADS + threadIdx.x;
+  float rel = 0.f;
+  if (idx < (size_t)nrows * N) {
+    const int i = (int)(idx / N), n = (int)(idx % N);
+    const float got = (float)C[(size_t)rows[i] * N + n], want = ref[idx];
+    rel = fabsf(got - want) / fmaxf(1.f, fabsf(want));
+    if (!(rel == rel)) rel = __builtin_inff();
   }
-#pragma unroll
-  for (int i = 0; i < REF_ROWS; ++i) {
-    float v = acc[i];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0 && i < nr) out[(size_t)(r0 + i) * N + n] = v;
-  }
+  for (int off = 32; off > 0; off >>= 1) rel = fmaxf(rel, __shfl_xor(rel, off));
+  if ((threadIdx.x & 63) == 0) atomicMax(worst, __float_as_int(rel));
 }
 
 __global__ void abft_inject(__bf16* C, size_t at, float delta) {
@@ -277,6 +337,7 @@ __global__ void abft_inject(__bf16* C, size_t at, float delta) {
 
 struct AbftLayout {
   int J, I;          // N-strips (tile columns), M-strips (tile rows)
+  ExSplit xr, xc;    // K slicing of the row-check and column-check expectations
   size_t wb, wbabs, wa, waabs, erow, eabsrow, srow, urow, ecol, eabscol, scol, ucol, flags, worst, bytes;
 };
 
@@ -284,6 +345,8 @@ AbftLayout abft_layout(int M, int N, int K, int TM, int TN) {
   AbftLayout L{};
   L.J = (N + TN - 1) / TN;
   L.I = (M + TM - 1) / TM;
+  L.xr = ex_split(M, L.J, K);
+  L.xc = ex_split(N, L.I, K);
   size_t off = 0;
   auto take = [&](size_t floats) {
     const size_t at = off;
@@ -294,12 +357,12 @@ AbftLayout abft_layout(int M, int N, int K, int TM, int TN) {
   L.wbabs = take((size_t)L.J * K);
   L.wa = take((size_t)L.I * K);
   L.waabs = take((size_t)L.I * K);
-  L.erow = take((size_t)M * L.J);
-  L.eabsrow = take((size_t)M * L.J);
+  L.erow = take((size_t)L.xr.slices * M * L.J);
+  L.eabsrow = take((size_t)L.xr.slices * M * L.J);
   L.srow = take((size_t)M * L.J);
   L.urow = take((size_t)M * L.J);
-  L.ecol = take((size_t)N * L.I);
-  L.eabscol = take((size_t)N * L.I);
+  L.ecol = take((size_t)L.xc.slices * N * L.I);
+  L.eabscol = take((size_t)L.xc.slices * N * L.I);
   L.scol = take((size_t)N * L.I);
   L.ucol = take((size_t)N * L.I);
   L.flags = take((size_t)L.I * L.J);
@@ -316,10 +379,12 @@ hipError_t abft_operand_side(const T* A, const T* Bt, int M, int N, int K, int T
                      at(L.wb), at(L.wbabs));
   hipLaunchKernelGGL(abft_strip_sums<T>, dim3((K + 255) / 256, L.I), dim3(ABFT_THREADS), 0, s, A, M, K, TM,
                      at(L.wa), at(L.waabs));
-  hipLaunchKernelGGL(abft_expect<T>, dim3((M + EX_R - 1) / EX_R, (L.J + EX_J - 1) / EX_J), dim3(ABFT_THREADS), 0, s,
-                     A, M, K, (const float*)at(L.wb), L.J, at(L.erow), at(L.eabsrow));
-  hipLaunchKernelGGL(abft_expect<T>, dim3((N + EX_R - 1) / EX_R, (L.I + EX_J - 1) / EX_J), dim3(ABFT_THREADS), 0, s,
-                     Bt, N, K, (const float*)at(L.wa), L.I, at(L.ecol), at(L.eabscol));
+  hipLaunchKernelGGL(abft_expect<T>, dim3((M + EX_R - 1) / EX_R, (L.J + EX_J - 1) / EX_J, L.xr.slices),
+                     dim3(ABFT_THREADS), 0, s, A, M, K, (const float*)at(L.wb), L.J, L.xr.kper, at(L.erow),
+                     at(L.eabsrow));
+  hipLaunchKernelGGL(abft_expect<T>, dim3((N + EX_R - 1) / EX_R, (L.I + EX_J - 1) / EX_J, L.xc.slices),
+                     dim3(ABFT_THREADS), 0, s, Bt, N, K, (const float*)at(L.wa), L.I, L.xc.kper, at(L.ecol),
+                     at(L.eabscol));
   return hipGetLastError();
 }
 
@@ -378,10 +443,10 @@ int amdgo_abft_check(int dtype, const void* A, const void* Bt, const void* C, in
   const size_t nrow = (size_t)M * L.J, ncol = (size_t)N * L.I;
   hipLaunchKernelGGL(abft_compare, dim3((unsigned)((nrow + 255) / 256)), dim3(ABFT_THREADS), 0, s,
                      (const float*)at(L.srow), (const float*)at(L.urow), (const float*)at(L.erow),
-                     (const float*)at(L.eabsrow), M, L.J, TM, L.J, 0, kSigma, kRel, flags, worst);
+                     (const float*)at(L.eabsrow), L.xr.slices, M, L.J, TM, L.J, 0, kSigma, kRel, flags, worst);
   hipLaunchKernelGGL(abft_compare, dim3((unsigned)((ncol + 255) / 256)), dim3(ABFT_THREADS), 0, s,
                      (const float*)at(L.scol), (const float*)at(L.ucol), (const float*)at(L.ecol),
-                     (const float*)at(L.eabscol), N, L.I, TN, L.J, 1, kSigma, kRel, flags, worst);
+                     (const float*)at(L.eabscol), L.xc.slices, N, L.I, TN, L.J, 1, kSigma, kRel, flags, worst);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   if ((e = hipMemcpyAsync(tile_flags, flags, (size_t)L.I * L.J * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return (int)e;
@@ -393,17 +458,56 @@ int amdgo_abft_check(int dtype, const void* A, const void* Bt, const void* C, in
 }
 
 // fp32 reference rows (dtype 0 = bf16, 1 = fp8 e4m3fn operands): out[i][n] = sum_k A[rows[i]][k] Bt[n][k].
+// Scratch comes from the stream-ordered pool (hipMallocAsync), released on the stream.
 int amdgo_ref_rows(int dtype, const void* A, const void* Bt, const int* rows, int nrows, float* out, int N, int K,
                    void* stream) {
   if (nrows <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
-  const dim3 grid((N + 3) / 4, (nrows + REF_ROWS - 1) / REF_ROWS);
-  if (dtype == 1)
-    hipLaunchKernelGGL(ref_rows_wave<uint8_t>, grid, dim3(ABFT_THREADS), 0, (hipStream_t)stream, (const uint8_t*)A,
-                       (const uint8_t*)Bt, rows, nrows, out, N, K);
-  else
-    hipLaunchKernelGGL(ref_rows_wave<__bf16>, grid, dim3(ABFT_THREADS), 0, (hipStream_t)stream, (const __bf16*)A,
-                       (const __bf16*)Bt, rows, nrows, out, N, K);
-  return (int)hipGetLastError();
+  hipStream_t s = (hipStream_t)stream;
+  const ExSplit x = ex_split(N, nrows, K);
+  float *w = nullptr, *e = nullptr;
+  hipError_t err = hipMallocAsync((void**)&w, (size_t)nrows * K * 4, s);
+  if (err != hipSuccess) return (int)err;
+  if ((err = hipMallocAsync((void**)&e, (size_t)2 * x.slices * N * nrows * 4, s)) != hipSuccess) {
+    (void)hipFreeAsync(w, s);
+    return (int)err;
+  }
+  float* eabs = e + (size_t)x.slices * N * nrows;
+  const dim3 gg((K + ABFT_THREADS - 1) / ABFT_THREADS < 64 ? (K + ABFT_THREADS - 1) / ABFT_THREADS : 64, nrows);
+  const dim3 ge((N + EX_R - 1) / EX_R, (nrows + EX_J - 1) / EX_J, x.slices);
+  if (dtype == 1) {
+    hipLaunchKernelGGL(gather_rows_f32<uint8_t>, gg, dim3(ABFT_THREADS), 0, s, (const uint8_t*)A, rows, nrows, K, w);
+    hipLaunchKernelGGL(abft_expect<uint8_t>, ge, dim3(ABFT_THREADS), 0, s, (const uint8_t*)Bt, N, K, (const float*)w,
+                       nrows, x.kper, e, eabs);
+  } else {
+    hipLaunchKernelGGL(gather_rows_f32<__bf16>, gg, dim3(ABFT_THREADS), 0, s, (const __bf16*)A, rows, nrows, K, w);
+    hipLaunchKernelGGL(abft_expect<__bf16>, ge, dim3(ABFT_THREADS), 0, s, (const __bf16*)Bt, N, K, (const float*)w,
+                       nrows, x.kper, e, eabs);
+  }
+  hipLaunchKernelGGL(ref_rows_finish, dim3((unsigned)(((size_t)N * nrows + 255) / 256)), dim3(ABFT_THREADS), 0, s, e,
+                     x.slices, N, nrows, out);
+  err = hipGetLastError();
+  (void)hipFreeAsync(w, s);
+  (void)hipFreeAsync(e, s);
+  return (int)err;
+}
+
+// The sampled-row comparison on the device: *max_rel_err (host; the stream synchronised) = the largest
+// |C[rows[i]][n] - ref[i][n]| / max(1, |ref|) over every sampled element (+inf for a NaN). One 4-byte
+// readback instead of one copy per row. `scratch`: 4 bytes of device memory.
+int amdgo_rows_max_rel_err(const void* C, const int* rows, int nrows, const float* ref, int N, void* scratch,
+                           float* max_rel_err, void* stream) {
+  if (nrows <= 0 || N <= 0 || !scratch || !max_rel_err) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(scratch, 0, 4, s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rows_max_rel_err, dim3((unsigned)(((size_t)nrows * N + 255) / 256)), dim3(ABFT_THREADS), 0, s,
+                     (const __bf16*)C, rows, nrows, ref, N, (int*)scratch);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  int bits = 0;
+  if ((e = hipMemcpyAsync(&bits, scratch, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+  std::memcpy(max_rel_err, &bits, 4);
+  return 0;
 }
 
 // Test hook: C[row][col] += delta (one bf16 element; delta NaN makes it NaN), ordered on `stream`.

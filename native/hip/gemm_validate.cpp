@@ -130,6 +130,8 @@ long long amdgo_abft_workspace_bytes(int M, int N, int K, int TM, int TN);
 int amdgo_abft_check(int dtype, const void* A, const void* Bt, const void* C, int M, int N, int K, int TM, int TN,
                      void* ws, long long ws_bytes, int* tile_flags, float* worst_ratio, void* stream);
 int amdgo_abft_inject(void* C, int M, int N, int row, int col, float delta, void* stream);
+int amdgo_rows_max_rel_err(const void* C, const int* rows, int nrows, const float* ref, int N, void* scratch,
+                           float* max_rel_err, void* stream);
 }
 
 static constexpr size_t kSmokeElements = 50000;
@@ -263,7 +265,7 @@ struct Result {
 
 // Every device object of one run_one call; freed on every return path.
 struct Resources {
-  void *A = nullptr, *B = nullptr, *C = nullptr, *abft_ws = nullptr;
+  void *A = nullptr, *B = nullptr, *C = nullptr, *abft_ws = nullptr, *scratch = nullptr;
   float* ref = nullptr;
   int* rows = nullptr;
   uint32_t* placement = nullptr;
@@ -272,7 +274,7 @@ struct Resources {
   ~Resources() {
     if (st) (void)hipStreamSynchronize(st);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
-    for (void* p : {A, B, C, abft_ws, (void*)ref, (void*)rows, (void*)placement})
+    for (void* p : {A, B, C, abft_ws, scratch, (void*)ref, (void*)rows, (void*)placement})
       if (p) (void)hipFree(p);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -317,13 +319,6 @@ static bool parse_index_list(const char* spec, std::vector<int>& out) {
     pos = c + 1;
   }
   return true;
-}
-
-static float bf16_to_f32(uint16_t b) {
-  uint32_t u = (uint32_t)b << 16;
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
 }
 
 // Whether the per-GPU floors apply to this shape (see the header).
@@ -410,8 +405,10 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   r.abft.tile_m = tile_m;
   r.abft.tile_n = tile_n;
   // what this shape needs against what the GPU has free: a tenant may hold most of the HBM
+  // (+ the reference rows' pool scratch: the gathered rows and up to 8 K-slices of 2 x rows x N floats)
   r.need_bytes = na * dt.esize + nb * dt.esize + nc * 2 + (size_t)check_rows * s.n * 4 + (size_t)check_rows * 4 +
-                 (size_t)abft_bytes + (size_t)grid * 8;
+                 (size_t)abft_bytes + (size_t)grid * 8 + 256 + (size_t)check_rows * s.k * 4 +
+                 (size_t)16 * check_rows * s.n * 4;
   size_t total = 0;
   CHECK(hipMemGetInfo(&r.free_bytes, &total));
   if (r.need_bytes > r.free_bytes) {
@@ -431,7 +428,8 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   };
   if (!alloc(&res.A, na * dt.esize, "A") || !alloc(&res.B, nb * dt.esize, "B") || !alloc(&res.C, nc * 2, "C") ||
       !alloc((void**)&res.ref, (size_t)check_rows * s.n * 4, "ref") || !alloc((void**)&res.rows, check_rows * 4, "rows") ||
-      !alloc(&res.abft_ws, (size_t)abft_bytes, "abft") || !alloc((void**)&res.placement, (size_t)grid * 8, "placement"))
+      !alloc(&res.abft_ws, (size_t)abft_bytes, "abft") || !alloc((void**)&res.placement, (size_t)grid * 8, "placement") ||
+      !alloc(&res.scratch, 256, "scratch"))
     return false;
   if (dt.fill(res.A, na, 1000 + dev, res.st) || dt.fill(res.B, nb, 2000 + dev, res.st)) {
     r.error = "fill failed";
@@ -550,19 +548,13 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
     r.error = "reference launch failed";
     return false;
   }
-  std::vector<float> href((size_t)check_rows * s.n);
-  std::vector<uint16_t> hc((size_t)s.n);
-  CHECK(hipMemcpyAsync(href.data(), res.ref, href.size() * 4, hipMemcpyDeviceToHost, res.st));
-  CHECK(hipStreamSynchronize(res.st));
-  double worst_rel = 0;
-  for (int i = 0; i < check_rows; ++i) {
-    CHECK(hipMemcpy(hc.data(), (uint16_t*)res.C + (size_t)hrows[i] * s.n, s.n * 2, hipMemcpyDeviceToHost));
-    for (int j = 0; j < s.n; ++j) {
-      const double got = bf16_to_f32(hc[j]), want = href[(size_t)i * s.n + j];
-      const double rel = std::fabs(got - want) / std::max(1.0, std::fabs(want));
-      worst_rel = std::isnan(rel) ? INFINITY : std::max(worst_rel, rel);
-    }
+  float worst_rel_f = 0.f;
+  if (const int err = amdgo_rows_max_rel_err(res.C, res.rows, check_rows, res.ref, s.n, res.scratch, &worst_rel_f,
+                                             res.st)) {
+    r.error = std::string("sampled-row compare: ") + hipGetErrorString((hipError_t)err);
+    return false;
   }
+  const double worst_rel = worst_rel_f;
   r.max_rel_err = worst_rel;
   ab.check_ms = ms_since(t_check);
   const bool rows_ok = std::isfinite(worst_rel) && worst_rel <= 1.0 / 128;

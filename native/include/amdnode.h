@@ -97,6 +97,12 @@ struct Telemetry {
   double sclk_mhz = -1, mclk_mhz = -1;
   int64_t ecc_correctable = -1, ecc_uncorrectable = -1;
   double pcie_bw_bytes = -1;
+  // RAS over every block the driver reports (ras/<block>_err_count: umc, gfx, sdma, mmhub, xgmi_wafl,
+  // ...; -1 when the device has no RAS directory), the blocks with uncorrectable errors, and the HBM
+  // pages the driver retired or holds pending retirement (ras/gpu_vram_bad_pages: R / P entries).
+  int64_t ras_ue_total = -1, ras_ce_total = -1;
+  std::string ras_ue_blocks;            // comma list, e.g. "umc,gfx"
+  int64_t bad_pages_retired = -1, bad_pages_pending = -1;
 };
 
 // Decoded sysfs `gpu_metrics` (the PMFW metrics table the amdgpu driver exports per device).

@@ -381,10 +381,35 @@ std::vector<Telemetry> read_telemetry(const std::string& root) {
     if (!mbusy.empty()) t.mem_busy_pct = (double)to_i64(mbusy);
     t.sclk_mhz = current_dpm_mhz(dev + "/pp_dpm_sclk");
     t.mclk_mhz = current_dpm_mhz(dev + "/pp_dpm_mclk");
-    // RAS: "ue: N" / "ce: M"
+    // RAS: "ue: N" / "ce: M" per block; the HBM (umc) counts are the ECC fields
     auto ras = read_kv(dev + "/ras/umc_err_count");
     if (ras.count("ue:")) t.ecc_uncorrectable = to_i64(ras["ue:"]);
     if (ras.count("ce:")) t.ecc_correctable = to_i64(ras["ce:"]);
+    for (const auto& f : list_dir(dev + "/ras")) {
+      const std::string suffix = "_err_count";
+      if (f.size() <= suffix.size() || f.compare(f.size() - suffix.size(), suffix.size(), suffix) != 0) continue;
+      auto kv = read_kv(dev + "/ras/" + f);
+      if (!kv.count("ue:") && !kv.count("ce:")) continue;
+      const int64_t ue = kv.count("ue:") ? std::max<int64_t>(0, to_i64(kv["ue:"])) : 0;
+      const int64_t ce = kv.count("ce:") ? std::max<int64_t>(0, to_i64(kv["ce:"])) : 0;
+      t.ras_ue_total = std::max<int64_t>(0, t.ras_ue_total) + ue;
+      t.ras_ce_total = std::max<int64_t>(0, t.ras_ce_total) + ce;
+      if (ue > 0) t.ras_ue_blocks += (t.ras_ue_blocks.empty() ? "" : ",") + f.substr(0, f.size() - suffix.size());
+    }
+    // "0x<page> : 0x<size> : R|P|F" per line (retired / pending / failed to retire)
+    const std::string bp = dev + "/ras/gpu_vram_bad_pages";
+    if (exists(bp)) {
+      t.bad_pages_retired = t.bad_pages_pending = 0;
+      std::istringstream in(read_file(bp));
+      for (std::string line; std::getline(in, line);) {
+        const size_t c = line.find_last_of(':');
+        if (c == std::string::npos) continue;
+        std::string flag = line.substr(c + 1);
+        flag.erase(0, flag.find_first_not_of(" \t"));
+        if (flag.rfind("R", 0) == 0) ++t.bad_pages_retired;
+        else if (flag.rfind("P", 0) == 0) ++t.bad_pages_pending;
+      }
+    }
     const std::string bw = read_file(dev + "/pcie_bw");
     if (!bw.empty()) {
       // "<received> <sent> <max payload>": packets in the last second

@@ -87,7 +87,12 @@ PYBIND11_MODULE(_amdnode, m) {
       .def_readonly("mclk_mhz", &Telemetry::mclk_mhz)
       .def_readonly("ecc_correctable", &Telemetry::ecc_correctable)
       .def_readonly("ecc_uncorrectable", &Telemetry::ecc_uncorrectable)
-      .def_readonly("pcie_bw_bytes", &Telemetry::pcie_bw_bytes);
+      .def_readonly("pcie_bw_bytes", &Telemetry::pcie_bw_bytes)
+      .def_readonly("ras_ue_total", &Telemetry::ras_ue_total)
+      .def_readonly("ras_ce_total", &Telemetry::ras_ce_total)
+      .def_readonly("ras_ue_blocks", &Telemetry::ras_ue_blocks)
+      .def_readonly("bad_pages_retired", &Telemetry::bad_pages_retired)
+      .def_readonly("bad_pages_pending", &Telemetry::bad_pages_pending);
 
   py::class_<GpuMetrics>(m, "GpuMetrics")
       .def_readonly("index", &GpuMetrics::index)

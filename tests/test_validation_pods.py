@@ -99,6 +99,32 @@ def test_a_gpu_below_the_floor_fails_the_pod_at_once_and_names_the_device(tmp_pa
     assert not ctx.status.exists(S.HIP_READY)
 
 
+def test_a_wrong_tile_fails_at_once_and_names_tile_xcd_and_cu(tmp_path, node):
+    """amd-gemm-validate's ABFT check finds a wrong output tile on GPU 3: a correctness failure -- no
+    re-measure (a wrong result is not a throughput fluke) -- whose error names the device, the tile,
+    the XCD and the CU, with the location structured on the GateFailure."""
+    c, k, root, state = node
+    _set_script(k, "badtile:3@5.7.2")
+    ctx = _ctx(tmp_path, c, root, "badtile:3@5.7.2")
+    with pytest.raises(comp.ValidationError) as e:
+        comp.validate_hip(ctx)
+    msg = str(e.value)
+    assert "device 3" in msg and "[5, 7]" in msg and "XCD 2" in msg and "se1.sh0.cu4" in msg, msg
+    f = [x for x in e.value.failures if x.kind == "correctness"]
+    assert f and f[0].where["tile"] == [5, 7] and f[0].where["xcd"] == 2 and f[0].where["device"] == 3
+    assert _runs(state) == 1
+    assert not ctx.status.exists(S.HIP_READY)
+
+
+def test_a_passing_run_records_full_coverage(tmp_path, node):
+    c, k, root, state = node
+    _set_script(k, "fast")
+    ctx = _ctx(tmp_path, c, root, "fast")
+    info = comp.validate_hip(ctx)
+    assert info["checked_fraction"] == 1.0 and info["abft_worst_ratio"] < 1.0
+    assert ctx.status.read(S.HIP_READY)["checked_fraction"] == 1.0
+
+
 def test_a_slow_first_run_is_measured_once_more_and_passes(tmp_path, node):
     """Case (2): slow on the first run, healthy on the second -> hip-ready after exactly one extra pod."""
     c, k, root, state = node
