@@ -394,6 +394,10 @@ int amdgo_gemm_bf16_placed(const void* A, const void* Bt, void* C, int M, int N,
   return gemm_bf16_dispatch<kRecord>(A, Bt, C, M, N, K, (hipStream_t)stream);
 }
 
+// One-time setup of the placement record on the current device (the first hipMemcpyToSymbol of a
+// process resolves the symbol: ~9 ms, which the first checked dispatch paid inside the probe).
+int amdgo_gemm_bf16_placement_init() { return (int)set_placement_record(nullptr, nullptr); }
+
 // The dispatch's raster for a shape on the current device: fills `info` (GemmRasterInfo fields, see
 // gemm_raster_host.h) and, when `owners` is non-null, the owning workgroup and round of every
 // (tile, piece) -- `cap` ints per array. Returns the tile count, or -1 when `cap` is too small.

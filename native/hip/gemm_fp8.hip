@@ -291,6 +291,8 @@ int amdgo_gemm_fp8_placed(const void* A, const void* Bt, void* C, int M, int N, 
   return gemm_fp8_dispatch<kRecord>(A, Bt, C, M, N, K, (hipStream_t)stream);
 }
 
+int amdgo_gemm_fp8_placement_init() { return (int)set_placement_record(nullptr, nullptr); }
+
 // The dispatch's raster (amdgo_gemm_bf16_raster).
 int amdgo_gemm_fp8_raster(int M, int N, int K, int* info, int* owners, int* rounds, int cap) {
   return raster_fill(raster_fp8(M, N, K, device_cu_count(nullptr)), M, N, info, owners, rounds, cap);

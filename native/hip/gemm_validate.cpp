@@ -130,6 +130,8 @@ long long amdgo_abft_workspace_bytes(int M, int N, int K, int TM, int TN);
 int amdgo_abft_check(int dtype, const void* A, const void* Bt, const void* C, int M, int N, int K, int TM, int TN,
                      void* ws, long long ws_bytes, int* tile_flags, float* worst_ratio, void* stream);
 int amdgo_abft_inject(void* C, int M, int N, int row, int col, float delta, void* stream);
+int amdgo_gemm_bf16_placement_init();
+int amdgo_gemm_fp8_placement_init();
 int amdgo_rows_max_rel_err(const void* C, const int* rows, int nrows, const float* ref, int N, void* scratch,
                            float* max_rel_err, void* stream);
 }
@@ -246,6 +248,7 @@ struct AbftOut {
   bool ran = false;
   int variant = -1, tile_m = 0, tile_n = 0, bad_tiles = 0;
   double worst_ratio = 0, checked_fraction = 0, check_ms = 0, abft_ms = 0;
+  double dispatch_ms = 0, rows_ms = 0;   // the checked phase's other parts: poison + recorded dispatch, sampled rows
   // the first bad tile (row-major order): its workgroup (piece 0), round, XCD (-1: pieces of a split-K
   // tile ran on different XCDs, see `list`) and hardware id fields
   int tm = -1, tn = -1, wg = -1, round = -1, xcd = -1, se = -1, sh = -1, cu = -1;
@@ -488,6 +491,7 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
     r.error = std::string("checked dispatch: ") + hipGetErrorString((hipError_t)err);
     return false;
   }
+  CHECK(hipStreamSynchronize(res.st));
   if (o.inject_tm >= 0 && o.inject_tn >= 0) {
     const int row = std::min(s.m - 1, o.inject_tm * tile_m + tile_m / 2);
     const int col = std::min(s.n - 1, o.inject_tn * tile_n + tile_n / 3);
@@ -509,6 +513,7 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   };
   AbftOut& ab = r.abft;
   ab.abft_ms = ms_since(t_abft);
+  ab.dispatch_ms = std::chrono::duration<double, std::milli>(t_abft - t_check).count();
   ab.ran = true;
   ab.worst_ratio = worst;
   ab.checked_fraction = 1.0;   // every element is in one row sum and one column sum (gemm_abft.hip)
@@ -541,6 +546,7 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   }
   if (ab.list.empty()) ab.list = "-";
   // second opinion: sampled rows against the independent fp32 reference kernel
+  const auto t_rows = std::chrono::steady_clock::now();
   std::vector<int> hrows(check_rows);
   for (int i = 0; i < check_rows; ++i) hrows[i] = (int)(((uint64_t)i * 2654435761u + dev) % s.m);
   CHECK(hipMemcpyAsync(res.rows, hrows.data(), check_rows * 4, hipMemcpyHostToDevice, res.st));
@@ -556,6 +562,7 @@ static bool run_one(const DType& dt, int dev, const Shape& s, const Options& o, 
   }
   const double worst_rel = worst_rel_f;
   r.max_rel_err = worst_rel;
+  ab.rows_ms = ms_since(t_rows);
   ab.check_ms = ms_since(t_check);
   const bool rows_ok = std::isfinite(worst_rel) && worst_rel <= 1.0 / 128;
   r.ok = rows_ok && ab.bad_tiles == 0;
@@ -652,9 +659,10 @@ static std::string abft_json(const Result& r) {
   char buf[512];
   std::snprintf(buf, sizeof buf,
                 ",\"checked_fraction\":%.3f,\"abft_worst_ratio\":%.4f,\"bad_tiles\":%d,\"variant\":%d,\"tile_m\":%d,"
-                "\"tile_n\":%d,\"check_ms\":%.3f,\"abft_ms\":%.3f,\"probe_ms\":%.1f",
+                "\"tile_n\":%d,\"check_ms\":%.3f,\"check_dispatch_ms\":%.3f,\"abft_ms\":%.3f,\"check_rows_ms\":%.3f,"
+                "\"probe_ms\":%.1f",
                 a.checked_fraction, std::isfinite(a.worst_ratio) ? a.worst_ratio : 1e30, a.bad_tiles, a.variant, a.tile_m,
-                a.tile_n, a.check_ms, a.abft_ms, r.probe_ms);
+                a.tile_n, a.check_ms, a.dispatch_ms, a.abft_ms, a.rows_ms, r.probe_ms);
   std::string out = buf;
   if (a.bad_tiles > 0) {
     std::snprintf(buf, sizeof buf, ",\"tile\":[%d,%d],\"workgroup\":%d,\"round\":%d,\"xcd\":", a.tm, a.tn, a.wg,
@@ -979,6 +987,9 @@ static int worker_main(const Options& o, bool run_smoke) {
   std::printf("S %d %s %s %d %zu\n", ndev, bus, prop.gcnArchName, prop.multiProcessorCount,
               (size_t)prop.sharedMemPerBlock);
   std::fflush(stdout);
+  (void)hipSetDevice(0);
+  (void)amdgo_gemm_bf16_placement_init();   // process setup of the checked dispatch, not the probe's
+  (void)amdgo_gemm_fp8_placement_init();
   if (run_smoke) {
     std::printf("H %d\n", smoke_failures({0}) == 0 ? 1 : 0);
     std::fflush(stdout);
@@ -1015,11 +1026,11 @@ static int worker_main(const Options& o, bool run_smoke) {
       if (c == '\n' || c == '\r') c = ' ';
     const AbftOut& a = r.abft;
     std::printf("R %d %d %d %d %.17g %.17g %.17g %d %.17g %zu %zu %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %.17g "
-                "%.17g %.17g %.17g %.17g %s %s\n",
+                "%.17g %.17g %.17g %.17g %.17g %.17g %s %s\n",
                 id, r.launched, r.ok, r.oom, r.tflops, r.ms, r.max_rel_err, r.stab_dispatches, r.stab_spread, r.need_bytes,
                 r.free_bytes, r.iters, r.ramp, a.ran, a.variant, a.tile_m, a.tile_n, a.bad_tiles, a.tm, a.tn, a.wg, a.round,
                 a.xcd, a.se, a.sh, a.cu, a.worst_ratio, a.checked_fraction, a.check_ms, a.abft_ms, r.probe_ms,
-                a.list.empty() ? "-" : a.list.c_str(), err.c_str());
+                a.dispatch_ms, a.rows_ms, a.list.empty() ? "-" : a.list.c_str(), err.c_str());
     std::fflush(stdout);
   }
   return 0;
@@ -1033,12 +1044,13 @@ static bool parse_result_line(const std::string& ln, int& id, Result& r) {
   AbftOut& a = r.abft;
   const int n = std::sscanf(ln.c_str(),
                             "R %d %d %d %d %lf %lf %lf %d %lf %zu %zu %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %lf %lf "
-                            "%lf %lf %lf %255s %n",
+                            "%lf %lf %lf %lf %lf %255s %n",
                             &id, &launched, &ok, &oom, &r.tflops, &r.ms, &r.max_rel_err, &r.stab_dispatches,
                             &r.stab_spread, &r.need_bytes, &r.free_bytes, &r.iters, &r.ramp, &ran, &a.variant, &a.tile_m,
                             &a.tile_n, &a.bad_tiles, &a.tm, &a.tn, &a.wg, &a.round, &a.xcd, &a.se, &a.sh, &a.cu,
-                            &a.worst_ratio, &a.checked_fraction, &a.check_ms, &a.abft_ms, &r.probe_ms, list, &off);
-  if (n < 32) return false;
+                            &a.worst_ratio, &a.checked_fraction, &a.check_ms, &a.abft_ms, &r.probe_ms, &a.dispatch_ms,
+                            &a.rows_ms, list, &off);
+  if (n < 34) return false;
   r.launched = launched, r.ok = ok, r.oom = oom, a.ran = ran;
   a.list = list;
   r.error = off > 0 && (size_t)off <= ln.size() ? ln.substr((size_t)off) : "";
@@ -1286,6 +1298,8 @@ int main(int argc, char** argv) {
               devs.size(), ndev, prop.gcnArchName, prop.multiProcessorCount, (size_t)prop.sharedMemPerBlock,
               o.iters, o.stabilise ? "true" : "false", o.min_window_ms);
   bool all_ok = true;
+  for (int d : devs)
+    if (hipSetDevice(d) == hipSuccess) (void)amdgo_gemm_bf16_placement_init(), (void)amdgo_gemm_fp8_placement_init();
   if (run_smoke) {
     const int failures = smoke_failures(devs);
     print_smoke(devs.size(), failures);
