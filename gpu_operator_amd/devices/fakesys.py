@@ -113,6 +113,9 @@ def make_node(root, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
         _w(dev / "pp_dpm_sclk", "0: 500Mhz\n1: 2100Mhz *\n2: 2400Mhz")
         _w(dev / "pp_dpm_mclk", "0: 900Mhz\n1: 1900Mhz *")
         _w(dev / "ras/umc_err_count", "ue: 0\nce: 3")
+        _w(dev / "ras/gfx_err_count", "ue: 0\nce: 0")
+        _w(dev / "ras/sdma_err_count", "ue: 0\nce: 0")
+        _w(dev / "ras/gpu_vram_bad_pages", "")
         (dev / "gpu_metrics").write_bytes(encode_gpu_metrics_v18())
         hw = dev / "hwmon/hwmon3"
         _w(hw / "power1_average", 750_000_000)
@@ -177,6 +180,24 @@ def make_node(root, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
                    {"type": t, "node_from": a, "node_to": to, "weight": w,
                     "min_bandwidth": 50000 if t == 11 else 32000, "max_bandwidth": 153000 if t == 11 else 64000})
     return root
+
+
+def _bdf_of(root, gpu: int) -> str:
+    return f"0000:{0x05 + 0x10 * gpu:02x}:00.0"       # make_node's numbering
+
+
+def set_ras(root, gpu: int, block: str = "umc", ue: int = 0, ce: int = 0) -> None:
+    """The RAS error counts of one block of GPU ``gpu`` (ras/<block>_err_count)."""
+    _w(Path(root) / "sys/bus/pci/devices" / _bdf_of(root, gpu) / f"ras/{block}_err_count", f"ue: {ue}\nce: {ce}")
+
+
+def add_bad_pages(root, gpu: int, n: int, flag: str = "R") -> None:
+    """Append ``n`` entries to GPU ``gpu``'s ras/gpu_vram_bad_pages (R retired, P pending, F failed)."""
+    p = Path(root) / "sys/bus/pci/devices" / _bdf_of(root, gpu) / "ras/gpu_vram_bad_pages"
+    old = p.read_text() if p.exists() else ""
+    start = old.count("\n")
+    rows = "".join(f"0x{0x1000 + start + i:08x} : 0x00001000 : {flag}\n" for i in range(n))
+    p.write_text(old + rows)
 
 
 def set_compute_partition(root, compute: str, memory: Optional[str] = None) -> None:

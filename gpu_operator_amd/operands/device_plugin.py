@@ -17,12 +17,21 @@ the MI355X-native counterpart the north star asks for:
   device, as the reference's e2e exercises with NVIDIA's plugin (tests/scripts/update-
   clusterpolicy.sh);
 * re-registers when kubelet restarts (inotify on kubelet.sock) and reloads its config on
-  SIGHUP (sent by the config-manager sidecar).
+  SIGHUP (sent by the config-manager sidecar);
+* health (``check_health``, every ``DP_HEALTH_PERIOD_S``): a device is Unhealthy -- the kubelet stops
+  allocating it -- when the driver is not live, its KFD agent vanished, it reports uncorrectable RAS
+  errors in any block (HBM/umc, gfx, sdma, xgmi, ... above ``DP_HEALTH_UE_MAX``, default 0) or its
+  retired HBM pages reach ``DP_HEALTH_RETIRED_PAGES_MAX`` (default 128). The RAS counters are the
+  libamdnode telemetry the metrics exporter publishes. The reference ships NVIDIA's plugin, which
+  withdraws devices on critical XID events; in-repo it re-validates the driver every 60 s
+  (reference: validator/metrics.go:237-250). Each device's state and reason go to the node status
+  directory (``device-health``) for the node metrics exporter (``node_device_unhealthy``).
 """
 
 from __future__ import annotations
 
 import argparse
+import json
 import logging
 import os
 import signal
@@ -42,6 +51,7 @@ from . import kubeletapi as K
 log = logging.getLogger("amd-device-plugin")
 
 GPU_RESOURCE = "amd.com/gpu"
+DEVICE_HEALTH_FILE = "device-health"     # in the node status directory (validator/status.py)
 PARTITION_PREFIX = "amd.com/partition-"
 REPLICA_SEP = "::"
 
@@ -66,6 +76,7 @@ class Device:
     partition: str
     hive: int
     healthy: bool = True
+    reason: str = ""             # why it is unhealthy ("" when healthy)
     replica_of: Optional[str] = None
     vram_bytes: int = 0          # this device's HBM share from sysfs (a partition's under CPX/NPSx)
 
@@ -101,6 +112,35 @@ class Config:
             for r in ts.get("resources") or []:
                 c.replicas[r["name"]] = int(r.get("replicas", 1))
         return c
+
+
+@dataclass
+class HealthPolicy:
+    """When a device stops being allocatable (module docstring). ``ue_max``: uncorrectable RAS errors
+    tolerated over all blocks (-1: not checked); ``retired_pages_max``: retired HBM pages at which the
+    device is withdrawn (-1: not checked)."""
+    ue_max: int = 0
+    retired_pages_max: int = 128
+
+    @classmethod
+    def from_env(cls, env: Dict[str, str]) -> "HealthPolicy":
+        return cls(ue_max=int(env.get("DP_HEALTH_UE_MAX", "0") or 0),
+                   retired_pages_max=int(env.get("DP_HEALTH_RETIRED_PAGES_MAX", "128") or 128))
+
+    def verdict(self, tele: Optional[Dict]) -> str:
+        """"" when the telemetry is healthy, else the reason."""
+        if not tele:
+            return ""
+        ue = tele.get("ras_ue_total", -1)
+        if ue is None or ue < 0:
+            ue = tele.get("ecc_uncorrectable", -1)
+        if self.ue_max >= 0 and ue is not None and ue > self.ue_max:
+            blocks = tele.get("ras_ue_blocks") or "umc"
+            return f"uncorrectable RAS errors: {ue} ({blocks})"
+        retired = tele.get("bad_pages_retired", -1)
+        if self.retired_pages_max >= 0 and retired is not None and retired >= self.retired_pages_max:
+            return f"retired HBM pages: {retired} (limit {self.retired_pages_max})"
+        return ""
 
 
 def discover(cfg: Config, root: Optional[str] = None) -> List[Device]:
@@ -275,11 +315,14 @@ class ResourceServer:
 
 class DevicePlugin:
     def __init__(self, cfg: Config, root: Optional[str] = None, plugin_dir: str = K.DEVICE_PLUGIN_PATH,
-                 health_period: float = 5.0):
+                 health_period: float = 5.0, policy: Optional[HealthPolicy] = None,
+                 status_dir: Optional[str] = None):
         self.cfg = cfg
         self.root = root
         self.plugin_dir = plugin_dir
         self.health_period = health_period
+        self.policy = policy or HealthPolicy()
+        self.status_dir = status_dir
         self.devices: List[Device] = []
         self.servers: Dict[str, ResourceServer] = {}
         self._stop = threading.Event()
@@ -294,25 +337,59 @@ class DevicePlugin:
             for s in self.servers.values():
                 s.register(os.path.join(self.plugin_dir, "kubelet.sock"))
         log.info("serving %s", {r: len(s.devices()) for r, s in self.servers.items()})
+        self.check_health()              # a device that is already sick is never advertised Healthy
 
     def check_health(self) -> bool:
-        """Mark devices unhealthy when the driver is gone or their KFD agent vanished."""
+        """Re-evaluate every device (module docstring): driver live, KFD agent present, RAS within the
+        policy. Streams a ListAndWatch update when any device changed; returns whether one did."""
+        live_driver = False
+        agents: Dict[int, Dict] = {}
+        tele: Dict[int, Dict] = {}
         try:
-            st = devices.driver_state(self.root)
-            live = {g["drm_render_minor"] for g in devices.enumerate_gpus(self.root)} if st["live"] else set()
-        except Exception:  # noqa: BLE001
-            live = set()
+            live_driver = bool(devices.driver_state(self.root)["live"])
+            if live_driver:
+                gpus = devices.enumerate_gpus(self.root)
+                agents = {g["drm_render_minor"]: g for g in gpus}
+                by_index = {t["index"]: t for t in devices.read_telemetry(self.root)}
+                tele = {g["drm_render_minor"]: by_index.get(g["index"]) for g in gpus}
+        except Exception as e:  # noqa: BLE001 -- a failed read withdraws nothing but is logged
+            log.warning("health read failed: %s", e)
+            if not agents:
+                live_driver, agents = False, {}
         changed = False
         for d in self.devices:
-            ok = d.render_minor in live
-            if ok != d.healthy:
-                d.healthy = ok
-                changed = True
-                log.warning("device %s is now %s", d.id, "healthy" if ok else "unhealthy")
+            if not live_driver:
+                why = "amdgpu driver not live"
+            elif d.render_minor not in agents:
+                why = "KFD agent lost"
+            else:
+                why = self.policy.verdict(tele.get(d.render_minor))
+            ok = not why
+            if ok != d.healthy or why != d.reason:
+                if ok != d.healthy:
+                    changed = True
+                    log.warning("device %s is now %s%s", d.id, "healthy" if ok else "unhealthy",
+                                "" if ok else f": {why}")
+                d.healthy, d.reason = ok, why
+        self._publish_health()           # before the stream update: whoever sees it finds the reason
         if changed:
             for s in self.servers.values():
                 s.notify()
         return changed
+
+    def _publish_health(self) -> None:
+        """``device-health`` in the node status directory: every device's state and reason, read by the
+        node metrics exporter. Best effort (the directory may not be mounted)."""
+        if not self.status_dir:
+            return
+        from ..validator import status as S
+        try:
+            S.StatusDir(self.status_dir).write_raw(DEVICE_HEALTH_FILE, json.dumps({
+                "ts": time.time(),
+                "devices": {d.id: {"healthy": d.healthy, "reason": d.reason, "resource": d.resource, "bdf": d.bdf}
+                            for d in self.devices}}))
+        except OSError as e:
+            log.debug("device-health not written: %s", e)
 
     def stop(self) -> None:
         self._stop.set()
@@ -343,6 +420,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="amd-device-plugin")
     ap.add_argument("--config-file", default=os.environ.get("CONFIG_FILE"))
     ap.add_argument("--plugin-dir", default=mounts.path(K.DEVICE_PLUGIN_PATH))
+    ap.add_argument("--status-dir", default=os.environ.get("VALIDATIONS_DIR", mounts.path("/run/amd/validations")))
+    ap.add_argument("--health-period", type=float, default=float(os.environ.get("DP_HEALTH_PERIOD_S", "5")))
     a = ap.parse_args(argv)
     stop = threading.Event()
     reload_ = threading.Event()
@@ -350,7 +429,8 @@ def main(argv=None) -> int:
     signal.signal(signal.SIGHUP, lambda *_: reload_.set())
     while not stop.is_set():
         cfg = Config.load(a.config_file, dict(os.environ))
-        p = DevicePlugin(cfg, plugin_dir=a.plugin_dir)
+        p = DevicePlugin(cfg, plugin_dir=a.plugin_dir, health_period=a.health_period,
+                         policy=HealthPolicy.from_env(dict(os.environ)), status_dir=a.status_dir)
         try:
             p.start()
         except Exception as e:  # noqa: BLE001

@@ -47,6 +47,10 @@ FIELDS = {
     "gpu_ecc_correctable_total": ("ecc_correctable", "counter", "Correctable ECC errors"),
     "gpu_ecc_uncorrectable_total": ("ecc_uncorrectable", "counter", "Uncorrectable ECC errors"),
     "gpu_pcie_bandwidth_bytes": ("pcie_bw_bytes", "gauge", "PCIe bandwidth estimate (bytes/s)"),
+    "gpu_ras_uncorrectable_total": ("ras_ue_total", "counter", "Uncorrectable RAS errors over every block"),
+    "gpu_ras_correctable_total": ("ras_ce_total", "counter", "Correctable RAS errors over every block"),
+    "gpu_retired_pages": ("bad_pages_retired", "gauge", "HBM pages the driver retired"),
+    "gpu_pending_retired_pages": ("bad_pages_pending", "gauge", "HBM pages pending retirement"),
     "gpu_xgmi_link_count": ("xgmi_links", "gauge", "xGMI links to other GPUs (KFD io_links)"),
 }
 
@@ -72,7 +76,8 @@ ALL_FIELDS = list(FIELDS) + list(GM_FIELDS) + list(LINK_FIELDS)
 # partition agent would report the same value again
 DEVICE_LEVEL_FIELDS = frozenset({"gpu_power_watts", "gpu_temperature_edge_celsius", "gpu_temperature_junction_celsius",
                                  "gpu_temperature_memory_celsius", "gpu_ecc_correctable_total",
-                                 "gpu_ecc_uncorrectable_total", "gpu_pcie_bandwidth_bytes"})
+                                 "gpu_ecc_uncorrectable_total", "gpu_pcie_bandwidth_bytes", "gpu_ras_uncorrectable_total",
+                                 "gpu_ras_correctable_total", "gpu_retired_pages", "gpu_pending_retired_pages"})
 
 
 def load_fields(path: Optional[str]) -> List[str]:

@@ -61,6 +61,12 @@ class NodeMetrics:
         self.gemm_gpu_tflops = Gauge(p + "validator_gemm_gpu_tflops",
                                      "validator MFMA GEMM throughput of one GPU (its best over the sweep's sets)",
                                      node + ["gpu", "dtype", "m", "n", "k"], registry=r)
+        self.dev_unhealthy = Gauge(p + "node_device_unhealthy",
+                                   "1 for a device the device plugin withdrew from the kubelet, with its reason "
+                                   "(RAS uncorrectable errors, retired HBM pages, agent lost, driver not live)",
+                                   node + ["device", "bdf", "reason"], registry=r)
+        self.dev_unhealthy_total = Gauge(p + "node_devices_unhealthy", "devices the device plugin reports Unhealthy",
+                                         node, registry=r)
         self.gemm_checked = Gauge(p + "validator_gemm_checked_fraction",
                                   "fraction of the validator GEMM's output elements verified (ABFT tile checksums; "
                                   "the least covered GEMM of the last passing run)", node, registry=r)
@@ -112,6 +118,7 @@ class NodeMetrics:
             for gpu, v in (line.get("tflops") or {}).items():
                 self.gemm_gpu_tflops.labels(n, str(gpu), comp._dtype_key(line.get("dtype", "bf16")), str(line.get("m")),
                                             str(line.get("n")), str(line.get("k"))).set(v)
+        self.refresh_device_health()
         rc = sd.read(S.RCCL_READY) or {}
         if rc.get("peak_busbw_gbps") is not None:
             self.busbw.labels(n, str(rc.get("ranks"))).set(rc["peak_busbw_gbps"])
@@ -124,6 +131,22 @@ class NodeMetrics:
         for ranks, bw in (rc.get("busbw_by_ranks") or {}).items():     # the 2/4/8-rank sweep
             if bw is not None:
                 self.busbw.labels(n, str(ranks)).set(bw)
+
+    def refresh_device_health(self) -> None:
+        """The device plugin's health verdicts (device-health in the status directory)."""
+        from ..operands.device_plugin import DEVICE_HEALTH_FILE
+        n = self.ctx.node_name
+        doc = self.ctx.status.read(DEVICE_HEALTH_FILE) or {}
+        devs = doc.get("devices") or {}
+        if not isinstance(devs, dict):
+            return
+        self.dev_unhealthy.clear()
+        bad = 0
+        for did, d in sorted(devs.items()):
+            if isinstance(d, dict) and not d.get("healthy", True):
+                bad += 1
+                self.dev_unhealthy.labels(n, did, str(d.get("bdf", "")), str(d.get("reason", ""))).set(1)
+        self.dev_unhealthy_total.labels(n).set(bad)
 
     def refresh_driver(self) -> None:
         n = self.ctx.node_name

@@ -134,3 +134,86 @@ def test_cdi_device_list_strategy(tmp_path, short_tmp):
     req.container_requests.add(devicesIDs=[p.devices[0].id])
     r = srv.Allocate(req, None).container_responses[0]
     assert [c.name for c in r.cdi_devices] == [f"amd.com/gpu={p.devices[0].id}"] and not r.devices
+
+
+def _health_stream(tmp_path, short_tmp, policy=None, n_gpus=8):
+    root = str(fakesys.make_node(tmp_path / "r", n_gpus=n_gpus))
+    kubelet = FakeKubelet(short_tmp)
+    status = str(tmp_path / "validations")
+    p = DPM.DevicePlugin(cfg(), root=root, plugin_dir=short_tmp, health_period=0.2, policy=policy, status_dir=status)
+    p.start()
+    return root, kubelet, p, status
+
+
+def test_uncorrectable_ecc_withdraws_only_that_gpu_within_one_period(tmp_path, short_tmp):
+    """ecc_uncorrectable goes up on GPU 3 -> ListAndWatch streams GPU 3 Unhealthy
+    within one health period while the other seven stay Healthy; the reason reaches the status dir."""
+    import json
+    root, kubelet, p, status = _health_stream(tmp_path, short_tmp)
+    t = threading.Thread(target=p.run_forever, daemon=True)
+    t.start()
+    try:
+        reg = kubelet.registered[0]
+        with grpc.insecure_channel("unix://" + os.path.join(short_tmp, reg.endpoint)) as ch:
+            stream = K.device_plugin_stub(ch)["ListAndWatch"](K.DP["Empty"]())
+            first = next(stream)
+            assert all(d.health == "Healthy" for d in first.devices)
+            gpu3 = p.devices[3].id
+            fakesys.set_ras(root, 3, "umc", ue=1, ce=7)
+            t0 = time.monotonic()
+            upd = next(stream)
+            took = time.monotonic() - t0
+            health = {d.ID: d.health for d in upd.devices}
+            assert health[gpu3] == "Unhealthy" and took < 0.2 + 0.5, took
+            assert [i for i, h in health.items() if h != "Healthy"] == [gpu3]
+            stream.cancel()
+        with open(os.path.join(status, DPM.DEVICE_HEALTH_FILE)) as f:
+            doc = json.load(f)
+        assert doc["devices"][gpu3] == {"healthy": False, "reason": "uncorrectable RAS errors: 1 (umc)",
+                                        "resource": "amd.com/gpu", "bdf": p.devices[3].bdf}
+        assert sum(1 for d in doc["devices"].values() if d["healthy"]) == 7
+    finally:
+        p.stop()
+        t.join(2)
+        kubelet.stop()
+
+
+def test_ras_in_any_block_and_retired_pages_withdraw_a_gpu(tmp_path, short_tmp):
+    root, kubelet, p, status = _health_stream(tmp_path, short_tmp, policy=DPM.HealthPolicy(ue_max=0,
+                                                                                          retired_pages_max=4))
+    try:
+        fakesys.set_ras(root, 1, "gfx", ue=2)                  # a compute-block uncorrectable error
+        fakesys.add_bad_pages(root, 5, 3)                      # below the limit: still healthy
+        fakesys.add_bad_pages(root, 6, 2, flag="P")            # pending pages do not count
+        assert p.check_health()
+        bad = {d.id: d.reason for d in p.devices if not d.healthy}
+        assert bad == {p.devices[1].id: "uncorrectable RAS errors: 2 (gfx)"}
+        fakesys.add_bad_pages(root, 5, 1)                      # the 4th retired page
+        assert p.check_health()
+        assert not p.devices[5].healthy and p.devices[5].reason == "retired HBM pages: 4 (limit 4)"
+        assert not p.check_health()                            # no change, no stream update
+        # the counts clear (driver reload): the device comes back
+        fakesys.set_ras(root, 1, "gfx", ue=0)
+        assert p.check_health() and p.devices[1].healthy and p.devices[1].reason == ""
+    finally:
+        p.stop()
+        kubelet.stop()
+
+
+def test_health_policy_from_env_and_a_sick_gpu_is_never_advertised(tmp_path, short_tmp):
+    pol = DPM.HealthPolicy.from_env({"DP_HEALTH_UE_MAX": "5", "DP_HEALTH_RETIRED_PAGES_MAX": "-1"})
+    assert (pol.ue_max, pol.retired_pages_max) == (5, -1)
+    assert pol.verdict({"ras_ue_total": 5, "bad_pages_retired": 10 ** 6}) == ""
+    assert pol.verdict({"ras_ue_total": 6, "ras_ue_blocks": "umc,xgmi_wafl"}).endswith("(umc,xgmi_wafl)")
+    assert DPM.HealthPolicy(ue_max=-1).verdict({"ras_ue_total": 99}) == ""
+    # already sick at start: the first ListAndWatch response carries Unhealthy
+    root = str(fakesys.make_node(tmp_path / "r2", n_gpus=2))
+    fakesys.set_ras(root, 0, "umc", ue=3)
+    kubelet = FakeKubelet(short_tmp)
+    p = DPM.DevicePlugin(cfg(), root=root, plugin_dir=short_tmp)
+    try:
+        p.start()
+        assert [d.healthy for d in p.devices] == [False, True]
+    finally:
+        p.stop()
+        kubelet.stop()

@@ -290,6 +290,10 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
                                          "8": {"total_tflops": 10900.0, "per_gpu_tflops": 1362.5,
                                                "efficiency": 0.9732}}}})
     sd.create(S.PLUGIN_READY, {"ts": t + 9.5})
+    import json as _json
+    sd.write_raw("device-health", _json.dumps({"ts": t, "devices": {
+        "amdgpu-a": {"healthy": True, "reason": "", "bdf": "0000:05:00.0"},
+        "amdgpu-b": {"healthy": False, "reason": "uncorrectable RAS errors: 1 (umc)", "bdf": "0000:15:00.0"}}}))
     sd.create(S.RCCL_READY, {"ts": t + 14.0, "peak_busbw_gbps": 310.0, "ranks": 8,
                              "busbw_by_ranks": {"2": 141.0, "4": 230.5, "8": 310.0}})
     assert S.time_to_ready(sd) == pytest.approx(14.0)
@@ -300,6 +304,11 @@ def test_time_to_ready_and_node_metrics(tmp_path, node_root):
     from prometheus_client import generate_latest
     text = generate_latest(m.registry).decode()
     assert 'amd_gpu_operator_node_time_to_ready_seconds{node="n1"} 14.0' in text
+    # the device plugin's health verdicts (device-health), one series per withdrawn device with its reason
+    assert ('amd_gpu_operator_node_device_unhealthy{bdf="0000:15:00.0",device="amdgpu-b",node="n1",'
+            'reason="uncorrectable RAS errors: 1 (umc)"} 1.0') in text
+    assert 'amd_gpu_operator_node_devices_unhealthy{node="n1"} 1.0' in text
+    assert 'device="amdgpu-a"' not in text
     assert 'amd_gpu_operator_validator_gemm_tflops{dtype="bf16",gpus="8",node="n1",scope="node"} 10900.0' in text
     assert 'amd_gpu_operator_validator_gemm_tflops{dtype="bf16",gpus="1",node="n1",scope="per_gpu"} 1400.0' in text
     assert 'amd_gpu_operator_validator_gemm_scaling_efficiency{dtype="bf16",gpus="8",node="n1"} 0.9732' in text
