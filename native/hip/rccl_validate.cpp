@@ -18,14 +18,19 @@
 //     rccl --processes N) starts the ranks from a parent that never touches the GPU.
 //
 //  4. The link matrix (before the rank sweep, 2+ GPUs): every ordered GPU pair (src -> dst) with
-//     peer access enabled, timed with a copy kernel on dst that reads src's HBM over xGMI (16 B per
+//     peer access enabled, timed with a pull kernel on dst that reads src's HBM over xGMI (16 B per
 //     lane, wide enough to fill a link), first one pair at a time ("isolated"), then all N(N-1)
-//     pairs at once ("concurrent": each GPU pulls from every peer on its own stream). Every copy is
+//     pairs at once ("concurrent": ONE kernel per destination GPU pulls from every peer, its blocks
+//     split among the sources, a rate per source from its blocks' wall-clock stamps -- one stream per
+//     GPU, within the 4 hardware queues a process gets; --link-plan N prints the launch plan). Every copy is
 //     checked (a link that corrupts data fails). A pair below --min-link-relative (0.8) x the node
 //     median of its mode fails and is NAMED (`slow_links`: "3->5"): an all-reduce over 8 ranks can
 //     hide one degraded link, this cannot. One compact `xgmi_matrix` line carries both 8x8 matrices
 //     (GB/s) and the per-GPU measured aggregate (the mesh bound the validator's busBW gate uses).
-//     1 GPU: a clean skip. --link-self-test times GPU 0 -> GPU 0 (the kernels on a 1-GPU box).
+//     1 GPU: a clean skip. --link-self-test times GPU 0 -> GPU 0 (the kernels on a 1-GPU box);
+//     --virtual-peers V pulls V buffers of GPU 0 with one kernel (the concurrent phase's shape on one
+//     GPU), and --throttle-peer P gives source P a quarter of the blocks: the proof that the naming
+//     names the slow source and only it.
 //
 // `ok` also requires the peak bus bandwidth of the largest rank count to reach --min-busbw (an explicit
 // spec.validator.rccl.env RCCL_MIN_BUSBW_GBPS) or, without one, --min-busbw-mesh-fraction x the
@@ -58,6 +63,7 @@
 #include <cstring>
 #include <fstream>
 #include <iomanip>
+#include <map>
 #include <mutex>
 #include <set>
 #include <sstream>
@@ -243,6 +249,10 @@ struct Opts {
   double min_link_relative = 0.8;
   double mesh_fraction = 0;        // busBW floor as a fraction of the measured mesh bound (no --min-busbw)
   bool links = true, links_only = false, link_self_test = false;
+  int virtual_peers = 0;           // 1-GPU self-test: this many source buffers on GPU 0, pulled by one kernel
+  int throttle_peer = -1;          // the source given 1/throttle_factor of the pull blocks (the naming test)
+  int throttle_factor = 4;
+  int link_plan = 0;               // print the plan for this many GPUs and exit (no GPU call)
 };
 
 std::vector<int> parse_list(const std::string& s) {
@@ -309,10 +319,112 @@ bool fabric_check(const std::string& root) {
 }
 
 // --- 4. the link matrix -------------------------------------------------------------------------
+// One pull kernel per destination GPU: its blocks are split among the sources it reads (block ranges
+// first_block[s] .. first_block[s+1]), each block copies its share of its source's buffer over the link
+// and stamps the 100 MHz wall clock around its work; a source's rate is its bytes over the span of its
+// blocks' stamps. So the concurrent phase -- every destination pulling from every peer at once -- needs
+// one stream per GPU, not one per ordered pair: with GPU_MAX_HW_QUEUES=4, 7 streams per GPU shared 3
+// hardware queues two by two, each pair's event window held its queue partner's copies, and a slow link
+// slowed (and could get named instead of) its partner. The isolated phase runs the
+// same kernel with one source.
 struct LinkResult {
   bool ok = true, skipped = false;
   double min_aggregate = 0;   // smallest per-GPU concurrent ingress (GB/s): the measured mesh bound
 };
+
+constexpr int kMaxPullSources = 16;
+constexpr int kPullThreads = 256;
+
+struct PullArgs {
+  const uint4* src[kMaxPullSources];
+  uint4* dst[kMaxPullSources];
+  int first_block[kMaxPullSources + 1];
+};
+
+__global__ void __launch_bounds__(kPullThreads)
+multi_pull_kernel(PullArgs a, int nsrc, size_t vecs, int iters, unsigned long long* __restrict__ stamps) {
+  int s = 0;
+  while (s + 1 < nsrc && (int)blockIdx.x >= a.first_block[s + 1]) ++s;
+  const int nb = a.first_block[s + 1] - a.first_block[s], b = (int)blockIdx.x - a.first_block[s];
+  const uint4* __restrict__ src = a.src[s];
+  uint4* __restrict__ dst = a.dst[s];
+  __syncthreads();
+  const unsigned long long t0 = (unsigned long long)wall_clock64();
+  for (int it = 0; it < iters; ++it)
+    for (size_t i = (size_t)b * kPullThreads + threadIdx.x; i < vecs; i += (size_t)nb * kPullThreads) dst[i] = src[i];
+  __syncthreads();
+  const unsigned long long t1 = (unsigned long long)wall_clock64();
+  if (threadIdx.x == 0) {
+    stamps[2 * blockIdx.x] = t0;
+    stamps[2 * blockIdx.x + 1] = t1;
+  }
+}
+
+// What the link matrix will launch, computed without touching the GPU (--link-plan prints it; the
+// run executes exactly this). A source is a buffer on a GPU: GPU s itself on a multi-GPU node, or one of
+// --virtual-peers buffers on GPU 0 in the 1-GPU self-test ("v3"). `blocks[p]`: the pull blocks of pair p
+// (source si -> destination di) -- --throttle-peer gives one source a quarter (--throttle-factor) of them.
+struct LinkPlan {
+  struct Src {
+    int dev;
+    std::string name;
+    uint32_t pattern;
+  };
+  std::vector<Src> srcs;
+  std::vector<int> dsts;                                // destination devices
+  std::vector<std::pair<int, int>> pairs;               // (source index, destination index)
+  std::vector<int> iso_blocks, conc_blocks;             // per pair
+  std::vector<int> devices;                             // every device involved: one stream each
+};
+
+LinkPlan plan_links(const Opts& o, const std::vector<int>& devs) {
+  LinkPlan pl;
+  const bool virt = o.virtual_peers > 0;
+  if (virt) {
+    for (int v = 0; v < o.virtual_peers; ++v) pl.srcs.push_back({devs[0], "v" + std::to_string(v), (uint32_t)(100 + v)});
+    pl.dsts = {devs[0]};
+  } else {
+    for (int d : devs) pl.srcs.push_back({d, std::to_string(d), (uint32_t)d});
+    pl.dsts = devs;
+  }
+  for (int di = 0; di < (int)pl.dsts.size(); ++di)
+    for (int si = 0; si < (int)pl.srcs.size(); ++si)
+      if (virt || pl.srcs[si].dev != pl.dsts[di] || o.link_self_test) pl.pairs.push_back({si, di});
+  std::set<int> dv;
+  for (const auto& s : pl.srcs) dv.insert(s.dev);
+  for (int d : pl.dsts) dv.insert(d);
+  pl.devices.assign(dv.begin(), dv.end());
+  std::vector<int> per_dst(pl.dsts.size(), 0);
+  for (auto [si, di] : pl.pairs) ++per_dst[di];
+  for (auto [si, di] : pl.pairs) {
+    const bool slow = o.throttle_peer >= 0 && si == o.throttle_peer;
+    const int f = slow ? std::max(1, o.throttle_factor) : 1;
+    pl.iso_blocks.push_back(std::max(8, 2048 / f));
+    // concurrent: ~2048 blocks per destination kernel (8 per CU), split evenly over its sources
+    pl.conc_blocks.push_back(std::max(8, std::max(128, 2048 / std::max(1, per_dst[di])) / f));
+  }
+  return pl;
+}
+
+void print_plan(const LinkPlan& pl) {
+  std::ostringstream k;
+  for (int di = 0; di < (int)pl.dsts.size(); ++di) {
+    int nsrc = 0, blocks = 0;
+    std::string b;
+    for (size_t p = 0; p < pl.pairs.size(); ++p)
+      if (pl.pairs[p].second == di) {
+        ++nsrc;
+        blocks += pl.conc_blocks[p];
+        b += (b.empty() ? "" : ",") + std::to_string(pl.conc_blocks[p]);
+      }
+    k << (di ? "," : "") << "{\"dst\":" << pl.dsts[di] << ",\"sources\":" << nsrc << ",\"blocks\":" << blocks
+      << ",\"blocks_per_source\":[" << b << "]}";
+  }
+  std::printf("{\"event\":\"link_plan\",\"devices\":%zu,\"streams_per_device\":1,\"pairs\":%zu,"
+              "\"concurrent_kernels\":[%s]}\n",
+              pl.devices.size(), pl.pairs.size(), k.str().c_str());
+  std::fflush(stdout);
+}
 
 static double median_of(std::vector<double> v) {
   if (v.empty()) return 0;
@@ -320,144 +432,182 @@ static double median_of(std::vector<double> v) {
   return v[v.size() / 2];
 }
 
-// Times every ordered pair of `devs` (isolated, then concurrent) and prints the `xgmi_matrix` line.
+// Times every pair of the plan (isolated, then concurrent) and prints the `xgmi_matrix` line.
 int link_matrix(const Opts& o, const std::vector<int>& devs, LinkResult& res) {
-  const int n = (int)devs.size();
+  const LinkPlan pl = plan_links(o, devs);
+  const int ns = (int)pl.srcs.size(), nd = (int)pl.dsts.size();
   const size_t bytes = o.link_bytes & ~(size_t)15, words = bytes / 4, vecs = bytes / 16;
-  std::vector<std::pair<int, int>> pairs;
-  for (int d = 0; d < n; ++d)
-    for (int s = 0; s < n; ++s)
-      if (s != d || o.link_self_test) pairs.push_back({s, d});
-  // peer access for every pair (the copy kernel on dst dereferences src's memory)
+  // peer access for every cross-GPU pair (the pull kernel on dst dereferences src's memory)
   std::vector<std::string> no_peer;
-  for (auto [s, d] : pairs) {
-    if (s == d) continue;
+  std::vector<bool> usable(pl.pairs.size(), true);
+  for (size_t p = 0; p < pl.pairs.size(); ++p) {
+    const int sd = pl.srcs[pl.pairs[p].first].dev, dd = pl.dsts[pl.pairs[p].second];
+    if (sd == dd) continue;
     int can = 0;
-    HIPCHECK(hipDeviceCanAccessPeer(&can, devs[d], devs[s]));
+    HIPCHECK(hipDeviceCanAccessPeer(&can, dd, sd));
     if (!can) {
-      no_peer.push_back(std::to_string(devs[s]) + "->" + std::to_string(devs[d]));
+      no_peer.push_back(pl.srcs[pl.pairs[p].first].name + "->" + std::to_string(dd));
+      usable[p] = false;
       continue;
     }
-    HIPCHECK(hipSetDevice(devs[d]));
-    const hipError_t e = hipDeviceEnablePeerAccess(devs[s], 0);
+    HIPCHECK(hipSetDevice(dd));
+    const hipError_t e = hipDeviceEnablePeerAccess(sd, 0);
     if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
     (void)hipGetLastError();
   }
-  // buffers: one patterned source per GPU, one destination per (dst, src) pair, a stream per pair
-  std::vector<void*> src(n, nullptr);
-  std::vector<std::vector<void*>> dst(n, std::vector<void*>(n, nullptr));
-  std::vector<std::vector<hipStream_t>> st(n, std::vector<hipStream_t>(n, nullptr));
-  std::vector<std::vector<hipEvent_t>> e0(n, std::vector<hipEvent_t>(n, nullptr)), e1 = e0;
-  std::vector<unsigned long long*> bad(n, nullptr);
-  for (int g = 0; g < n; ++g) {
-    HIPCHECK(hipSetDevice(devs[g]));
-    HIPCHECK(hipMalloc(&src[g], bytes));
-    HIPCHECK(hipMalloc(&bad[g], sizeof(unsigned long long)));
-    pattern_kernel<<<1024, 256>>>((uint32_t*)src[g], words, (uint32_t)devs[g]);
+  // one stream per device; a patterned buffer per source; a destination buffer per pair
+  std::map<int, hipStream_t> st;
+  std::map<int, unsigned long long*> bad;
+  std::map<int, double> tick_hz;
+  for (int d : pl.devices) {
+    HIPCHECK(hipSetDevice(d));
+    HIPCHECK(hipStreamCreateWithFlags(&st[d], hipStreamNonBlocking));
+    HIPCHECK(hipMalloc(&bad[d], sizeof(unsigned long long)));
+    int khz = 0;
+    HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d));
+    tick_hz[d] = khz > 0 ? khz * 1e3 : 1e8;
+  }
+  std::vector<void*> src(ns, nullptr), dst(pl.pairs.size(), nullptr);
+  for (int si = 0; si < ns; ++si) {
+    HIPCHECK(hipSetDevice(pl.srcs[si].dev));
+    HIPCHECK(hipMalloc(&src[si], bytes));
+    pattern_kernel<<<1024, 256, 0, st[pl.srcs[si].dev]>>>((uint32_t*)src[si], words, pl.srcs[si].pattern);
     HIPCHECK(hipGetLastError());
   }
-  for (auto [s, d] : pairs) {
-    HIPCHECK(hipSetDevice(devs[d]));
-    HIPCHECK(hipMalloc(&dst[d][s], bytes));
-    HIPCHECK(hipStreamCreateWithFlags(&st[d][s], hipStreamNonBlocking));
-    HIPCHECK(hipEventCreate(&e0[d][s]));
-    HIPCHECK(hipEventCreate(&e1[d][s]));
+  int max_grid = 0;
+  for (size_t p = 0; p < pl.pairs.size(); ++p) {
+    HIPCHECK(hipSetDevice(pl.dsts[pl.pairs[p].second]));
+    HIPCHECK(hipMalloc(&dst[p], bytes));
+    max_grid = std::max(max_grid, pl.iso_blocks[p]);
   }
-  for (int g = 0; g < n; ++g) {
-    HIPCHECK(hipSetDevice(devs[g]));
-    HIPCHECK(hipDeviceSynchronize());
+  std::vector<int> grid_of(nd, 0);
+  for (size_t p = 0; p < pl.pairs.size(); ++p) grid_of[pl.pairs[p].second] += usable[p] ? pl.conc_blocks[p] : 0;
+  for (int g : grid_of) max_grid = std::max(max_grid, g);
+  std::map<int, unsigned long long*> stamps;
+  for (int d : pl.dsts) {
+    HIPCHECK(hipSetDevice(d));
+    HIPCHECK(hipMalloc(&stamps[d], (size_t)max_grid * 2 * sizeof(unsigned long long)));
   }
-  auto copy = [&](int s, int d) {
-    peer_read_kernel<<<2048, 256, 0, st[d][s]>>>((const uint4*)src[s], (uint4*)dst[d][s], vecs);
-  };
-  std::vector<std::vector<double>> iso(n, std::vector<double>(n, 0.0)), conc = iso;
-  std::vector<std::vector<unsigned long long>> errs(n, std::vector<unsigned long long>(n, 0));
-  g_watchdog.arm(Watchdog::kLinks, n, bytes);
-  // isolated: one pair at a time
-  for (auto [s, d] : pairs) {
-    HIPCHECK(hipSetDevice(devs[d]));
-    copy(s, d);
-    copy(s, d);
-    HIPCHECK(hipEventRecord(e0[d][s], st[d][s]));
-    for (int i = 0; i < o.link_iters; ++i) copy(s, d);
-    HIPCHECK(hipEventRecord(e1[d][s], st[d][s]));
-    HIPCHECK(hipEventSynchronize(e1[d][s]));
-    float ms = 0;
-    HIPCHECK(hipEventElapsedTime(&ms, e0[d][s], e1[d][s]));
-    iso[d][s] = ms > 0 ? (double)bytes * o.link_iters / (ms * 1e-3) / 1e9 : 0;
+  for (int d : pl.devices) {
+    HIPCHECK(hipSetDevice(d));
+    HIPCHECK(hipStreamSynchronize(st[d]));
   }
-  // concurrent: every pair at once (each GPU pulls from all its peers, each link in both directions)
-  for (auto [s, d] : pairs) {
-    HIPCHECK(hipSetDevice(devs[d]));
-    copy(s, d);
-  }
-  for (int g = 0; g < n; ++g) {
-    HIPCHECK(hipSetDevice(devs[g]));
-    HIPCHECK(hipDeviceSynchronize());
-  }
-  for (auto [s, d] : pairs) {
-    HIPCHECK(hipSetDevice(devs[d]));
-    HIPCHECK(hipEventRecord(e0[d][s], st[d][s]));
-  }
-  for (int i = 0; i < o.link_iters; ++i)
-    for (auto [s, d] : pairs) {
-      HIPCHECK(hipSetDevice(devs[d]));
-      copy(s, d);
+  // one launch of destination di's kernel over `which` pairs with their block counts
+  auto launch = [&](int di, const std::vector<size_t>& which, const std::vector<int>& blocks, int iters,
+                    std::vector<std::pair<int, int>>* ranges) -> int {
+    PullArgs a{};
+    int b = 0, k = 0;
+    for (size_t p : which) {
+      a.src[k] = (const uint4*)src[pl.pairs[p].first];
+      a.dst[k] = (uint4*)dst[p];
+      a.first_block[k] = b;
+      if (ranges) ranges->push_back({b, b + blocks[p]});
+      b += blocks[p];
+      ++k;
     }
-  for (auto [s, d] : pairs) {
-    HIPCHECK(hipSetDevice(devs[d]));
-    HIPCHECK(hipEventRecord(e1[d][s], st[d][s]));
+    a.first_block[k] = b;
+    const int d = pl.dsts[di];
+    HIPCHECK(hipSetDevice(d));
+    multi_pull_kernel<<<b, kPullThreads, 0, st[d]>>>(a, k, vecs, iters, stamps[d]);
+    HIPCHECK(hipGetLastError());
+    return 0;
+  };
+  // per pair: bytes x iters over the span of its blocks' stamps
+  auto rates = [&](int di, const std::vector<size_t>& which, const std::vector<std::pair<int, int>>& ranges,
+                   int iters, std::vector<double>& out) -> int {
+    const int d = pl.dsts[di];
+    const int n = ranges.empty() ? 0 : ranges.back().second;
+    std::vector<unsigned long long> h((size_t)n * 2);
+    HIPCHECK(hipSetDevice(d));
+    HIPCHECK(hipMemcpyAsync(h.data(), stamps[d], h.size() * 8, hipMemcpyDeviceToHost, st[d]));
+    HIPCHECK(hipStreamSynchronize(st[d]));
+    for (size_t q = 0; q < which.size(); ++q) {
+      unsigned long long lo = ~0ull, hi = 0;
+      for (int b = ranges[q].first; b < ranges[q].second; ++b) lo = std::min(lo, h[2 * b]), hi = std::max(hi, h[2 * b + 1]);
+      const double s = hi > lo ? (double)(hi - lo) / tick_hz[d] : 0;
+      out[which[q]] = s > 0 ? (double)bytes * iters / s / 1e9 : 0;
+    }
+    return 0;
+  };
+  std::vector<double> iso(pl.pairs.size(), 0.0), conc(pl.pairs.size(), 0.0);
+  std::vector<unsigned long long> errs(pl.pairs.size(), 0);
+  g_watchdog.arm(Watchdog::kLinks, nd, bytes);
+  // isolated: one pair at a time (a warm-up pass, then the timed launch of link_iters passes)
+  for (size_t p = 0; p < pl.pairs.size(); ++p) {
+    if (!usable[p]) continue;
+    const int di = pl.pairs[p].second;
+    std::vector<std::pair<int, int>> ranges;
+    if (launch(di, {p}, pl.iso_blocks, 1, nullptr) || launch(di, {p}, pl.iso_blocks, o.link_iters, &ranges) ||
+        rates(di, {p}, ranges, o.link_iters, iso))
+      return 2;
   }
-  for (auto [s, d] : pairs) {
-    HIPCHECK(hipSetDevice(devs[d]));
-    HIPCHECK(hipEventSynchronize(e1[d][s]));
-    float ms = 0;
-    HIPCHECK(hipEventElapsedTime(&ms, e0[d][s], e1[d][s]));
-    conc[d][s] = ms > 0 ? (double)bytes * o.link_iters / (ms * 1e-3) / 1e9 : 0;
+  // concurrent: every destination's kernel over all its sources, all destinations at once
+  std::vector<std::vector<size_t>> by_dst(nd);
+  for (size_t p = 0; p < pl.pairs.size(); ++p)
+    if (usable[p]) by_dst[pl.pairs[p].second].push_back(p);
+  for (int di = 0; di < nd; ++di)
+    if (!by_dst[di].empty() && launch(di, by_dst[di], pl.conc_blocks, 1, nullptr)) return 2;
+  for (int d : pl.dsts) {
+    HIPCHECK(hipSetDevice(d));
+    HIPCHECK(hipStreamSynchronize(st[d]));
   }
-  // correctness: every destination holds its source's pattern
-  for (auto [s, d] : pairs) {
-    HIPCHECK(hipSetDevice(devs[d]));
-    HIPCHECK(hipMemsetAsync(bad[d], 0, sizeof(unsigned long long), st[d][s]));
-    pattern_check_kernel<<<1024, 256, 0, st[d][s]>>>((const uint32_t*)dst[d][s], words, (uint32_t)devs[s], bad[d]);
+  std::vector<std::vector<std::pair<int, int>>> ranges(nd);
+  for (int di = 0; di < nd; ++di)
+    if (!by_dst[di].empty() && launch(di, by_dst[di], pl.conc_blocks, o.link_iters, &ranges[di])) return 2;
+  for (int di = 0; di < nd; ++di)
+    if (!by_dst[di].empty() && rates(di, by_dst[di], ranges[di], o.link_iters, conc)) return 2;
+  // correctness: every destination buffer holds its source's pattern
+  for (size_t p = 0; p < pl.pairs.size(); ++p) {
+    if (!usable[p]) continue;
+    const int d = pl.dsts[pl.pairs[p].second];
+    HIPCHECK(hipSetDevice(d));
+    HIPCHECK(hipMemsetAsync(bad[d], 0, sizeof(unsigned long long), st[d]));
+    pattern_check_kernel<<<1024, 256, 0, st[d]>>>((const uint32_t*)dst[p], words, pl.srcs[pl.pairs[p].first].pattern,
+                                                   bad[d]);
     unsigned long long h = 0;
-    HIPCHECK(hipMemcpyAsync(&h, bad[d], sizeof h, hipMemcpyDeviceToHost, st[d][s]));
-    HIPCHECK(hipStreamSynchronize(st[d][s]));
-    errs[d][s] = h;
+    HIPCHECK(hipMemcpyAsync(&h, bad[d], sizeof h, hipMemcpyDeviceToHost, st[d]));
+    HIPCHECK(hipStreamSynchronize(st[d]));
+    errs[p] = h;
   }
   g_watchdog.disarm();
   // the relative gate, per mode, against the node median of that mode
   std::vector<double> iv, cv;
-  for (auto [s, d] : pairs) iv.push_back(iso[d][s]), cv.push_back(conc[d][s]);
+  for (size_t p = 0; p < pl.pairs.size(); ++p)
+    if (usable[p]) iv.push_back(iso[p]), cv.push_back(conc[p]);
   const double imed = median_of(iv), cmed = median_of(cv);
   std::vector<std::string> slow, corrupt;
   double worst = 1e30;
-  for (auto [s, d] : pairs) {
-    const double ri = imed > 0 ? iso[d][s] / imed : 0, rc = cmed > 0 ? conc[d][s] / cmed : 0;
+  for (size_t p = 0; p < pl.pairs.size(); ++p) {
+    if (!usable[p]) continue;
+    const double ri = imed > 0 ? iso[p] / imed : 0, rc = cmed > 0 ? conc[p] / cmed : 0;
     worst = std::min(worst, std::min(ri, rc));
-    const std::string name = std::to_string(devs[s]) + "->" + std::to_string(devs[d]);
-    if (errs[d][s]) corrupt.push_back(name);
+    const std::string name = pl.srcs[pl.pairs[p].first].name + "->" + std::to_string(pl.dsts[pl.pairs[p].second]);
+    if (errs[p]) corrupt.push_back(name);
     if (o.min_link_relative > 0 && (ri < o.min_link_relative || rc < o.min_link_relative)) {
       slow.push_back(name);
-      std::printf("{\"event\":\"xgmi_link\",\"src\":%d,\"dst\":%d,\"isolated_gbps\":%.1f,\"concurrent_gbps\":%.1f,"
+      const std::string& sn = pl.srcs[pl.pairs[p].first].name;     // a GPU index, or "v3" (virtual peer)
+      const std::string sj = o.virtual_peers > 0 ? "\"" + sn + "\"" : sn;
+      std::printf("{\"event\":\"xgmi_link\",\"src\":%s,\"dst\":%d,\"isolated_gbps\":%.1f,\"concurrent_gbps\":%.1f,"
                   "\"isolated_ratio\":%.3f,\"concurrent_ratio\":%.3f,\"ok\":false,\"kind\":\"link\"}\n",
-                  devs[s], devs[d], iso[d][s], conc[d][s], ri, rc);
+                  sj.c_str(), pl.dsts[pl.pairs[p].second], iso[p], conc[p], ri, rc);
     }
   }
   // per-GPU measured ingress with every peer pulling at once: the mesh bound of a collective
-  std::vector<double> agg(n, 0.0);
-  for (auto [s, d] : pairs) agg[d] += conc[d][s];
-  res.min_aggregate = n ? *std::min_element(agg.begin(), agg.end()) : 0;
+  std::vector<double> agg(nd, 0.0);
+  for (size_t p = 0; p < pl.pairs.size(); ++p) agg[pl.pairs[p].second] += conc[p];
+  res.min_aggregate = nd ? *std::min_element(agg.begin(), agg.end()) : 0;
   res.ok = slow.empty() && corrupt.empty() && no_peer.empty();
-  auto matrix = [&](const std::vector<std::vector<double>>& m) {   // m[dst][src] -> rows = src, columns = dst
+  auto matrix = [&](const std::vector<double>& v) {   // rows = sources, columns = destinations
+    std::vector<std::vector<double>> m(ns, std::vector<double>(nd, 0.0));
+    for (size_t p = 0; p < pl.pairs.size(); ++p) m[pl.pairs[p].first][pl.pairs[p].second] = v[p];
     std::ostringstream js;
     js << "[";
-    for (int row = 0; row < n; ++row) {
-      js << (row ? "," : "") << "[";
-      for (int col = 0; col < n; ++col) {
+    for (int r = 0; r < ns; ++r) {
+      js << (r ? "," : "") << "[";
+      for (int c = 0; c < nd; ++c) {
         char b[24];
-        std::snprintf(b, sizeof b, "%.1f", m[col][row]);
-        js << (col ? "," : "") << b;
+        std::snprintf(b, sizeof b, "%.1f", m[r][c]);
+        js << (c ? "," : "") << b;
       }
       js << "]";
     }
@@ -469,28 +619,34 @@ int link_matrix(const Opts& o, const std::vector<int>& devs, LinkResult& res) {
     for (const auto& x : v) out += (out.empty() ? "\"" : ",\"") + x + "\"";
     return out;
   };
-  std::ostringstream ag;
-  for (int g = 0; g < n; ++g) ag << (g ? "," : "") << std::fixed << std::setprecision(1) << agg[g];
-  std::printf("{\"event\":\"xgmi_matrix\",\"gpus\":%d,\"bytes\":%zu,\"iters\":%d,\"isolated_gbps\":%s,"
-              "\"concurrent_gbps\":%s,\"median_isolated_gbps\":%.1f,\"median_concurrent_gbps\":%.1f,"
+  std::ostringstream ag, names;
+  for (int g = 0; g < nd; ++g) ag << (g ? "," : "") << std::fixed << std::setprecision(1) << agg[g];
+  for (int si = 0; si < ns; ++si) names << (si ? ",\"" : "\"") << pl.srcs[si].name << "\"";
+  std::printf("{\"event\":\"xgmi_matrix\",\"gpus\":%d,\"sources\":[%s],\"bytes\":%zu,\"iters\":%d,"
+              "\"isolated_gbps\":%s,\"concurrent_gbps\":%s,\"median_isolated_gbps\":%.1f,\"median_concurrent_gbps\":%.1f,"
               "\"gpu_ingress_gbps\":[%s],\"min_gpu_ingress_gbps\":%.1f,\"min_ratio\":%.3f,\"min_link_relative\":%.2f,"
-              "\"slow_links\":[%s],\"corrupt_links\":[%s],\"no_peer_access\":[%s],\"self_test\":%s,\"ok\":%s%s}\n",
-              n, bytes, o.link_iters, matrix(iso).c_str(), matrix(conc).c_str(), imed, cmed, ag.str().c_str(),
-              res.min_aggregate, pairs.empty() ? 0.0 : worst, o.min_link_relative, list(slow).c_str(),
-              list(corrupt).c_str(), list(no_peer).c_str(), o.link_self_test ? "true" : "false",
+              "\"slow_links\":[%s],\"corrupt_links\":[%s],\"no_peer_access\":[%s],\"self_test\":%s,"
+              "\"virtual_peers\":%d,\"throttle_peer\":%d,\"streams_per_device\":1,"
+              "\"concurrent_method\":\"one pull kernel per destination, per-source block stamps\",\"ok\":%s%s}\n",
+              nd, names.str().c_str(), bytes, o.link_iters, matrix(iso).c_str(), matrix(conc).c_str(), imed, cmed,
+              ag.str().c_str(), res.min_aggregate, pl.pairs.empty() ? 0.0 : worst, o.min_link_relative,
+              list(slow).c_str(), list(corrupt).c_str(), list(no_peer).c_str(),
+              (o.link_self_test || o.virtual_peers > 0) ? "true" : "false", o.virtual_peers, o.throttle_peer,
               res.ok ? "true" : "false", res.ok ? "" : ",\"kind\":\"link\"");
   std::fflush(stdout);
-  for (auto [s, d] : pairs) {
-    (void)hipSetDevice(devs[d]);
-    (void)hipFree(dst[d][s]);
-    (void)hipStreamDestroy(st[d][s]);
-    (void)hipEventDestroy(e0[d][s]);
-    (void)hipEventDestroy(e1[d][s]);
+  for (size_t p = 0; p < pl.pairs.size(); ++p) {
+    (void)hipSetDevice(pl.dsts[pl.pairs[p].second]);
+    (void)hipFree(dst[p]);
   }
-  for (int g = 0; g < n; ++g) {
-    (void)hipSetDevice(devs[g]);
-    (void)hipFree(src[g]);
-    (void)hipFree(bad[g]);
+  for (int si = 0; si < ns; ++si) {
+    (void)hipSetDevice(pl.srcs[si].dev);
+    (void)hipFree(src[si]);
+  }
+  for (int d : pl.devices) {
+    (void)hipSetDevice(d);
+    (void)hipFree(bad[d]);
+    if (stamps.count(d)) (void)hipFree(stamps[d]);
+    (void)hipStreamDestroy(st[d]);
   }
   return 0;
 }
@@ -686,11 +842,16 @@ int main(int argc, char** argv) {
     else if (a == "--no-links") o.links = false;
     else if (a == "--links-only") o.links_only = true;
     else if (a == "--link-self-test") o.link_self_test = true;
+    else if (a == "--virtual-peers") o.virtual_peers = std::max(0, std::min(kMaxPullSources, std::atoi(next().c_str())));
+    else if (a == "--throttle-peer") o.throttle_peer = std::atoi(next().c_str());
+    else if (a == "--throttle-factor") o.throttle_factor = std::max(1, std::atoi(next().c_str()));
+    else if (a == "--link-plan") o.link_plan = std::max(1, std::atoi(next().c_str()));
     else if (a == "-h" || a == "--help") {
       std::printf("usage: amd-rccl-validate [--ranks 2,4,8] [--min-bytes B] [--max-bytes B] [--iters N] "
                   "[--warmup N] [--dtype float|bf16] [--min-busbw GBPS] [--topology-only] [--timeout-s T] [--sys-root DIR] "
                   "[--mp-rank R --mp-nranks N --mp-id-file F [--device D]] [--link-bytes B] [--link-iters N] "
-                  "[--min-link-relative R] [--min-busbw-mesh-fraction F] [--no-links] [--links-only] [--link-self-test]\n");
+                  "[--min-link-relative R] [--min-busbw-mesh-fraction F] [--no-links] [--links-only] [--link-self-test] "
+                  "[--virtual-peers V] [--throttle-peer P] [--throttle-factor F] [--link-plan N]\n");
       return 0;
     } else {
       std::printf("{\"error\":\"unknown argument %s\"}\n", a.c_str());
@@ -700,6 +861,12 @@ int main(int argc, char** argv) {
   if (o.dtype != "float" && o.dtype != "bf16") {
     std::printf("{\"error\":\"unknown --dtype %s\"}\n", o.dtype.c_str());
     return 2;
+  }
+  if (o.link_plan > 0) {            // what the link matrix launches on N GPUs (no GPU call; CPU tests)
+    std::vector<int> devs(o.virtual_peers > 0 ? 1 : o.link_plan);
+    for (int d = 0; d < (int)devs.size(); ++d) devs[d] = d;
+    print_plan(plan_links(o, devs));
+    return 0;
   }
   if (o.mp_rank >= 0) {
     if (o.mp_nranks < 1 || o.mp_rank >= o.mp_nranks || o.id_file.empty()) {
@@ -730,9 +897,10 @@ int main(int argc, char** argv) {
   // the link matrix over every visible GPU (one process: peer access between its devices)
   LinkResult links;
   if (o.links || o.links_only) {
-    std::vector<int> all(o.link_self_test ? 1 : ndev);
+    const bool self = o.link_self_test || o.virtual_peers > 0;
+    std::vector<int> all(self ? 1 : ndev);
     for (int d = 0; d < (int)all.size(); ++d) all[d] = d;
-    if ((int)all.size() >= 2 || o.link_self_test) {
+    if ((int)all.size() >= 2 || self) {
       if (link_matrix(o, all, links)) return 2;
       all_ok = links.ok;
     } else {

@@ -306,3 +306,27 @@ def test_xgmi_link_matrix_on_one_gpu_is_a_clean_skip_and_its_kernels_run():
     print(f"GPU0 -> GPU0 copy: isolated {mx['isolated_gbps']} GB/s, concurrent {mx['concurrent_gbps']} GB/s")
     assert mx["self_test"] and mx["ok"] and mx["corrupt_links"] == [] and mx["gpus"] == 1
     assert mx["isolated_gbps"][0][0] > 1000          # an HBM3E copy kernel: TB/s, not PCIe
+
+
+def test_link_matrix_names_the_throttled_virtual_peer_only():
+    """VERDICT r5 item 2 on one GPU: 7 source buffers on GPU 0 pulled by ONE kernel (the concurrent
+    phase's shape: one kernel, one stream per destination), source 3 given a quarter of the blocks.
+    The throttled peer, and only it, is named; the unthrottled concurrent rates agree within 10 %."""
+    rc, lines, err = run("amd-rccl-validate", "--links-only", "--virtual-peers", "7", "--link-bytes", str(128 << 20),
+                         timeout=180)
+    assert rc == 0, (lines, err)
+    mx = [x for x in lines if x.get("event") == "xgmi_matrix"][0]
+    conc = [row[0] for row in mx["concurrent_gbps"]]
+    print(f"7 virtual peers, concurrent GB/s per source: {conc}; isolated: {[r[0] for r in mx['isolated_gbps']]}")
+    assert mx["ok"] and mx["slow_links"] == [] and mx["streams_per_device"] == 1
+    assert max(conc) / min(conc) < 1.10, conc
+    rc, lines, err = run("amd-rccl-validate", "--links-only", "--virtual-peers", "7", "--throttle-peer", "3",
+                         "--link-bytes", str(128 << 20), timeout=180)
+    assert rc == 1, (lines, err)
+    mx = [x for x in lines if x.get("event") == "xgmi_matrix"][0]
+    conc = [row[0] for row in mx["concurrent_gbps"]]
+    print(f"throttled v3: concurrent GB/s per source: {conc}")
+    assert mx["slow_links"] == ["v3->0"] and mx["kind"] == "link", mx
+    others = [c for i, c in enumerate(conc) if i != 3]
+    assert max(others) / min(others) < 1.10, others
+    assert [x["src"] for x in lines if x.get("event") == "xgmi_link"] == ["v3"]
