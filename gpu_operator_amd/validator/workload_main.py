@@ -41,8 +41,8 @@ BIN_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 # instruction the fp8 kernel issues is counted under F8 or F6F4 depending on the firmware, so the
 # fp8 pass collects both and sums them.
 PMC_PASSES = {
-    "bf16": {"kernel": "gemm_bf16_256x256", "mops": ["SQ_INSTS_VALU_MFMA_MOPS_BF16"]},
-    "fp8": {"kernel": "gemm_fp8_256x256", "mops": ["SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_INSTS_VALU_MFMA_MOPS_F6F4"]},
+    "bf16": {"kernel": "gemm_", "mops": ["SQ_INSTS_VALU_MFMA_MOPS_BF16"]},
+    "fp8": {"kernel": "gemm_", "mops": ["SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_INSTS_VALU_MFMA_MOPS_F6F4"]},
 }
 PMC_COMMON = ["SQ_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "TCC_HIT_sum", "TCC_MISS_sum"]
 PMC_COUNTERS = PMC_PASSES["bf16"]["mops"] + PMC_COMMON      # the bf16 pass (kept for callers)
@@ -157,6 +157,24 @@ def _shape_mnk(shape: str):
     return (parts[0],) * 3 if len(parts) == 1 else tuple(parts[:3])
 
 
+def timed_gemm_kernel(name: str) -> bool:
+    """Whether a profiled kernel is the probe's timed GEMM dispatch: any kernel of the GEMM family the
+    dispatch picked (256x256 asm pipeline, gemm_mfma_small / _sk, generic) in its timed instantiation --
+    not the placement-recording one of the checked dispatch (Rec 1, gemm_tile_common.h), not the ABFT,
+    reference or fill kernels. The template argument reads ``3RecE0E`` mangled, ``Rec)0`` demangled."""
+    n = name or ""
+    return "gemm_" in n and ("3RecE0E" in n or "Rec)0" in n) and "ref_rows" not in n
+
+
+def _short_kernel(name: str) -> str:
+    for fam in ("gemm_mfma_small_sk", "gemm_mfma_small", "gemm_bf16_256x256_w4ap", "gemm_bf16_256x256_w4sp",
+                "gemm_bf16_256x256_w4s", "gemm_fp8_256x256_q16ap", "gemm_fp8_256x256_q16p", "gemm_fp8_256x256_q16",
+                "gemm_fp8_256x256_w4sp", "gemm_bf16_generic", "gemm_fp8_generic"):
+        if fam in name:
+            return fam
+    return name[:60]
+
+
 def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "bf16",
                      visible: Optional[List[int]] = None) -> List[Dict]:
     """One profiled GEMM dispatch of ``dtype`` under rocprofv3 (counters only: no sys/runtime
@@ -180,18 +198,20 @@ def collect_counters(shape: str, run: Callable = subprocess.run, dtype: str = "b
             return [{"event": "counters", "dtype": dtype, "ok": False,
                      "error": f"rocprofv3 exit {p.returncode}: {(p.stderr or '')[-300:]}"}]
         agg: Dict[str, float] = {}
+        kernels = set()
         with open(files[0]) as f:
             for row in csv.DictReader(f):
-                if spec["kernel"] not in row.get("Kernel_Name", ""):
+                if not timed_gemm_kernel(row.get("Kernel_Name", "")):
                     continue
+                kernels.add(_short_kernel(row.get("Kernel_Name", "")))
                 agg[row["Counter_Name"]] = agg.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
         if not agg:
-            return [{"event": "counters", "dtype": dtype, "ok": False,
-                     "error": f"no {spec['kernel']} dispatch in the counter records"}]
+            return [{"event": "counters", "dtype": dtype, "shape": shape, "ok": False,
+                     "error": "no timed GEMM dispatch in the counter records"}]
         m, n, k = _shape_mnk(shape)
         mops = sum(agg.get(c, 0.0) for c in spec["mops"])
         want = 2.0 * m * n * k / 512
-        res = {"event": "counters", "dtype": dtype, "kernel": spec["kernel"], "shape": shape, **agg,
+        res = {"event": "counters", "dtype": dtype, "kernel": ",".join(sorted(kernels)), "shape": shape, **agg,
                "mfma_mops": mops, "mfma_mops_expected": want, "mfma_mops_match": abs(mops - want) <= 1e-6 * want,
                "lds_conflict_free": agg.get("SQ_LDS_BANK_CONFLICT", 1.0) == 0.0}
         res["ok"] = res["mfma_mops_match"]
@@ -262,10 +282,12 @@ def run_hip(shapes: List[str], counters: bool = False, iters: int = 50,
             results.append({"event": "gemm", "probe": True, "ok": False, "rc": rc})
     results += gpu_tflops_lines(results)
     if counters and full:
+        # every shape of the plan, each dtype: the counters follow whichever kernel the dispatch picks
         for d in (["bf16", "fp8"] if dtype == "both" else [dtype]):
-            # the profiler writes its counters from the child's exit path: wait for it (subprocess.run)
-            results += collect_counters(shapes[0], subprocess.run if run is stream_run else run, dtype=d,
-                                        visible=devices[:1] if devices else None)
+            for shape in shapes:
+                # the profiler writes its counters from the child's exit path: wait for it (subprocess.run)
+                results += collect_counters(shape, subprocess.run if run is stream_run else run, dtype=d,
+                                            visible=devices[:1] if devices else None)
     return results
 
 

@@ -135,6 +135,23 @@ def test_node_probe_on_real_hardware():
     assert any(g["gfx"] == "gfx950" for g in j["gpus"])
 
 
+def test_counters_follow_the_dispatched_kernel_for_every_shape_and_dtype():
+    """GEMM_SHAPES=1024,8192 with --counters -> an ok counters line per shape and
+    dtype, MFMA ops matching 2MNK/512 -- 1024^3 runs gemm_mfma_small (v60), 8192^3 the asm pipeline --
+    and only the timed dispatch is counted (the checked dispatch's recording kernel is not)."""
+    from gpu_operator_amd.validator import workload_main as W
+    if W.rocprofv3_path() is None:
+        pytest.skip("rocprofv3 not installed")
+    results = W.run_hip(["1024", "8192"], counters=True, iters=5, dtype="both")
+    ctr = {(r["dtype"], r["shape"]): r for r in results if r.get("event") == "counters"}
+    assert set(ctr) == {(d, s) for d in ("bf16", "fp8") for s in ("1024", "8192")}, list(ctr)
+    for key, c in ctr.items():
+        print(key, c.get("kernel"), c.get("mfma_mops"), c.get("mfma_mops_expected"))
+        assert c["ok"] and c["mfma_mops_match"], (key, c)
+    assert "gemm_mfma_small" in ctr[("bf16", "1024")]["kernel"] and "gemm_mfma_small" in ctr[("fp8", "1024")]["kernel"]
+    assert ctr[("bf16", "8192")]["kernel"] == "gemm_bf16_256x256_w4ap"
+
+
 def test_validator_workload_hip_with_counters(tmp_path):
     """Counters for both kernels when the pod runs --gemm-dtype both; rocprofv3 ships in this image,
     so a skipped or failed collection fails the test (it cannot pass vacuously)."""

@@ -174,3 +174,19 @@ def test_stream_run_without_done_line_waits_and_times_out(tmp_path):
     with pytest.raises(subprocess.TimeoutExpired):
         WM.stream_run([hang], timeout=1.0)
     assert time.monotonic() - t < 5.0
+
+
+def test_counter_filter_takes_the_timed_gemm_only():
+    """The counter pass keeps the timed GEMM dispatch of any family and drops the checked dispatch's
+    placement-recording instantiation and the ABFT / reference / fill kernels."""
+    f = WM.timed_gemm_kernel
+    assert f("_ZN12_GLOBAL__N_122gemm_bf16_256x256_w4apILi19ELb1ELb0ELi8ELi0ELNS_3RecE0EEEvPKDF16bS3_PDF16biii")
+    assert not f("_ZN12_GLOBAL__N_122gemm_bf16_256x256_w4apILi19ELb1ELb0ELi8ELi0ELNS_3RecE1EEEvPKDF16bS3_PDF16biii")
+    assert f("void (anonymous namespace)::gemm_mfma_small<false, 128, ((anonymous namespace)::Rec)0>(void const*)")
+    assert f("void (anonymous namespace)::gemm_fp8_256x256_q16ap<2, true, true, 17, 2, ((anonymous namespace)::Rec)0>()")
+    assert not f("void (anonymous namespace)::gemm_fp8_256x256_q16ap<2, true, true, 17, 2, ((anonymous namespace)::Rec)1>()")
+    for other in ("(anonymous namespace)::abft_compare(float const*)", "void (anonymous namespace)::abft_expect<unsigned char>()",
+                  "(anonymous namespace)::fill_uniform_bf16(bool _Accum*, unsigned int)"):
+        assert not f(other)
+    assert WM._short_kernel("void (anonymous namespace)::gemm_mfma_small_sk<true, 128, ((anonymous namespace)::Rec)0>") \
+        == "gemm_mfma_small_sk"
