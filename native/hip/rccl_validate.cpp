@@ -29,7 +29,7 @@
 //     (GB/s) and the per-GPU measured aggregate (the mesh bound the validator's busBW gate uses).
 //     1 GPU: a clean skip. --link-self-test times GPU 0 -> GPU 0 (the kernels on a 1-GPU box);
 //     --virtual-peers V pulls V buffers of GPU 0 with one kernel (the concurrent phase's shape on one
-//     GPU), and --throttle-peer P gives source P a quarter of the blocks: the proof that the naming
+//     GPU), and --throttle-peer P gives source P an eighth of the blocks: the proof that the naming
 //     names the slow source and only it.
 //
 // `ok` also requires the peak bus bandwidth of the largest rank count to reach --min-busbw (an explicit
@@ -251,7 +251,7 @@ struct Opts {
   bool links = true, links_only = false, link_self_test = false;
   int virtual_peers = 0;           // 1-GPU self-test: this many source buffers on GPU 0, pulled by one kernel
   int throttle_peer = -1;          // the source given 1/throttle_factor of the pull blocks (the naming test)
-  int throttle_factor = 4;
+  int throttle_factor = 8;
   int link_plan = 0;               // print the plan for this many GPUs and exit (no GPU call)
 };
 
@@ -319,7 +319,7 @@ bool fabric_check(const std::string& root) {
 }
 
 // --- 4. the link matrix -------------------------------------------------------------------------
-// One pull kernel per destination GPU: its blocks are split among the sources it reads (block ranges
+// One pull kernel per destination GPU: its blocks are split among the sources it reads (block table
 // first_block[s] .. first_block[s+1]), each block copies its share of its source's buffer over the link
 // and stamps the 100 MHz wall clock around its work; a source's rate is its bytes over the span of its
 // blocks' stamps. So the concurrent phase -- every destination pulling from every peer at once -- needs
@@ -338,14 +338,18 @@ constexpr int kPullThreads = 256;
 struct PullArgs {
   const uint4* src[kMaxPullSources];
   uint4* dst[kMaxPullSources];
-  int first_block[kMaxPullSources + 1];
+  int blocks[kMaxPullSources];      // blocks per source
 };
 
+// Block -> (source, index among that source's blocks): `table` (device memory, one int2 per block)
+// deals each source's blocks evenly over the grid. Contiguous ranges ran source 0's blocks as the
+// oldest waves of every CU: the sequencer's age priority let them finish first, and 7 equal sources
+// measured 462 down to 361 GB/s in block order (one MI355X, --virtual-peers 7).
 __global__ void __launch_bounds__(kPullThreads)
-multi_pull_kernel(PullArgs a, int nsrc, size_t vecs, int iters, unsigned long long* __restrict__ stamps) {
-  int s = 0;
-  while (s + 1 < nsrc && (int)blockIdx.x >= a.first_block[s + 1]) ++s;
-  const int nb = a.first_block[s + 1] - a.first_block[s], b = (int)blockIdx.x - a.first_block[s];
+multi_pull_kernel(PullArgs a, const int2* __restrict__ table, size_t vecs, int iters,
+                  unsigned long long* __restrict__ stamps) {
+  const int2 t = table[blockIdx.x];
+  const int s = t.x, b = t.y, nb = a.blocks[s];
   const uint4* __restrict__ src = a.src[s];
   uint4* __restrict__ dst = a.dst[s];
   __syncthreads();
@@ -363,7 +367,7 @@ multi_pull_kernel(PullArgs a, int nsrc, size_t vecs, int iters, unsigned long lo
 // What the link matrix will launch, computed without touching the GPU (--link-plan prints it; the
 // run executes exactly this). A source is a buffer on a GPU: GPU s itself on a multi-GPU node, or one of
 // --virtual-peers buffers on GPU 0 in the 1-GPU self-test ("v3"). `blocks[p]`: the pull blocks of pair p
-// (source si -> destination di) -- --throttle-peer gives one source a quarter (--throttle-factor) of them.
+// (source si -> destination di) -- --throttle-peer gives one source 1/--throttle-factor (8) of them.
 struct LinkPlan {
   struct Src {
     int dev;
@@ -404,6 +408,27 @@ LinkPlan plan_links(const Opts& o, const std::vector<int>& devs) {
     pl.conc_blocks.push_back(std::max(8, std::max(128, 2048 / std::max(1, per_dst[di])) / f));
   }
   return pl;
+}
+
+// The block table of one pull kernel: each block goes to the source furthest behind its share
+// (assigned / wanted), so every source's blocks are spread evenly over the grid's dispatch order.
+std::vector<std::pair<int, int>> deal_blocks(const std::vector<int>& want) {
+  int total = 0;
+  for (int w : want) total += w;
+  std::vector<int> got(want.size(), 0);
+  std::vector<std::pair<int, int>> out;
+  out.reserve(total);
+  for (int b = 0; b < total; ++b) {
+    int best = -1;
+    double key = 1e30;
+    for (size_t s = 0; s < want.size(); ++s) {
+      if (got[s] >= want[s]) continue;
+      const double k = (got[s] + 0.5) / want[s];
+      if (k < key) key = k, best = (int)s;
+    }
+    out.push_back({best, got[best]++});
+  }
+  return out;
 }
 
 void print_plan(const LinkPlan& pl) {
@@ -492,39 +517,53 @@ int link_matrix(const Opts& o, const std::vector<int>& devs, LinkResult& res) {
     HIPCHECK(hipSetDevice(d));
     HIPCHECK(hipStreamSynchronize(st[d]));
   }
-  // one launch of destination di's kernel over `which` pairs with their block counts
+  // one launch of destination di's kernel over `which` pairs with their block counts; `deal` gets the
+  // block table (block -> source slot, index) for the rates
+  // the block table of a launch, uploaded before anything is timed: the isolated launches of a
+  // destination share the single-source table (block b -> source 0, index b), the concurrent launch
+  // has its own
+  std::vector<int2*> iso_table(nd, nullptr), conc_table(nd, nullptr);
+  auto upload = [&](int di, const std::vector<std::pair<int, int>>& deal, int2** out) -> int {
+    std::vector<int2> ht(deal.size());
+    for (size_t b = 0; b < deal.size(); ++b) ht[b] = make_int2(deal[b].first, deal[b].second);
+    HIPCHECK(hipSetDevice(pl.dsts[di]));
+    HIPCHECK(hipMalloc(out, std::max<size_t>(1, ht.size()) * sizeof(int2)));
+    HIPCHECK(hipMemcpy(*out, ht.data(), ht.size() * sizeof(int2), hipMemcpyHostToDevice));
+    return 0;
+  };
+  // one launch of destination di's kernel over `which` pairs with their block counts and block table
   auto launch = [&](int di, const std::vector<size_t>& which, const std::vector<int>& blocks, int iters,
-                    std::vector<std::pair<int, int>>* ranges) -> int {
+                    const int2* table, int grid) -> int {
     PullArgs a{};
-    int b = 0, k = 0;
+    int k = 0;
     for (size_t p : which) {
       a.src[k] = (const uint4*)src[pl.pairs[p].first];
       a.dst[k] = (uint4*)dst[p];
-      a.first_block[k] = b;
-      if (ranges) ranges->push_back({b, b + blocks[p]});
-      b += blocks[p];
+      a.blocks[k] = blocks[p];
       ++k;
     }
-    a.first_block[k] = b;
     const int d = pl.dsts[di];
     HIPCHECK(hipSetDevice(d));
-    multi_pull_kernel<<<b, kPullThreads, 0, st[d]>>>(a, k, vecs, iters, stamps[d]);
+    multi_pull_kernel<<<grid, kPullThreads, 0, st[d]>>>(a, table, vecs, iters, stamps[d]);
     HIPCHECK(hipGetLastError());
     return 0;
   };
   // per pair: bytes x iters over the span of its blocks' stamps
-  auto rates = [&](int di, const std::vector<size_t>& which, const std::vector<std::pair<int, int>>& ranges,
+  auto rates = [&](int di, const std::vector<size_t>& which, const std::vector<std::pair<int, int>>& deal,
                    int iters, std::vector<double>& out) -> int {
     const int d = pl.dsts[di];
-    const int n = ranges.empty() ? 0 : ranges.back().second;
-    std::vector<unsigned long long> h((size_t)n * 2);
+    std::vector<unsigned long long> h(deal.size() * 2);
     HIPCHECK(hipSetDevice(d));
     HIPCHECK(hipMemcpyAsync(h.data(), stamps[d], h.size() * 8, hipMemcpyDeviceToHost, st[d]));
     HIPCHECK(hipStreamSynchronize(st[d]));
+    std::vector<unsigned long long> lo(which.size(), ~0ull), hi(which.size(), 0);
+    for (size_t b = 0; b < deal.size(); ++b) {
+      const int q = deal[b].first;
+      lo[q] = std::min(lo[q], h[2 * b]);
+      hi[q] = std::max(hi[q], h[2 * b + 1]);
+    }
     for (size_t q = 0; q < which.size(); ++q) {
-      unsigned long long lo = ~0ull, hi = 0;
-      for (int b = ranges[q].first; b < ranges[q].second; ++b) lo = std::min(lo, h[2 * b]), hi = std::max(hi, h[2 * b + 1]);
-      const double s = hi > lo ? (double)(hi - lo) / tick_hz[d] : 0;
+      const double s = hi[q] > lo[q] ? (double)(hi[q] - lo[q]) / tick_hz[d] : 0;
       out[which[q]] = s > 0 ? (double)bytes * iters / s / 1e9 : 0;
     }
     return 0;
@@ -532,30 +571,44 @@ int link_matrix(const Opts& o, const std::vector<int>& devs, LinkResult& res) {
   std::vector<double> iso(pl.pairs.size(), 0.0), conc(pl.pairs.size(), 0.0);
   std::vector<unsigned long long> errs(pl.pairs.size(), 0);
   g_watchdog.arm(Watchdog::kLinks, nd, bytes);
+  std::vector<std::vector<size_t>> by_dst(nd);
+  for (size_t p = 0; p < pl.pairs.size(); ++p)
+    if (usable[p]) by_dst[pl.pairs[p].second].push_back(p);
+  std::vector<std::vector<std::pair<int, int>>> conc_deal(nd);
+  for (int di = 0; di < nd; ++di) {
+    int most = 0;
+    std::vector<int> want;
+    for (size_t p : by_dst[di]) most = std::max(most, pl.iso_blocks[p]), want.push_back(pl.conc_blocks[p]);
+    if (upload(di, deal_blocks({most}), &iso_table[di])) return 2;
+    conc_deal[di] = deal_blocks(want);
+    if (upload(di, conc_deal[di], &conc_table[di])) return 2;
+  }
   // isolated: one pair at a time (a warm-up pass, then the timed launch of link_iters passes)
   for (size_t p = 0; p < pl.pairs.size(); ++p) {
     if (!usable[p]) continue;
     const int di = pl.pairs[p].second;
-    std::vector<std::pair<int, int>> ranges;
-    if (launch(di, {p}, pl.iso_blocks, 1, nullptr) || launch(di, {p}, pl.iso_blocks, o.link_iters, &ranges) ||
-        rates(di, {p}, ranges, o.link_iters, iso))
+    std::vector<std::pair<int, int>> deal(pl.iso_blocks[p]);
+    for (int b = 0; b < pl.iso_blocks[p]; ++b) deal[b] = {0, b};
+    if (launch(di, {p}, pl.iso_blocks, 1, iso_table[di], pl.iso_blocks[p]) ||
+        launch(di, {p}, pl.iso_blocks, o.link_iters, iso_table[di], pl.iso_blocks[p]) ||
+        rates(di, {p}, deal, o.link_iters, iso))
       return 2;
   }
   // concurrent: every destination's kernel over all its sources, all destinations at once
-  std::vector<std::vector<size_t>> by_dst(nd);
-  for (size_t p = 0; p < pl.pairs.size(); ++p)
-    if (usable[p]) by_dst[pl.pairs[p].second].push_back(p);
   for (int di = 0; di < nd; ++di)
-    if (!by_dst[di].empty() && launch(di, by_dst[di], pl.conc_blocks, 1, nullptr)) return 2;
+    if (!by_dst[di].empty() &&
+        launch(di, by_dst[di], pl.conc_blocks, 1, conc_table[di], (int)conc_deal[di].size()))
+      return 2;
   for (int d : pl.dsts) {
     HIPCHECK(hipSetDevice(d));
     HIPCHECK(hipStreamSynchronize(st[d]));
   }
-  std::vector<std::vector<std::pair<int, int>>> ranges(nd);
   for (int di = 0; di < nd; ++di)
-    if (!by_dst[di].empty() && launch(di, by_dst[di], pl.conc_blocks, o.link_iters, &ranges[di])) return 2;
+    if (!by_dst[di].empty() &&
+        launch(di, by_dst[di], pl.conc_blocks, o.link_iters, conc_table[di], (int)conc_deal[di].size()))
+      return 2;
   for (int di = 0; di < nd; ++di)
-    if (!by_dst[di].empty() && rates(di, by_dst[di], ranges[di], o.link_iters, conc)) return 2;
+    if (!by_dst[di].empty() && rates(di, by_dst[di], conc_deal[di], o.link_iters, conc)) return 2;
   // correctness: every destination buffer holds its source's pattern
   for (size_t p = 0; p < pl.pairs.size(); ++p) {
     if (!usable[p]) continue;
@@ -641,6 +694,11 @@ int link_matrix(const Opts& o, const std::vector<int>& devs, LinkResult& res) {
   for (int si = 0; si < ns; ++si) {
     (void)hipSetDevice(pl.srcs[si].dev);
     (void)hipFree(src[si]);
+  }
+  for (int di = 0; di < nd; ++di) {
+    (void)hipSetDevice(pl.dsts[di]);
+    if (iso_table[di]) (void)hipFree(iso_table[di]);
+    if (conc_table[di]) (void)hipFree(conc_table[di]);
   }
   for (int d : pl.devices) {
     (void)hipSetDevice(d);

@@ -37,4 +37,4 @@ def test_virtual_peers_and_throttle_plan():
     k = pl["concurrent_kernels"]
     assert pl["devices"] == 1 and len(k) == 1 and k[0]["sources"] == 7
     b = k[0]["blocks_per_source"]
-    assert b[3] * 4 == b[0] and len({x for i, x in enumerate(b) if i != 3}) == 1
+    assert b[3] == b[0] // 8 and len({x for i, x in enumerate(b) if i != 3}) == 1

@@ -327,7 +327,7 @@ def test_xgmi_link_matrix_on_one_gpu_is_a_clean_skip_and_its_kernels_run():
 
 def test_link_matrix_names_the_throttled_virtual_peer_only():
     """VERDICT r5 item 2 on one GPU: 7 source buffers on GPU 0 pulled by ONE kernel (the concurrent
-    phase's shape: one kernel, one stream per destination), source 3 given a quarter of the blocks.
+    phase's shape: one kernel, one stream per destination), source 3 given an eighth of the blocks.
     The throttled peer, and only it, is named; the unthrottled concurrent rates agree within 10 %."""
     rc, lines, err = run("amd-rccl-validate", "--links-only", "--virtual-peers", "7", "--link-bytes", str(128 << 20),
                          timeout=180)
