@@ -447,7 +447,37 @@ def transform_metrics_exporter(obj: Obj, spec: cp.ClusterPolicySpec, n) -> None:
             if v["name"] == "fields":
                 v["configMap"] = {"name": cfg.name}
         o.set_env(c, "METRICS_EXPORTER_FIELDS", "/etc/amd-metrics-exporter/fields.csv")
+    if n.openshift:
+        _add_pod_resources_relabel(obj, spec)
     set_runtime_class(obj, n.runtime, spec.operator.runtime_class())
+
+
+RELABEL_INIT = "init-pod-resources-relabel"
+RELABEL_CONFIGMAP = "amd-metrics-exporter-relabel"
+
+
+def _add_pod_resources_relabel(obj: Obj, spec: cp.ClusterPolicySpec) -> None:
+    """OpenShift: a privileged init container relabels /var/lib/kubelet/pod-resources container_file_t
+    (the script of 0850_configmap_openshift.yaml), so the exporter container itself needs no privilege
+    to reach the pod-resources socket (reference: object_controls.go:1393-1431, which does the same for
+    dcgm-exporter with the operator's init-container image)."""
+    ps = o.pod_spec(obj)
+    inits = [x for x in ps.get("initContainers", []) if x.get("name") != RELABEL_INIT]
+    init_spec = spec.operator.initContainer or cp.InitContainerSpec()
+    try:
+        image = cp.image_path(init_spec)
+    except (ValueError, TypeError):
+        image = cp.image_path(spec.validator)      # no ROCm base image configured: the validator image has chcon
+    inits.append({"name": RELABEL_INIT, "image": image,
+                  "imagePullPolicy": cp.image_pull_policy(init_spec.imagePullPolicy),
+                  "command": ["/bin/entrypoint.sh"], "securityContext": {"privileged": True},
+                  "volumeMounts": [{"name": "pod-gpu-resources", "mountPath": "/var/lib/kubelet/pod-resources"},
+                                   {"name": "relabel-entrypoint", "mountPath": "/bin/entrypoint.sh", "readOnly": True,
+                                    "subPath": "entrypoint.sh"}]})
+    ps["initContainers"] = inits
+    vols = [v for v in ps.get("volumes", []) if v.get("name") != "relabel-entrypoint"]
+    vols.append({"name": "relabel-entrypoint", "configMap": {"name": RELABEL_CONFIGMAP, "defaultMode": 0o700}})
+    ps["volumes"] = vols
 
 
 def transform_node_status_exporter(obj: Obj, spec: cp.ClusterPolicySpec, n) -> None:

@@ -554,8 +554,13 @@ class UpgradeStateManager:
                 deferred, self._worker.deferred = self._worker.deferred, None
                 with self._lock:
                     self._inflight.discard(node)
+                # each deferred label on its own: a failed PATCH is logged (a Future nobody reads would
+                # swallow it) and does not drop the states after it
                 for n, st in deferred:
-                    self.set_state(n, st)
+                    try:
+                        self.set_state(n, st)
+                    except Exception:  # noqa: BLE001
+                        log.exception("upgrade worker for node %s: publishing state %s failed", node, st)
         if self._pool is None:
             run()
         else:

@@ -131,6 +131,10 @@ class Response:
 
 
 _IDEMPOTENT = frozenset({"GET", "HEAD", "PUT", "DELETE", "OPTIONS"})
+# merge patches set fields to values: applying one twice gives the same object (a JSON patch's "add" to a
+# list does not), so a merge PATCH may be re-sent after a dropped kept-alive connection
+_MERGE_PATCH_TYPES = frozenset({"application/merge-patch+json", "application/strategic-merge-patch+json",
+                                "application/apply-patch+yaml"})
 _KEEPALIVE_TRUST_S = 5.0    # a kept-alive connection idle longer than this is not reused for POST/PATCH
 
 
@@ -171,13 +175,15 @@ class _Transport:
                 conn.close()
                 return Response(r.status, data)
             return Response(r.status, stream=r, conn=conn)
-        idempotent = method in _IDEMPOTENT
+        ctype = next((v for k, v in headers.items() if k.lower() == "content-type"), "").split(";")[0].strip()
+        idempotent = method in _IDEMPOTENT or (method == "PATCH" and ctype in _MERGE_PATCH_TYPES)
         for attempt in (0, 1):
             conn = getattr(self._local, "conn", None)
-            if conn is not None and not idempotent and \
-                    time.monotonic() - getattr(self._local, "last", 0.0) > _KEEPALIVE_TRUST_S:
-                # a POST/PATCH is never sent twice: rather than risk it on a connection the server may
-                # have closed while idle, open a fresh one
+            if conn is not None and not idempotent and (
+                    method == "POST" or time.monotonic() - getattr(self._local, "last", 0.0) > _KEEPALIVE_TRUST_S):
+                # a POST (or a JSON patch) is never sent twice: rather than risk it on a kept-alive
+                # connection the server -- or a proxy with a shorter idle timeout than ours -- may have
+                # closed, a POST always goes out on a fresh connection, a JSON patch when idle
                 conn.close()
                 conn = self._local.conn = None
             fresh = conn is None

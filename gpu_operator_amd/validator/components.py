@@ -282,10 +282,25 @@ def _requests_gpu(pod: Dict[str, Any]) -> bool:
     return False
 
 
-def gpu_pods_on_node(ctx: Context) -> List[str]:
+def _pod_start(p: Dict[str, Any]) -> Optional[float]:
+    """A pod's ``status.startTime`` (when the kubelet accepted it) as epoch seconds; None if unknown."""
+    ts = (p.get("status") or {}).get("startTime")
+    if not ts:
+        return None
+    try:
+        import datetime
+        return datetime.datetime.fromisoformat(str(ts).replace("Z", "+00:00")).timestamp()
+    except ValueError:
+        return None
+
+
+def gpu_pods_on_node(ctx: Context, started_before: Optional[float] = None,
+                     later: Optional[List[str]] = None) -> List[str]:
     """Running pods on this node that hold GPU resources (``amd.com/gpu`` or a partition
     resource), excluding the validator's own validation pods. A throughput number taken beside
-    them measures the sharing, not the hardware."""
+    them measures the sharing, not the hardware. ``started_before``: only pods whose start time is
+    not later than it (unknown start times count: never assume a tenant arrived late); the ones left
+    out are appended to ``later``."""
     if ctx.client is None or not ctx.node_name:
         return []
     try:
@@ -299,6 +314,11 @@ def gpu_pods_on_node(ctx: Context) -> List[str]:
         if (p.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
             continue
         if o.get_labels(p).get("app") in own or not _requests_gpu(p):
+            continue
+        start = _pod_start(p)
+        if started_before is not None and start is not None and start > started_before:
+            if later is not None:
+                later.append(f"{o.namespace(p)}/{o.name(p)}")
             continue
         out.append(f"{o.namespace(p)}/{o.name(p)}")
     return sorted(out)
@@ -707,22 +727,27 @@ def throughput_only(bad: List[GateFailure]) -> bool:
     return bool(bad) and all(b.kind in THROUGHPUT_KINDS for b in bad)
 
 
-def disturbed_gpus(ctx: Context, plan: Dict[str, Any], gpus: List[Dict[str, Any]]) -> Dict[str, Any]:
-    """GPUs of the full sweep that a tenant holds now (the HIP pod is privileged and requests no GPU
-    resource, so the device plugin kept advertising them while it ran): ``devices`` (HIP indices),
-    ``pods`` and ``attribution``. Without a device mapping for a running GPU pod every GPU of the
-    sweep counts as disturbed (held_gpus never guesses a tenant's GPU is free). Reference: the plugin
+def disturbed_gpus(ctx: Context, plan: Dict[str, Any], gpus: List[Dict[str, Any]],
+                   sweep_end: Optional[float] = None) -> Dict[str, Any]:
+    """GPUs of the full sweep that a tenant was given while it ran (the HIP pod is privileged and
+    requests no GPU resource, so the device plugin kept advertising them): ``devices`` (HIP indices),
+    ``pods`` and ``attribution``. A tenant that started after ``sweep_end`` shared nothing with the
+    sweep: its GPUs stay gated (``arrived_after``) -- a slow GPU cannot hide behind a pod scheduled
+    onto it after the run. Without a device mapping for a running GPU pod every GPU of the sweep
+    counts as disturbed (held_gpus never guesses a tenant's GPU is free). Reference: the plugin
     workload asks the scheduler for its GPU (validator/main.go:978-983), so it cannot share one."""
-    now = gpu_pods_on_node(ctx)
+    later: List[str] = []
+    now = gpu_pods_on_node(ctx, started_before=None if sweep_end is None else sweep_end + 1.0, later=later)
     if not now:
-        return {"devices": [], "pods": [], "attribution": "none"}
+        return {"devices": [], "pods": [], "attribution": "none", **({"arrived_after": later[:16]} if later else {})}
     held = held_gpus(ctx, now, gpus)
     hb = set(held["held_bdfs"])
     full = None if plan["full"] is None else set(plan["full"])
     devs = sorted(g["index"] for g in gpus if g["pci_bdf"] in hb and (full is None or g["index"] in full))
     if not gpus and held["attribution"] == "unattributed":
         devs = ["all"]
-    return {"devices": devs, "pods": now[:16], "attribution": held["attribution"]}
+    return {"devices": devs, "pods": now[:16], "attribution": held["attribution"],
+            **({"arrived_after": later[:16]} if later else {})}
 
 
 def validate_hip(ctx: Context) -> Dict[str, Any]:
@@ -773,6 +798,7 @@ def validate_hip(ctx: Context) -> Dict[str, Any]:
                                       [GateFailure("correctness", f"timeout after {ctx.pod_timeout:.0f}s")])
             except RuntimeError as e:          # the pod was deleted under the validator
                 raise ValidationError(f"HIP validation pod: {e}", [GateFailure("correctness", str(e))])
+        sweep_end = time.time()
         info = summarize_gemm(results)
         info["floors_tflops"] = floors
         info["plan"] = {"full": "all" if plan["full"] is None else plan["full"], "probe": plan["probe"],
@@ -780,14 +806,16 @@ def validate_hip(ctx: Context) -> Dict[str, Any]:
         if busy:
             info["busy"] = f"{len(busy)} GPU pod(s) on the node hold {len(plan['held_bdfs'])} GPU(s) " \
                            f"({plan['attribution']}): full sweep on {len(plan['full'])} free, probe on {len(plan['probe'])}"
-        dist = disturbed_gpus(ctx, plan, gpus) if mode != "local" or ctx.client is not None else {"devices": []}
+        dist = disturbed_gpus(ctx, plan, gpus, sweep_end) if mode != "local" or ctx.client is not None \
+            else {"devices": []}
         # a tenant that held its GPUs before the run is in the plan already (probe only): only the
         # sweep's own GPUs can be disturbed
         devs = frozenset(d for d in dist["devices"] if d != "all")
         if "all" in dist["devices"]:
             devs = frozenset(r.get("device") for r in info["gemm"])
         if devs:
-            info["disturbed"] = {**dist, "devices": sorted(devs, key=str)}
+            # recorded in hip-ready: throughput was not gated on these GPUs (correctness was)
+            info["disturbed"] = {**dist, "devices": sorted(devs, key=str), "throughput_gated": False}
         bad = gate_gemm(info, floors, busy, min_relative=min_rel, min_efficiency=min_eff, disturbed=devs)
         if failed is not None:
             info["pod_failed"] = {"exit_code": failed.exit_code, "reason": failed.reason}

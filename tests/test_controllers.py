@@ -207,6 +207,46 @@ def test_metrics_exporter_stays_off_the_host_network_with_rdc_enabled():
     assert port["hostPort"] == 50555
 
 
+def _privileged(c) -> bool:
+    return bool((c.get("securityContext") or {}).get("privileged"))
+
+
+def test_metrics_exporter_is_unprivileged_and_gains_the_relabel_init_on_openshift():
+    """off OpenShift no container of the exporter is privileged (/sys read-only,
+    capabilities dropped); on OpenShift a privileged init container relabels pod-resources (reference:
+    object_controls.go:1393-1431) and its ConfigMap is created, the exporter itself still unprivileged."""
+    c = cluster()
+    reconcile_once(c)
+    ex = daemonset(c, C.DS_METRICS_EXPORTER)
+    ps = ex["spec"]["template"]["spec"]
+    every = ps.get("initContainers", []) + ps["containers"]
+    assert not [x["name"] for x in every if _privileged(x)]
+    main = container(ex, "amd-metrics-exporter")
+    assert main["securityContext"]["capabilities"]["drop"] == ["ALL"]
+    assert main["securityContext"]["allowPrivilegeEscalation"] is False
+    assert {m["mountPath"]: m.get("readOnly") for m in main["volumeMounts"]}["/sys"] is True
+    assert not [x for x in ps.get("initContainers", []) if x["name"] == "init-pod-resources-relabel"]
+    with pytest.raises(errors.NotFound):
+        c.get("v1", "ConfigMap", "amd-metrics-exporter-relabel", NS)
+    # OpenShift
+    oc = _ocp_cluster()
+    reconcile_once(oc)
+    ex = daemonset(oc, C.DS_METRICS_EXPORTER)
+    ps = ex["spec"]["template"]["spec"]
+    relabel = [x for x in ps["initContainers"] if x["name"] == "init-pod-resources-relabel"]
+    assert len(relabel) == 1 and _privileged(relabel[0]) and relabel[0]["command"] == ["/bin/entrypoint.sh"]
+    assert {m["name"] for m in relabel[0]["volumeMounts"]} == {"pod-gpu-resources", "relabel-entrypoint"}
+    vols = {v["name"]: v for v in ps["volumes"]}
+    assert vols["relabel-entrypoint"]["configMap"]["name"] == "amd-metrics-exporter-relabel"
+    assert "chcon -t container_file_t" in oc.get("v1", "ConfigMap", "amd-metrics-exporter-relabel", NS)["data"][
+        "entrypoint.sh"]
+    assert [x["name"] for x in ps["containers"] if _privileged(x)] == []
+    reconcile_once(oc)                                    # idempotent: one relabel init, one volume
+    ps = daemonset(oc, C.DS_METRICS_EXPORTER)["spec"]["template"]["spec"]
+    assert [x["name"] for x in ps["initContainers"]].count("init-pod-resources-relabel") == 1
+    assert [v["name"] for v in ps["volumes"]].count("relabel-entrypoint") == 1
+
+
 def test_service_monitor_requires_crd_when_enabled():
     c = cluster(cp=sample_cp(**{"metricsExporter.serviceMonitor": {"enabled": True}}))
     rec = reconciler(c)

@@ -189,9 +189,10 @@ class _ScriptedServer:
     (the connection closes with no response byte, as a server closing an idle kept-alive
     connection does) or "hang" (no response until the client gives up)."""
 
-    def __init__(self, script):
+    def __init__(self, script, idle_close_s=None):
         import socket as so
         self.script, self.seen = list(script), []
+        self.idle_close_s = idle_close_s        # close a kept-alive connection idle this long (a proxy)
         self.sock = so.socket()
         self.sock.bind(("127.0.0.1", 0))
         self.sock.listen(8)
@@ -207,10 +208,15 @@ class _ScriptedServer:
             threading.Thread(target=self._conn, args=(c,), daemon=True).start()
 
     def _conn(self, c):
+        import socket as so
         buf = b""
+        c.settimeout(self.idle_close_s)
         while True:
             while b"\r\n\r\n" not in buf:
-                d = c.recv(65536)
+                try:
+                    d = c.recv(65536)
+                except so.timeout:
+                    d = b""
                 if not d:
                     c.close()
                     return
@@ -276,4 +282,31 @@ def test_transport_retries_only_idempotent_requests_on_a_dropped_keepalive(monke
         t.request("GET", "/x", None, {}, 0.5)
     time.sleep(0.2)
     assert srv.seen == ["GET", "GET"]
+    srv.stop()
+
+
+def test_merge_patch_and_post_survive_a_proxy_that_closes_idle_connections_after_1s():
+    """with a proxy closing idle kept-alive connections after 1 s (sooner than the 5 s we
+    trust one), a label merge-PATCH on the reused connection used to raise to its caller (the upgrade
+    FSM does not retry). A merge patch is safe to re-send: it is retried once on a fresh connection.
+    A POST always takes a fresh connection, so it is sent once and succeeds."""
+    from gpu_operator_amd.k8s import rest
+    srv = _ScriptedServer([], idle_close_s=1.0)
+    t = rest._Transport(Config(srv.url, verify=False))
+    merge = {"Content-Type": "application/merge-patch+json"}
+    assert t.request("GET", "/api/v1/nodes/a", None, {}, 5).status_code == 200
+    time.sleep(1.5)                                  # the proxy has closed the kept-alive connection
+    assert t.request("PATCH", "/api/v1/nodes/a", b'{"metadata":{"labels":{"x":"1"}}}', merge, 5).status_code == 200
+    time.sleep(1.5)
+    assert t.request("POST", "/api/v1/namespaces/d/pods", b"{}", {"Content-Type": "application/json"},
+                     5).status_code == 200
+    assert srv.seen == ["GET", "PATCH", "POST"]       # each applied exactly once
+    # a JSON patch (not idempotent) inside the trust window on a dropped connection: an error, sent once
+    srv.stop()
+    srv = _ScriptedServer(["ok", "drop", "ok"])
+    t = rest._Transport(Config(srv.url, verify=False))
+    t.request("GET", "/x", None, {}, 5)
+    with pytest.raises(OSError):
+        t.request("PATCH", "/x", b"[]", {"Content-Type": "application/json-patch+json"}, 5)
+    assert srv.seen == ["GET", "PATCH"]
     srv.stop()

@@ -496,3 +496,35 @@ def test_async_worker_publishes_its_state_after_leaving_inflight():
     ran = threading.Event()
     mgr._schedule("n0", ran.set)
     assert ran.wait(2)
+
+
+def test_a_failed_deferred_publish_is_logged_and_the_others_still_land(caplog):
+    """the deferred set_state calls ran in `finally` after the except that logs; a PATCH that
+    raised there vanished into the pool's Future and skipped the states after it."""
+    import logging
+    import threading
+    from gpu_operator_amd.k8s.fake import FakeClient
+
+    nodes = [{"apiVersion": "v1", "kind": "Node", "metadata": {"name": n, "labels": {}}} for n in ("n0", "n1")]
+    c = FakeClient(nodes)
+    mgr = U.UpgradeStateManager(c, NS, run_async=True, workers=1)
+    orig_patch = c.patch
+
+    def patch(av, kind, name, body, *a, **kw):
+        labels = ((body.get("metadata") or {}).get("labels") or {})
+        if name == "n0" and U.UPGRADE_STATE_LABEL in labels:
+            raise RuntimeError("apiserver went away")
+        return orig_patch(av, kind, name, body, *a, **kw)
+    c.patch = patch
+
+    def work():
+        mgr.set_state(c.get("v1", "Node", "n0"), U.DRAIN_REQUIRED)       # fails when published
+        mgr.set_state(c.get("v1", "Node", "n1"), U.DRAIN_REQUIRED)       # must still land
+    done = threading.Event()
+    with caplog.at_level(logging.ERROR):
+        mgr._schedule("n0", work)
+        mgr._schedule("n9", done.set)           # same single worker: runs after the first job
+        assert done.wait(5)
+    assert o.get_labels(c.get("v1", "Node", "n1")).get(U.UPGRADE_STATE_LABEL) == U.DRAIN_REQUIRED
+    assert any("publishing state" in r.getMessage() and "n0" in r.getMessage() for r in caplog.records)
+    assert "n0" not in mgr._inflight

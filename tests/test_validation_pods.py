@@ -176,3 +176,41 @@ def test_a_tenant_scheduled_during_the_sweep_is_disturbed_not_failed(tmp_path, n
     assert ctx.status.exists(S.HIP_READY) and _runs(state) == 1
     assert info["disturbed"]["devices"] == [3] and info["disturbed"]["pods"] == ["default/train-0"]
     assert "remeasured" not in info and info.get("pod_failed", {}).get("exit_code") == 1
+
+
+def test_a_tenant_that_arrives_after_the_sweep_exempts_nothing(tmp_path, node, monkeypatch):
+    """the post-run re-check used to exempt every GPU a tenant held at that moment, also one
+    scheduled after the sweep ended -- so a genuinely slow GPU could open hip-ready unchecked. A pod whose
+    startTime is after the sweep shared nothing with it: GPU 3 stays gated, its slow result fails (after
+    the one re-measure a throughput failure gets), and the late tenant is recorded as arrived_after."""
+    import datetime
+    c, k, root, state = node
+    _set_script(k, "slow:3")
+    from gpu_operator_amd import devices as D
+    g3 = [g for g in D.enumerate_gpus(root) if g["index"] == 3][0]
+    monkeypatch.setattr(comp, "_pod_device_ids",
+                        lambda ctx: {"default/late-0": [f"amdgpu-{g3['unique_id']:016x}"]})
+    late = (datetime.datetime.now(datetime.timezone.utc) + datetime.timedelta(hours=1)).isoformat()
+
+    def tenant_arrives():
+        for _ in range(400):
+            if os.path.exists(state + ".running"):
+                break
+            time.sleep(0.025)
+        c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "late-0", "namespace": "default"},
+                  "spec": {"nodeName": NODE,
+                           "containers": [{"name": "t", "resources": {"limits": {"amd.com/gpu": "1"}}}]},
+                  "status": {"phase": "Running", "startTime": late}})
+    th = threading.Thread(target=tenant_arrives)
+    k.hold_admission = lambda p: o.name(p) == "late-0"
+    th.start()
+    ctx = _ctx(tmp_path, c, root, "slow:3", GEMM_REMEASURE="0")
+    with pytest.raises(comp.ValidationError) as e:
+        comp.validate_hip(ctx)
+    th.join()
+    assert "device 3" in str(e.value) and {f.kind for f in e.value.failures} == {"floor"}
+    assert not ctx.status.exists(S.HIP_READY)
+    # the start-time filter itself
+    assert comp.gpu_pods_on_node(ctx) == ["default/late-0"]
+    later = []
+    assert comp.gpu_pods_on_node(ctx, started_before=time.time(), later=later) == [] and later == ["default/late-0"]
