@@ -107,6 +107,9 @@
 #include <vector>
 
 #include "amdnode.h"
+#include "validate_protocol.h"
+
+using namespace vproto;
 
 extern char** environ;
 
@@ -226,46 +229,6 @@ class Rendezvous {
   size_t n_, count_ = 0, gen_ = 0;
 };
 
-struct Shape {
-  int m, n, k;
-};
-
-struct Options {
-  int iters = 50, warmup = 5, check_rows = 32;
-  int inject_tm = -1, inject_tn = -1;   // --inject-fault TM,TN[,DELTA]: perturb one element of that tile
-  double inject_delta = 64.0;
-  double stabilise_max_s = 6.0;
-  double min_window_ms = 100.0;   // the timed loop covers at least this much GPU time
-  double ramp_ms = 60.0;          // re-ramp after the rendezvous: at least this much GPU time (profiles/r5_ramp)
-  double pre_idle_ms = 0.0;       // test hook: host idle after the rendezvous
-  bool stabilise = true;
-};
-
-// The ABFT check of the checked dispatch (gemm_abft.hip): every output element covered, a failing
-// tile named with the workgroup that computed it and, from that dispatch's placement record, the
-// XCD and CU it ran on.
-struct AbftOut {
-  bool ran = false;
-  int variant = -1, tile_m = 0, tile_n = 0, bad_tiles = 0;
-  double worst_ratio = 0, checked_fraction = 0, check_ms = 0, abft_ms = 0;
-  double dispatch_ms = 0, rows_ms = 0;   // the checked phase's other parts: poison + recorded dispatch, sampled rows
-  // the first bad tile (row-major order): its workgroup (piece 0), round, XCD (-1: pieces of a split-K
-  // tile ran on different XCDs, see `list`) and hardware id fields
-  int tm = -1, tn = -1, wg = -1, round = -1, xcd = -1, se = -1, sh = -1, cu = -1;
-  std::string list;   // up to 8 bad tiles "tm.tn.xcd" joined by ';' ("-": none)
-};
-
-struct Result {
-  int device = 0;
-  Shape s{};
-  double tflops = 0, ms = 0, max_rel_err = 0, stab_spread = -1, stab_ms = 0, probe_ms = 0;
-  int stab_dispatches = 0, iters = 0, ramp = 0;
-  bool launched = false, ok = false, oom = false;
-  size_t need_bytes = 0, free_bytes = 0;
-  AbftOut abft;
-  std::string error;
-};
-
 // Every device object of one run_one call; freed on every return path.
 struct Resources {
   void *A = nullptr, *B = nullptr, *C = nullptr, *abft_ws = nullptr, *scratch = nullptr;
@@ -282,47 +245,6 @@ struct Resources {
     if (st) (void)hipStreamDestroy(st);
   }
 };
-
-static std::vector<Shape> parse_shapes(const std::string& spec) {
-  std::vector<Shape> out;
-  size_t pos = 0;
-  while (pos <= spec.size()) {
-    size_t c = spec.find(',', pos);
-    std::string t = spec.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
-    if (!t.empty()) {
-      int m, n, k;
-      if (std::sscanf(t.c_str(), "%dx%dx%d", &m, &n, &k) == 3) out.push_back({m, n, k});
-      else out.push_back({std::atoi(t.c_str()), std::atoi(t.c_str()), std::atoi(t.c_str())});
-    }
-    if (c == std::string::npos) break;
-    pos = c + 1;
-  }
-  return out;
-}
-
-static std::vector<int> parse_ints(const std::string& spec) {
-  std::vector<int> out;
-  for (const auto& s : parse_shapes(spec)) out.push_back(s.m);
-  return out;
-}
-
-// A comma list of non-negative integers; false when any entry is not one (a UUID, say).
-static bool parse_index_list(const char* spec, std::vector<int>& out) {
-  out.clear();
-  std::string s = spec;
-  size_t pos = 0;
-  while (pos <= s.size()) {
-    size_t c = s.find(',', pos);
-    std::string t = s.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
-    if (!t.empty()) {
-      if (!std::all_of(t.begin(), t.end(), ::isdigit)) return false;
-      out.push_back(std::atoi(t.c_str()));
-    }
-    if (c == std::string::npos) break;
-    pos = c + 1;
-  }
-  return true;
-}
 
 // Whether the per-GPU floors apply to this shape (see the header).
 static bool floor_applies(const Shape& s) { return (double)s.m * s.n >= 256.0 * 65536.0 && s.k >= 4096; }
@@ -951,23 +873,6 @@ static bool spawn_worker(Worker& w, int hip_index, const std::vector<std::string
   return true;
 }
 
-static std::string fmt_opts(const Options& o) {
-  char buf[320];
-  std::snprintf(buf, sizeof buf, "%d %d %d %.17g %.17g %.17g %.17g %d %d %d %.17g", o.iters, o.warmup, o.check_rows,
-                o.stabilise_max_s, o.min_window_ms, o.ramp_ms, o.pre_idle_ms, o.stabilise ? 1 : 0, o.inject_tm,
-                o.inject_tn, o.inject_delta);
-  return buf;
-}
-
-static bool parse_opts(const std::string& s, Options& o) {
-  int stab = 1;
-  const int n = std::sscanf(s.c_str(), "%d %d %d %lf %lf %lf %lf %d %d %d %lf", &o.iters, &o.warmup, &o.check_rows,
-                            &o.stabilise_max_s, &o.min_window_ms, &o.ramp_ms, &o.pre_idle_ms, &stab, &o.inject_tm,
-                            &o.inject_tn, &o.inject_delta);
-  o.stabilise = stab != 0;
-  return n == 11;
-}
-
 // --worker: one GPU (HIP device 0 under the HIP_VISIBLE_DEVICES the launcher set). After its start
 // (and smoke) line it reads its part of the plan from stdin, "P <id>:<dtype>:<m>x<n>x<k>:<gpus>;..." --
 // the sets it takes part in, in plan order, with their sizes -- or "Q" (no part: the launcher dropped it).
@@ -975,7 +880,7 @@ static int worker_main(const Options& o, bool run_smoke) {
   std::signal(SIGPIPE, SIG_IGN);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
-    std::printf("S 0 - - 0 0\n");
+    std::printf("%s\n", fmt_start_line({0, "-", "-", 0, 0}).c_str());
     std::fflush(stdout);
     return 3;
   }
@@ -984,8 +889,8 @@ static int worker_main(const Options& o, bool run_smoke) {
   char bus[64] = "-";
   if (hipDeviceGetPCIBusId(bus, sizeof bus, 0) != hipSuccess) std::strcpy(bus, "-");
   for (char* c = bus; *c; ++c) *c = (char)std::tolower(*c);
-  std::printf("S %d %s %s %d %zu\n", ndev, bus, prop.gcnArchName, prop.multiProcessorCount,
-              (size_t)prop.sharedMemPerBlock);
+  std::printf("%s\n", fmt_start_line({ndev, bus, prop.gcnArchName, prop.multiProcessorCount,
+                                       (size_t)prop.sharedMemPerBlock}).c_str());
   std::fflush(stdout);
   (void)hipSetDevice(0);
   (void)amdgo_gemm_bf16_placement_init();   // process setup of the checked dispatch, not the probe's
@@ -994,24 +899,16 @@ static int worker_main(const Options& o, bool run_smoke) {
     std::printf("H %d\n", smoke_failures({0}) == 0 ? 1 : 0);
     std::fflush(stdout);
   }
-  std::string sets;
+  std::vector<PlanItem> items;
   {
     std::vector<char> line(1 << 16);
     if (!std::fgets(line.data(), (int)line.size(), stdin) || line[0] != 'P') return 0;
-    sets = line.data() + 1;
-    while (!sets.empty() && (sets.back() == '\n' || sets.back() == '\r' || sets.back() == ' ')) sets.pop_back();
-    while (!sets.empty() && sets.front() == ' ') sets.erase(0, 1);
+    if (!parse_plan_line(line.data(), items)) return 2;
   }
-  size_t pos = 0;
-  while (pos < sets.size()) {
-    size_t e = sets.find(';', pos);
-    const std::string item = sets.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
-    pos = e == std::string::npos ? sets.size() : e + 1;
-    int id = 0, set_size = 1;
-    char dtn[32] = "";
-    Shape s{};
-    if (std::sscanf(item.c_str(), "%d:%31[^:]:%dx%dx%d:%d", &id, dtn, &s.m, &s.n, &s.k, &set_size) != 6) return 2;
-    const DType* dt = dtype_by_name(dtn);
+  for (const PlanItem& it : items) {
+    const int id = it.id, set_size = it.set_size;
+    const Shape s = it.s;
+    const DType* dt = dtype_by_name(it.dtype);
     if (!dt) return 2;
     const std::function<void()> barrier = [&] {
       std::printf("W %d\n", id);
@@ -1021,40 +918,10 @@ static int worker_main(const Options& o, bool run_smoke) {
     };
     Result r;
     run_one(*dt, 0, s, o, barrier, set_size, r);
-    std::string err = r.error;
-    for (char& c : err)
-      if (c == '\n' || c == '\r') c = ' ';
-    const AbftOut& a = r.abft;
-    std::printf("R %d %d %d %d %.17g %.17g %.17g %d %.17g %zu %zu %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %.17g "
-                "%.17g %.17g %.17g %.17g %.17g %.17g %s %s\n",
-                id, r.launched, r.ok, r.oom, r.tflops, r.ms, r.max_rel_err, r.stab_dispatches, r.stab_spread, r.need_bytes,
-                r.free_bytes, r.iters, r.ramp, a.ran, a.variant, a.tile_m, a.tile_n, a.bad_tiles, a.tm, a.tn, a.wg, a.round,
-                a.xcd, a.se, a.sh, a.cu, a.worst_ratio, a.checked_fraction, a.check_ms, a.abft_ms, r.probe_ms,
-                a.dispatch_ms, a.rows_ms, a.list.empty() ? "-" : a.list.c_str(), err.c_str());
+    std::printf("%s\n", fmt_result_line(id, r).c_str());
     std::fflush(stdout);
   }
   return 0;
-}
-
-// One worker result line (worker_main's "R" format). False when it does not parse; the error text is
-// whatever follows the last field (possibly empty).
-static bool parse_result_line(const std::string& ln, int& id, Result& r) {
-  int launched = 0, ok = 0, oom = 0, ran = 0, off = 0;
-  char list[256] = "";
-  AbftOut& a = r.abft;
-  const int n = std::sscanf(ln.c_str(),
-                            "R %d %d %d %d %lf %lf %lf %d %lf %zu %zu %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %lf %lf "
-                            "%lf %lf %lf %lf %lf %255s %n",
-                            &id, &launched, &ok, &oom, &r.tflops, &r.ms, &r.max_rel_err, &r.stab_dispatches,
-                            &r.stab_spread, &r.need_bytes, &r.free_bytes, &r.iters, &r.ramp, &ran, &a.variant, &a.tile_m,
-                            &a.tile_n, &a.bad_tiles, &a.tm, &a.tn, &a.wg, &a.round, &a.xcd, &a.se, &a.sh, &a.cu,
-                            &a.worst_ratio, &a.checked_fraction, &a.check_ms, &a.abft_ms, &r.probe_ms, &a.dispatch_ms,
-                            &a.rows_ms, list, &off);
-  if (n < 34) return false;
-  r.launched = launched, r.ok = ok, r.oom = oom, a.ran = ran;
-  a.list = list;
-  r.error = off > 0 && (size_t)off <= ln.size() ? ln.substr((size_t)off) : "";
-  return true;
 }
 
 static constexpr double kWorkerReplyS = 600.0;   // one set's worst case is seconds; a GPU hang is not
@@ -1084,10 +951,11 @@ static int launch_processes(const std::vector<int>& devs_in, bool all, const std
   for (auto& w : spawned) {
     std::string ln;
     if (w.line(ln, 300.0)) {
-      int n = 0, c = 0;
-      size_t l = 0;
-      char bus[64] = "", a[96] = "";
-      const bool parsed = std::sscanf(ln.c_str(), "S %d %63s %95s %d %zu", &n, bus, a, &c, &l) == 5;
+      StartLine sl;
+      const bool parsed = parse_start_line(ln, sl);
+      const int n = sl.ndev, c = sl.cus;
+      const size_t l = sl.lds;
+      const std::string bus = sl.bus, a = sl.arch;
       if (parsed && n < 1 && all) {
         dropped += (dropped.empty() ? "" : ",") + std::to_string(w.slot);
         w.fail("dropped: the runtime sees no GPU there");
@@ -1128,10 +996,7 @@ static int launch_processes(const std::vector<int>& devs_in, bool all, const std
     std::string sets;
     for (const Set& st : plan)
       if (std::find(st.slots.begin(), st.slots.end(), (int)i) != st.slots.end()) {
-        char buf[96];
-        std::snprintf(buf, sizeof buf, "%s%d:%s:%dx%dx%d:%zu", sets.empty() ? "" : ";", st.id, st.dt->name, st.s.m,
-                      st.s.n, st.s.k, st.slots.size());
-        sets += buf;
+        sets += (sets.empty() ? "" : ";") + fmt_plan_item({st.id, st.dt->name, st.s, (int)st.slots.size()});
       }
     ws[i].send(("P " + sets + "\n").c_str());
   }
@@ -1249,7 +1114,11 @@ int main(int argc, char** argv) {
     std::printf("{\"error\":\"unknown --dtype %s (bf16, fp8 or both)\"}\n", json_safe(dtype).c_str());
     return 2;
   }
-  const std::vector<Shape> shape_list = parse_shapes(shapes);
+  std::vector<Shape> shape_list;
+  if (!parse_shapes_strict(shapes, shape_list)) {
+    std::printf("{\"error\":\"bad --shapes %s (N or MxNxK, comma separated)\"}\n", json_safe(shapes).c_str());
+    return 2;
+  }
   for (const auto& s : shape_list)
     if (s.m <= 0 || s.n <= 0 || s.k <= 0) {
       std::printf("{\"error\":\"bad shape %dx%dx%d\"}\n", s.m, s.n, s.k);

@@ -151,16 +151,29 @@ class Parser {
     --depth_;
     return v;
   }
+  // RFC 8259 number: -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)? -- its text is kept and written back
+  // verbatim, so anything looser ("1.", "--1", ".5", "1e") would make a rewritten config.json invalid
+  // (tests/native/fuzz_minijson.cpp found the loose form accepting "[.]").
   Value number() {
-    size_t s = p_;
+    const size_t s = p_;
+    auto digit = [&] { return p_ < t_.size() && t_[p_] >= '0' && t_[p_] <= '9'; };
+    auto digits = [&] {
+      const size_t b = p_;
+      while (digit()) ++p_;
+      return p_ > b;
+    };
     if (p_ < t_.size() && t_[p_] == '-') ++p_;
-    bool digits = false;
-    while (p_ < t_.size() && ((t_[p_] >= '0' && t_[p_] <= '9') || t_[p_] == '.' || t_[p_] == 'e' ||
-                              t_[p_] == 'E' || t_[p_] == '+' || t_[p_] == '-')) {
-      digits = true;
+    if (p_ < t_.size() && t_[p_] == '0') ++p_;
+    else if (!digits()) fail("invalid value");
+    if (p_ < t_.size() && t_[p_] == '.') {
       ++p_;
+      if (!digits()) fail("invalid number");
     }
-    if (!digits) fail("invalid value");
+    if (p_ < t_.size() && (t_[p_] == 'e' || t_[p_] == 'E')) {
+      ++p_;
+      if (p_ < t_.size() && (t_[p_] == '+' || t_[p_] == '-')) ++p_;
+      if (!digits()) fail("invalid number");
+    }
     return Value::number_text(t_.substr(s, p_ - s));
   }
   unsigned hex4() {
@@ -206,10 +219,14 @@ class Parser {
         case 't': out += '\t'; break;
         case 'u': {
           unsigned cp = hex4();
-          if (cp >= 0xD800 && cp < 0xDC00 && p_ + 1 < t_.size() && t_[p_] == '\\' && t_[p_ + 1] == 'u') {
+          if (cp >= 0xD800 && cp < 0xDC00) {      // a high surrogate must be followed by a low one
+            if (!(p_ + 1 < t_.size() && t_[p_] == '\\' && t_[p_ + 1] == 'u')) fail("lone surrogate");
             p_ += 2;
-            unsigned lo = hex4();
+            const unsigned lo = hex4();
+            if (lo < 0xDC00 || lo > 0xDFFF) fail("bad surrogate pair");
             cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          } else if (cp >= 0xDC00 && cp <= 0xDFFF) {
+            fail("lone surrogate");
           }
           utf8(out, cp);
           break;
