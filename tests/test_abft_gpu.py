@@ -230,3 +230,44 @@ def test_split_k_workspaces_are_capped(cuda_device):
             free_at[i] = torch.cuda.mem_get_info(cuda_device)[0]
     assert G.small_workspace_count(cuda_device.index or 0) <= 16
     assert abs(free_at[99] - free_at[30]) < 64 << 20, free_at
+
+
+def test_split_k_workspace_per_thread_stream(cuda_device):
+    """the per-thread default stream handle names a different stream in every host
+    thread; keyed by (device, handle) alone, two threads running v61 at once shared one set of fp32
+    slabs and arrival counters. Two threads, each on hipStreamPerThread, each its own operands, 40
+    launches each: every result equals its single-threaded reference."""
+    import threading
+    import torch
+    from gpu_operator_amd.ops import _lib
+    from gpu_operator_amd.ops import gemm as G
+
+    m, n, k = 1024, 1024, 4096
+    assert G.resolve_variant(m, n, k) == 61
+    lib = _lib.load()
+    per_thread = 2                                    # hipStreamPerThread
+    jobs = []
+    for seed in (11, 23):
+        a, bt = _operands(m, n, k, "bf16", cuda_device, seed=seed)
+        jobs.append((a, bt, G.gemm_bf16(a, bt), torch.empty((m, n), dtype=torch.bfloat16, device=cuda_device)))
+    torch.cuda.synchronize()
+    bad = []
+
+    def run(j):
+        a, bt, want, out = jobs[j]
+        torch.cuda.set_device(cuda_device)
+        for _ in range(40):
+            err = lib.amdgo_gemm_bf16(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k, per_thread)
+            if err:
+                bad.append(f"thread {j}: hipError {err}")
+                return
+            torch.cuda.synchronize()
+            if not torch.equal(out, want):
+                bad.append(f"thread {j}: result differs")
+                return
+    th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not bad, bad
