@@ -834,9 +834,25 @@ def validate_hip(ctx: Context) -> Dict[str, Any]:
         info["remeasured"] = {"first_failure": [str(b) for b in first[:8]],
                               "first_kinds": sorted({b.kind for b in first})}
     if bad:
+        _record_hip_failure(ctx, bad)
         raise ValidationError(f"HIP validation failed: {[str(b) for b in bad[:8]]}", bad)
+    ctx.status.delete(S.HIP_LAST_FAILURE)
     ctx.status.create(S.HIP_READY, info)
     return info
+
+
+def _record_hip_failure(ctx: Context, bad: List[GateFailure]) -> None:
+    """The node-local record of a failed HIP validation: every gate's kind and text, and where each
+    wrong result was computed (GPU, tile, XCD, CU) -- what the node metrics exporter publishes as
+    validator_gemm_bad_tile, so a bad CU is visible without reading pod logs. A node-local file: the
+    validator needs no write access to Nodes."""
+    try:
+        ctx.status.create(S.HIP_LAST_FAILURE, {
+            "ts": round(time.time(), 3),
+            "failures": [{"kind": b.kind, "text": b.text[:300], **({"where": b.where} if b.where else {})}
+                         for b in bad[:16]]})
+    except OSError as e:
+        log.warning("hip-last-failure not written: %s", e)
 
 
 # ---------------------------------------------------------------------------------------------

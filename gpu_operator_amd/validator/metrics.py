@@ -67,6 +67,13 @@ class NodeMetrics:
                                    node + ["device", "bdf", "reason"], registry=r)
         self.dev_unhealthy_total = Gauge(p + "node_devices_unhealthy", "devices the device plugin reports Unhealthy",
                                          node, registry=r)
+        self.gemm_bad_tile = Gauge(p + "validator_gemm_bad_tile",
+                                   "1 for each wrong GEMM output tile the last failed HIP validation found, with the "
+                                   "GPU, the XCD and the CU that computed it (ABFT check of amd-gemm-validate)",
+                                   node + ["gpu", "dtype", "tile", "xcd", "cu"], registry=r)
+        self.hip_failure_ts = Gauge(p + "validator_hip_last_failure_ts_seconds",
+                                    "time of the last failed HIP validation (0: the last one passed)", node,
+                                    registry=r)
         self.gemm_checked = Gauge(p + "validator_gemm_checked_fraction",
                                   "fraction of the validator GEMM's output elements verified (ABFT tile checksums; "
                                   "the least covered GEMM of the last passing run)", node, registry=r)
@@ -119,6 +126,7 @@ class NodeMetrics:
                 self.gemm_gpu_tflops.labels(n, str(gpu), comp._dtype_key(line.get("dtype", "bf16")), str(line.get("m")),
                                             str(line.get("n")), str(line.get("k"))).set(v)
         self.refresh_device_health()
+        self.refresh_hip_failure()
         rc = sd.read(S.RCCL_READY) or {}
         if rc.get("peak_busbw_gbps") is not None:
             self.busbw.labels(n, str(rc.get("ranks"))).set(rc["peak_busbw_gbps"])
@@ -131,6 +139,24 @@ class NodeMetrics:
         for ranks, bw in (rc.get("busbw_by_ranks") or {}).items():     # the 2/4/8-rank sweep
             if bw is not None:
                 self.busbw.labels(n, str(ranks)).set(bw)
+
+    def refresh_hip_failure(self) -> None:
+        n = self.ctx.node_name
+        doc = self.ctx.status.read(S.HIP_LAST_FAILURE)
+        self.gemm_bad_tile.clear()
+        if not doc:
+            self.hip_failure_ts.labels(n).set(0)
+            return
+        self.hip_failure_ts.labels(n).set(doc.get("ts", 0))
+        for f in doc.get("failures") or []:
+            w = f.get("where") if isinstance(f, dict) else None
+            if not isinstance(w, dict) or "tile" not in w:
+                continue
+            cu = w.get("cu") or {}
+            cu_s = f"se{cu.get('se')}.sh{cu.get('sh')}.cu{cu.get('cu')}" if cu else ""
+            xcd = "" if w.get("xcd") is None else str(w.get("xcd"))
+            self.gemm_bad_tile.labels(n, str(w.get("device")), comp._dtype_key(str(w.get("dtype", "bf16"))),
+                                      ",".join(str(x) for x in w.get("tile") or []), xcd, cu_s).set(1)
 
     def refresh_device_health(self) -> None:
         """The device plugin's health verdicts (device-health in the status directory)."""

@@ -33,6 +33,9 @@ WORKLOAD_TYPE = "workload-type"
 # the last full RCCL fabric result (no "-ready" suffix: it outlives validator restarts, whose preStop
 # removes *-ready; tmpfs, so a reboot -- after which the fabric is measured again -- clears it)
 FABRIC_LAST_FULL = "fabric-last-full"
+# the last failed HIP validation with the location of every wrong result it found (tile, XCD, CU): kept
+# across validator restarts (no "-ready" suffix), removed by the next passing validation
+HIP_LAST_FAILURE = "hip-last-failure"
 
 CONTAINER_CHAIN = [DRIVER_READY, TOOLKIT_READY, HIP_READY, PLUGIN_READY, RCCL_READY]
 

@@ -114,6 +114,22 @@ def test_a_wrong_tile_fails_at_once_and_names_tile_xcd_and_cu(tmp_path, node):
     assert f and f[0].where["tile"] == [5, 7] and f[0].where["xcd"] == 2 and f[0].where["device"] == 3
     assert _runs(state) == 1
     assert not ctx.status.exists(S.HIP_READY)
+    # the node-local record and its metric: the bad CU without reading pod logs
+    rec = ctx.status.read(S.HIP_LAST_FAILURE)
+    assert rec["failures"][0]["where"]["xcd"] == 2
+    from prometheus_client import generate_latest
+    from gpu_operator_amd.validator.metrics import NodeMetrics
+    m = NodeMetrics(ctx)
+    m.refresh_status()
+    text = generate_latest(m.registry).decode()
+    assert ('amd_gpu_operator_validator_gemm_bad_tile{cu="se1.sh0.cu4",dtype="bf16",gpu="3",node="n1",tile="5,7",'
+            'xcd="2"} 1.0') in text, [ln for ln in text.splitlines() if "bad_tile" in ln]
+    # the next passing validation clears it
+    _set_script(k, "fast")
+    comp.validate_hip(_ctx(tmp_path, c, root, "fast"))
+    assert not ctx.status.exists(S.HIP_LAST_FAILURE)
+    m.refresh_status()
+    assert "validator_gemm_bad_tile{" not in generate_latest(m.registry).decode()
 
 
 def test_a_passing_run_records_full_coverage(tmp_path, node):

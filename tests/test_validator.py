@@ -837,3 +837,19 @@ def test_link_gate_names_corrupt_and_unreachable_pairs():
     got = [str(f) for f in comp.gate_links(links, 0.8)]
     assert got == ["xGMI link 0->1: copied data corrupted", "xGMI link 1->0: no peer access"]
     assert comp.gate_links({"skipped": "1 GPU visible", "ok": True}, 0.8) == []
+
+
+def test_node_status_alerts_reference_metrics_the_exporter_serves(tmp_path, node_root):
+    """Every metric an alert of the node-status PrometheusRule queries is one the node metrics exporter
+    registers: a renamed gauge cannot leave an alert that never fires."""
+    import re
+    import yaml
+    rule = yaml.safe_load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                            "gpu_operator_amd/assets/state-node-status-exporter/0800_prometheus_rule.yaml")))
+    exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]
+    used = {m for e in exprs for m in re.findall(r"amd_gpu_operator_\w+", e)}
+    ctx = ctx_for(tmp_path, node_root, client=FakeClient([node_obj()]))
+    m = NodeMetrics(ctx)
+    served = set(m.registry._names_to_collectors)
+    assert used and used <= served, sorted(used - served)
+    assert {"amd_gpu_operator_validator_gemm_bad_tile", "amd_gpu_operator_node_device_unhealthy"} <= used
