@@ -35,6 +35,15 @@ def load() -> ctypes.CDLL:
         if not p.exists():
             raise NativeLibraryMissing(
                 f"{p} not found: build it with `python -m gpu_operator_amd._build` (hipcc, gfx950)")
+        # torch first: it ships its own libamdhip64. Loaded before it, this library would pull in
+        # /opt/rocm's copy, torch would then run on a runtime it was not built with, and every HIP
+        # call of the process failed with hipErrorNoDevice (a GPU test session whose collection
+        # loaded this library first: 437 failures). With torch loaded, the dependency resolves to its
+        # runtime, the one the tensors passed here live in.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(str(p))
         vp, i, sz, u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32
         lib.amdgo_gemm_bf16.argtypes = [vp, vp, vp, i, i, i, vp]

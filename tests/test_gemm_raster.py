@@ -5,18 +5,14 @@ bijection between (tile, K piece) and the launch's (workgroup, round) slots for 
 dispatch can pick, and it must agree with the launch grid the dispatch uses."""
 
 import itertools
+import os
 
 import pytest
 
 from gpu_operator_amd.ops import _lib
 
-try:
-    _lib.load()
-    HAVE_LIB = True
-except Exception:  # noqa: BLE001 -- not built: the build test reports that
-    HAVE_LIB = False
-
-pytestmark = pytest.mark.skipif(not HAVE_LIB, reason="libamdgo_hip.so not built")
+# no load at import: collection must not load the HIP library (ops/_lib.py: torch's runtime first)
+pytestmark = pytest.mark.skipif(not _lib.lib_path().exists(), reason="libamdgo_hip.so not built")
 
 SHAPES = [
     (8192, 8192, 8192), (16384, 16384, 16384), (4096, 4096, 4096), (2560, 2560, 2560), (1024, 1024, 4096),
@@ -81,3 +77,18 @@ def test_raster_kinds_follow_the_dispatch():
     # a CPX partition (32 CUs) gets its own raster: a persistent grid of 32
     r = G.raster(8192, 8192, 8192, "bf16", cus=32)
     assert r.grid in (0, 32) or r.kind != "persistent"
+
+
+def test_library_binds_to_torchs_hip_runtime_whatever_the_import_order():
+    """Loaded before torch, libamdgo_hip.so pulled in /opt/rocm's libamdhip64 and torch then ran on a
+    runtime it was not built with: every HIP call of that GPU test session failed with hipErrorNoDevice.
+    _lib.load() imports torch first, so one runtime is mapped -- torch's."""
+    import subprocess
+    import sys
+    code = ("from gpu_operator_amd.ops import _lib\n_lib.load()\n"
+            "maps = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+            "import torch, os\nprint(len(maps), all(m.startswith(os.path.dirname(torch.__file__)) for m in maps))\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["1", "True"]

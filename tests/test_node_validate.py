@@ -186,8 +186,9 @@ def test_plugin_hands_over_what_it_does_not_handle(tmp_path, node):
         assert native("plugin", node, tmp_path / "b", dict(base, VALIDATOR_WAIT_MODE="poll"))[0] == 3
         assert native("plugin", node, tmp_path / "c", dict(base, NODE_NAME=""))[0] == 3
         assert native("plugin", node, tmp_path / "d", dict(base, KUBECONFIG=str(tmp_path / "none")))[0] == 3
-        rc, _, _ = native("plugin", node, tmp_path / "e", dict(base, PARTITION_STRATEGY="mixed"))
-        assert rc == 0 and barriers(tmp_path / "e")["plugin-ready"]["devices"] == 16
+        rc, _, err = native("plugin", node, tmp_path / "e", dict(base, PARTITION_STRATEGY="mixed"))
+        assert rc == 0, err
+        assert barriers(tmp_path / "e")["plugin-ready"]["devices"] == 16
         assert not any(os.listdir(tmp_path / d) for d in "abcd" if os.path.isdir(tmp_path / d))
     finally:
         srv.stop()
