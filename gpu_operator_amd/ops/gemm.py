@@ -80,8 +80,8 @@ def gemm_fp8(a, bt, out=None, *, generic: bool = False):
 
 # Production variant sets (native/hip/gemm_bf16.hip, gemm_fp8.hip): 0 = automatic dispatch, any
 # other member pins that kernel. Everything else lives in the tools-only lab library.
-BF16_VARIANTS = (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61, 62)
-FP8_VARIANTS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61, 62)
+BF16_VARIANTS = (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 60, 61, 62)
+FP8_VARIANTS = (0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 24, 60, 61, 62)
 
 
 def set_variant(v: int) -> None:
@@ -98,6 +98,13 @@ def set_split_target(t: int) -> None:
     """v61 (split-K 128x128): aim for ``t`` workgroups per CU (1..8; per host thread)."""
     if _lib.load().amdgo_gemm_set_split_target(int(t)) != 0:
         raise ValueError(f"split target {t} outside 1..8")
+
+
+def set_asm_split(splits: int = 0, last_permille: int = 0) -> None:
+    """v57 / fp8 v24 (split-K in the 256x256 asm frame), per host thread: force ``splits`` K pieces per
+    tile (0 = automatic) and give the last piece ``last_permille`` of K (0 = the default)."""
+    if _lib.load().amdgo_gemm_set_asm_split(int(splits), int(last_permille)) != 0:
+        raise ValueError(f"asm split ({splits}, {last_permille}) outside 0..64 / 0..999")
 
 
 def small_splits(m: int, n: int, k: int, cus: int = 256) -> int:
@@ -206,7 +213,7 @@ def verify(a, bt, c, nrows: int = 64, seed: int = 0, rows: Optional[list] = None
 # ---------------------------------------------------------------------------------------------
 # The dispatch's raster and the ABFT check (native/hip/gemm_raster_host.h, gemm_abft.hip)
 # ---------------------------------------------------------------------------------------------
-RASTER_KINDS = ("generic", "grid", "grid_sq", "persistent", "persistent_sq", "small")
+RASTER_KINDS = ("generic", "grid", "grid_sq", "persistent", "persistent_sq", "small", "split")
 
 
 @dataclass

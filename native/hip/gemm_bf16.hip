@@ -183,6 +183,8 @@ static constexpr Bf16Need kBf16Needs[] = {
     {54, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
     {55, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
     {56, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && c.K >= 4 * BK && c.pgrid >= NXCD; }, 44},
+    // the split-K asm form: even K-tile pieces of >= 16, at least 2 of them per tile within the CUs
+    {57, [](const Bf16Shape& c) { return c.K % (2 * BK) == 0 && asm_splits(c.nwg, c.K / BK, c.cus) > 1; }, 55},
     // the square raster needs 16x16 super-tiles and exactly 256 workgroups
     {54, [](const Bf16Shape& c) { return c.sq && c.mi355; }, 53},
     {56, [](const Bf16Shape& c) { return c.sq && c.mi355; }, 55},
@@ -231,7 +233,7 @@ int amdgo_ref_rows(int dtype, const void* A, const void* Bt, const int* rows, in
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_set_variant(int v) {
   if (v != 0 && v != 18 && v != 25 && v != 42 && v != 44 && v != 45 && v != 47 && v != 48 && v != 50 &&
-      v != 51 && v != 52 && v != 53 && v != 54 && v != 55 && v != 56 && v != 60 && v != 61 && v != 62)
+      v != 51 && v != 52 && v != 53 && v != 54 && v != 55 && v != 56 && v != 57 && v != 60 && v != 61 && v != 62)
     return (int)hipErrorInvalidValue;
   g_variant = v;
   return 0;
@@ -241,6 +243,13 @@ int amdgo_gemm_get_variant() { return g_variant; }
 int amdgo_gemm_set_split_target(int t) {
   if (t < 1 || t > 8) return (int)hipErrorInvalidValue;
   small_split_target() = t;
+  return 0;
+}
+// v57 / fp8 v24 sweep knobs for the calling host thread: a forced piece count (0 = automatic) and the
+// last piece's share of K in permille (0 = default). gemm_small_host.h AsmSplitKnobs.
+int amdgo_gemm_set_asm_split(int splits, int last_permille) {
+  if (splits < 0 || splits > 64 || last_permille < 0 || last_permille >= 1000) return (int)hipErrorInvalidValue;
+  asm_split_knobs() = AsmSplitKnobs{splits, last_permille};
   return 0;
 }
 int amdgo_gemm_small_splits(int M, int N, int K, int cus) {
@@ -341,6 +350,16 @@ static int gemm_bf16_dispatch(const void* A, const void* Bt, void* C, int M, int
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap<W4AP_SC_LONGK, true, false, W4AP_EPI_STAGED_ZC, 0, REC>),
                          dim3(persistent(nwg)), dim3(W4_THREADS), 0, s, a, b, c, M, N, K);
       break;
+    case 57: {
+      const int splits = asm_splits(nwg, K / BK, cus);   // > 1: kBf16Needs
+      SmallWorkspace* w = small_workspace(s, (size_t)nwg * splits * kAsmSlabFloats, nwg * 2);
+      if (!w) return (int)hipErrorOutOfMemory;
+      hipLaunchKernelGGL((gemm_bf16_256x256_w4ap_sk<W4VP_SC_G4_ZC, W4AP_EPI_LEAN, 2, REC>), dim3(nwg * splits),
+                         dim3(W4_THREADS), 0, s, a, b, c, M, N, K, splits, w->ws, w->cnt,
+                         asm_last_pairs(K / BK, splits));
+      (void)hipEventRecord(w->done, s);
+      break;
+    }
     default: {
       dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
       hipLaunchKernelGGL(gemm_bf16_generic<REC>, grid, dim3(256), 0, s, a, b, c, M, N, K);
@@ -373,6 +392,8 @@ static GemmRaster raster_bf16(int M, int N, int K, int cus) {
       return GemmRaster::persistent(v, BM, BN, persistent_launch_grid(nwg, cus), false);
     case 51: case 54: case 56:
       return GemmRaster::persistent(v, BM, BN, 256, true);
+    case 57:
+      return GemmRaster::split(v, asm_splits(nwg, K / BK, cus));
     default:
       return GemmRaster::generic(v, GBM, GBN);
   }

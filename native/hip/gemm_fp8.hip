@@ -126,6 +126,7 @@ static constexpr Fp8Need kFp8Needs[] = {
     {21, [](const Fp8Shape& c) { return c.ap; }, -1},
     {22, [](const Fp8Shape& c) { return c.ap; }, -1},
     {23, [](const Fp8Shape& c) { return c.ap; }, -1},
+    {24, [](const Fp8Shape& c) { return c.ap && asm_splits(c.nwg, c.K / F8_BK, c.cus) > 1; }, 23},
     {21, [](const Fp8Shape& c) { return c.sq; }, 20},
     {22, [](const Fp8Shape& c) { return c.sq; }, 23},
     {16, [](const Fp8Shape& c) { return c.sq; }, 15},
@@ -171,7 +172,7 @@ int amdgo_ref_rows(int dtype, const void* A, const void* Bt, const int* rows, in
 
 // 0 on success; hipErrorInvalidValue for a variant outside the production set.
 int amdgo_gemm_fp8_set_variant(int v) {
-  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21 && v != 22 && v != 23 &&
+  if (v != 0 && v != 10 && v != 15 && v != 16 && v != 17 && v != 18 && v != 20 && v != 21 && v != 22 && v != 23 && v != 24 &&
       v != 60 && v != 61 && v != 62)
     return (int)hipErrorInvalidValue;
   g_fp8_variant = v;
@@ -232,6 +233,16 @@ static int gemm_fp8_dispatch(const void* A, const void* Bt, void* C, int M, int 
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap<F8VP_SC_P_ZC, false, false, W4AP_EPI_LEAN, 2, REC>), dim3(pgrid),
                          dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
+    case 24: {
+      const int splits = asm_splits(nwg, K / F8_BK, cus);   // > 1: kFp8Needs
+      SmallWorkspace* w = small_workspace(s, (size_t)nwg * splits * kAsmSlabFloats, nwg * 2);
+      if (!w) return (int)hipErrorOutOfMemory;
+      hipLaunchKernelGGL((gemm_fp8_256x256_q16ap_sk<F8VP_SC_P_ZC, W4AP_EPI_LEAN, 2, REC>), dim3(nwg * splits),
+                         dim3(F8_THREADS), 0, s, a, b, c, M, N, K, splits, w->ws, w->cnt,
+                         asm_last_pairs(K / F8_BK, splits));
+      (void)hipEventRecord(w->done, s);
+      break;
+    }
     case 15:
       hipLaunchKernelGGL(Q16(32, false, REC), dim3(nwg), dim3(F8_THREADS), 0, s, a, b, c, M, N, K);
       break;
@@ -271,6 +282,8 @@ static GemmRaster raster_fp8(int M, int N, int K, int cus) {
       return GemmRaster::persistent(v, F8_BM, F8_BN, persistent_launch_grid(nwg, cus), false);
     case 21: case 22:
       return GemmRaster::persistent(v, F8_BM, F8_BN, 256, true);
+    case 24:
+      return GemmRaster::split(v, asm_splits(nwg, K / F8_BK, cus));
     default:
       return GemmRaster::generic(v, G8, G8);
   }

@@ -920,6 +920,19 @@ gemm_fp8_256x256_q16ap(const uint8_t* __restrict__ A, const uint8_t* __restrict_
   w4ap_run<SC, SERP, SQ, true, EPI, DM>((const char*)A, (const char*)Bt, C, M, N, K, smem);
 }
 
+// q16ap split-K (fp8 v24): one (tile, K piece) per workgroup, the piece sums reduced by each tile's last
+// arriving waves (gemm_w4ap.h SPLIT; the bf16 v57's frame with the fp8 K-tile body).
+template <int SC, int EPI, int DM, Rec REC = kTimed>
+__global__ void __launch_bounds__(F8_THREADS, 1)
+gemm_fp8_256x256_q16ap_sk(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt, __bf16* __restrict__ C,
+                          int M, int N, int K, int splits, float* __restrict__ ws, int* __restrict__ cnt,
+                          int last_pairs) {
+  __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
+  note_placement<REC>();
+  w4ap_run<SC, false, false, true, EPI, DM, true>((const char*)A, (const char*)Bt, C, M, N, K, smem,
+                                                  W4Split{splits, ws, cnt, last_pairs});
+}
+
 // OCP e4m3fn -> f32 in software (independent of the matrix cores): bias 7, no infinities,
 // S.1111.111 = NaN, exponent 0 = subnormal m/8 * 2^-6.
 __device__ __forceinline__ float e4m3_to_f32(uint8_t v) {

@@ -14,7 +14,9 @@ struct GemmRaster {
   // tile through xcd_remap + tile_coords / tile_coords_sq; PERSISTENT / PERSISTENT_SQ: `grid` workgroups
   // walking XCD-contiguous tile runs / the square super-tiles in rounds; SMALL: one workgroup per
   // (tile, K piece) through xcd_remap (gemm_small.h).
-  enum Kind { GENERIC = 0, GRID = 1, GRID_SQ = 2, PERSISTENT = 3, PERSISTENT_SQ = 4, SMALL = 5 };
+  // SPLIT: one workgroup per (tile, K piece) of the asm frame's split-K form, piece-major through
+  // xcd_remap, tiles in tile_coords order (gemm_w4ap.h SPLIT).
+  enum Kind { GENERIC = 0, GRID = 1, GRID_SQ = 2, PERSISTENT = 3, PERSISTENT_SQ = 4, SMALL = 5, SPLIT = 6 };
   int kind = GENERIC, variant = 0, tile_m = 64, tile_n = 64, grid = 0, splits = 1, pmajor = 0;
 
   static GemmRaster generic(int v, int tm, int tn) { return {GENERIC, v, tm, tn, 0, 1, 0}; }
@@ -23,6 +25,7 @@ struct GemmRaster {
     return {sq ? PERSISTENT_SQ : PERSISTENT, v, tm, tn, g, 1, 0};
   }
   static GemmRaster small(int v, int tm, int tn, int splits, int pmajor) { return {SMALL, v, tm, tn, 0, splits, pmajor}; }
+  static GemmRaster split(int v, int splits) { return {SPLIT, v, 256, 256, 0, splits, 1}; }
 };
 
 // `info` (8 ints): variant, kind, tile_m, tile_n, tiles_m, tiles_n, launch grid (workgroups), pieces per
@@ -32,10 +35,10 @@ struct GemmRaster {
 inline int raster_fill(const GemmRaster& r, int M, int N, int* info, int* owners, int* rounds, int cap) {
   const int tiles_m = (M + r.tile_m - 1) / r.tile_m, tiles_n = (N + r.tile_n - 1) / r.tile_n;
   const int nt = tiles_m * tiles_n;
-  const int pieces = r.kind == GemmRaster::SMALL ? r.splits : 1;
+  const int pieces = r.kind == GemmRaster::SMALL || r.kind == GemmRaster::SPLIT ? r.splits : 1;
   int grid = r.grid;
   if (r.kind == GemmRaster::GENERIC) grid = nt;
-  if (r.kind == GemmRaster::SMALL) grid = nt * r.splits;
+  if (r.kind == GemmRaster::SMALL || r.kind == GemmRaster::SPLIT) grid = nt * r.splits;
   if (info) {
     const int v[8] = {r.variant, r.kind, r.tile_m, r.tile_n, tiles_m, tiles_n, grid, pieces};
     for (int i = 0; i < 8; ++i) info[i] = v[i];
@@ -101,6 +104,17 @@ inline int raster_fill(const GemmRaster& r, int M, int N, int* info, int* owners
           tile = r.pmajor ? item - piece * nt : item / r.splits;
         }
         put(tile / tiles_n, tile % tiles_n, piece, b, 0);
+      }
+      break;
+    }
+    case GemmRaster::SPLIT: {
+      const int items = nt * r.splits;
+      for (int b = 0; b < items; ++b) {
+        const int item = xcd_remap(b, items);
+        const int piece = item / nt;
+        int tm, tn;
+        tile_coords(item - piece * nt, tiles_m, tiles_n, tm, tn);
+        put(tm, tn, piece, b, 0);
       }
       break;
     }

@@ -32,6 +32,45 @@ inline int small_splits(int tiles, int nk, int cus) {
   return splits > 1 ? splits : 1;
 }
 
+// The split-K form of the 256x256 asm frame (bf16 v57, fp8 v24; gemm_w4ap.h SPLIT): K pieces per
+// tile -- as many as fit the CUs in one wave (cus / tiles), each of at least kAsmPieceMinKt K-tiles (an
+// even count); 1 = no split.
+constexpr int kAsmPieceMinKt = 16;
+// Sweep knobs of the split-K asm form, per host thread (amdgo_gemm_set_asm_split): a forced piece count
+// (0 = the automatic one below; forced pieces keep >= 4 K-tiles) and the last piece's share of K in
+// permille (0 = the default, asm_last_pairs).
+struct AsmSplitKnobs {
+  int splits = 0;
+  int last_permille = 0;
+};
+inline AsmSplitKnobs& asm_split_knobs() {
+  static thread_local AsmSplitKnobs k;
+  return k;
+}
+inline int asm_splits(int tiles, int nk, int cus) {
+  if (tiles <= 0) return 1;
+  if (const int forced = asm_split_knobs().splits) {
+    const int s = forced < nk / 4 ? forced : nk / 4;
+    return s > 1 ? s : 1;
+  }
+  int s = cus / tiles;
+  const int most = nk / kAsmPieceMinKt;
+  if (s > most) s = most;
+  return s > 1 ? s : 1;
+}
+// K-tile pairs of the last piece (0 = even pieces). The tile's last arrival sums the others' slabs; a
+// longer last piece lets the other pieces' slab stores and release run under its K-loop instead of
+// after it. Every piece keeps >= 2 pairs.
+inline int asm_last_pairs(int nk, int splits) {
+  const int pm = asm_split_knobs().last_permille;
+  if (splits < 2 || pm <= 0) return 0;
+  const int pairs = nk / 2;
+  const int last = (pairs * pm + 500) / 1000;
+  if (last < 2 || pairs - last < 2 * (splits - 1)) return 0;
+  return last;
+}
+constexpr size_t kAsmSlabFloats = 256 * 256;   // one 256x256 fp32 partial per (tile, piece)
+
 // v61's item order: piece-major for pieces of >= 32 K-tiles (gemm_small.h, gemm_mfma_small_sk).
 inline int small_piece_major(int nk, int splits) { return nk / splits >= 32 ? 1 : 0; }
 

@@ -171,20 +171,149 @@ struct W4apEpi {
   }
 };
 
+// The split-K form (SPLIT, v57 / fp8 v24): one (tile, K piece) item per workgroup, gridDim = tiles x
+// splits <= the CU count, so the 65-128-tile and the long-K 64-tile grids fill the chip in 256x256
+// tiles instead of falling to the smaller tiles of the small-grid frame (gemm_small.h). Items are
+// piece-major through xcd_remap: an XCD runs neighbouring tiles (tile_coords) at one K range, so its
+// workgroups share A and B panel slices in its L2. Piece p runs K-tile pairs [p P / S, (p + 1) P / S)
+// (P = K-tiles / 2: every piece an even count, host: >= 4), or with `last_pairs` the last piece that
+// many pairs and the others the rest evenly.
+// The reduction, per tile on two counters (arrivals, done): a workgroup draws an arrival ticket first.
+// Every arrival but the last stores its fp32 partial as lane-major slabs (per wave 64 accumulator quads
+// x 64 lanes x 16 B, one contiguous KiB per store) with plain stores, drains them, meets its waves at a
+// barrier, releases ONCE at agent scope and counts itself done; the last arrival keeps its partial in
+// its accumulators, waits for the done count of the S - 1 workgroups that arrived before it, acquires
+// (agent scope) and sums every piece in piece order -- its own from its accumulators at its place -- so
+// the result does not depend on arrival order (cdna_hip_programming.md §5 "In-launch split-K reduction",
+// §6 Guideline 16). The wait is only ever for workgroups that have already arrived, i.e. are running
+// and owe nothing but their stores: no co-residency is assumed. The last arrival resets both counters
+// for the next launch, then runs the ordinary epilogue. Only S - 1 of S partials travel, and each writer
+// workgroup releases once: the first form of this reduction stored all S partials and released every
+// wave's separately (4 L2 write-backs per workgroup), 490 TF/s at 2560^3 (profiles/r6_splitk/).
+struct W4Split {
+  int splits = 1;
+  float* ws = nullptr;   // tiles x splits x 4 waves x 64 KiB
+  int* cnt = nullptr;    // tiles x 2 (arrivals, done), zero between launches
+  int last_pairs = 0;    // K-tile pairs of the last piece; 0 = even pieces (gemm_small_host.h asm_last_pairs)
+};
+
+// SPLIT: this workgroup's reduction (every wave calls it). False: the workgroup stored its partial and
+// is finished. True: it was the tile's last arrival and its accumulators now hold the sum over every
+// piece. `flag`: one LDS word no wave touches until the epilogue (wave 0's epilogue staging).
+__device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, int piece, int wid, int lane,
+                                                  int* flag) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int WAVE_F4 = 64 * 64;   // 64 accumulator quads x 64 lanes
+  const int S = sp.splits;
+  int* const arrive = sp.cnt + tile * 2;
+  int* const done = arrive + 1;
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // the last MFMAs' results
+  if (wid == 0 && lane == 0) *flag = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ticket = __builtin_amdgcn_readfirstlane(*flag);
+  // piece p's slab of this wave: quad i of lane l at float4 index ((tile S + p) 4 + wid) 4096 + 64 i + l
+  auto slab = [&](int p) { return ((tile * S + p) * 4 + wid) * WAVE_F4 + lane; };
+  f4* const ws4 = (f4*)sp.ws;
+  auto own = [&](auto I) {
+    constexpr int i = decltype(I)::value;
+    float x0, x1, x2, x3;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+                 : "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3));
+    return f4{x0, x1, x2, x3};
+  };
+  if (ticket < S - 1) {
+    f4* const mine = ws4 + slab(piece);
+    static_for<0, 64>([&](auto I) { mine[decltype(I)::value * 64] = own(I); });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wid == 0 && lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return false;
+  }
+  if (wid == 0 && lane == 0) {
+    // every workgroup counted here has arrived and owes only its stores; bounded all the same (~1 s)
+    for (unsigned spins = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1 &&
+                             spins < (1u << 24); ++spins)
+      __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *arrive = 0;                       // ready for the next launch on this stream
+    *done = 0;
+  }
+  __syncthreads();
+  auto put = [&](auto I, f4 t) {
+    constexpr int i = decltype(I)::value;
+    asm volatile("v_accvgpr_write_b32 a%c0, %4\n\tv_accvgpr_write_b32 a%c1, %5\n\t"
+                 "v_accvgpr_write_b32 a%c2, %6\n\tv_accvgpr_write_b32 a%c3, %7"
+                 :: "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3),
+                    "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]));
+  };
+  if (S == 2) {
+    // two pieces: own + other == other + own exactly; 32 quads (128 VGPRs) of the other slab in flight
+    const f4* const other = ws4 + slab(1 - piece);
+    static_for<0, 2>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      f4 t[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) t[j] = other[(q * 32 + j) * 64];
+      static_for<0, 32>([&](auto J) {
+        constexpr int i = q * 32 + decltype(J)::value;
+        const f4 tj = t[decltype(J)::value];   // (a generic lambda does not capture a name used only in asm operands)
+        put(std::integral_constant<int, i>{}, tj + own(std::integral_constant<int, i>{}));
+      });
+    });
+  } else {
+    static_for<0, 4>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      f4 acc[16];
+      for (int p = 0; p < S; ++p) {
+        f4 t[16];
+        if (p == piece) {
+          static_for<0, 16>([&](auto J) { t[decltype(J)::value] = own(std::integral_constant<int, q * 16 + decltype(J)::value>{}); });
+        } else {
+          const f4* const src = ws4 + slab(p);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = src[(q * 16 + j) * 64];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = p == 0 ? t[j] : acc[j] + t[j];
+      }
+      static_for<0, 16>([&](auto J) {
+        const f4 aj = acc[decltype(J)::value];
+        put(std::integral_constant<int, q * 16 + decltype(J)::value>{}, aj);
+      });
+    });
+  }
+  return true;
+}
+
 // A, Bt: K-major operands (element size 1 for F8, else 2); C: bf16; smem: W4AP_LDS bytes.
 // DM (DMA form): 0 = one lane offset + per-row-block SGPR soffsets, SC indexes W4AP/F8AP schedules;
 // 1 = VP (per-piece VGPR lane offsets, SGPR K offset), SC indexes the VP schedules; 2 = VP with the
 // A-panel pieces reading rows 32 apart (PA; the epilogue maps LDS slot s to C row 32 (s & 7) + (s >> 3)).
 // EPI: the W4AP_EPI_* forms above (W4apEpi says what the staged epilogue does for each).
-template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0>
+template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0, bool SPLIT = false>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
-                                         __bf16* __restrict__ C, int M, int N, int K, char* smem) {
+                                         __bf16* __restrict__ C, int M, int N, int K, char* smem,
+                                         W4Split sp = W4Split{}) {
   constexpr int ESZ = F8 ? 1 : 2;
   const int tiles_m = M / W4AP_TILE;
   const int tiles_n = N / W4AP_TILE;
   const int nwg = tiles_m * tiles_n;
-  int tile, per, t_end;
-  if constexpr (SQ) {
+  int tile, per, t_end, piece = 0;
+  if constexpr (SPLIT) {
+    const int items = nwg * sp.splits;                    // gridDim == items
+    const int item = xcd_remap((int)blockIdx.x, items);
+    piece = item / nwg;
+    tile = item - piece * nwg;
+    per = items;                                          // one item per workgroup: no next tile
+    t_end = nwg;
+  } else if constexpr (SQ) {
     tile = (int)blockIdx.x;
     per = (int)gridDim.x;
     t_end = nwg;
@@ -217,7 +346,19 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     return r;
   };
   const int par = wid & 1;
-  const int ktiles = (int)(row_bytes / W4AP_ROW);
+  int ktiles = (int)(row_bytes / W4AP_ROW);
+  size_t kbyte0 = 0;                                      // SPLIT: the piece's first K-tile, in bytes
+  if constexpr (SPLIT) {
+    const int pairs = ktiles >> 1;
+    int p0 = piece * pairs / sp.splits, p1 = (piece + 1) * pairs / sp.splits;
+    if (sp.last_pairs > 0) {            // the first S - 1 pieces share pairs - last_pairs evenly
+      const int rest = pairs - sp.last_pairs, n = sp.splits - 1;
+      p0 = piece < n ? piece * rest / n : rest;
+      p1 = piece < n ? (piece + 1) * rest / n : pairs;
+    }
+    kbyte0 = (size_t)(2 * p0) * W4AP_ROW;
+    ktiles = 2 * (p1 - p0);
+  }
   const uint32_t lane_dma = (uint32_t)(lane >> 3) * row_bytes +
                             (uint32_t)(((lane & 7) ^ ((par * 4 + (lane >> 4)) & 7)) * 16);
   // the lane offset of a tile's first DMA K-tile, and its K step, by walking direction
@@ -297,7 +438,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   int tm, tn;
   coords(tile, tm, tn);
   bool rev = false;
-  w4a_u32x4 sA = mk_rs(A + (size_t)tm * panel_bytes), sB = mk_rs(Bt + (size_t)tn * panel_bytes);
+  w4a_u32x4 sA = mk_rs(A + (size_t)tm * panel_bytes + kbyte0), sB = mk_rs(Bt + (size_t)tn * panel_bytes + kbyte0);
   uint32_t voff_k = voff0(rev);
   uint32_t koff = koff0(rev);
   int kstep = kst(rev);
@@ -350,6 +491,10 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
       F8AP_LOOP_SELECT(SC)
     } else {
       W4AP_LOOP_SELECT(SC)
+    }
+
+    if constexpr (SPLIT) {
+      if (sp.splits > 1 && !w4ap_split_reduce(sp, tile, piece, wid, lane, (int*)(smem + 2 * W4AP_BUF))) return;
     }
 
     // wave-private epilogue (the K buffers may be receiving the next tile's DMA): 4 passes of

@@ -62,7 +62,7 @@ def asm_lab(tmp_path_factory):
 def w4(request):
     asm = request.getfixturevalue("asm" if request.param == "production" else "asm_lab")
     # the hand-scheduled asm K pipeline (w4a/w4ap) has no compiler loop: audited separately below
-    return [k for k in _kernels(asm, "gemm_bf16_256x256_w4") if not re.match(r"\w*w4ap?I", k[0])]
+    return [k for k in _kernels(asm, "gemm_bf16_256x256_w4") if not re.match(r"\w*w4ap?(?:_sk)?I", k[0])]
 
 
 def test_production_library_kernel_set(asm):
@@ -221,6 +221,22 @@ def test_w4ap_production_pipeline(asm):
         # the zc schedules (every production form) peel the first K-tile pair (src C = 0): 8 bodies
         assert _audit_asm_pipeline(body, st) == 8 * 128
         assert "v_accvgpr_write" not in body      # src C = 0 instead of zeroing writes
+
+
+def test_w4ap_split_k_pipeline(asm):
+    """Production v57: the asm K pipeline of v55 (VP + PA, LEAN epilogue) in its split-K form -- the same
+    8 K-tile bodies, plus the reduction (gemm_w4ap.h SPLIT): an arrival ticket and a done count per
+    tile (two agent atomics), the partial slab as 64 16-byte stores per wave, one release per writing
+    workgroup and one acquire per reducing one, and the last arrival's sum written back into the 256
+    accumulators (the two-piece path and the general one)."""
+    kernels = _kernels(asm, "gemm_bf16_256x256_w4ap_skI")
+    assert len(kernels) == 1
+    for body, st in kernels:
+        assert _audit_asm_pipeline(body, st) == 8 * 128
+        assert body.count("v_accvgpr_write_b32") == 2 * 256
+        assert len(re.findall(r"global_atomic_add\b", body)) == 2
+        assert len(re.findall(r"global_store_dwordx4\b", body)) >= 64
+        assert body.count("buffer_wbl2") == 1 and body.count("buffer_inv") == 1
 
 
 def test_w4a_lab_pipelines(tmp_path_factory):

@@ -239,3 +239,35 @@ def test_persistent_launch_grid_rounds_up_to_whole_xcd_groups(lib):
             assert n % 8 == 0 and n <= cus
             if nwg <= (cus // 8) * 8:
                 assert n // 8 >= -(-nwg // 8)           # workgroups per XCD >= its tiles: one round
+
+
+def _asm_splits(tiles, nk, cus):
+    """gemm_small_host.h asm_splits: the split-K asm form's pieces per 256x256 tile (>= 16 K-tiles)."""
+    return max(1, min(cus // tiles, nk // 16)) if tiles else 1
+
+
+def test_split_k_asm_pins_run_where_they_can_and_fall_back_otherwise(lib):
+    """bf16 v57 / fp8 v24 (the asm frame's split-K form) pinned: they run on 256x256-tileable shapes
+    with an even K-tile count and >= 2 pieces of >= 16 K-tiles within the CUs; otherwise they fall
+    back to the one-wave asm kernels (v55 / v23) and on from there."""
+    bad = []
+    for M, N in itertools.product(DIMS, DIMS[::2]):
+        for K, cus in itertools.product(KS, CUS):
+            nwg = (M // 256) * (N // 256)
+            tiles = M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and K >= 128
+            ok = tiles and K % 128 == 0 and _asm_splits(nwg, K // 64, cus) > 1
+            got = lib.amdgo_gemm_plan_bf16(M, N, K, cus, 57)
+            want = 57 if ok else lib.amdgo_gemm_plan_bf16(M, N, K, cus, 55)
+            if got != want:
+                bad.append(("bf16", M, N, K, cus, got, want))
+        for K, cus in itertools.product(FP8_KS, CUS):
+            nwg = (M // 256) * (N // 256)
+            tiles = M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and K >= 256
+            pgrid = (min(nwg, cus) // 8) * 8
+            ap = cus == 256 and K % 256 == 0 and K >= 512 and pgrid >= 8
+            ok = tiles and ap and _asm_splits(nwg, K // 128, cus) > 1
+            got = lib.amdgo_gemm_plan_fp8(M, N, K, cus, 24)
+            want = 24 if ok else lib.amdgo_gemm_plan_fp8(M, N, K, cus, 23)
+            if got != want:
+                bad.append(("fp8", M, N, K, cus, got, want))
+    assert not bad, bad[:20]

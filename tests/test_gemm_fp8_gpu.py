@@ -20,7 +20,7 @@ def _rand_fp8(shape, gen, dev):
     return (torch.rand(shape, generator=gen, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
 
 
-@pytest.fixture(params=[0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 60, 61, 62])   # the production set (gemm.FP8_VARIANTS)
+@pytest.fixture(params=[0, 10, 15, 16, 17, 18, 20, 21, 22, 23, 24, 60, 61, 62])   # the production set (gemm.FP8_VARIANTS)
 def fp8_variant(request):
     from gpu_operator_amd.ops import gemm as G
 

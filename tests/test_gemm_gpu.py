@@ -9,7 +9,7 @@ def _ref(a, bt):
     return a.float() @ bt.float().t()
 
 
-@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61, 62])   # the production set (gemm.BF16_VARIANTS)
+@pytest.fixture(params=[0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 60, 61, 62])   # the production set (gemm.BF16_VARIANTS)
 def variant(request):
     from gpu_operator_amd.ops import gemm as G
     old = G.get_variant()
@@ -153,7 +153,7 @@ def test_production_variant_set_is_closed(cuda_device):
     """Only exact, shipped kernels are reachable: lab/knock-out numbers are refused."""
     from gpu_operator_amd.ops import gemm as G
 
-    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 60, 61, 62)
+    assert tuple(G.BF16_VARIANTS) == (0, 18, 25, 42, 44, 45, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 60, 61, 62)
     for bad in (1, 2, 10, 20, 24, 27, 40, 46, 99, -1):
         with pytest.raises(ValueError):
             G.set_variant(bad)
@@ -273,6 +273,65 @@ def test_small_grid_kernel_v60_matches_fp32_reference(cuda_device, v, m, n, k):
     finally:
         G.set_variant(old)
     assert G.resolve_variant(1024, 1024, 1024) == 60          # the automatic choice for a 16-tile grid
+
+
+@pytest.mark.parametrize("m,n,k,splits", [(2560, 2560, 2560, 2), (2048, 2048, 8192, 4), (1024, 1024, 4096, 4),
+                                          (512, 512, 8192, 8), (2048, 512, 4096, 4), (1536, 2560, 3072, 3)])
+def test_split_k_asm_v57_matches_fp32_reference_on_repeat(cuda_device, m, n, k, splits):
+    """v57: the asm 256x256 frame, one (tile, K piece) per workgroup; each tile's last arriving waves
+    sum the fp32 slabs in piece order. Repeated launches on one stream (the counters must be reset),
+    one on a side stream, all against the fp32 reference and bitwise equal to each other."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+    from gpu_operator_amd.ops import _lib
+
+    old = G.get_variant()
+    G.set_variant(57)
+    try:
+        assert G.resolve_variant(m, n, k) == 57
+        info = G.raster(m, n, k, "bf16")
+        assert info.pieces == splits and info.grid == (m // 256) * (n // 256) * splits
+        g = torch.Generator(device=cuda_device).manual_seed(m + 5 * n + k)
+        a = (torch.rand((m, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand((n, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        ref = _ref(a, bt)
+        outs = [G.gemm_bf16(a, bt) for _ in range(3)]
+        side = torch.cuda.Stream(device=cuda_device)
+        with torch.cuda.stream(side):
+            outs.append(G.gemm_bf16(a, bt))
+        torch.cuda.synchronize()
+        for c in outs:
+            torch.testing.assert_close(c.float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+        assert all(torch.equal(outs[0], c) for c in outs[1:])     # piece order fixed: arrival order is not
+    finally:
+        G.set_variant(old)
+
+
+@pytest.mark.parametrize("m,n,k,splits,permille", [(2560, 2560, 8192, 2, 540), (2048, 2048, 8192, 4, 340),
+                                                   (2048, 2048, 8192, 3, 400), (1024, 1024, 4096, 2, 700)])
+def test_split_k_asm_v57_uneven_pieces(cuda_device, m, n, k, splits, permille):
+    """v57 with forced piece counts and a longer last piece (the first pieces' slabs stored under the
+    last one's K-loop): against the fp32 reference, repeated launches bitwise equal."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    old = G.get_variant()
+    G.set_variant(57)
+    G.set_asm_split(splits, permille)
+    try:
+        assert G.raster(m, n, k, "bf16").pieces == splits
+        g = torch.Generator(device=cuda_device).manual_seed(m + 3 * n + k + permille)
+        a = (torch.rand((m, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand((n, k), generator=g, device=cuda_device) * 2 - 1).to(torch.bfloat16)
+        ref = _ref(a, bt)
+        outs = [G.gemm_bf16(a, bt) for _ in range(3)]
+        torch.cuda.synchronize()
+        for c in outs:
+            torch.testing.assert_close(c.float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+        assert all(torch.equal(outs[0], c) for c in outs[1:])
+    finally:
+        G.set_asm_split(0, 0)
+        G.set_variant(old)
 
 
 @pytest.mark.parametrize("v", [61])

@@ -43,7 +43,7 @@ def test_raster_is_a_bijection(dtype, shape):
     slots = _check_bijection(r)
     assert len(slots) == r.tiles_m * r.tiles_n * r.pieces
     assert r.tile_n in (64, 128, 256, 512)            # the ABFT strip widths gemm_abft.hip supports
-    if r.kind in ("generic", "grid", "grid_sq", "small"):
+    if r.kind in ("generic", "grid", "grid_sq", "small", "split"):
         assert {b for b, _ in slots} == set(range(r.grid))          # every workgroup owns exactly one item
         assert all(rnd == 0 for _, rnd in slots)
     if r.kind == "persistent":
@@ -55,6 +55,36 @@ def test_raster_is_a_bijection(dtype, shape):
             per_wg.setdefault(b, []).append(rnd)
         for rounds in per_wg.values():
             assert sorted(rounds) == list(range(len(rounds)))
+
+
+@pytest.mark.parametrize("shape", [(2560, 2560, 2560), (2048, 2048, 8192), (1024, 1024, 4096), (512, 512, 8192),
+                                   (2560, 2560, 8192), (4096, 4096, 4096), (1024, 1024, 1024)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_split_k_asm_raster_pinned(shape):
+    """v57 pinned: a bijection of (tile, piece) onto the grid; piece-major, so each XCD's run of
+    workgroups covers neighbouring tiles at one K range. Shapes it cannot split fall back to v55."""
+    from gpu_operator_amd.ops import gemm as G
+
+    m, n, k = shape
+    old = G.get_variant()
+    G.set_variant(57)
+    try:
+        r = G.raster(m, n, k, "bf16", cus=256)
+    finally:
+        G.set_variant(old)
+    tiles = (m // 256) * (n // 256)
+    splits = min(256 // tiles, (k // 64) // 16)
+    if splits < 2:
+        assert r.variant == 55 and r.kind == "persistent"
+        return
+    assert (r.variant, r.kind, r.pieces, r.grid) == (57, "split", splits, tiles * splits)
+    slots = _check_bijection(r)
+    assert {b for b, _ in slots} == set(range(r.grid))
+    # the workgroups of one XCD (b % 8) hold one piece except where the piece-major order wraps
+    pieces_of_xcd = {}
+    for tm, tn, p in itertools.product(range(r.tiles_m), range(r.tiles_n), range(r.pieces)):
+        pieces_of_xcd.setdefault(r.owner[tm][tn][p] % 8, set()).add(p)
+    assert all(len(ps) <= 2 for ps in pieces_of_xcd.values())
 
 
 def test_raster_kinds_follow_the_dispatch():

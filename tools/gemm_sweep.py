@@ -36,7 +36,12 @@ class _Pinned:
     def __init__(self, G, spec: str, dtype: str):
         self.G, self.dtype = G, dtype
         self.split = None
-        if spec.startswith("p") and "s" in spec[1:]:          # p61s2: v61 aiming at 2 workgroups per CU
+        self.asm = None
+        if spec.startswith("p") and "b" in spec[1:]:          # p57s2b540: v57 / v24 in 2 pieces, the last 54 % of K
+            v, rest = spec[1:].split("s")
+            s, b = rest.split("b")
+            self.v, self.lab, self.asm = int(v), None, (int(s), int(b))
+        elif spec.startswith("p") and "s" in spec[1:]:          # p61s2: v61 aiming at 2 workgroups per CU
             v, t = spec[1:].split("s")
             self.v, self.lab, self.split = int(v), None, int(t)
         elif spec.startswith("p"):
@@ -50,6 +55,7 @@ class _Pinned:
             (self.G.set_variant if self.dtype == "bf16" else self.G.set_fp8_variant)(self.v)
             if self.dtype == "bf16":
                 self.G.set_split_target(self.split or 1)
+            self.G.set_asm_split(*(self.asm or (0, 0)))
 
     def __call__(self, A, Bt, C):
         if self.lab is not None:
