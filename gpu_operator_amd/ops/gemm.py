@@ -100,10 +100,11 @@ def set_split_target(t: int) -> None:
         raise ValueError(f"split target {t} outside 1..8")
 
 
-def set_asm_split(splits: int = 0, last_permille: int = 0) -> None:
+def set_asm_split(splits: int = 0, last_permille: int = 0, piece_major: bool = False) -> None:
     """v57 / fp8 v24 (split-K in the 256x256 asm frame), per host thread: force ``splits`` K pieces per
-    tile (0 = automatic) and give the last piece ``last_permille`` of K (0 = the default)."""
-    if _lib.load().amdgo_gemm_set_asm_split(int(splits), int(last_permille)) != 0:
+    tile (0 = automatic), give the last piece ``last_permille`` of K (0 = the default 52 %, 500 = even),
+    and order the items piece-major instead of tile-major (a tile's pieces on one XCD, the default)."""
+    if _lib.load().amdgo_gemm_set_asm_split(int(splits), int(last_permille), int(bool(piece_major))) != 0:
         raise ValueError(f"asm split ({splits}, {last_permille}) outside 0..64 / 0..999")
 
 

@@ -39,7 +39,11 @@
 //        (a 256-tile grid of at most a quarter of the CUs) and for shapes only 128-tileable; 61 = its
 //        split-K form when the 128x128 grid is under the CU count and K leaves pieces of >= 16
 //        K-tiles; 62 = 256x128 tiles for 256-tile grids of a quarter to a half of the CUs.
-//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 / 60 / 61 / 62 = that kernel pinned (no automatic switch; still falls back to a
+//   57 (round 6) = v55 in the split-K form of the asm frame (gemm_w4ap.h SPLIT): one (tile, K piece) per
+//        workgroup, two pieces (the last 52 % of K), a tile's pieces on one XCD, the tile's last arrival
+//        sums; the default over v62 for 65-128-tile grids with K >= 4096 (2560^2x8192 1.12x v62,
+//        2048x4096x16384 1.27x; profiles/r6_splitk/band_bf16.jsonl).
+//   18 / 25 / 42 / 44 / 45 / 47 / 48 / 50 / 51 / 52 / 53 / 54 / 55 / 56 / 57 / 60 / 61 / 62 = that kernel pinned (no automatic switch; still falls back to a
 //        kernel that can run the shape or the device).
 // The automatic choice is the first matching row of the declarative table kBf16Rules below (each row
 // cites its sweep); what each kernel needs, and where a pinned one falls back, is kBf16Needs. Both are
@@ -123,6 +127,10 @@ static constexpr Bf16Rule kBf16Rules[] = {
     {60, [](const Bf16Shape& c) { return c.tiles128 && (!c.tiles256 || 4 * c.nwg <= c.cus); },
      "profiles/r5_small/sweep_v62.jsonl (1024^3 1.36x, 1536^3 1.01x, 2048^2x1024 1.35x hipBLASLt)"},
     {0, [](const Bf16Shape& c) { return !c.tiles256; }, "generic bounds-checked kernel"},
+    // a quarter to a half of the CUs in 256x256 tiles with K >= 4096: the asm frame split in two K pieces
+    {57, [](const Bf16Shape& c) { return c.mi355 && 4 * c.nwg > c.cus && 2 * c.nwg <= c.cus && c.K % (2 * BK) == 0 &&
+                                         c.K >= 64 * BK; },
+     "profiles/r6_splitk/band_bf16.jsonl (2560^2x8192 1.12x v62, 2048x4096x16384 1.27x, 2304^2x4096 1.06x)"},
     // a quarter to a half of the CUs in 256x256 tiles: 256x128 tiles fill the chip in one wave
     {62, [](const Bf16Shape& c) { return 4 * c.nwg > c.cus && 2 * c.nwg <= c.cus; },
      "profiles/r5_small/sweep_tile256x128.jsonl, sweep_tile256x128_mid.jsonl (2560^3 878 vs 773, 2816^3 1060 vs 969)"},
@@ -246,10 +254,12 @@ int amdgo_gemm_set_split_target(int t) {
   return 0;
 }
 // v57 / fp8 v24 sweep knobs for the calling host thread: a forced piece count (0 = automatic) and the
-// last piece's share of K in permille (0 = default). gemm_small_host.h AsmSplitKnobs.
-int amdgo_gemm_set_asm_split(int splits, int last_permille) {
-  if (splits < 0 || splits > 64 || last_permille < 0 || last_permille >= 1000) return (int)hipErrorInvalidValue;
-  asm_split_knobs() = AsmSplitKnobs{splits, last_permille};
+// last piece's share of K in permille (0 = default), and the item order (1 = piece-major). gemm_small_host.h
+// AsmSplitKnobs.
+int amdgo_gemm_set_asm_split(int splits, int last_permille, int piece_major) {
+  if (splits < 0 || splits > 64 || last_permille < 0 || last_permille >= 1000 || piece_major < 0 || piece_major > 1)
+    return (int)hipErrorInvalidValue;
+  asm_split_knobs() = AsmSplitKnobs{splits, last_permille, piece_major};
   return 0;
 }
 int amdgo_gemm_small_splits(int M, int N, int K, int cus) {
@@ -356,7 +366,7 @@ static int gemm_bf16_dispatch(const void* A, const void* Bt, void* C, int M, int
       if (!w) return (int)hipErrorOutOfMemory;
       hipLaunchKernelGGL((gemm_bf16_256x256_w4ap_sk<W4VP_SC_G4_ZC, W4AP_EPI_LEAN, 2, REC>), dim3(nwg * splits),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K, splits, w->ws, w->cnt,
-                         asm_last_pairs(K / BK, splits));
+                         asm_last_pairs(K / BK, splits), asm_piece_major());
       (void)hipEventRecord(w->done, s);
       break;
     }
@@ -393,7 +403,7 @@ static GemmRaster raster_bf16(int M, int N, int K, int cus) {
     case 51: case 54: case 56:
       return GemmRaster::persistent(v, BM, BN, 256, true);
     case 57:
-      return GemmRaster::split(v, asm_splits(nwg, K / BK, cus));
+      return GemmRaster::split(v, asm_splits(nwg, K / BK, cus), asm_piece_major());
     default:
       return GemmRaster::generic(v, GBM, GBN);
   }

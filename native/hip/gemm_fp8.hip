@@ -32,7 +32,10 @@
 //       double-rate v_mfma_f32_16x16x128_f8f6f4, whole-tile or split-K, for grids the 256x256 tiling
 //       leaves mostly idle (and shapes only 128-tileable).
 //   62 (round 5): the same frame in 256x128 tiles for 256-tile grids of a quarter to a half of the CUs.
-//   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 / 60 / 61 / 62 = that kernel pinned (no automatic switch; falls back when the
+//   24 (round 6): v23 in the split-K form of the asm frame (gemm_w4ap.h SPLIT): one (tile, K piece) per
+//       workgroup, two pieces, the tile's last arrival sums; the default over v62 for 65-128-tile grids
+//       with K >= 8192 (2560^2x16384 1.19x v62, 1.17x hipBLASLt; profiles/r6_splitk/band_fp8.jsonl).
+//   10 / 15 / 16 / 17 / 18 / 20 / 21 / 22 / 23 / 24 / 60 / 61 / 62 = that kernel pinned (no automatic switch; falls back when the
 //       shape or the device cannot run it).
 // q16 vs the round-1 default (block-scaled 32x32x64, lab v9), same process, 4 boxes
 // (profiles/r2_fp8_q16/): 8192^3 +5.3 %, 16384^3 +3.1 %, 4096^3 +4.1 %, 16384x8192x8192 +2.2 %.
@@ -88,6 +91,9 @@ static constexpr Fp8Rule kFp8Rules[] = {
     {60, [](const Fp8Shape& c) { return c.tiles128 && (!c.tiles || 4 * c.nwg <= c.cus); },
      "profiles/r5_small/ (fp8 128x128)"},
     {0, [](const Fp8Shape& c) { return !c.tiles; }, "generic bounds-checked kernel"},
+    // a quarter to a half of the CUs in 256x256 tiles with K >= 8192: the asm frame split in two K pieces
+    {24, [](const Fp8Shape& c) { return c.ap && 4 * c.nwg > c.cus && 2 * c.nwg <= c.cus && c.K >= 64 * F8_BK; },
+     "profiles/r6_splitk/band_fp8.jsonl (2560^2x8192 1.02x v62, 2560^2x16384 1.19x, 2048x4096x16384 1.16x)"},
     // a quarter to a half of the CUs in 256x256 tiles: 256x128 tiles fill the chip in one wave
     {62, [](const Fp8Shape& c) { return 4 * c.nwg > c.cus && 2 * c.nwg <= c.cus; },
      "profiles/r5_small/sweep_tile256x128_mid_fp8.jsonl (2560^3 1591 vs 1412, 2560^2x8192 2032 vs 1713)"},
@@ -239,7 +245,7 @@ static int gemm_fp8_dispatch(const void* A, const void* Bt, void* C, int M, int 
       if (!w) return (int)hipErrorOutOfMemory;
       hipLaunchKernelGGL((gemm_fp8_256x256_q16ap_sk<F8VP_SC_P_ZC, W4AP_EPI_LEAN, 2, REC>), dim3(nwg * splits),
                          dim3(F8_THREADS), 0, s, a, b, c, M, N, K, splits, w->ws, w->cnt,
-                         asm_last_pairs(K / F8_BK, splits));
+                         asm_last_pairs(K / F8_BK, splits), asm_piece_major());
       (void)hipEventRecord(w->done, s);
       break;
     }
@@ -283,7 +289,7 @@ static GemmRaster raster_fp8(int M, int N, int K, int cus) {
     case 21: case 22:
       return GemmRaster::persistent(v, F8_BM, F8_BN, 256, true);
     case 24:
-      return GemmRaster::split(v, asm_splits(nwg, K / F8_BK, cus));
+      return GemmRaster::split(v, asm_splits(nwg, K / F8_BK, cus), asm_piece_major());
     default:
       return GemmRaster::generic(v, G8, G8);
   }

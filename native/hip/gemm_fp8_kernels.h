@@ -926,11 +926,11 @@ template <int SC, int EPI, int DM, Rec REC = kTimed>
 __global__ void __launch_bounds__(F8_THREADS, 1)
 gemm_fp8_256x256_q16ap_sk(const uint8_t* __restrict__ A, const uint8_t* __restrict__ Bt, __bf16* __restrict__ C,
                           int M, int N, int K, int splits, float* __restrict__ ws, int* __restrict__ cnt,
-                          int last_pairs) {
+                          int last_pairs, int pmajor) {
   __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
   note_placement<REC>();
   w4ap_run<SC, false, false, true, EPI, DM, true>((const char*)A, (const char*)Bt, C, M, N, K, smem,
-                                                  W4Split{splits, ws, cnt, last_pairs});
+                                                  W4Split{splits, ws, cnt, last_pairs, pmajor});
 }
 
 // OCP e4m3fn -> f32 in software (independent of the matrix cores): bias 7, no infinities,

@@ -25,7 +25,7 @@ struct GemmRaster {
     return {sq ? PERSISTENT_SQ : PERSISTENT, v, tm, tn, g, 1, 0};
   }
   static GemmRaster small(int v, int tm, int tn, int splits, int pmajor) { return {SMALL, v, tm, tn, 0, splits, pmajor}; }
-  static GemmRaster split(int v, int splits) { return {SPLIT, v, 256, 256, 0, splits, 1}; }
+  static GemmRaster split(int v, int splits, int pmajor) { return {SPLIT, v, 256, 256, 0, splits, pmajor}; }
 };
 
 // `info` (8 ints): variant, kind, tile_m, tile_n, tiles_m, tiles_n, launch grid (workgroups), pieces per
@@ -111,9 +111,9 @@ inline int raster_fill(const GemmRaster& r, int M, int N, int* info, int* owners
       const int items = nt * r.splits;
       for (int b = 0; b < items; ++b) {
         const int item = xcd_remap(b, items);
-        const int piece = item / nt;
+        const int piece = r.pmajor ? item / nt : item % r.splits;
         int tm, tn;
-        tile_coords(item - piece * nt, tiles_m, tiles_n, tm, tn);
+        tile_coords(r.pmajor ? item - piece * nt : item / r.splits, tiles_m, tiles_n, tm, tn);
         put(tm, tn, piece, b, 0);
       }
       break;

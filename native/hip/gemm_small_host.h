@@ -33,15 +33,25 @@ inline int small_splits(int tiles, int nk, int cus) {
 }
 
 // The split-K form of the 256x256 asm frame (bf16 v57, fp8 v24; gemm_w4ap.h SPLIT): K pieces per
-// tile -- as many as fit the CUs in one wave (cus / tiles), each of at least kAsmPieceMinKt K-tiles (an
-// even count); 1 = no split.
+// tile -- as many as fit the CUs in one wave (cus / tiles), at most 2, each of at least kAsmPieceMinKt
+// K-tiles (an even count); 1 = no split. Three or four pieces of a 64-tile grid lost to the 128x128
+// kernels (2048^2x8192: 902-964 vs 1003 TF/s; the last arrival's serial reads of 2-3 slabs),
+// profiles/r6_splitk/sweep_v57_s3_s4.jsonl, order_s34.jsonl.
 constexpr int kAsmPieceMinKt = 16;
+constexpr int kAsmMaxSplits = 2;
+// The last piece's default share of K: 52 % (profiles/r6_splitk/band_bf16.jsonl, band_fp8.jsonl: +1-5 %
+// over even pieces at K 4096-8192; the first piece's slab stores and release run under the last one's
+// K-loop).
+constexpr int kAsmLastPermille = 520;
 // Sweep knobs of the split-K asm form, per host thread (amdgo_gemm_set_asm_split): a forced piece count
-// (0 = the automatic one below; forced pieces keep >= 4 K-tiles) and the last piece's share of K in
-// permille (0 = the default, asm_last_pairs).
+// (0 = the automatic one below; forced pieces keep >= 4 K-tiles), the last piece's share of K in
+// permille (0 = kAsmLastPermille; 500 = even pieces) and the item order.
 struct AsmSplitKnobs {
   int splits = 0;
   int last_permille = 0;
+  int piece_major = 0;   // 1: piece-major items; 0 (default): a tile's pieces adjacent, on one XCD, so the
+                         // last arrival reads the other slab from its own L2 (2048x4096x8192 1309 -> 1329,
+                         // 2560^3 735 -> 811 TF/s; profiles/r6_splitk/order_s2.jsonl)
 };
 inline AsmSplitKnobs& asm_split_knobs() {
   static thread_local AsmSplitKnobs k;
@@ -56,14 +66,16 @@ inline int asm_splits(int tiles, int nk, int cus) {
   int s = cus / tiles;
   const int most = nk / kAsmPieceMinKt;
   if (s > most) s = most;
+  if (s > kAsmMaxSplits) s = kAsmMaxSplits;
   return s > 1 ? s : 1;
 }
+inline int asm_piece_major() { return asm_split_knobs().piece_major; }
 // K-tile pairs of the last piece (0 = even pieces). The tile's last arrival sums the others' slabs; a
 // longer last piece lets the other pieces' slab stores and release run under its K-loop instead of
 // after it. Every piece keeps >= 2 pairs.
 inline int asm_last_pairs(int nk, int splits) {
-  const int pm = asm_split_knobs().last_permille;
-  if (splits < 2 || pm <= 0) return 0;
+  const int pm = asm_split_knobs().last_permille ? asm_split_knobs().last_permille : kAsmLastPermille;
+  if (splits < 2) return 0;
   const int pairs = nk / 2;
   const int last = (pairs * pm + 500) / 1000;
   if (last < 2 || pairs - last < 2 * (splits - 1)) return 0;

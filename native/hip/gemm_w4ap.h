@@ -195,6 +195,7 @@ struct W4Split {
   float* ws = nullptr;   // tiles x splits x 4 waves x 64 KiB
   int* cnt = nullptr;    // tiles x 2 (arrivals, done), zero between launches
   int last_pairs = 0;    // K-tile pairs of the last piece; 0 = even pieces (gemm_small_host.h asm_last_pairs)
+  int pmajor = 1;        // item order: 1 piece-major, 0 tile-major (a tile's pieces adjacent, on one XCD)
 };
 
 // SPLIT: this workgroup's reduction (every wave calls it). False: the workgroup stored its partial and
@@ -309,8 +310,8 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
   if constexpr (SPLIT) {
     const int items = nwg * sp.splits;                    // gridDim == items
     const int item = xcd_remap((int)blockIdx.x, items);
-    piece = item / nwg;
-    tile = item - piece * nwg;
+    piece = sp.pmajor ? item / nwg : item % sp.splits;
+    tile = sp.pmajor ? item - piece * nwg : item / sp.splits;
     per = items;                                          // one item per workgroup: no next tile
     t_end = nwg;
   } else if constexpr (SQ) {

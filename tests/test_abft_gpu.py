@@ -99,7 +99,7 @@ def test_abft_catches_an_unwritten_tile(cuda_device):
     assert len(G.abft_check(a, bt, c, r.tile_m, r.tile_n).bad_tiles) == r.tiles_m * r.tiles_n
 
 
-@pytest.mark.parametrize("variant", [50, 51, 52, 53, 54, 55, 56, 25, 44, 45, 42, 18, 47, 48, 60, 61, 62, 0])
+@pytest.mark.parametrize("variant", [50, 51, 52, 53, 54, 55, 56, 57, 25, 44, 45, 42, 18, 47, 48, 60, 61, 62, 0])
 def test_placed_dispatch_is_bitwise_the_timed_one_bf16(cuda_device, variant):
     """Every production bf16 kernel's placement-recording instantiation computes bit-for-bit the timed
     kernel's C, and records one placement per workgroup of the raster's grid."""
@@ -108,8 +108,8 @@ def test_placed_dispatch_is_bitwise_the_timed_one_bf16(cuda_device, variant):
 
     m, n, k = {50: (8192, 8192, 4096), 51: (4096, 4096, 8192), 52: (2048, 2048, 32768), 53: (4096, 4096, 3072),
                54: (4096, 4096, 3072), 55: (2048, 2048, 2048), 56: (4096, 4096, 2048), 25: (4096, 4096, 1024),
-               60: (1024, 1024, 1024), 61: (1024, 1024, 4096), 62: (2560, 2560, 2560), 0: (1000, 768, 512)}.get(
-                   variant, (4096, 4096, 4096))
+               60: (1024, 1024, 1024), 61: (1024, 1024, 4096), 62: (2560, 2560, 2560), 0: (1000, 768, 512),
+               57: (2560, 2560, 8192)}.get(variant, (4096, 4096, 4096))
     a, bt = _operands(m, n, k, "bf16", cuda_device, seed=3)
     G.set_variant(variant)
     try:
@@ -126,13 +126,14 @@ def test_placed_dispatch_is_bitwise_the_timed_one_bf16(cuda_device, variant):
     assert all(0 <= x < 8 for x in xcc) and -1 not in place.cpu().tolist(), f"v{r.variant}: {xcc[:16]}"
 
 
-@pytest.mark.parametrize("variant", [20, 21, 22, 23, 10, 18, 15, 16, 17, 60, 61, 62, 0])
+@pytest.mark.parametrize("variant", [20, 21, 22, 23, 24, 10, 18, 15, 16, 17, 60, 61, 62, 0])
 def test_placed_dispatch_is_bitwise_the_timed_one_fp8(cuda_device, variant):
     import torch
     from gpu_operator_amd.ops import gemm as G
 
     m, n, k = {10: (8192, 8192, 512), 18: (8192, 8192, 2048), 60: (1024, 1024, 1024), 61: (1024, 1024, 16384),
-               62: (2560, 2560, 2560), 0: (1000, 768, 512), 21: (8192, 8192, 2048), 22: (8192, 8192, 4096)}.get(
+               62: (2560, 2560, 2560), 0: (1000, 768, 512), 21: (8192, 8192, 2048), 22: (8192, 8192, 4096),
+               24: (2560, 2560, 16384)}.get(
                    variant, (4096, 4096, 4096))
     a, bt = _operands(m, n, k, "fp8", cuda_device, seed=5)
     G.set_fp8_variant(variant)
@@ -182,7 +183,8 @@ def _validate(*args, timeout=600):
 
 
 @pytest.mark.parametrize("dtype,shape,tile", [("bf16", "8192", (5, 7)), ("fp8", "8192", (31, 0)),
-                                              ("bf16", "1024x1024x4096", (3, 6)), ("bf16", "2560", (9, 1))])
+                                              ("bf16", "1024x1024x4096", (3, 6)), ("bf16", "2560", (9, 1)),
+                                              ("bf16", "2560x2560x8192", (4, 8)), ("fp8", "2560x2560x16384", (2, 3))])
 def test_validator_names_the_injected_tile(dtype, shape, tile):
     rc, lines, err = _validate("--shapes", shape, "--dtype", dtype, "--iters", "5", "--inject-fault",
                                f"{tile[0]},{tile[1]}")
@@ -191,7 +193,7 @@ def test_validator_names_the_injected_tile(dtype, shape, tile):
     assert not g["ok"] and g["kind"] == "correctness", g
     assert g["tile"] == list(tile) and g["bad_tiles"] == 1 and g["checked_fraction"] == 1.0, g
     assert g["xcd"] is None or 0 <= g["xcd"] < 8, g
-    if g["variant"] != 61:                    # split-K: the pieces of a tile may sit on several XCDs
+    if g["variant"] not in (61, 57, 24):      # split-K: the pieces of a tile may sit on several XCDs
         assert isinstance(g["xcd"], int) and set(g["cu"]) == {"se", "sh", "cu"}, g
     assert g["bad_tile_list"][0][:2] == list(tile)
     print(json.dumps({k: g[k] for k in ("variant", "tile", "workgroup", "round", "xcd", "cu") if k in g}))

@@ -84,6 +84,8 @@ def _small(M, N, K, cus):
     tiles128 = M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and K >= 64
     nwg = (M // BM) * (N // BN)
     if tiles256 and 4 * nwg > cus and 2 * nwg <= cus:
+        if cus == 256 and K % 128 == 0 and K >= 4096:
+            return 57                               # round 6: the asm frame in two K pieces
         return 62                                   # 256x128 tiles: one wave of the chip
     if not (tiles128 and (not tiles256 or 4 * nwg <= cus)):
         return None
@@ -186,6 +188,9 @@ def _small_fp8(M, N, K, cus, pin):
     if pin == 0 and tiles128 and (not tiles256 or 4 * nwg <= cus):
         return 61 if _splits((M // 128) * (N // 128), K // 128, cus) > 1 else 60
     if pin == 0 and tiles256 and 4 * nwg > cus and 2 * nwg <= cus:
+        pgrid = (min(nwg, cus) // 8) * 8
+        if cus == 256 and K % 256 == 0 and K >= 8192 and pgrid >= 8:
+            return 24                               # round 6: the asm frame in two K pieces
         return 62
     return None
 
@@ -243,7 +248,7 @@ def test_persistent_launch_grid_rounds_up_to_whole_xcd_groups(lib):
 
 def _asm_splits(tiles, nk, cus):
     """gemm_small_host.h asm_splits: the split-K asm form's pieces per 256x256 tile (>= 16 K-tiles)."""
-    return max(1, min(cus // tiles, nk // 16)) if tiles else 1
+    return max(1, min(cus // tiles, nk // 16, 2)) if tiles else 1
 
 
 def test_split_k_asm_pins_run_where_they_can_and_fall_back_otherwise(lib):

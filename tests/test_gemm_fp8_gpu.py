@@ -149,7 +149,7 @@ def test_fp8_production_variant_set_is_closed(cuda_device):
     import torch
     from gpu_operator_amd.ops import gemm as G
 
-    for bad in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 19, 24, 28, 40, 99):
+    for bad in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 19, 25, 28, 40, 99):
         with pytest.raises(ValueError):
             G.set_fp8_variant(bad)
     assert G.get_fp8_variant() == 0
@@ -163,6 +163,7 @@ def test_fp8_production_variant_set_is_closed(cuda_device):
         assert G.resolve_fp8_variant(12288, 4096, 1024) == 21            # a 16-tile side keeps v21
         assert G.resolve_fp8_variant(4096, 4096, 4096) == 22                # one dispatch wave
         assert G.resolve_fp8_variant(2048, 4096, 4096) == 62                # 128 tiles: 256x128 tiles fill the chip
+        assert G.resolve_fp8_variant(2048, 4096, 16384) == 24               # 128 tiles, long K: two K pieces
         assert G.resolve_fp8_variant(4096, 8192, 4096) == 22                # a 16-tile side, K >= 4096
         assert G.resolve_fp8_variant(4096 + 256, 4096, 4096) == 20
         assert G.resolve_fp8_variant(8192, 8192, 8192 + 128) in (16, 18)   # odd K-tile count

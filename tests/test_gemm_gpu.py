@@ -170,14 +170,16 @@ def test_production_variant_set_is_closed(cuda_device):
                                         (8192, 8192, 128, 25), (256, 256, 64, 60), (300, 256, 256, 0),
                                         (1024, 1024, 1024, 60), (2048, 2048, 2048, 60), (1152, 1152, 1024, 60),
                                         (1024, 1024, 8192, 61), (1024, 1024, 2048, 61), (1024, 1024, 512, 60),
-                                        (2560, 2560, 2560, 62), (4096, 2048, 4096, 62), (3072, 3072, 3072, 53)])
+                                        (2560, 2560, 2560, 62), (4096, 2048, 4096, 57), (3072, 3072, 3072, 53),
+                                        (2560, 2560, 8192, 57), (2560, 2560, 2048, 62)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""
     import torch
     from gpu_operator_amd.ops import gemm as G
 
     if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
-        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42, 53: 42, 54: 42, 55: 42, 56: 42}.get(want, want)
+        want = {44: 42, 45: 42, 47: 42, 48: 42, 50: 42, 51: 42, 52: 42, 53: 42, 54: 42, 55: 42, 56: 42,
+                57: 62}.get(want, want)
     assert G.get_variant() == 0
     assert G.resolve_variant(m, n, k) == want
 
@@ -275,8 +277,8 @@ def test_small_grid_kernel_v60_matches_fp32_reference(cuda_device, v, m, n, k):
     assert G.resolve_variant(1024, 1024, 1024) == 60          # the automatic choice for a 16-tile grid
 
 
-@pytest.mark.parametrize("m,n,k,splits", [(2560, 2560, 2560, 2), (2048, 2048, 8192, 4), (1024, 1024, 4096, 4),
-                                          (512, 512, 8192, 8), (2048, 512, 4096, 4), (1536, 2560, 3072, 3)])
+@pytest.mark.parametrize("m,n,k,splits", [(2560, 2560, 2560, 2), (2048, 2048, 8192, 2), (1024, 1024, 4096, 2),
+                                          (512, 512, 8192, 2), (2048, 512, 4096, 2), (1536, 2560, 3072, 2)])
 def test_split_k_asm_v57_matches_fp32_reference_on_repeat(cuda_device, m, n, k, splits):
     """v57: the asm 256x256 frame, one (tile, K piece) per workgroup; each tile's last arriving waves
     sum the fp32 slabs in piece order. Repeated launches on one stream (the counters must be reset),
@@ -307,17 +309,18 @@ def test_split_k_asm_v57_matches_fp32_reference_on_repeat(cuda_device, m, n, k, 
         G.set_variant(old)
 
 
-@pytest.mark.parametrize("m,n,k,splits,permille", [(2560, 2560, 8192, 2, 540), (2048, 2048, 8192, 4, 340),
-                                                   (2048, 2048, 8192, 3, 400), (1024, 1024, 4096, 2, 700)])
-def test_split_k_asm_v57_uneven_pieces(cuda_device, m, n, k, splits, permille):
-    """v57 with forced piece counts and a longer last piece (the first pieces' slabs stored under the
-    last one's K-loop): against the fp32 reference, repeated launches bitwise equal."""
+@pytest.mark.parametrize("m,n,k,splits,permille,tile_major", [
+    (2560, 2560, 8192, 2, 540, False), (2048, 2048, 8192, 4, 340, False), (2048, 2048, 8192, 3, 400, True),
+    (1024, 1024, 4096, 2, 700, False), (2048, 4096, 8192, 2, 540, True), (2048, 2048, 8192, 4, 0, True)])
+def test_split_k_asm_v57_uneven_pieces(cuda_device, m, n, k, splits, permille, tile_major):
+    """v57 with forced piece counts, a longer last piece (the first pieces' slabs stored under the last
+    one's K-loop) and either item order: against the fp32 reference, repeated launches bitwise equal."""
     import torch
     from gpu_operator_amd.ops import gemm as G
 
     old = G.get_variant()
     G.set_variant(57)
-    G.set_asm_split(splits, permille)
+    G.set_asm_split(splits, permille, piece_major=not tile_major)
     try:
         assert G.raster(m, n, k, "bf16").pieces == splits
         g = torch.Generator(device=cuda_device).manual_seed(m + 3 * n + k + permille)

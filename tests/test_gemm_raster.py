@@ -19,6 +19,7 @@ SHAPES = [
     (1024, 1024, 16384), (512, 512, 8192), (2048, 2048, 8192), (12288, 12288, 12288), (8192, 8192, 2048),
     (4096, 4096, 32768), (16384, 16384, 1024), (1000, 1000, 1000), (768, 512, 1024), (4096, 8192, 12288),
     (2816, 2816, 2816), (1536, 1536, 1536), (256, 256, 256), (3000, 200, 4096),
+    (2560, 2560, 8192), (2560, 2560, 16384), (2048, 4096, 8192),     # v57 / fp8 v24: split-K asm frame
 ]
 
 
@@ -60,26 +61,36 @@ def test_raster_is_a_bijection(dtype, shape):
 @pytest.mark.parametrize("shape", [(2560, 2560, 2560), (2048, 2048, 8192), (1024, 1024, 4096), (512, 512, 8192),
                                    (2560, 2560, 8192), (4096, 4096, 4096), (1024, 1024, 1024)],
                          ids=lambda s: "x".join(map(str, s)))
-def test_split_k_asm_raster_pinned(shape):
-    """v57 pinned: a bijection of (tile, piece) onto the grid; piece-major, so each XCD's run of
-    workgroups covers neighbouring tiles at one K range. Shapes it cannot split fall back to v55."""
+@pytest.mark.parametrize("tile_major", [False, True])
+def test_split_k_asm_raster_pinned(shape, tile_major):
+    """v57 pinned: a bijection of (tile, piece) onto the grid; piece-major, each XCD's run of workgroups
+    covers neighbouring tiles at one K range; tile-major, a tile's pieces are adjacent workgroups of one
+    XCD. Shapes it cannot split fall back to v55."""
     from gpu_operator_amd.ops import gemm as G
 
     m, n, k = shape
     old = G.get_variant()
     G.set_variant(57)
+    G.set_asm_split(0, 0, piece_major=not tile_major)
     try:
         r = G.raster(m, n, k, "bf16", cus=256)
     finally:
+        G.set_asm_split()
         G.set_variant(old)
     tiles = (m // 256) * (n // 256)
-    splits = min(256 // tiles, (k // 64) // 16)
+    splits = min(256 // tiles, (k // 64) // 16, 2)
     if splits < 2:
         assert r.variant == 55 and r.kind == "persistent"
         return
     assert (r.variant, r.kind, r.pieces, r.grid) == (57, "split", splits, tiles * splits)
     slots = _check_bijection(r)
     assert {b for b, _ in slots} == set(range(r.grid))
+    if tile_major:
+        # every tile's pieces on one XCD (b % 8) whenever the XCD's run holds whole tiles
+        if (tiles * splits) % 8 == 0 and ((tiles * splits) // 8) % splits == 0:
+            for tm, tn in itertools.product(range(r.tiles_m), range(r.tiles_n)):
+                assert len({b % 8 for b in r.owner[tm][tn]}) == 1
+        return
     # the workgroups of one XCD (b % 8) hold one piece except where the piece-major order wraps
     pieces_of_xcd = {}
     for tm, tn, p in itertools.product(range(r.tiles_m), range(r.tiles_n), range(r.pieces)):
@@ -95,7 +106,7 @@ def test_raster_kinds_follow_the_dispatch():
         for m, n, k in SHAPES:
             r = G.raster(m, n, k, dtype, cus=256)
             assert r.variant == plan(m, n, k, 256, 0), (dtype, m, n, k)
-            want = {60: "small", 61: "small", 62: "small", 0: "generic"}.get(r.variant)
+            want = {60: "small", 61: "small", 62: "small", 0: "generic", 57: "split", 24: "split"}.get(r.variant)
             if want:
                 assert r.kind == want, (dtype, m, n, k, r.variant, r.kind)
             if r.variant == 61:

@@ -37,10 +37,11 @@ class _Pinned:
         self.G, self.dtype = G, dtype
         self.split = None
         self.asm = None
-        if spec.startswith("p") and "b" in spec[1:]:          # p57s2b540: v57 / v24 in 2 pieces, the last 54 % of K
-            v, rest = spec[1:].split("s")
+        if spec.startswith("p") and "b" in spec[1:]:          # p57s2b540[p]: v57 / v24 in 2 pieces, the last 54 % of K
+            v, rest = spec[1:].split("s")                     # (p: piece-major items; t, the default: tile-major)
             s, b = rest.split("b")
-            self.v, self.lab, self.asm = int(v), None, (int(s), int(b))
+            pm = b.endswith("p")
+            self.v, self.lab, self.asm = int(v), None, (int(s), int(b.rstrip("tp")), pm)
         elif spec.startswith("p") and "s" in spec[1:]:          # p61s2: v61 aiming at 2 workgroups per CU
             v, t = spec[1:].split("s")
             self.v, self.lab, self.split = int(v), None, int(t)
