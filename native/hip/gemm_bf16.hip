@@ -120,6 +120,10 @@ struct Bf16Rule {
 static constexpr Bf16Rule kBf16Rules[] = {
     // a 256x256 grid of at most a quarter of the CUs (or a shape only 128-tileable): 128x128 tiles, 4x
     // the workgroups; split-K too when the 128x128 grid is still far below the chip and K is long
+    // 33-64 256x256 tiles with K >= 16384: the asm frame split in up to four K pieces
+    {57, [](const Bf16Shape& c) { return c.mi355 && c.tiles256 && 8 * c.nwg > c.cus && 4 * c.nwg <= c.cus &&
+                                         c.K % (2 * BK) == 0 && c.K >= 256 * BK; },
+     "profiles/r6_splitk/tree_s34.jsonl (2048^2x16384 1189 vs v60 1012 TF/s, 1.07x hipBLASLt)"},
     {61, [](const Bf16Shape& c) {
        return c.tiles128 && (!c.tiles256 || 4 * c.nwg <= c.cus) &&
               small_splits((c.M / S_BM) * (c.N / S_BN), c.K / S_BK, c.cus) > 1; },

@@ -33,12 +33,13 @@ inline int small_splits(int tiles, int nk, int cus) {
 }
 
 // The split-K form of the 256x256 asm frame (bf16 v57, fp8 v24; gemm_w4ap.h SPLIT): K pieces per
-// tile -- as many as fit the CUs in one wave (cus / tiles), at most 2, each of at least kAsmPieceMinKt
-// K-tiles (an even count); 1 = no split. Three or four pieces of a 64-tile grid lost to the 128x128
-// kernels (2048^2x8192: 902-964 vs 1003 TF/s; the last arrival's serial reads of 2-3 slabs),
-// profiles/r6_splitk/sweep_v57_s3_s4.jsonl, order_s34.jsonl.
+// tile -- as many as fit the CUs in one wave (cus / tiles), each of at least kAsmPieceMinKt K-tiles (an
+// even count); 1 = no split. At most 2 for grids of more than a quarter of the CUs (the measured band),
+// at most 4 below that: four pieces of a 64-tile grid win at K 16384 (2048^2x16384 1189 vs 1012 TF/s
+// for the 128x128 kernel, 1.07x hipBLASLt) and lose at 8192 (900-918 vs 977; three pieces tie),
+// profiles/r6_splitk/tree_s34.jsonl, order_s34.jsonl.
 constexpr int kAsmPieceMinKt = 16;
-constexpr int kAsmMaxSplits = 2;
+constexpr int kAsmMaxSplits = 4;
 // The last piece's default share of K: 52 % (profiles/r6_splitk/band_bf16.jsonl, band_fp8.jsonl: +1-5 %
 // over even pieces at K 4096-8192; the first piece's slab stores and release run under the last one's
 // K-loop).
@@ -66,7 +67,8 @@ inline int asm_splits(int tiles, int nk, int cus) {
   int s = cus / tiles;
   const int most = nk / kAsmPieceMinKt;
   if (s > most) s = most;
-  if (s > kAsmMaxSplits) s = kAsmMaxSplits;
+  const int cap = 4 * tiles > cus ? 2 : kAsmMaxSplits;
+  if (s > cap) s = cap;
   return s > 1 ? s : 1;
 }
 inline int asm_piece_major() { return asm_split_knobs().piece_major; }
@@ -74,8 +76,11 @@ inline int asm_piece_major() { return asm_split_knobs().piece_major; }
 // longer last piece lets the other pieces' slab stores and release run under its K-loop instead of
 // after it. Every piece keeps >= 2 pairs.
 inline int asm_last_pairs(int nk, int splits) {
-  const int pm = asm_split_knobs().last_permille ? asm_split_knobs().last_permille : kAsmLastPermille;
-  if (splits < 2) return 0;
+  // the longer last piece is measured for two pieces; three and four run even (2048^2x16384: 4 even
+  // 1189, the last 28 % 1179, 31 % 1118 TF/s)
+  const int pm = asm_split_knobs().last_permille ? asm_split_knobs().last_permille
+                                                 : (splits == 2 ? kAsmLastPermille : 0);
+  if (splits < 2 || pm <= 0) return 0;
   const int pairs = nk / 2;
   const int last = (pairs * pm + 500) / 1000;
   if (last < 2 || pairs - last < 2 * (splits - 1)) return 0;

@@ -183,8 +183,8 @@ struct W4apEpi {
 // x 64 lanes x 16 B, one contiguous KiB per store) with plain stores, drains them, meets its waves at a
 // barrier, releases ONCE at agent scope and counts itself done; the last arrival keeps its partial in
 // its accumulators, waits for the done count of the S - 1 workgroups that arrived before it, acquires
-// (agent scope) and sums every piece in piece order -- its own from its accumulators at its place -- so
-// the result does not depend on arrival order (cdna_hip_programming.md §5 "In-launch split-K reduction",
+// (agent scope) and sums every piece in a fixed tree of commutative two-input adds -- its own partial
+// from its accumulators -- so the result does not depend on arrival order (cdna_hip_programming.md §5 "In-launch split-K reduction",
 // §6 Guideline 16). The wait is only ever for workgroups that have already arrived, i.e. are running
 // and owe nothing but their stores: no co-residency is assumed. The last arrival resets both counters
 // for the next launch, then runs the ordinary epilogue. Only S - 1 of S partials travel, and each writer
@@ -254,21 +254,56 @@ __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, i
                  :: "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3),
                     "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]));
   };
-  if (S == 2) {
-    // two pieces: own + other == other + own exactly; 32 quads (128 VGPRs) of the other slab in flight
-    const f4* const other = ws4 + slab(1 - piece);
+  // The sum is a fixed tree of two-input adds -- S = 2: p0 + p1; 3: (p0 + p1) + p2; 4: (p0 + p1) + (p2 + p3)
+  // -- and a two-input add is commutative, so whichever piece reduces, holding its own partial in its
+  // accumulators, computes the same bits. add_slab: accumulators += slab p (32 quads, 128 VGPRs, in flight
+  // at once); add_pair: accumulators += (slab a + slab b), both slabs' 16-quad chunks in flight together.
+  auto add_slab = [&](int p) {
+    const f4* const src = ws4 + slab(p);
     static_for<0, 2>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       f4 t[32];
 #pragma unroll
-      for (int j = 0; j < 32; ++j) t[j] = other[(q * 32 + j) * 64];
+      for (int j = 0; j < 32; ++j) t[j] = src[(q * 32 + j) * 64];
       static_for<0, 32>([&](auto J) {
         constexpr int i = q * 32 + decltype(J)::value;
         const f4 tj = t[decltype(J)::value];   // (a generic lambda does not capture a name used only in asm operands)
-        put(std::integral_constant<int, i>{}, tj + own(std::integral_constant<int, i>{}));
+        put(std::integral_constant<int, i>{}, own(std::integral_constant<int, i>{}) + tj);
       });
     });
+  };
+  auto add_pair = [&](int pa, int pb) {
+    const f4* const sa = ws4 + slab(pa);
+    const f4* const sb = ws4 + slab(pb);
+    static_for<0, 4>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      f4 ta[16], tb[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        ta[j] = sa[(q * 16 + j) * 64];
+        tb[j] = sb[(q * 16 + j) * 64];
+      }
+      static_for<0, 16>([&](auto J) {
+        constexpr int i = q * 16 + decltype(J)::value;
+        const f4 pj = ta[decltype(J)::value] + tb[decltype(J)::value];
+        put(std::integral_constant<int, i>{}, own(std::integral_constant<int, i>{}) + pj);
+      });
+    });
+  };
+  if (S == 2) {
+    add_slab(1 - piece);
+  } else if (S == 3) {
+    if (piece == 2) {
+      add_pair(0, 1);
+    } else {
+      add_slab(1 - piece);
+      add_slab(2);
+    }
+  } else if (S == 4) {
+    add_slab(piece ^ 1);
+    add_pair(piece < 2 ? 2 : 0, piece < 2 ? 3 : 1);
   } else {
+    // more pieces (forced only): piece order, 16 quads at a time
     static_for<0, 4>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       f4 acc[16];

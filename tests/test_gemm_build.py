@@ -233,7 +233,8 @@ def test_w4ap_split_k_pipeline(asm):
     assert len(kernels) == 1
     for body, st in kernels:
         assert _audit_asm_pipeline(body, st) == 8 * 128
-        assert body.count("v_accvgpr_write_b32") == 2 * 256
+        writes = body.count("v_accvgpr_write_b32")
+        assert writes % 256 == 0 and writes >= 2 * 256, writes
         assert len(re.findall(r"global_atomic_add\b", body)) == 2
         assert len(re.findall(r"global_store_dwordx4\b", body)) >= 64
         assert body.count("buffer_wbl2") == 1 and body.count("buffer_inv") == 1
@@ -372,6 +373,7 @@ def test_placement_record_only_in_rec_kernels(request, which):
         assert has == _is_rec(n), n
         if _is_rec(n):
             # the record costs no scratch and leaves the pinned accumulators to the asm blocks
-            assert "scratch_" not in body and "ScratchSize: 0" in asm[asm.index(n + ":"):][:200000], n
+            tail = asm[asm.index(n + ":"):]
+            assert "scratch_" not in body and re.search(r"ScratchSize: (\d+)", tail).group(1) == "0", n
             if "256x256" in n:      # the asm-pinned families (the small kernels' accumulators are hipcc's)
                 _no_compiler_agpr_access(body)

@@ -87,6 +87,8 @@ def _small(M, N, K, cus):
         if cus == 256 and K % 128 == 0 and K >= 4096:
             return 57                               # round 6: the asm frame in two K pieces
         return 62                                   # 256x128 tiles: one wave of the chip
+    if tiles256 and 8 * nwg > cus and 4 * nwg <= cus and cus == 256 and K % 128 == 0 and K >= 16384:
+        return 57                                   # round 6: the asm frame in up to four K pieces
     if not (tiles128 and (not tiles256 or 4 * nwg <= cus)):
         return None
     return 61 if _splits((M // 128) * (N // 128), K // 64, cus) > 1 else 60
@@ -248,7 +250,7 @@ def test_persistent_launch_grid_rounds_up_to_whole_xcd_groups(lib):
 
 def _asm_splits(tiles, nk, cus):
     """gemm_small_host.h asm_splits: the split-K asm form's pieces per 256x256 tile (>= 16 K-tiles)."""
-    return max(1, min(cus // tiles, nk // 16, 2)) if tiles else 1
+    return max(1, min(cus // tiles, nk // 16, 2 if 4 * tiles > cus else 4)) if tiles else 1
 
 
 def test_split_k_asm_pins_run_where_they_can_and_fall_back_otherwise(lib):

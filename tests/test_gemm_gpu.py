@@ -171,7 +171,8 @@ def test_production_variant_set_is_closed(cuda_device):
                                         (1024, 1024, 1024, 60), (2048, 2048, 2048, 60), (1152, 1152, 1024, 60),
                                         (1024, 1024, 8192, 61), (1024, 1024, 2048, 61), (1024, 1024, 512, 60),
                                         (2560, 2560, 2560, 62), (4096, 2048, 4096, 57), (3072, 3072, 3072, 53),
-                                        (2560, 2560, 8192, 57), (2560, 2560, 2048, 62)])
+                                        (2560, 2560, 8192, 57), (2560, 2560, 2048, 62), (2048, 2048, 16384, 57),
+                                        (2048, 2048, 8192, 60)])
 def test_automatic_dispatch_resolution(cuda_device, m, n, k, want):
     """The automatic dispatch picks the kernel documented in gemm_bf16.hip (256-CU MI355X)."""
     import torch
@@ -277,8 +278,8 @@ def test_small_grid_kernel_v60_matches_fp32_reference(cuda_device, v, m, n, k):
     assert G.resolve_variant(1024, 1024, 1024) == 60          # the automatic choice for a 16-tile grid
 
 
-@pytest.mark.parametrize("m,n,k,splits", [(2560, 2560, 2560, 2), (2048, 2048, 8192, 2), (1024, 1024, 4096, 2),
-                                          (512, 512, 8192, 2), (2048, 512, 4096, 2), (1536, 2560, 3072, 2)])
+@pytest.mark.parametrize("m,n,k,splits", [(2560, 2560, 2560, 2), (2048, 2048, 8192, 4), (1024, 1024, 4096, 4),
+                                          (512, 512, 8192, 4), (2048, 512, 4096, 4), (1536, 2560, 3072, 3)])
 def test_split_k_asm_v57_matches_fp32_reference_on_repeat(cuda_device, m, n, k, splits):
     """v57: the asm 256x256 frame, one (tile, K piece) per workgroup; each tile's last arriving waves
     sum the fp32 slabs in piece order. Repeated launches on one stream (the counters must be reset),

@@ -78,7 +78,7 @@ def test_split_k_asm_raster_pinned(shape, tile_major):
         G.set_asm_split()
         G.set_variant(old)
     tiles = (m // 256) * (n // 256)
-    splits = min(256 // tiles, (k // 64) // 16, 2)
+    splits = min(256 // tiles, (k // 64) // 16, 2 if 4 * tiles > 256 else 4)
     if splits < 2:
         assert r.variant == 55 and r.kind == "persistent"
         return
