@@ -84,6 +84,9 @@ struct Fp8Rule {
 static constexpr Fp8Rule kFp8Rules[] = {
     // a 256x256 grid of at most a quarter of the CUs (or a shape only 128-tileable): the 128x128
     // kernel, split-K when the 128x128 grid is under the CU count (the bf16 rows' rule, same kernel frame)
+    // 33-64 256x256 tiles with K >= 32768: the asm frame split in four K pieces
+    {24, [](const Fp8Shape& c) { return c.ap && c.tiles && 8 * c.nwg > c.cus && 4 * c.nwg <= c.cus && c.K >= 256 * F8_BK; },
+     "profiles/r6_splitk/fp8_s34.jsonl (2048^2x32768 2357 vs 2004 TF/s, 1024x4096x32768 2466 vs 1762; 1.5x hipBLASLt)"},
     {61, [](const Fp8Shape& c) {
        return c.tiles128 && (!c.tiles || 4 * c.nwg <= c.cus) &&
               small_splits((c.M / S_BM) * (c.N / S_BN), c.K / 128, c.cus) > 1; },

@@ -187,6 +187,10 @@ def _small_fp8(M, N, K, cus, pin):
     if pin == 62:
         return 62 if tiles128 and M % 256 == 0 else 0
     nwg = (M // 256) * (N // 256)
+    pgrid = (min(nwg, cus) // 8) * 8
+    if (pin == 0 and tiles256 and 8 * nwg > cus and 4 * nwg <= cus and cus == 256 and K % 256 == 0 and K >= 32768
+            and pgrid >= 8):
+        return 24                                   # round 6: the asm frame in four K pieces
     if pin == 0 and tiles128 and (not tiles256 or 4 * nwg <= cus):
         return 61 if _splits((M // 128) * (N // 128), K // 128, cus) > 1 else 60
     if pin == 0 and tiles256 and 4 * nwg > cus and 2 * nwg <= cus:

@@ -164,7 +164,31 @@ def test_fp8_production_variant_set_is_closed(cuda_device):
         assert G.resolve_fp8_variant(4096, 4096, 4096) == 22                # one dispatch wave
         assert G.resolve_fp8_variant(2048, 4096, 4096) == 62                # 128 tiles: 256x128 tiles fill the chip
         assert G.resolve_fp8_variant(2048, 4096, 16384) == 24               # 128 tiles, long K: two K pieces
+        assert G.resolve_fp8_variant(2048, 2048, 32768) == 24               # 64 tiles, K >= 32768: four pieces
         assert G.resolve_fp8_variant(4096, 8192, 4096) == 22                # a 16-tile side, K >= 4096
         assert G.resolve_fp8_variant(4096 + 256, 4096, 4096) == 20
         assert G.resolve_fp8_variant(8192, 8192, 8192 + 128) in (16, 18)   # odd K-tile count
     assert G.resolve_fp8_variant(300, 256, 256) == 0
+
+
+@pytest.mark.parametrize("m,n,k,pieces", [(2560, 2560, 16384, 2), (2048, 2048, 32768, 4), (1536, 2560, 32768, 4)])
+def test_fp8_split_k_asm_v24_matches_fp32_reference_on_repeat(cuda_device, m, n, k, pieces):
+    """fp8 v24 (the q16ap frame's split-K form) as the automatic dispatch runs it: two pieces on a
+    100-tile grid, four on 60-64 tiles; sampled rows of every tile row against the fp32 reference,
+    repeated launches bitwise equal (the pieces are summed in a fixed tree)."""
+    import torch
+    from gpu_operator_amd.ops import gemm as G
+
+    if torch.cuda.get_device_properties(cuda_device).multi_processor_count != 256:
+        pytest.skip("the asm frame runs on the 256-CU MI355X")
+    assert G.resolve_fp8_variant(m, n, k) == 24
+    assert G.raster(m, n, k, "fp8").pieces == pieces
+    g = torch.Generator(device=cuda_device).manual_seed(m + n + k)
+    a = _rand_fp8((m, k), g, cuda_device)
+    bt = _rand_fp8((n, k), g, cuda_device)
+    outs = [G.gemm_fp8(a, bt) for _ in range(3)]
+    torch.cuda.synchronize()
+    rows = torch.tensor([tm * 256 + (tm * 37) % 256 for tm in range(m // 256)], device=cuda_device)
+    ref = a[rows].float() @ bt.float().t()
+    torch.testing.assert_close(outs[0][rows].float(), ref, atol=2e-2 * (k ** 0.5) / 8, rtol=1e-2)
+    assert all(torch.equal(outs[0], c) for c in outs[1:])
