@@ -200,7 +200,7 @@ struct W4Split {
 
 // SPLIT: this workgroup's reduction (every wave calls it). False: the workgroup stored its partial and
 // is finished. True: it was the tile's last arrival and its accumulators now hold the sum over every
-// piece. `flag`: one LDS word no wave touches until the epilogue (wave 0's epilogue staging).
+// piece. `flag`: two LDS words no wave touches until the epilogue (wave 0's epilogue staging).
 __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, int piece, int wid, int lane,
                                                   int* flag) {
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -238,13 +238,15 @@ __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, i
   }
   if (wid == 0 && lane == 0) {
     // every workgroup counted here has arrived and owes only its stores; bounded all the same (~1 s)
-    for (unsigned spins = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1 &&
+    bool seen = false;
+    for (unsigned spins = 0; !(seen = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= S - 1) &&
                              spins < (1u << 24); ++spins)
       __builtin_amdgcn_s_sleep(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     *arrive = 0;                       // ready for the next launch on this stream
     *done = 0;
+    flag[1] = seen;                    // (flag[0] holds the ticket the other waves may still be reading)
   }
   __syncthreads();
   auto put = [&](auto I, f4 t) {
@@ -254,6 +256,12 @@ __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, i
                  :: "i"(4 * i), "i"(4 * i + 1), "i"(4 * i + 2), "i"(4 * i + 3),
                     "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]));
   };
+  if (!__builtin_amdgcn_readfirstlane(flag[1])) {
+    // the wait gave up (a writer that never counted itself done): a NaN tile, never a silent partial sum
+    const float nan = __builtin_nanf("");
+    static_for<0, 64>([&](auto I) { put(I, f4{nan, nan, nan, nan}); });
+    return true;
+  }
   // The sum is a fixed tree of two-input adds -- S = 2: p0 + p1; 3: (p0 + p1) + p2; 4: (p0 + p1) + (p2 + p3)
   // -- and a two-input add is commutative, so whichever piece reduces, holding its own partial in its
   // accumulators, computes the same bits. add_slab: accumulators += slab p (32 quads, 128 VGPRs, in flight
