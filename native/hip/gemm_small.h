@@ -227,11 +227,11 @@ gemm_mfma_small(const void* __restrict__ A, const void* __restrict__ Bt, __bf16*
 // v61, split-K: `splits` workgroups per output tile; piece s of a tile runs K-tiles
 // [s nk / splits, (s + 1) nk / splits), so every tile is cut at the same K offsets and the workgroups
 // sharing an A or B panel stream the same K-slices at the same time (L2 hits). A piece stores its fp32
-// slab (thread-major float4s: one coalesced KiB per wave and accumulator) and draws a ticket from the
-// tile's counter (cdna_hip_programming.md "Projection GEMM at M = 256" item 2: plain 16-B stores, drain,
-// barrier, ONE lane releases at agent scope and counts; the last arriver acquires). The tile's last
-// arriver sums every piece's slab in piece order -- its own included, re-read -- so the result does not
-// depend on arrival order, and writes the bf16 tile. Nobody waits for anybody: the grid needs no
+// slab (thread-major float4s: one coalesced KiB per wave and accumulator) -- round 6: only the pieces
+// that draw an arrival ticket before the last one do (cdna_hip_programming.md "Projection GEMM at M =
+// 256" item 2: plain 16-B stores, drain, barrier, ONE lane releases at agent scope and counts itself
+// done); the last arrival waits for their done count, acquires, and sums the pieces in piece order with
+// its own from its registers, so the result does not depend on arrival order, and writes the bf16 tile. Nobody waits for anybody: the grid needs no
 // co-residency. Item order: pieces of >= 32 K-tiles go piece-major (item = piece x tiles + tile), so
 // the XCD remap gives an XCD a run of neighbouring tiles at ONE K range -- 1024^2x16384 in 4 pieces
 // streams 6 MiB of A and B per XCD instead of 18 (tile-major, every XCD read all of B): bf16 617 ->
@@ -265,33 +265,61 @@ gemm_mfma_small_sk(const void* __restrict__ A, const void* __restrict__ Bt, __bf
   SmallAcc<BMT> acc;
   small_mainloop<F8, BMT>((const char*)A, (const char*)Bt, row_b, tm, tn, kt0, kt1 - kt0, lds, acc);
   if (splits > 1) {
+    // ticket first (the asm frame's protocol, gemm_w4ap.h SPLIT): only the earlier arrivals store their
+    // slab and release; the last arrival keeps its partial in registers, waits for their done count (they
+    // have arrived: they owe only their stores), acquires, and sums the pieces in piece order with its
+    // own at its place -- the same bits whichever piece reduces.
     constexpr size_t SLAB = (size_t)BMT * S_BN;     // floats per tile
     f4* flat = (f4*)&acc[0][0];
-    f4* slab = (f4*)(ws + ((size_t)tile * splits + piece) * SLAB);
-#pragma unroll
-    for (int a = 0; a < Cfg::NACC; ++a) slab[a * S_THREADS + tid] = flat[a];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* const arrive = cnt + 2 * tile;
+    int* const done = arrive + 1;
+    if (tid == 0) flag[0] = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int ticket = flag[0];
+    if (ticket < splits - 1) {
+      f4* slab = (f4*)(ws + ((size_t)tile * splits + piece) * SLAB);
+#pragma unroll
+      for (int a = 0; a < Cfg::NACC; ++a) slab[a * S_THREADS + tid] = flat[a];
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int ticket = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = ticket == splits - 1;
-      if (ticket == splits - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (tid == 0) {
+      bool seen = false;       // bounded (~1 s) although every awaited workgroup is running
+      for (unsigned spins = 0;
+           !(seen = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= splits - 1) &&
+           spins < (1u << 24);
+           ++spins)
+        __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *arrive = 0;             // ready for the next launch on this stream
+      *done = 0;
+      flag[1] = seen;          // (flag[0] holds the ticket the other waves may still be reading)
+    }
+    __syncthreads();
+    if (!flag[1]) {            // the wait gave up: a NaN tile, never a silent partial sum
+#pragma unroll
+      for (int a = 0; a < Cfg::NACC; ++a) flat[a] = f4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
+                                                      __builtin_nanf("")};
+    } else {
+      f4 mine[Cfg::NACC];
+#pragma unroll
+      for (int a = 0; a < Cfg::NACC; ++a) mine[a] = flat[a];
+      for (int p = 0; p < splits; ++p) {
+        const f4* part = (const f4*)(ws + ((size_t)tile * splits + p) * SLAB);
+#pragma unroll
+        for (int a = 0; a < Cfg::NACC; ++a) {
+          const f4 x = p == piece ? mine[a] : part[a * S_THREADS + tid];
+          flat[a] = p == 0 ? x : flat[a] + x;
+        }
       }
     }
-    __syncthreads();
-    if (!*flag) return;
-#pragma unroll
-    for (int a = 0; a < Cfg::NACC; ++a) flat[a] = f4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < splits; ++s) {
-      const f4* part = (const f4*)(ws + ((size_t)tile * splits + s) * SLAB);
-#pragma unroll
-      for (int a = 0; a < Cfg::NACC; ++a) flat[a] += part[a * S_THREADS + tid];
-    }
-    if (tid == 0) cnt[tile] = 0;   // ready for the next launch on this stream
   }
   small_store_c<BMT>(C, N, tm, tn, acc);
 }

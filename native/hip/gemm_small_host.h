@@ -220,7 +220,7 @@ inline void launch_small(const void* a, const void* b, __bf16* c, int M, int N, 
   const int tiles = (M / BMT) * (N / S_BN);
   const int nk = (int)((size_t)K * (F8 ? 1 : 2) / 128);
   const int splits = split ? small_splits(tiles, nk, cus) : 1;
-  SmallWorkspace* w = splits > 1 ? small_workspace(s, (size_t)tiles * splits * BMT * S_BN, tiles) : nullptr;
+  SmallWorkspace* w = splits > 1 ? small_workspace(s, (size_t)tiles * splits * BMT * S_BN, 2 * tiles) : nullptr;
   if (w) {
     hipLaunchKernelGGL((gemm_mfma_small_sk<F8, BMT, REC>), dim3(tiles * splits), dim3(S_THREADS), 0, s, a, b, c, M, N,
                        K, splits, small_piece_major(nk, splits), w->ws, w->cnt);
