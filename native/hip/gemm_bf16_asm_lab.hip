@@ -45,6 +45,7 @@
 #include "gemm_fp8_asm_loop_lab.h"  // every schedule (masks the production header)
 #include "gemm_bf16_kernels.h"
 #include "gemm_fp8_kernels.h"
+#include "gemm_small_host.h"
 
 namespace {
 
@@ -104,7 +105,27 @@ int amdgo_asmlab_gemm_bf16(int v, const void* A, const void* Bt, void* C, int M,
   const auto* b = (const __bf16*)Bt;
   auto* c = (__bf16*)C;
   const int nwg = (M / BM) * (N / BN);
+  // 300-307: the production split-K form (v57) with its reduction knocked out piece by piece
+  // (gemm_w4ap.h w4ap_split_reduce SKO = v - 300: 1 no release, 2 no slab reads, 4 no slab stores);
+  // the pieces, last-piece share and item order are the production defaults
+  auto split_ko = [&](auto KO) -> int {
+    const int splits = asm_splits(nwg, K / BK, device_cu_count(s));
+    if (splits < 2) return (int)hipErrorInvalidValue;
+    SmallWorkspace* w = small_workspace(s, (size_t)nwg * splits * kAsmSlabFloats, nwg * 2);
+    if (!w) return (int)hipErrorOutOfMemory;
+    hipLaunchKernelGGL((gemm_bf16_256x256_w4ap_sk<W4VP_SC_G4_ZC, W4AP_EPI_LEAN, 2, kTimed, decltype(KO)::value>),
+                       dim3(nwg * splits), dim3(W4_THREADS), 0, s, a, b, c, M, N, K, splits, w->ws, w->cnt,
+                       asm_last_pairs(K / BK, splits), asm_piece_major());
+    (void)hipEventRecord(w->done, s);
+    return (int)hipGetLastError();
+  };
   switch (v) {
+    case 300: return split_ko(std::integral_constant<int, 0>{});
+    case 301: return split_ko(std::integral_constant<int, 1>{});
+    case 302: return split_ko(std::integral_constant<int, 2>{});
+    case 303: return split_ko(std::integral_constant<int, 3>{});
+    case 305: return split_ko(std::integral_constant<int, 5>{});
+    case 307: return split_ko(std::integral_constant<int, 7>{});
     case 44:
       hipLaunchKernelGGL((gemm_bf16_256x256_w4s<17, 19, 5, 80, 40, 32, true, false, true>), dim3(nwg),
                          dim3(W4_THREADS), 0, s, a, b, c, M, N, K);

@@ -713,14 +713,14 @@ gemm_bf16_256x256_w4ap(const __bf16* __restrict__ A, const __bf16* __restrict__ 
 
 // w4ap split-K (v57): one (tile, K piece) per workgroup, the piece sums reduced by each tile's last
 // arriving waves (gemm_w4ap.h SPLIT). ws / cnt: gemm_small_host.h's per-(device, stream) workspace.
-template <int SC, int EPI, int DM, Rec REC = kTimed>
+template <int SC, int EPI, int DM, Rec REC = kTimed, int SKO = 0>
 __global__ void __launch_bounds__(W4_THREADS, 1)
 gemm_bf16_256x256_w4ap_sk(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, __bf16* __restrict__ C,
                           int M, int N, int K, int splits, float* __restrict__ ws, int* __restrict__ cnt,
                           int last_pairs, int pmajor) {
   __shared__ __attribute__((aligned(16))) char smem[W4AP_LDS];
   note_placement<REC>();
-  w4ap_run<SC, false, false, false, EPI, DM, true>((const char*)A, (const char*)Bt, C, M, N, K, smem,
+  w4ap_run<SC, false, false, false, EPI, DM, true, SKO>((const char*)A, (const char*)Bt, C, M, N, K, smem,
                                                    W4Split{splits, ws, cnt, last_pairs, pmajor});
 }
 

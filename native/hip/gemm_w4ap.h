@@ -201,6 +201,10 @@ struct W4Split {
 // SPLIT: this workgroup's reduction (every wave calls it). False: the workgroup stored its partial and
 // is finished. True: it was the tile's last arrival and its accumulators now hold the sum over every
 // piece. `flag`: two LDS words no wave touches until the epilogue (wave 0's epilogue staging).
+// SKO: knock-outs for timing in the tools-only lab library (gemm_bf16_asm_lab.hip), wrong results by
+// design -- 1: the writers' release, 2: the reducer's slab reads, 4: the writers' slab stores. Every
+// production instantiation has SKO = 0.
+template <int SKO = 0>
 __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, int piece, int wid, int lane,
                                                   int* flag) {
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -226,11 +230,11 @@ __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, i
   };
   if (ticket < S - 1) {
     f4* const mine = ws4 + slab(piece);
-    static_for<0, 64>([&](auto I) { mine[decltype(I)::value * 64] = own(I); });
+    if constexpr (!(SKO & 4)) static_for<0, 64>([&](auto I) { mine[decltype(I)::value * 64] = own(I); });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wid == 0 && lane == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if constexpr (!(SKO & 1)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -298,7 +302,8 @@ __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, i
       });
     });
   };
-  if (S == 2) {
+  if constexpr (SKO & 2) {
+  } else if (S == 2) {
     add_slab(1 - piece);
   } else if (S == 3) {
     if (piece == 2) {
@@ -341,7 +346,7 @@ __device__ __forceinline__ bool w4ap_split_reduce(const W4Split& sp, int tile, i
 // 1 = VP (per-piece VGPR lane offsets, SGPR K offset), SC indexes the VP schedules; 2 = VP with the
 // A-panel pieces reading rows 32 apart (PA; the epilogue maps LDS slot s to C row 32 (s & 7) + (s >> 3)).
 // EPI: the W4AP_EPI_* forms above (W4apEpi says what the staged epilogue does for each).
-template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0, bool SPLIT = false>
+template <int SC, bool SERP, bool SQ, bool F8, int EPI = 0, int DM = 0, bool SPLIT = false, int SKO = 0>
 __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char* __restrict__ Bt,
                                          __bf16* __restrict__ C, int M, int N, int K, char* smem,
                                          W4Split sp = W4Split{}) {
@@ -538,7 +543,7 @@ __device__ __forceinline__ void w4ap_run(const char* __restrict__ A, const char*
     }
 
     if constexpr (SPLIT) {
-      if (sp.splits > 1 && !w4ap_split_reduce(sp, tile, piece, wid, lane, (int*)(smem + 2 * W4AP_BUF))) return;
+      if (sp.splits > 1 && !w4ap_split_reduce<SKO>(sp, tile, piece, wid, lane, (int*)(smem + 2 * W4AP_BUF))) return;
     }
 
     // wave-private epilogue (the K buffers may be receiving the next tile's DMA): 4 passes of
